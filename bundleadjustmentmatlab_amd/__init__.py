@@ -1,0 +1,13 @@
+"""bundleadjustmentmatlab_amd -- MI355X-native Euclidean bundle adjustment.
+
+Drop-in for the Levenberg-Marquardt path of caomw/BundleAdjustmentMatlab
+(VLG toolbox/bundle: bundle_euclid.m + mex_bundle_{1,2,3}*.c), built on
+hand-written gfx950 HIP kernels behind the C ABI in include/vlgba.h
+(libvlgba.so, built in-tree).
+"""
+from .bundle import (BundleAdjuster, bundle_euclid, bundle_euclid_obs,  # noqa: F401
+                     mex_bundle_1_XABeUVWeAeB, mex_bundle_2_Se_, mex_bundle_3_db_new,
+                     parse_options)
+from ._lib import LIB_PATH, VlgbaError, lib  # noqa: F401
+
+__version__ = "0.1.0"

@@ -1,0 +1,97 @@
+"""ctypes binding of libvlgba.so (include/vlgba.h).
+
+The shared library is built in-tree by ``__graft_entry__.build()`` (or
+``make -C bundleadjustmentmatlab_amd/csrc``).  There is no fallback: if the
+library is missing or cannot be loaded, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libvlgba.so")
+
+c_int, c_double, c_ll = ctypes.c_int, ctypes.c_double, ctypes.c_longlong
+c_dp = ctypes.POINTER(ctypes.c_double)
+c_ip = ctypes.POINTER(ctypes.c_int)
+c_up = ctypes.POINTER(ctypes.c_ubyte)
+
+
+class VlgbaProblem(ctypes.Structure):
+    _fields_ = [("m", c_int), ("n", c_int), ("num_a", c_int), ("num_obs", c_ll),
+                ("obs_pt", c_ip), ("obs_cam", c_ip), ("obs_x", c_dp), ("K", c_dp),
+                ("num_vis", c_double)]
+
+
+class VlgbaOptions(ctypes.Structure):
+    _fields_ = [("fix_structure", c_int), ("fix_motion", c_int), ("pivot", c_up),
+                ("verbose", c_int), ("max_iter", c_int), ("max_iter2", c_int),
+                ("lambda0", c_double), ("device", c_int), ("rank", c_int),
+                ("world_size", c_int), ("comm_id", ctypes.c_void_p)]
+
+
+class VlgbaStats(ctypes.Structure):
+    _fields_ = [("iterations", c_int), ("accepted", c_int), ("num_error", c_int),
+                ("lambda_", c_double), ("seconds", c_double)]
+
+
+class VlgbaStepInfo(ctypes.Structure):
+    _fields_ = [("old_sse", c_double), ("new_sse", c_double), ("dpg", c_double),
+                ("rho", c_double), ("lambda_", c_double), ("accepted", c_int),
+                ("chol_failed", c_int)]
+
+
+# name -> (restype, argtypes); must match include/vlgba.h exactly
+SIGNATURES = {
+    "vlgba_solve": (c_int, [ctypes.POINTER(VlgbaProblem), ctypes.POINTER(VlgbaOptions), c_dp,
+                            c_dp, c_dp, ctypes.POINTER(VlgbaStats)]),
+    "vlgba_create": (c_int, [ctypes.POINTER(VlgbaProblem), ctypes.POINTER(VlgbaOptions),
+                             ctypes.POINTER(ctypes.c_void_p)]),
+    "vlgba_set_params": (c_int, [ctypes.c_void_p, c_dp, c_dp]),
+    "vlgba_get_params": (c_int, [ctypes.c_void_p, c_dp, c_dp]),
+    "vlgba_step": (c_int, [ctypes.c_void_p, c_int, c_int, ctypes.POINTER(VlgbaStepInfo)]),
+    "vlgba_run": (c_int, [ctypes.c_void_p, c_dp, ctypes.POINTER(VlgbaStats)]),
+    "vlgba_sync": (c_int, [ctypes.c_void_p]),
+    "vlgba_destroy": (None, [ctypes.c_void_p]),
+    "vlgba_set_timing": (c_int, [ctypes.c_void_p, c_int]),
+    "vlgba_phase_ms": (c_int, [ctypes.c_void_p, c_dp]),
+    "vlgba_mex_bundle_1": (c_int, [c_int, c_int, c_int] + [c_dp] * 14),
+    "vlgba_mex_bundle_2": (c_int, [c_int, c_int, c_int] + [c_dp] * 7),
+    "vlgba_mex_bundle_3": (c_int, [c_int, c_int, c_int] + [c_dp] * 13),
+    "vlgba_version": (c_int, [ctypes.c_char_p, c_int]),
+    "vlgba_get_unique_id": (c_int, [ctypes.c_void_p]),
+    "vlgba_device_count": (c_int, []),
+}
+
+ERRORS = {-1001: "bad argument", -1002: "num_a must be 6, 7 or 10",
+          -1003: "duplicate (point, camera) observation", -1004: "out of host memory",
+          -1005: "RCCL communicator failure"}
+
+_lib = None
+
+
+class VlgbaError(RuntimeError):
+    pass
+
+
+def lib():
+    """The loaded libvlgba (raises if the HIP library is not built / loadable)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise VlgbaError(f"{LIB_PATH} not built: run __graft_entry__.build() or "
+                             "make -C bundleadjustmentmatlab_amd/csrc")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = "vlgba"):
+    if rc != 0:
+        msg = ERRORS.get(rc, f"HIP error {-rc}" if -1000 < rc < 0 else f"code {rc}")
+        raise VlgbaError(f"{what} failed: {msg} ({rc})")

@@ -1,0 +1,290 @@
+"""Host mirror of the reference's MATLAB entry points, running on libvlgba.
+
+``bundle_euclid`` keeps the signature, option names, argument meaning and
+output semantics of toolbox/bundle/bundle_euclid.m:1-269::
+
+    K_, Te_, w_, Xe_, error_ = bundle_euclid(K, Te, w, Xe, x, 'fix_calibration',
+                                             'visibility', vis, 'verbose')
+
+with arrays MATLAB-shaped (K 4xm, Te 3xm, w 3xm, Xe 4xn, x 3xnxm).  The whole
+LM loop (bundle_euclid.m:111-249) runs on the GPU through ``vlgba_solve``.
+
+``bundle_euclid_obs`` takes the same problem as a COO observation list, the
+form that scales to the 1000-camera / 500k-point configs (a dense x at that
+size is 12 GB).
+
+``mex_bundle_1_XABeUVWeAeB`` / ``mex_bundle_2_Se_`` / ``mex_bundle_3_db_new``
+mirror the three MEX stages with their exact argument layouts.
+"""
+from __future__ import annotations
+
+import ctypes
+import numpy as np
+
+from ._lib import (VlgbaOptions, VlgbaProblem, VlgbaStats, VlgbaStepInfo, c_dp, c_ip, c_up,
+                   check, lib)
+
+__all__ = ["bundle_euclid", "bundle_euclid_obs", "BundleAdjuster", "parse_options",
+           "mex_bundle_1_XABeUVWeAeB", "mex_bundle_2_Se_", "mex_bundle_3_db_new"]
+
+
+def _F(a):
+    return np.asfortranarray(a, dtype=np.float64)
+
+
+def _dp(a):
+    return a.ctypes.data_as(c_dp)
+
+
+# ---------------------------------------------------------------------------
+# options (bundle_euclid.m:44-82)
+# ---------------------------------------------------------------------------
+def parse_options(m, n, varargin, x=None):
+    """Name/value options of bundle_euclid.m:53-78.  Unknown names are
+    ignored, as the reference's switch statement ignores them."""
+    o = dict(fix_structure=False, fix_motion=False, fix_pivot=False,
+             pivot=np.zeros(m, dtype=bool), num_variableK=4, visible=None, verbose=False)
+    k = 0
+    varargin = list(varargin)
+    while k < len(varargin):
+        name = varargin[k]
+        name = name.lower() if isinstance(name, str) else name
+        if name == "fix_structure":
+            o["fix_structure"] = True
+        elif name == "fix_motion":
+            o["fix_motion"] = True
+        elif name == "fix_pivot":
+            o["fix_pivot"] = True
+            o["pivot"] = np.asarray(varargin[k + 1], dtype=bool).reshape(-1)
+            k += 1
+        elif name == "fix_calibration":
+            o["num_variableK"] = 0
+        elif name == "fix_principal":
+            o["num_variableK"] = 1
+        elif name == "visibility":
+            o["visible"] = np.asarray(varargin[k + 1])
+            k += 1
+        elif name == "verbose":
+            o["verbose"] = True
+        k += 1
+    if o["visible"] is None and x is not None:
+        o["visible"] = (x[0] != 0) | (x[1] != 0)          # bundle_euclid.m:50
+    if o["visible"] is not None:
+        o["visible"] = np.asarray(o["visible"], dtype=np.float64).reshape(n, m, order="F")
+    return o
+
+
+def pack_a(K, Te, w, nvk):
+    """a = [w; T; (K)] (bundle_euclid.m:89-96)."""
+    m = w.shape[1]
+    a = np.zeros((6 + nvk, m), order="F")
+    a[0:3] = w
+    a[3:6] = Te
+    if nvk == 1:
+        a[6] = K[0]
+    elif nvk == 4:
+        a[6:10] = K
+    return a
+
+
+def unpack(K, a, b, Xe4, nvk):
+    """bundle_euclid.m:255-267 (Xe_(4,:) is the input Xe(4,:), App. A Q5)."""
+    K_ = np.array(K, dtype=np.float64, order="F")
+    if nvk == 1:
+        K_[0] = a[6]
+        K_[1] = a[6]
+    elif nvk == 4:
+        K_[:] = a[6:10]
+    return K_, a[3:6].copy(order="F"), a[0:3].copy(order="F"), np.vstack([b, Xe4])
+
+
+# ---------------------------------------------------------------------------
+# the GPU solver handle
+# ---------------------------------------------------------------------------
+class BundleAdjuster:
+    """One problem resident on one GPU (vlgba_ctx).
+
+    obs_pt / obs_cam (0-based) and obs_x (N, 2) describe the visible
+    observations; K is 4 x m; num_a is 6 (fix_calibration), 7 (fix_principal)
+    or 10 (variable K).  Options follow bundle_euclid.m's names.
+    """
+
+    def __init__(self, K, obs_pt, obs_cam, obs_x, n, num_a=6, *, fix_structure=False,
+                 fix_motion=False, pivot=None, verbose=False, num_vis=0.0, device=0,
+                 rank=0, world_size=1, comm_id=None, max_iter=0, max_iter2=0, lambda0=0.0):
+        L = lib()
+        self.K = _F(K)
+        self.m = self.K.shape[1]
+        self.n = int(n)
+        self.num_a = int(num_a)
+        self._pt = np.ascontiguousarray(obs_pt, dtype=np.int32)
+        self._cam = np.ascontiguousarray(obs_cam, dtype=np.int32)
+        self._x = np.ascontiguousarray(obs_x, dtype=np.float64).reshape(-1, 2)
+        self.num_obs = len(self._pt)
+        prob = VlgbaProblem(self.m, self.n, self.num_a, self.num_obs,
+                            self._pt.ctypes.data_as(c_ip), self._cam.ctypes.data_as(c_ip),
+                            _dp(self._x), _dp(self.K), float(num_vis))
+        self._pivot = None
+        if pivot is not None:
+            self._pivot = np.ascontiguousarray(np.asarray(pivot, dtype=bool).reshape(-1),
+                                               dtype=np.uint8)
+        self._comm = None
+        if comm_id is not None:
+            self._comm = ctypes.create_string_buffer(bytes(comm_id), 128)
+        opt = VlgbaOptions(int(fix_structure), int(fix_motion),
+                           self._pivot.ctypes.data_as(c_up) if self._pivot is not None else None,
+                           int(verbose), int(max_iter), int(max_iter2), float(lambda0),
+                           int(device), int(rank), int(world_size),
+                           ctypes.cast(self._comm, ctypes.c_void_p) if self._comm else None)
+        h = ctypes.c_void_p()
+        check(L.vlgba_create(ctypes.byref(prob), ctypes.byref(opt), ctypes.byref(h)),
+              "vlgba_create")
+        self._h = h
+        self._L = L
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.vlgba_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_params(self, a, b):
+        a = np.ascontiguousarray(_F(a).reshape(-1, order="F"))
+        b = np.ascontiguousarray(_F(b).reshape(-1, order="F"))
+        assert a.size == self.num_a * self.m and b.size == 3 * self.n
+        check(self._L.vlgba_set_params(self._h, _dp(a), _dp(b)), "vlgba_set_params")
+
+    def get_params(self):
+        a = np.zeros(self.num_a * self.m)
+        b = np.zeros(3 * self.n)
+        check(self._L.vlgba_get_params(self._h, _dp(a), _dp(b)), "vlgba_get_params")
+        return a.reshape(self.num_a, self.m, order="F"), b.reshape(3, self.n, order="F")
+
+    def step(self, relinearize=True, update_lm=True):
+        info = VlgbaStepInfo()
+        check(self._L.vlgba_step(self._h, int(relinearize), int(update_lm), ctypes.byref(info)),
+              "vlgba_step")
+        return info
+
+    def run(self, max_err=64):
+        err = np.zeros(max_err)
+        st = VlgbaStats()
+        check(self._L.vlgba_run(self._h, _dp(err), ctypes.byref(st)), "vlgba_run")
+        return err[: st.num_error].copy(), st
+
+    def sync(self):
+        check(self._L.vlgba_sync(self._h), "vlgba_sync")
+
+    def set_timing(self, on=True):
+        check(self._L.vlgba_set_timing(self._h, int(on)), "vlgba_set_timing")
+
+    def phase_ms(self):
+        ms = np.zeros(7)
+        check(self._L.vlgba_phase_ms(self._h, _dp(ms)), "vlgba_phase_ms")
+        return dict(zip(["linearize", "camera_reduce", "damp_y", "schur", "assemble",
+                         "cholesky_solve", "update"], ms.tolist()))
+
+
+# ---------------------------------------------------------------------------
+# drop-in drivers
+# ---------------------------------------------------------------------------
+def bundle_euclid_obs(K, Te, w, Xe, obs_pt, obs_cam, obs_x, *varargin, num_vis=0.0, device=0,
+                      rank=0, world_size=1, comm_id=None, return_stats=False):
+    """bundle_euclid on a COO observation list (0-based point / camera ids)."""
+    K, Te, w, Xe = _F(K), _F(Te), _F(w), _F(Xe)
+    m, n = w.shape[1], Xe.shape[1]
+    o = parse_options(m, n, varargin)
+    nvk = o["num_variableK"]
+    num_a = 6 + nvk
+    a = pack_a(K, Te, w, nvk)
+    b = _F(Xe[0:3])
+    with BundleAdjuster(K, obs_pt, obs_cam, obs_x, n, num_a,
+                        fix_structure=o["fix_structure"], fix_motion=o["fix_motion"],
+                        pivot=o["pivot"] if o["fix_pivot"] else None, verbose=o["verbose"],
+                        num_vis=num_vis, device=device, rank=rank, world_size=world_size,
+                        comm_id=comm_id) as ba:
+        ba.set_params(a, b)
+        err, st = ba.run()
+        a, b = ba.get_params()
+    out = unpack(K, a, b, Xe[3:4], nvk) + (err,)
+    return out + (st,) if return_stats else out
+
+
+def bundle_euclid(K, Te, w, Xe, x, *varargin, device=0, return_stats=False):
+    """[K_ Te_ w_ Xe_ error_] = bundle_euclid(K, Te, w, Xe, x, ...)  (bundle_euclid.m:1)."""
+    x = _F(x)
+    m, n = np.shape(w)[1], x.shape[1]
+    o = parse_options(m, n, varargin, x=x)
+    vis = o["visible"]
+    num_vis = float(vis.sum())                                     # bundle_euclid.m:82
+    pt, cam = np.nonzero(vis)                                      # point-major
+    obs_x = np.stack([x[0, pt, cam], x[1, pt, cam]], axis=1)
+    # re-emit the options without 'visibility' (already applied)
+    rest, k = [], 0
+    while k < len(varargin):
+        nm = varargin[k].lower() if isinstance(varargin[k], str) else varargin[k]
+        if nm == "visibility":
+            k += 2
+            continue
+        if nm == "fix_pivot":
+            rest += [varargin[k], varargin[k + 1]]
+            k += 2
+            continue
+        rest.append(varargin[k])
+        k += 1
+    return bundle_euclid_obs(K, Te, w, Xe, pt, cam, obs_x, *rest, num_vis=num_vis,
+                             device=device, return_stats=return_stats)
+
+
+# ---------------------------------------------------------------------------
+# MEX stage mirrors (exact argument layouts of the reference MEX files)
+# ---------------------------------------------------------------------------
+def mex_bundle_1_XABeUVWeAeB(K, a, b, X, visible):
+    """[X_hat A B e U V W eA eB] = mex_bundle_1_XABeUVWeAeB(K, a, b, X, visible)."""
+    K, a, b, X, vis = map(_F, (K, a, b, X, visible))
+    num_a, m = a.shape
+    n = b.shape[1]
+    z = lambda *s: np.zeros(s, order="F")
+    out = [z(2, n, m), z(2, num_a, n, m), z(2, 3, n, m), z(2, n, m), z(num_a, num_a, m),
+           z(3, 3, n), z(num_a, 3, n, m), z(num_a, m), z(3, n)]
+    check(lib().vlgba_mex_bundle_1(m, n, num_a, _dp(K), _dp(a), _dp(b), _dp(X), _dp(vis),
+                                   *[_dp(q) for q in out]), "mex_bundle_1_XABeUVWeAeB")
+    return tuple(out)
+
+
+def mex_bundle_2_Se_(Y, W, U, eA, eB):
+    """[S e_] = mex_bundle_2_Se_(Y, W, U, eA, eB)."""
+    Y, W, U, eA, eB = map(_F, (Y, W, U, eA, eB))
+    num_a, m = eA.shape
+    n = eB.shape[1]
+    S = np.zeros((num_a * m, num_a * m), order="F")
+    e_ = np.zeros((num_a * m, 1), order="F")
+    check(lib().vlgba_mex_bundle_2(m, n, num_a, _dp(Y), _dp(W), _dp(U), _dp(eA), _dp(eB),
+                                   _dp(S), _dp(e_)), "mex_bundle_2_Se_")
+    return S, e_
+
+
+def mex_bundle_3_db_new(W, da, eB, V_inv, K, a, b, X, visible):
+    """[db a_new b_new X_hat] = mex_bundle_3_db_new(W, da, eB, V_inv, K, a, b, X, visible)."""
+    W, da, eB, Vinv, K, a, b, X, vis = map(_F, (W, da, eB, V_inv, K, a, b, X, visible))
+    num_a, m = a.shape
+    n = b.shape[1]
+    db = np.zeros((3, n), order="F")
+    a_new = np.zeros((num_a, m), order="F")
+    b_new = np.zeros((3, n), order="F")
+    X_hat = np.zeros((2, n, m), order="F")
+    check(lib().vlgba_mex_bundle_3(m, n, num_a, _dp(W), _dp(da), _dp(eB), _dp(Vinv), _dp(K),
+                                   _dp(a), _dp(b), _dp(X), _dp(vis), _dp(db), _dp(a_new),
+                                   _dp(b_new), _dp(X_hat)), "mex_bundle_3_db_new")
+    return db, a_new, b_new, X_hat

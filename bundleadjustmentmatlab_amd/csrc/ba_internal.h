@@ -1,0 +1,85 @@
+// ba_internal.h -- device-side data layout and kernel launchers of libvlgba.
+//
+// One ba_dev per (problem, GPU).  Everything lives in HBM for the whole solve;
+// only scalars cross PCIe per LM iteration.  Layout (N = visible observations,
+// NA = num_a = 6 / 7 / 10 camera parameters, m cameras, n points):
+//
+//   observations, point-major (points ascending, cameras ascending inside a
+//   point = the reference's column-major (i + n*j) visiting order per point):
+//     obs_cam[N] int32, obs_x[N][2] f64, pt_ptr[n+1] int32
+//   camera-major view:  cam_ptr[m+1], cam_obs[N] (obs ids ascending)
+//   per observation:    jrec[N][JS]   A (2 x NA, column major) then e (2)
+//                       W[N][3*NA], Y[N][3*NA]  (NA x 3 column major, as W_ij)
+//                       t[N][NA]      Y_o * eB_i (the e_ contribution)
+//   per camera:         a[NA*m], a_new, K4[4*m], rot[m][5][9], rot_new[m][9],
+//                       U[NA*NA*m], eA[NA*m]
+//   per point:          b[3n], b_new, V[9n], eB[3n], Vinv[9n], db[3n]
+//   reduced system:     blocks (j >= k) with co-visibility: blk_jk[nb][2],
+//                       blk_ptr[nb+1], term[T][2] (obs pair, point ascending),
+//                       sblk[nb][NA*NA], dense S (NA*m)^2 column major, rhs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+#define VLGBA_CHECK(x)                                                              \
+    do {                                                                            \
+        hipError_t err__ = (x);                                                     \
+        if (err__ != hipSuccess) return -(int)err__;                                \
+    } while (0)
+
+struct ba_flags {
+    int fix_structure;  // V, W, eB = 0       (bundle_euclid.m:140-144)
+    int fix_motion;     // U, W, eA = 0       (:145-149)
+    int has_pivot;      // pivot[m] mask      (:150-154)
+};
+
+struct ba_dev {
+    int m, n, na, N, js;
+    // problem (read-only)
+    int *obs_cam, *pt_ptr, *cam_ptr, *cam_obs;
+    double *obs_x, *K4;
+    unsigned char *pivot;
+    // state
+    double *a, *b, *a_new, *b_new;
+    double *rot, *rot_new;
+    // linearisation
+    double *jrec, *W, *U, *eA, *V, *eB;
+    // per damping
+    double *Vinv, *Y, *t, *db;
+    // reduced system
+    int nb;            // blocks
+    long long T;       // terms
+    int *blk_jk, *blk_ptr, *term;
+    double *sblk, *rhs, *S, *da;
+    long long ld;      // NA*m
+    long long lds;     // ld rounded up to the Cholesky tile (padding rows = identity)
+    double *linv;      // [lds/64][64*64] inverses of the diagonal Cholesky tiles
+    double *ywork;     // [lds] forward-solve result
+    // reductions: partial sums per block of the reducing kernels, in fixed order
+    double *part;      // [3][PART_MAX]
+    double *scal;      // [8] : 0 old_sse, 1 new_sse, 2 dpg, 3 chol_status ...
+    int *chol_cnt;     // arrival counters for the triangular solves
+    // optional outputs / inputs of the MEX-compatible stage entries (else NULL)
+    double *xh_out;    // [N][2] projections (stage 1 and stage 3)
+    double *B_out;     // [N][6] point Jacobians (stage 1)
+    unsigned char *obs_vis;  // [N] stage 3: 0 = structural-only pair (no projection)
+    int schur_owner;   // this rank adds U* / eA into the reduced system
+    double scal_host[8];
+    hipStream_t stream;
+};
+
+#define BA_PART_MAX 65536
+
+// ---- ba_kernels.hip ----
+int ba_launch_rotations(ba_dev *d, const double *a, double *rot, int all5);
+int ba_launch_linearize(ba_dev *d, ba_flags f);
+int ba_launch_camera_reduce(ba_dev *d, ba_flags f);
+int ba_launch_damp_point(ba_dev *d, double lambda);
+int ba_launch_schur(ba_dev *d, double lambda);
+int ba_launch_assemble(ba_dev *d);
+int ba_launch_update(ba_dev *d, double lambda);
+int ba_launch_yeb(ba_dev *d);
+int ba_launch_assemble_plain(ba_dev *d, double *S, long long ld);
+// ---- ba_chol.hip ----
+int ba_chol_solve(ba_dev *d);

@@ -1,0 +1,605 @@
+// ba_kernels.hip -- gfx950 kernels of one Euclidean LM iteration (fp64).
+//
+// Reference path (toolbox/bundle/):
+//   k_rotations        vl_rodrigues per camera, hoisted out of reproject_point.h:44
+//   k_linearize        mex_bundle_1_XABeUVWeAeB.c:192-256 (projection + FD Jacobians)
+//                      and the per-point half of :266-334 (W_ij, V_i, eB_i)
+//   k_camera_reduce    the per-camera half of :266-334 (U_j, eA_j)
+//   k_damp_point       bundle_euclid.m:168-184 (V* = damp(V), pinv, Y = W V*^-1)
+//   k_schur            mex_bundle_2_Se_.c:72-155 (S_jk, e_) on the co-visible blocks
+//   k_assemble         dense S for the reduced solve (bundle_euclid.m:193)
+//   k_camera_update    mex_bundle_3_db_new.c:294-298 (a_new) + rotations of a_new
+//   k_point_update     mex_bundle_3_db_new.c:257-324 (db, b_new, new projections)
+//                      and the cost / rho terms of bundle_euclid.m:205-217
+//
+// Parity: every per-element expression keeps the reference's operation order,
+// the file is compiled with -ffp-contract=off, and every reduction that the
+// reference performs sequentially (U_j over points, V_i / eB_i over cameras,
+// S_jk / e_j over points) is performed sequentially in the same ascending order
+// here, so X_hat, A, B, e, U, V, W, eA, eB, Y, S and e_ are bit-identical to
+// the oracle's (and the reference's, modulo libm).  Only the scalar cost sums
+// use tree reductions (MATLAB's BLAS dot order is unknowable anyway).
+#include "ba_internal.h"
+#include "vlg_math.h"
+
+#define H_FD VLG_FD_H
+
+// -------------------------------------------------------------------------
+// block reduction of one double per thread -> partial[blockIdx.x]
+// -------------------------------------------------------------------------
+template <int BS>
+__device__ __forceinline__ void block_sum_to(double v, double *out)
+{
+    __shared__ double red[BS / 64];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s = red[0];
+#pragma unroll
+        for (int k = 1; k < BS / 64; k++) s += red[k];
+        *out = s;
+    }
+}
+
+// -------------------------------------------------------------------------
+// rotations: R(a), R(a + h e_k) k = 0..2, R(a + 0) per camera (5 x 9)
+// -------------------------------------------------------------------------
+template <int NA>
+__global__ void k_rotations(const double *__restrict__ a, double *__restrict__ rot, int m)
+{
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const double *aj = a + (size_t)NA * j;
+    double w[3] = {aj[0], aj[1], aj[2]};
+    double R[9];
+    double *out = rot + 45 * (size_t)j;
+    vlg_rodrigues(R, w);
+#pragma unroll
+    for (int q = 0; q < 9; q++) out[q] = R[q];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        // derivative_camera (mex_bundle_1_XABeUVWeAeB.c:30-33): a1 = a0 + h*da,
+        // da = e_k for k < 3; for k >= 3 the rotation part is a0 + h*0.
+        double w1[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++) w1[c] = w[c] + H_FD * ((c == k) ? 1.0 : 0.0);
+        vlg_rodrigues(R, w1);
+#pragma unroll
+        for (int q = 0; q < 9; q++) out[9 * (1 + k) + q] = R[q];
+    }
+}
+
+// -------------------------------------------------------------------------
+// linearisation, one thread per point (observations in ascending camera order)
+// -------------------------------------------------------------------------
+template <int NA>
+__global__ __launch_bounds__(256) void k_linearize(
+    const int *__restrict__ pt_ptr, const int *__restrict__ obs_cam,
+    const double *__restrict__ obs_x, const double *__restrict__ K4,
+    const double *__restrict__ a, const double *__restrict__ rot,
+    const double *__restrict__ b, int n, ba_flags f, const unsigned char *__restrict__ pivot,
+    double *__restrict__ jrec, double *__restrict__ W, double *__restrict__ V,
+    double *__restrict__ eB, double *__restrict__ part_sse, double *__restrict__ xh_out,
+    double *__restrict__ B_out)
+{
+    constexpr int JS = 2 * NA + 2;
+    constexpr int NVK = NA - 6;
+    double sse = 0.0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const double bi[3] = {b[3 * (size_t)i], b[3 * (size_t)i + 1], b[3 * (size_t)i + 2]};
+        double v[9], eb[3];
+#pragma unroll
+        for (int q = 0; q < 9; q++) v[q] = 0.0;
+        eb[0] = eb[1] = eb[2] = 0.0;
+        const int o_end = pt_ptr[i + 1];
+        for (int o = pt_ptr[i]; o < o_end; o++) {
+            const int j = obs_cam[o];
+            double a0[NA], k4[4];
+#pragma unroll
+            for (int c = 0; c < NA; c++) a0[c] = a[(size_t)NA * j + c];
+#pragma unroll
+            for (int c = 0; c < 4; c++) k4[c] = K4[4 * (size_t)j + c];
+            const double *R = rot + 45 * (size_t)j;
+            double Rl[9];
+#pragma unroll
+            for (int q = 0; q < 9; q++) Rl[q] = R[q];
+            double Kc[9], xh[2];
+            vlg_calib(Kc, k4, a0, NVK);
+            vlg_project(Kc, Rl, a0 + 3, bi, xh);
+            double A[2 * NA], B[6];
+            // camera derivatives, mex_bundle_1_XABeUVWeAeB.c:201-209, 14-41
+#pragma unroll
+            for (int k = 0; k < NA; k++) {
+                double a1[NA], Kc1[9], Rk[9], x1[2];
+#pragma unroll
+                for (int c = 0; c < NA; c++) a1[c] = a0[c] + H_FD * ((c == k) ? 1.0 : 0.0);
+                vlg_calib(Kc1, k4, a1, NVK);
+                const double *Rs = R + 9 * ((k < 3) ? (1 + k) : 4);
+#pragma unroll
+                for (int q = 0; q < 9; q++) Rk[q] = Rs[q];
+                vlg_project(Kc1, Rk, a1 + 3, bi, x1);
+                A[2 * k] = (x1[0] - xh[0]) / H_FD;
+                A[2 * k + 1] = (x1[1] - xh[1]) / H_FD;
+            }
+            // point derivatives, :211-219, 43-70
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                double b1[3], x1[2];
+#pragma unroll
+                for (int c = 0; c < 3; c++) b1[c] = bi[c] + H_FD * ((c == k) ? 1.0 : 0.0);
+                vlg_project(Kc, Rl, a0 + 3, b1, x1);
+                B[2 * k] = (x1[0] - xh[0]) / H_FD;
+                B[2 * k + 1] = (x1[1] - xh[1]) / H_FD;
+            }
+            const double e0 = obs_x[2 * (size_t)o] - xh[0];
+            const double e1 = obs_x[2 * (size_t)o + 1] - xh[1];
+            double *rec = jrec + (size_t)JS * o;
+#pragma unroll
+            for (int q = 0; q < 2 * NA; q += 2) {
+                double2 p = {A[q], A[q + 1]};
+                *reinterpret_cast<double2 *>(rec + q) = p;
+            }
+            *reinterpret_cast<double2 *>(rec + 2 * NA) = double2{e0, e1};
+            if (xh_out) {
+                xh_out[2 * (size_t)o] = xh[0];
+                xh_out[2 * (size_t)o + 1] = xh[1];
+            }
+            if (B_out) {
+#pragma unroll
+                for (int q = 0; q < 6; q++) B_out[6 * (size_t)o + q] = B[q];
+            }
+            // W_ij = A^T B onto a zeroed output (:305-314)
+            const bool wzero = f.fix_structure || f.fix_motion || (f.has_pivot && pivot[j]);
+            double *wo = W + (size_t)3 * NA * o;
+#pragma unroll
+            for (int c = 0; c < 3; c++)
+#pragma unroll
+                for (int r = 0; r < NA; r++)
+                    wo[r + NA * c] =
+                        wzero ? 0.0 : 0.0 + (A[2 * r] * B[2 * c] + A[2 * r + 1] * B[2 * c + 1]);
+            // V_i += B^T B, eB_i += B^T e (:293-302, :326-332)
+#pragma unroll
+            for (int c = 0; c < 3; c++)
+#pragma unroll
+                for (int r = 0; r < 3; r++)
+                    v[r + 3 * c] += B[2 * r] * B[2 * c] + B[2 * r + 1] * B[2 * c + 1];
+#pragma unroll
+            for (int r = 0; r < 3; r++) eb[r] += B[2 * r] * e0 + B[2 * r + 1] * e1;
+            sse += e0 * e0 + e1 * e1;
+        }
+        if (f.fix_structure) {
+#pragma unroll
+            for (int q = 0; q < 9; q++) v[q] = 0.0;
+            eb[0] = eb[1] = eb[2] = 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 9; q++) V[9 * (size_t)i + q] = v[q];
+#pragma unroll
+        for (int q = 0; q < 3; q++) eB[3 * (size_t)i + q] = eb[q];
+    }
+    block_sum_to<256>(sse, part_sse + blockIdx.x);
+}
+
+// -------------------------------------------------------------------------
+// U_j, eA_j: one workgroup per camera, each output owned by one lane and
+// summed sequentially over the camera's observations in ascending point order
+// (= mex_bundle_1_XABeUVWeAeB.c:266-323 with the exact zeros skipped).
+// -------------------------------------------------------------------------
+template <int NA>
+__global__ void k_camera_reduce(const int *__restrict__ cam_ptr, const int *__restrict__ cam_obs,
+                                const double *__restrict__ jrec, int m, ba_flags f,
+                                const unsigned char *__restrict__ pivot, double *__restrict__ U,
+                                double *__restrict__ eA)
+{
+    constexpr int JS = 2 * NA + 2;
+    constexpr int NU = NA * (NA + 1) / 2;
+    const int j = blockIdx.x;
+    const int l = threadIdx.x;
+    if (j >= m || l >= NU + NA) return;
+    int r, c;
+    if (l < NU) {  // lower-triangle entry (r >= c)
+        int q = l;
+        c = 0;
+        while (q >= NA - c) { q -= NA - c; c++; }
+        r = c + q;
+    } else {       // eA entry: column "c" = the residual slot
+        r = l - NU;
+        c = NA;
+    }
+    const int s0 = cam_ptr[j], s1 = cam_ptr[j + 1];
+    double acc = 0.0;
+    int s = s0;
+    for (; s + 4 <= s1; s += 4) {
+        const double *p0 = jrec + (size_t)JS * cam_obs[s];
+        const double *p1 = jrec + (size_t)JS * cam_obs[s + 1];
+        const double *p2 = jrec + (size_t)JS * cam_obs[s + 2];
+        const double *p3 = jrec + (size_t)JS * cam_obs[s + 3];
+        const double x00 = p0[2 * r], x01 = p0[2 * r + 1], y00 = p0[2 * c], y01 = p0[2 * c + 1];
+        const double x10 = p1[2 * r], x11 = p1[2 * r + 1], y10 = p1[2 * c], y11 = p1[2 * c + 1];
+        const double x20 = p2[2 * r], x21 = p2[2 * r + 1], y20 = p2[2 * c], y21 = p2[2 * c + 1];
+        const double x30 = p3[2 * r], x31 = p3[2 * r + 1], y30 = p3[2 * c], y31 = p3[2 * c + 1];
+        acc += x00 * y00 + x01 * y01;
+        acc += x10 * y10 + x11 * y11;
+        acc += x20 * y20 + x21 * y21;
+        acc += x30 * y30 + x31 * y31;
+    }
+    for (; s < s1; s++) {
+        const double *p = jrec + (size_t)JS * cam_obs[s];
+        acc += p[2 * r] * p[2 * c] + p[2 * r + 1] * p[2 * c + 1];
+    }
+    if (f.fix_motion || (f.has_pivot && pivot[j])) acc = 0.0;
+    if (c < NA) {
+        U[(size_t)NA * NA * j + r + NA * c] = acc;
+        U[(size_t)NA * NA * j + c + NA * r] = acc;
+    } else {
+        eA[(size_t)NA * j + r] = acc;
+    }
+}
+
+// -------------------------------------------------------------------------
+// per point, per damping value: V* -> V*^-1, Y_o = W_o V*^-1, t_o = Y_o eB_i
+// (bundle_euclid.m:168-184; e_ term of mex_bundle_2_Se_.c:143-147)
+// -------------------------------------------------------------------------
+template <int NA>
+__global__ __launch_bounds__(256) void k_damp_point(
+    const int *__restrict__ pt_ptr, const double *__restrict__ V,
+    const double *__restrict__ eB, const double *__restrict__ W, int n, double lambda,
+    double *__restrict__ Vinv, double *__restrict__ Y, double *__restrict__ t)
+{
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        double vs[9], vi[9];
+#pragma unroll
+        for (int q = 0; q < 9; q++) vs[q] = V[9 * (size_t)i + q];
+#pragma unroll
+        for (int k = 0; k < 3; k++) vs[4 * k] = (1 + lambda) * vs[4 * k];
+        vlg_pinv3(vs, vi);
+#pragma unroll
+        for (int q = 0; q < 9; q++) Vinv[9 * (size_t)i + q] = vi[q];
+        const double eb0 = eB[3 * (size_t)i], eb1 = eB[3 * (size_t)i + 1],
+                     eb2 = eB[3 * (size_t)i + 2];
+        const int o_end = pt_ptr[i + 1];
+        for (int o = pt_ptr[i]; o < o_end; o++) {
+            const double *w = W + (size_t)3 * NA * o;
+            double *y = Y + (size_t)3 * NA * o;
+            double wl[3 * NA], yl[3 * NA];
+#pragma unroll
+            for (int q = 0; q < 3 * NA; q++) wl[q] = w[q];
+#pragma unroll
+            for (int c = 0; c < 3; c++)
+#pragma unroll
+                for (int r = 0; r < NA; r++)
+                    yl[r + NA * c] = wl[r] * vi[3 * c] + wl[r + NA] * vi[1 + 3 * c] +
+                                     wl[r + 2 * NA] * vi[2 + 3 * c];
+#pragma unroll
+            for (int q = 0; q < 3 * NA; q++) y[q] = yl[q];
+#pragma unroll
+            for (int r = 0; r < NA; r++)
+                t[(size_t)NA * o + r] = yl[r] * eb0 + yl[r + NA] * eb1 + yl[r + 2 * NA] * eb2;
+        }
+    }
+}
+
+// -------------------------------------------------------------------------
+// Schur complement, one workgroup per co-visible block (j >= k):
+//   S_jk[r][c] = (j == k ? U*_j[r][c] : 0) - sum_i (Y_ij[r] . W_ik[c])
+// each entry summed over the block's points in ascending order
+// (mex_bundle_2_Se_.c:80-118).  The diagonal block's workgroup also forms
+// e_j = eA_j - sum_i Y_ij eB_i (:132-155).
+// -------------------------------------------------------------------------
+template <int NA>
+__global__ void k_schur(const int *__restrict__ blk_jk, const int *__restrict__ blk_ptr,
+                        const int *__restrict__ term, const double *__restrict__ Y,
+                        const double *__restrict__ W, const double *__restrict__ t,
+                        const double *__restrict__ U, const double *__restrict__ eA, int nb,
+                        double lambda, int owner, double *__restrict__ sblk,
+                        double *__restrict__ rhs)
+{
+    const int bk = blockIdx.x;
+    const int l = threadIdx.x;
+    if (bk >= nb) return;
+    const int j = blk_jk[2 * bk], k = blk_jk[2 * bk + 1];
+    const int s0 = blk_ptr[bk], s1 = blk_ptr[bk + 1];
+    if (l < NA * NA) {
+        const int r = l % NA, c = l / NA;
+        double acc = 0.0;
+        if (j == k && owner) {
+            const double u = U[(size_t)NA * NA * j + r + NA * c];
+            acc = (r == c) ? (1 + lambda) * u : u;
+        }
+        int s = s0;
+        for (; s + 2 <= s1; s += 2) {
+            const double *ya = Y + (size_t)3 * NA * term[2 * s];
+            const double *wb = W + (size_t)3 * NA * term[2 * s + 1];
+            const double *ya2 = Y + (size_t)3 * NA * term[2 * s + 2];
+            const double *wb2 = W + (size_t)3 * NA * term[2 * s + 3];
+            const double y0 = ya[r], y1 = ya[r + NA], y2 = ya[r + 2 * NA];
+            const double w0 = wb[c], w1 = wb[c + NA], w2 = wb[c + 2 * NA];
+            const double z0 = ya2[r], z1 = ya2[r + NA], z2 = ya2[r + 2 * NA];
+            const double v0 = wb2[c], v1 = wb2[c + NA], v2 = wb2[c + 2 * NA];
+            acc -= y0 * w0 + y1 * w1 + y2 * w2;
+            acc -= z0 * v0 + z1 * v1 + z2 * v2;
+        }
+        for (; s < s1; s++) {
+            const double *ya = Y + (size_t)3 * NA * term[2 * s];
+            const double *wb = W + (size_t)3 * NA * term[2 * s + 1];
+            acc -= ya[r] * wb[c] + ya[r + NA] * wb[c + NA] + ya[r + 2 * NA] * wb[c + 2 * NA];
+        }
+        sblk[(size_t)NA * NA * bk + l] = acc;
+    } else if (j == k && l < NA * NA + NA) {
+        const int r = l - NA * NA;
+        double acc = 0.0;
+        for (int s = s0; s < s1; s++) acc += t[(size_t)NA * term[2 * s] + r];
+        rhs[(size_t)NA * j + r] = (owner ? eA[(size_t)NA * j + r] : 0.0) - acc;
+    }
+}
+
+// t_o = Y_o eB_i for given Y (stage-2 entry; k_damp_point forms it otherwise)
+template <int NA>
+__global__ void k_point_yeb(const int *__restrict__ pt_ptr, const double *__restrict__ Y,
+                            const double *__restrict__ eB, int n, double *__restrict__ t)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double eb0 = eB[3 * (size_t)i], eb1 = eB[3 * (size_t)i + 1],
+                 eb2 = eB[3 * (size_t)i + 2];
+    for (int o = pt_ptr[i]; o < pt_ptr[i + 1]; o++) {
+        const double *y = Y + (size_t)3 * NA * o;
+#pragma unroll
+        for (int r = 0; r < NA; r++)
+            t[(size_t)NA * o + r] = y[r] * eb0 + y[r + NA] * eb1 + y[r + 2 * NA] * eb2;
+    }
+}
+
+// -------------------------------------------------------------------------
+// dense lower S from the blocks (off-diagonal blocks: j > k only)
+// -------------------------------------------------------------------------
+template <int NA>
+__global__ void k_assemble(const int *__restrict__ blk_jk, const double *__restrict__ sblk,
+                           int nb, long long lds, double *__restrict__ S)
+{
+    const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (long long)nb * NA * NA) return;
+    const int bk = (int)(g / (NA * NA)), l = (int)(g % (NA * NA));
+    const int j = blk_jk[2 * bk], k = blk_jk[2 * bk + 1];
+    const int r = l % NA, c = l / NA;
+    S[(long long)(NA * j + r) + lds * (long long)(NA * k + c)] = sblk[g];
+}
+
+// pinv semantics for exactly-zero rows (App. A Q2, Q8): a zero diagonal entry
+// of S marks a fixed parameter; make its row/column the identity, rhs 0.
+__global__ void k_fix_zero_rows(double *__restrict__ S, double *__restrict__ rhs, long long ld)
+{
+    const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= ld) return;
+    double *d = S + r + ld * r;
+    if (*d == 0.0) {
+        for (long long c = 0; c < r; c++) S[r + ld * c] = 0.0;
+        for (long long q = r + 1; q < ld; q++) S[q + ld * r] = 0.0;
+        *d = 1.0;
+        rhs[r] = 0.0;
+    }
+}
+
+// -------------------------------------------------------------------------
+// camera update: a_new = a + da (mex_bundle_3_db_new.c:294-298), R(a_new),
+// and the camera part of dp'(lambda dp + g) (bundle_euclid.m:215-217)
+// -------------------------------------------------------------------------
+template <int NA>
+__global__ __launch_bounds__(256) void k_camera_update(
+    const double *__restrict__ a, const double *__restrict__ da,
+    const double *__restrict__ eA, int m, double lambda, double *__restrict__ a_new,
+    double *__restrict__ rot_new, double *__restrict__ part)
+{
+    double acc = 0.0;
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < m) {
+        double an[NA];
+#pragma unroll
+        for (int c = 0; c < NA; c++) {
+            const double d = da[(size_t)NA * j + c];
+            an[c] = a[(size_t)NA * j + c] + d;
+            a_new[(size_t)NA * j + c] = an[c];
+            acc += d * (lambda * d + eA[(size_t)NA * j + c]);
+        }
+        double R[9];
+        vlg_rodrigues(R, an);
+#pragma unroll
+        for (int q = 0; q < 9; q++) rot_new[9 * (size_t)j + q] = R[q];
+    }
+    block_sum_to<256>(acc, part + blockIdx.x);
+}
+
+// -------------------------------------------------------------------------
+// point update: db_i (only da[0..5] per camera, App. A Q3), b_new, new
+// projections of the point's observations, new SSE and the point part of
+// dp'(lambda dp + g)
+// -------------------------------------------------------------------------
+template <int NA>
+__global__ __launch_bounds__(256) void k_point_update(
+    const int *__restrict__ pt_ptr, const int *__restrict__ obs_cam,
+    const double *__restrict__ obs_x, const double *__restrict__ K4,
+    const double *__restrict__ W, const double *__restrict__ da,
+    const double *__restrict__ eB, const double *__restrict__ Vinv,
+    const double *__restrict__ b, const double *__restrict__ a_new,
+    const double *__restrict__ rot_new, int n, double lambda, double *__restrict__ db,
+    double *__restrict__ b_new, double *__restrict__ part_sse, double *__restrict__ part_dpg,
+    const unsigned char *__restrict__ obs_vis, double *__restrict__ xh_out)
+{
+    constexpr int NVK = NA - 6;
+    double sse = 0.0, dpg = 0.0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        double rhs[3] = {eB[3 * (size_t)i], eB[3 * (size_t)i + 1], eB[3 * (size_t)i + 2]};
+        const int o0 = pt_ptr[i], o1 = pt_ptr[i + 1];
+        for (int o = o0; o < o1; o++) {
+            const double *w = W + (size_t)3 * NA * o;
+            const double *d = da + (size_t)NA * obs_cam[o];
+            double dl[6];
+#pragma unroll
+            for (int k = 0; k < 6; k++) dl[k] = d[k];
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                const double *wr = w + NA * r;
+                rhs[r] -= wr[0] * dl[0] + wr[1] * dl[1] + wr[2] * dl[2] + wr[3] * dl[3] +
+                          wr[4] * dl[4] + wr[5] * dl[5];
+            }
+        }
+        const double *vi = Vinv + 9 * (size_t)i;
+        double bn[3];
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            const double dbr = vi[r] * rhs[0] + vi[r + 3] * rhs[1] + vi[r + 6] * rhs[2];
+            db[3 * (size_t)i + r] = dbr;
+            bn[r] = b[3 * (size_t)i + r] + dbr;
+            b_new[3 * (size_t)i + r] = bn[r];
+            dpg += dbr * (lambda * dbr + eB[3 * (size_t)i + r]);
+        }
+        for (int o = o0; o < o1; o++) {
+            if (obs_vis && !obs_vis[o]) continue;
+            const int j = obs_cam[o];
+            double an[NA], k4[4], Kc[9], R[9], xh[2];
+#pragma unroll
+            for (int c = 0; c < NA; c++) an[c] = a_new[(size_t)NA * j + c];
+#pragma unroll
+            for (int c = 0; c < 4; c++) k4[c] = K4[4 * (size_t)j + c];
+#pragma unroll
+            for (int q = 0; q < 9; q++) R[q] = rot_new[9 * (size_t)j + q];
+            vlg_calib(Kc, k4, an, NVK);
+            vlg_project(Kc, R, an + 3, bn, xh);
+            const double d0 = obs_x[2 * (size_t)o] - xh[0];
+            const double d1 = obs_x[2 * (size_t)o + 1] - xh[1];
+            sse += d0 * d0 + d1 * d1;
+            if (xh_out) {
+                xh_out[2 * (size_t)o] = xh[0];
+                xh_out[2 * (size_t)o + 1] = xh[1];
+            }
+        }
+    }
+    block_sum_to<256>(sse, part_sse + blockIdx.x);
+    __syncthreads();
+    block_sum_to<256>(dpg, part_dpg + blockIdx.x);
+}
+
+// fixed-order sum of nparts partials -> out (one block)
+__global__ void k_sum_parts(const double *__restrict__ part, int nparts, double *__restrict__ out)
+{
+    double v = 0.0;
+    for (int q = threadIdx.x; q < nparts; q += 256) v += part[q];
+    block_sum_to<256>(v, out);
+}
+
+// =========================================================================
+// launchers
+// =========================================================================
+static inline int grid_for(long long work, int bs, int cap)
+{
+    long long g = (work + bs - 1) / bs;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+#define BA_DISPATCH(NAEXPR, CALL)                                                   \
+    switch (NAEXPR) {                                                               \
+    case 6: { constexpr int NA = 6; CALL; } break;                                  \
+    case 7: { constexpr int NA = 7; CALL; } break;                                  \
+    case 10: { constexpr int NA = 10; CALL; } break;                                \
+    default: return -1000;                                                          \
+    }
+
+static const int PT_GRID_CAP = 8192;  // partial-sum slots used by per-point kernels
+
+int ba_launch_rotations(ba_dev *d, const double *a, double *rot, int all5)
+{
+    (void)all5;
+    const int g = grid_for(d->m, 64, 1 << 30);
+    BA_DISPATCH(d->na, (k_rotations<NA><<<g, 64, 0, d->stream>>>(a, rot, d->m)));
+    return -(int)hipGetLastError();
+}
+
+int ba_launch_linearize(ba_dev *d, ba_flags f)
+{
+    const int g = grid_for(d->n, 256, PT_GRID_CAP);
+    BA_DISPATCH(d->na, (k_linearize<NA><<<g, 256, 0, d->stream>>>(
+                           d->pt_ptr, d->obs_cam, d->obs_x, d->K4, d->a, d->rot, d->b, d->n, f,
+                           d->pivot, d->jrec, d->W, d->V, d->eB, d->part, d->xh_out,
+                           d->B_out)));
+    k_sum_parts<<<1, 256, 0, d->stream>>>(d->part, g, d->scal + 0);
+    return -(int)hipGetLastError();
+}
+
+int ba_launch_camera_reduce(ba_dev *d, ba_flags f)
+{
+    const int bs = (d->na * (d->na + 1) / 2 + d->na) <= 64 ? 64 : 128;
+    BA_DISPATCH(d->na, (k_camera_reduce<NA><<<d->m, bs, 0, d->stream>>>(
+                           d->cam_ptr, d->cam_obs, d->jrec, d->m, f, d->pivot, d->U, d->eA)));
+    return -(int)hipGetLastError();
+}
+
+int ba_launch_damp_point(ba_dev *d, double lambda)
+{
+    const int g = grid_for(d->n, 256, PT_GRID_CAP);
+    BA_DISPATCH(d->na, (k_damp_point<NA><<<g, 256, 0, d->stream>>>(
+                           d->pt_ptr, d->V, d->eB, d->W, d->n, lambda, d->Vinv, d->Y, d->t)));
+    return -(int)hipGetLastError();
+}
+
+int ba_launch_schur(ba_dev *d, double lambda)
+{
+    const int bs = (d->na * d->na + d->na) <= 64 ? 64 : 128;
+    BA_DISPATCH(d->na, (k_schur<NA><<<d->nb, bs, 0, d->stream>>>(
+                           d->blk_jk, d->blk_ptr, d->term, d->Y, d->W, d->t, d->U, d->eA, d->nb,
+                           lambda, d->schur_owner, d->sblk, d->rhs)));
+    return -(int)hipGetLastError();
+}
+
+int ba_launch_yeb(ba_dev *d)
+{
+    const int g = grid_for(d->n, 256, 1 << 30);
+    BA_DISPATCH(d->na, (k_point_yeb<NA><<<g, 256, 0, d->stream>>>(d->pt_ptr, d->Y, d->eB, d->n,
+                                                                    d->t)));
+    return -(int)hipGetLastError();
+}
+
+int ba_launch_assemble(ba_dev *d)
+{
+    VLGBA_CHECK(hipMemsetAsync(d->S, 0, sizeof(double) * d->lds * d->lds, d->stream));
+    VLGBA_CHECK(hipMemsetAsync(d->rhs + d->ld, 0, sizeof(double) * (d->lds - d->ld), d->stream));
+    const long long work = (long long)d->nb * d->na * d->na;
+    const int g = (int)((work + 255) / 256);
+    BA_DISPATCH(d->na, (k_assemble<NA><<<g, 256, 0, d->stream>>>(d->blk_jk, d->sblk, d->nb,
+                                                                   d->lds, d->S)));
+    k_fix_zero_rows<<<(int)((d->lds + 255) / 256), 256, 0, d->stream>>>(d->S, d->rhs, d->lds);
+    return -(int)hipGetLastError();
+}
+
+int ba_launch_update(ba_dev *d, double lambda)
+{
+    const int gc = grid_for(d->m, 256, 1 << 30);
+    BA_DISPATCH(d->na, (k_camera_update<NA><<<gc, 256, 0, d->stream>>>(
+                           d->a, d->da, d->eA, d->m, lambda, d->a_new, d->rot_new, d->part)));
+    k_sum_parts<<<1, 256, 0, d->stream>>>(d->part, gc, d->scal + 2);
+    const int g = grid_for(d->n, 256, PT_GRID_CAP);
+    BA_DISPATCH(d->na, (k_point_update<NA><<<g, 256, 0, d->stream>>>(
+                           d->pt_ptr, d->obs_cam, d->obs_x, d->K4, d->W, d->da, d->eB, d->Vinv,
+                           d->b, d->a_new, d->rot_new, d->n, lambda, d->db, d->b_new,
+                           d->part + BA_PART_MAX, d->part + 2 * BA_PART_MAX, d->obs_vis,
+                           d->xh_out)));
+    k_sum_parts<<<1, 256, 0, d->stream>>>(d->part + BA_PART_MAX, g, d->scal + 1);
+    k_sum_parts<<<1, 256, 0, d->stream>>>(d->part + 2 * BA_PART_MAX, g, d->scal + 3);
+    return -(int)hipGetLastError();
+}
+
+// dense (unpadded, both triangles) S for the stage-2 entry
+int ba_launch_assemble_plain(ba_dev *d, double *S, long long ld)
+{
+    VLGBA_CHECK(hipMemsetAsync(S, 0, sizeof(double) * ld * ld, d->stream));
+    const long long work = (long long)d->nb * d->na * d->na;
+    const int g = (int)((work + 255) / 256);
+    if (g > 0)
+        BA_DISPATCH(d->na, (k_assemble<NA><<<g, 256, 0, d->stream>>>(d->blk_jk, d->sblk, d->nb,
+                                                                       ld, S)));
+    return -(int)hipGetLastError();
+}

@@ -1,0 +1,839 @@
+// ba_solver.cpp -- libvlgba host side: problem setup, the LM driver of
+// toolbox/bundle/bundle_euclid.m:111-249 and the C ABI of include/vlgba.h.
+//
+// The LM control flow stays on the host (it is a handful of scalars per pass,
+// exactly as bundle_euclid.m keeps it in MATLAB); every array stays in HBM.
+// One pass = rotations + linearize + camera reduce (skipped after a rejected
+// step: bundle_euclid.m:139 recomputes an identical linearisation, App. A Q12)
+// + damping/Y + Schur + dense Cholesky solve + update/new cost, then ONE
+// device->host copy of 5 scalars.
+//
+// Multi-GPU (one process per GPU): points are split into
+// contiguous ranges of balanced observation count; each rank linearises its
+// points, RCCL all-reduces U/eA/old-SSE once per linearisation and the packed
+// co-visible blocks of S + e_ once per pass, every rank runs the identical
+// dense solve, and a 3-scalar all-reduce drives the accept/reject decision.
+#include "ba_internal.h"
+#include "../../include/vlgba.h"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <numeric>
+#include <vector>
+
+#define VLGBA_VERSION_STR "vlgba 0.1 (gfx950, fp64, MFMA-f64 Cholesky)"
+
+namespace {
+
+template <typename T>
+int dalloc(T **p, size_t count)
+{
+    *p = nullptr;
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc((void **)p, sizeof(T) * count);
+    return e == hipSuccess ? 0 : -(int)e;
+}
+
+template <typename T>
+int upload(T *dst, const T *src, size_t count, hipStream_t s)
+{
+    if (count == 0) return 0;
+    hipError_t e = hipMemcpyAsync(dst, src, sizeof(T) * count, hipMemcpyHostToDevice, s);
+    return e == hipSuccess ? 0 : -(int)e;
+}
+
+template <typename T>
+int download(T *dst, const T *src, size_t count, hipStream_t s)
+{
+    if (count == 0) return 0;
+    hipError_t e = hipMemcpyAsync(dst, src, sizeof(T) * count, hipMemcpyDeviceToHost, s);
+    return e == hipSuccess ? 0 : -(int)e;
+}
+
+#define TRY(x)                                                                      \
+    do {                                                                            \
+        int rc__ = (x);                                                             \
+        if (rc__) return rc__;                                                      \
+    } while (0)
+
+// Observation list sorted point-major: points ascending, cameras ascending
+// within a point (the order of the reference's column-major n x m loops).
+struct host_obs {
+    std::vector<int> pt, cam;
+    std::vector<double> x;
+};
+
+int sort_obs(const vlgba_problem *p, host_obs &h)
+{
+    const long long N = p->num_obs;
+    std::vector<long long> cnt(p->n + 1, 0);
+    for (long long o = 0; o < N; o++) {
+        const int i = p->obs_pt[o], j = p->obs_cam[o];
+        if (i < 0 || i >= p->n || j < 0 || j >= p->m) return VLGBA_E_ARG;
+        cnt[i + 1]++;
+    }
+    for (int i = 0; i < p->n; i++) cnt[i + 1] += cnt[i];
+    std::vector<long long> pos(cnt.begin(), cnt.end() - 1);
+    std::vector<long long> perm(N);
+    for (long long o = 0; o < N; o++) perm[pos[p->obs_pt[o]]++] = o;
+    h.pt.resize(N);
+    h.cam.resize(N);
+    h.x.resize(2 * N);
+    for (int i = 0; i < p->n; i++) {
+        std::sort(perm.begin() + cnt[i], perm.begin() + cnt[i + 1],
+                  [&](long long u, long long v) { return p->obs_cam[u] < p->obs_cam[v]; });
+        for (long long q = cnt[i]; q < cnt[i + 1]; q++) {
+            const long long o = perm[q];
+            if (q > cnt[i] && p->obs_cam[o] == h.cam[q - 1]) return VLGBA_E_ORDER;
+            h.pt[q] = i;
+            h.cam[q] = p->obs_cam[o];
+            h.x[2 * q] = p->obs_x[2 * o];
+            h.x[2 * q + 1] = p->obs_x[2 * o + 1];
+        }
+    }
+    return 0;
+}
+
+// Co-visible camera-pair blocks and their term lists (obs pairs, point
+// ascending).  lower: blocks j >= k only (the Cholesky reads the lower
+// triangle); otherwise all ordered pairs (stage-2 entry: full S like
+// mex_bundle_2_Se_.c).  The block SET comes from all observations (so every
+// rank agrees on the packed layout); terms only from observations [o0, o1).
+struct host_blocks {
+    std::vector<int> jk, ptr, term;
+};
+
+void build_blocks(int m, const std::vector<int> &pt_ptr_all, const std::vector<int> &cam_all,
+                  int p0, int p1, long long obs_base, bool lower, bool all_diag, host_blocks &hb)
+{
+    const int n = (int)pt_ptr_all.size() - 1;
+    const bool dense_tab = (long long)m * m <= (1LL << 26);
+    std::vector<int> tab;
+    std::vector<std::vector<std::pair<int, int>>> rows;  // sparse fallback: (k, id)
+    if (dense_tab) tab.assign((size_t)m * m, -1);
+    else rows.resize(m);
+    auto find = [&](int j, int k) -> int {
+        if (dense_tab) return tab[(size_t)j * m + k];
+        for (auto &pr : rows[j]) if (pr.first == k) return pr.second;
+        return -1;
+    };
+    auto insert = [&](int j, int k) -> int {
+        int id = find(j, k);
+        if (id >= 0) return id;
+        id = (int)hb.jk.size() / 2;
+        hb.jk.push_back(j);
+        hb.jk.push_back(k);
+        if (dense_tab) tab[(size_t)j * m + k] = id;
+        else rows[j].push_back({k, id});
+        return id;
+    };
+    if (all_diag)
+        for (int j = 0; j < m; j++) insert(j, j);
+    for (int i = 0; i < n; i++)
+        for (int a = pt_ptr_all[i]; a < pt_ptr_all[i + 1]; a++)
+            for (int b = pt_ptr_all[i]; b < pt_ptr_all[i + 1]; b++) {
+                const int j = cam_all[a], k = cam_all[b];
+                if (lower && j < k) continue;
+                insert(j, k);
+            }
+    const int nb = (int)hb.jk.size() / 2;
+    std::vector<long long> cnt(nb + 1, 0);
+    for (int i = p0; i < p1; i++)
+        for (int a = pt_ptr_all[i]; a < pt_ptr_all[i + 1]; a++)
+            for (int b = pt_ptr_all[i]; b < pt_ptr_all[i + 1]; b++) {
+                const int j = cam_all[a], k = cam_all[b];
+                if (lower && j < k) continue;
+                cnt[find(j, k) + 1]++;
+            }
+    for (int q = 0; q < nb; q++) cnt[q + 1] += cnt[q];
+    hb.ptr.resize(nb + 1);
+    for (int q = 0; q <= nb; q++) hb.ptr[q] = (int)cnt[q];
+    hb.term.resize(2 * (size_t)cnt[nb]);
+    std::vector<long long> pos(cnt.begin(), cnt.end() - 1);
+    for (int i = p0; i < p1; i++)   // points ascending => terms ascending per block
+        for (int a = pt_ptr_all[i]; a < pt_ptr_all[i + 1]; a++)
+            for (int b = pt_ptr_all[i]; b < pt_ptr_all[i + 1]; b++) {
+                const int j = cam_all[a], k = cam_all[b];
+                if (lower && j < k) continue;
+                const long long s = pos[find(j, k)]++;
+                hb.term[2 * s] = (int)(a - obs_base);
+                hb.term[2 * s + 1] = (int)(b - obs_base);
+            }
+}
+
+}  // namespace
+
+// =========================================================================
+struct vlgba_ctx {
+    ba_dev d;
+    ba_flags flags;
+    int rank = 0, world = 1;
+    ncclComm_t comm = nullptr;
+    int p0 = 0, p1 = 0;          // global point range of this rank
+    int n_global = 0;
+    long long N_global = 0;
+    double num_vis = 0;
+    int max_iter = 20, max_iter2 = 10, verbose = 0;
+    double lambda = 1e-3, lambda0 = 1e-3, nu = 2.0;
+    int lin_valid = 0;
+    int timing = 0;
+    hipEvent_t ev[8] = {};
+    double phase_ms[7] = {};
+    std::vector<void *> allocs;
+    std::vector<double> hb_tmp;   // host staging for b gather
+};
+
+static void ctx_free(vlgba_ctx *c)
+{
+    if (!c) return;
+    if (c->d.stream) (void)hipStreamSynchronize(c->d.stream);
+    for (void *p : c->allocs) (void)hipFree(p);
+    for (auto &e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->comm) ncclCommDestroy(c->comm);
+    if (c->d.stream) (void)hipStreamDestroy(c->d.stream);
+    delete c;
+}
+
+template <typename T>
+static int ctx_alloc(vlgba_ctx *c, T **p, size_t count)
+{
+    TRY(dalloc(p, count));
+    c->allocs.push_back((void *)*p);
+    return 0;
+}
+
+static int allreduce(vlgba_ctx *c, double *buf, size_t count)
+{
+    if (c->world <= 1 || count == 0) return 0;
+    ncclResult_t r = ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c->comm, c->d.stream);
+    return r == ncclSuccess ? 0 : VLGBA_E_COMM;
+}
+
+// Device buffers + host-side structure for the observations of points [p0, p1).
+static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
+                     const std::vector<int> &pt_ptr_all, bool lower_blocks, bool all_diag,
+                     bool stage_mode)
+{
+    ba_dev &d = c->d;
+    const int na = p->num_a;
+    d.m = p->m;
+    d.na = na;
+    d.js = 2 * na + 2;
+    d.n = c->p1 - c->p0;
+    const long long o0 = pt_ptr_all[c->p0], o1 = pt_ptr_all[c->p1];
+    d.N = (int)(o1 - o0);
+    d.ld = (long long)na * p->m;
+    d.lds = ((d.ld + 63) / 64) * 64;
+    d.schur_owner = (c->rank == 0);
+    hipStream_t s = d.stream;
+
+    // local point-major arrays
+    std::vector<int> lptr(d.n + 1), lcam(h.cam.begin() + o0, h.cam.begin() + o1);
+    for (int i = 0; i <= d.n; i++) lptr[i] = pt_ptr_all[c->p0 + i] - (int)o0;
+    // camera-major view of the local observations (obs ids ascending per camera)
+    std::vector<int> cptr(p->m + 1, 0), cobs(d.N);
+    for (int o = 0; o < d.N; o++) cptr[lcam[o] + 1]++;
+    for (int j = 0; j < p->m; j++) cptr[j + 1] += cptr[j];
+    {
+        std::vector<int> pos(cptr.begin(), cptr.end() - 1);
+        for (int o = 0; o < d.N; o++) cobs[pos[lcam[o]]++] = o;
+    }
+    host_blocks hb;
+    build_blocks(p->m, pt_ptr_all, h.cam, c->p0, c->p1, o0, lower_blocks, all_diag, hb);
+    d.nb = (int)hb.jk.size() / 2;
+    d.T = (long long)hb.term.size() / 2;
+
+    TRY(ctx_alloc(c, &d.obs_cam, d.N));
+    TRY(ctx_alloc(c, &d.pt_ptr, d.n + 1));
+    TRY(ctx_alloc(c, &d.cam_ptr, p->m + 1));
+    TRY(ctx_alloc(c, &d.cam_obs, d.N));
+    TRY(ctx_alloc(c, &d.obs_x, 2 * (size_t)d.N));
+    TRY(ctx_alloc(c, &d.K4, 4 * (size_t)p->m));
+    TRY(ctx_alloc(c, &d.a, (size_t)d.ld));
+    TRY(ctx_alloc(c, &d.a_new, (size_t)d.ld));
+    TRY(ctx_alloc(c, &d.b, 3 * (size_t)d.n));
+    TRY(ctx_alloc(c, &d.b_new, 3 * (size_t)d.n));
+    TRY(ctx_alloc(c, &d.rot, 45 * (size_t)p->m));
+    TRY(ctx_alloc(c, &d.rot_new, 9 * (size_t)p->m));
+    TRY(ctx_alloc(c, &d.jrec, (size_t)d.js * d.N));
+    TRY(ctx_alloc(c, &d.W, (size_t)3 * na * d.N));
+    TRY(ctx_alloc(c, &d.Y, (size_t)3 * na * d.N));
+    TRY(ctx_alloc(c, &d.t, (size_t)na * d.N));
+    TRY(ctx_alloc(c, &d.U, (size_t)na * na * p->m + na * (size_t)p->m + 1));
+    d.eA = d.U + (size_t)na * na * p->m;     // U | eA | old_sse contiguous: one all-reduce
+    TRY(ctx_alloc(c, &d.V, 9 * (size_t)d.n));
+    TRY(ctx_alloc(c, &d.eB, 3 * (size_t)d.n));
+    TRY(ctx_alloc(c, &d.Vinv, 9 * (size_t)d.n));
+    TRY(ctx_alloc(c, &d.db, 3 * (size_t)d.n));
+    TRY(ctx_alloc(c, &d.blk_jk, 2 * (size_t)d.nb));
+    TRY(ctx_alloc(c, &d.blk_ptr, (size_t)d.nb + 1));
+    TRY(ctx_alloc(c, &d.term, 2 * (size_t)d.T));
+    TRY(ctx_alloc(c, &d.sblk, (size_t)na * na * d.nb + d.lds));
+    d.rhs = d.sblk + (size_t)na * na * d.nb;  // blocks | rhs contiguous: one all-reduce
+    if (!stage_mode) {
+        TRY(ctx_alloc(c, &d.S, (size_t)(d.lds * d.lds)));
+        TRY(ctx_alloc(c, &d.linv, (size_t)(d.lds / 64) * 64 * 64));
+        TRY(ctx_alloc(c, &d.ywork, (size_t)d.lds));
+        TRY(ctx_alloc(c, &d.da, (size_t)d.lds));
+    } else {
+        TRY(ctx_alloc(c, &d.da, (size_t)d.lds));
+    }
+    TRY(ctx_alloc(c, &d.part, 3 * (size_t)BA_PART_MAX));
+    TRY(ctx_alloc(c, &d.scal, 8));
+    if (p->num_obs > 0 || true) {
+        TRY(upload(d.obs_cam, lcam.data(), d.N, s));
+        TRY(upload(d.pt_ptr, lptr.data(), d.n + 1, s));
+        TRY(upload(d.cam_ptr, cptr.data(), p->m + 1, s));
+        TRY(upload(d.cam_obs, cobs.data(), d.N, s));
+        TRY(upload(d.obs_x, h.x.data() + 2 * o0, 2 * (size_t)d.N, s));
+        TRY(upload(d.K4, p->K, 4 * (size_t)p->m, s));
+        TRY(upload(d.blk_jk, hb.jk.data(), hb.jk.size(), s));
+        TRY(upload(d.blk_ptr, hb.ptr.data(), hb.ptr.size(), s));
+        TRY(upload(d.term, hb.term.data(), hb.term.size(), s));
+    }
+    VLGBA_CHECK(hipMemsetAsync(d.scal, 0, 8 * sizeof(double), s));
+    VLGBA_CHECK(hipStreamSynchronize(s));   // host vectors go out of scope
+    return 0;
+}
+
+static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx **out,
+                      bool lower_blocks, bool all_diag, bool stage_mode,
+                      std::vector<int> *pt_ptr_out = nullptr, host_obs *h_out = nullptr)
+{
+    *out = nullptr;
+    if (!p || p->m < 1 || p->n < 0 || p->num_obs < 0 || !p->K) return VLGBA_E_ARG;
+    if (p->num_a != 6 && p->num_a != 7 && p->num_a != 10) return VLGBA_E_NUMA;
+    if (p->num_obs > 0x7fffffffLL) return VLGBA_E_ARG;
+    vlgba_ctx *c = new (std::nothrow) vlgba_ctx();
+    if (!c) return VLGBA_E_NOMEM;
+    std::memset(&c->d, 0, sizeof(c->d));
+    vlgba_options defaults;
+    std::memset(&defaults, 0, sizeof defaults);
+    if (!o) o = &defaults;
+    int rc = 0;
+    do {
+        if (hipSetDevice(o->device) != hipSuccess) { rc = VLGBA_E_ARG; break; }
+        if (hipStreamCreateWithFlags(&c->d.stream, hipStreamNonBlocking) != hipSuccess) {
+            rc = -1;
+            break;
+        }
+        host_obs h;
+        rc = sort_obs(p, h);
+        if (rc) break;
+        std::vector<int> pt_ptr_all(p->n + 1, 0);
+        for (size_t q = 0; q < h.pt.size(); q++) pt_ptr_all[h.pt[q] + 1]++;
+        for (int i = 0; i < p->n; i++) pt_ptr_all[i + 1] += pt_ptr_all[i];
+        c->world = o->world_size > 1 ? o->world_size : 1;
+        c->rank = c->world > 1 ? o->rank : 0;
+        // contiguous point ranges with balanced observation counts
+        if (c->world > 1) {
+            const long long N = p->num_obs;
+            auto bound = [&](int r) -> int {
+                const long long target = (N * r) / c->world;
+                return (int)(std::lower_bound(pt_ptr_all.begin(), pt_ptr_all.end(), (int)target) -
+                             pt_ptr_all.begin());
+            };
+            c->p0 = c->rank == 0 ? 0 : std::min(bound(c->rank), p->n);
+            c->p1 = c->rank == c->world - 1 ? p->n : std::min(bound(c->rank + 1), p->n);
+            if (!o->comm_id) { rc = VLGBA_E_COMM; break; }
+            ncclUniqueId id;
+            std::memcpy(&id, o->comm_id, sizeof id);
+            if (ncclCommInitRank(&c->comm, c->world, id, c->rank) != ncclSuccess) {
+                rc = VLGBA_E_COMM;
+                break;
+            }
+        } else {
+            c->p0 = 0;
+            c->p1 = p->n;
+        }
+        c->n_global = p->n;
+        c->N_global = p->num_obs;
+        c->num_vis = p->num_vis > 0 ? p->num_vis : (double)p->num_obs;
+        c->flags.fix_structure = o->fix_structure;
+        c->flags.fix_motion = o->fix_motion;
+        c->flags.has_pivot = o->pivot != nullptr;
+        c->max_iter = o->max_iter > 0 ? o->max_iter : 20;
+        c->max_iter2 = o->max_iter2 > 0 ? o->max_iter2 : 10;
+        c->lambda0 = c->lambda = o->lambda0 > 0 ? o->lambda0 : 1e-3;
+        c->verbose = o->verbose;
+        rc = ctx_setup(c, p, h, pt_ptr_all, lower_blocks, all_diag, stage_mode);
+        if (rc) break;
+        if (o->pivot) {
+            rc = ctx_alloc(c, &c->d.pivot, (size_t)p->m);
+            if (rc) break;
+            rc = upload(c->d.pivot, o->pivot, (size_t)p->m, c->d.stream);
+            if (rc) break;
+        }
+        if (pt_ptr_out) *pt_ptr_out = pt_ptr_all;
+        if (h_out) *h_out = std::move(h);
+    } while (0);
+    if (rc) {
+        ctx_free(c);
+        return rc;
+    }
+    *out = c;
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// one LM pass
+// ---------------------------------------------------------------------------
+static inline void mark(vlgba_ctx *c, int q)
+{
+    if (c->timing) (void)hipEventRecord(c->ev[q], c->d.stream);
+}
+
+static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
+{
+    ba_dev &d = c->d;
+    const double lam = c->lambda;
+    mark(c, 0);
+    if (relinearize || !c->lin_valid) {
+        TRY(ba_launch_rotations(&d, d.a, d.rot, 1));
+        TRY(ba_launch_linearize(&d, c->flags));
+        mark(c, 1);
+        TRY(ba_launch_camera_reduce(&d, c->flags));
+        // U | eA | old_sse travel in one all-reduce
+        VLGBA_CHECK(hipMemcpyAsync(d.eA + d.ld, d.scal + 0, sizeof(double),
+                                   hipMemcpyDeviceToDevice, d.stream));
+        TRY(allreduce(c, d.U, (size_t)d.na * d.na * d.m + d.ld + 1));
+        c->lin_valid = 1;
+    } else {
+        mark(c, 1);
+    }
+    mark(c, 2);
+    TRY(ba_launch_damp_point(&d, lam));
+    mark(c, 3);
+    TRY(ba_launch_schur(&d, lam));
+    TRY(allreduce(c, d.sblk, (size_t)d.na * d.na * d.nb + d.ld));
+    mark(c, 4);
+    TRY(ba_launch_assemble(&d));
+    mark(c, 5);
+    TRY(ba_chol_solve(&d));
+    mark(c, 6);
+    TRY(ba_launch_update(&d, lam));
+    mark(c, 7);
+    // scalars: [0] old_sse(local) [1] new_sse [2] dpg cameras [3] dpg points [4] chol status
+    double hs[5];
+    VLGBA_CHECK(hipMemcpyAsync(d.scal + 0, d.eA + d.ld, sizeof(double), hipMemcpyDeviceToDevice,
+                               d.stream));
+    if (c->world > 1) {
+        // global old_sse is already in d.eA[ld]; new_sse and the point part of dpg
+        // are local; the camera part of dpg is identical on every rank.
+        TRY(allreduce(c, d.scal + 1, 1));
+        TRY(allreduce(c, d.scal + 3, 1));
+    }
+    TRY(download(hs, d.scal, 5, d.stream));
+    VLGBA_CHECK(hipStreamSynchronize(d.stream));
+    if (c->timing) {
+        float ms;
+        const int map[7][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {6, 7}};
+        for (int q = 0; q < 7; q++) {
+            (void)hipEventElapsedTime(&ms, c->ev[map[q][0]], c->ev[map[q][1]]);
+            c->phase_ms[q] = ms;
+        }
+    }
+    info->old_sse = hs[0];
+    info->new_sse = hs[1];
+    info->dpg = hs[2] + hs[3];
+    info->lambda = lam;
+    info->chol_failed = hs[4] != 0.0;
+    info->rho = (hs[0] - hs[1]) / info->dpg;
+    info->accepted = (hs[0] - hs[1]) > 0 && !info->chol_failed;
+    return 0;
+}
+
+// bundle_euclid.m:218-241 applied to the context
+static void lm_apply(vlgba_ctx *c, const vlgba_step_info *info)
+{
+    ba_dev &d = c->d;
+    if (info->accepted) {
+        std::swap(d.a, d.a_new);
+        std::swap(d.b, d.b_new);
+        c->lambda = c->lambda * std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * info->rho - 1.0, 3));
+        c->nu = 2.0;
+        c->lin_valid = 0;
+    } else {
+        c->lambda = c->lambda * c->nu;
+        c->nu = 2.0 * c->nu;
+    }
+}
+
+// =========================================================================
+// C ABI
+// =========================================================================
+extern "C" {
+
+int vlgba_version(char *buf, int len)
+{
+    const int n = (int)std::strlen(VLGBA_VERSION_STR);
+    if (buf && len > 0) {
+        std::strncpy(buf, VLGBA_VERSION_STR, (size_t)len - 1);
+        buf[len - 1] = 0;
+    }
+    return n;
+}
+
+int vlgba_get_unique_id(void *id128)
+{
+    if (!id128) return VLGBA_E_ARG;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return VLGBA_E_COMM;
+    static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
+    std::memcpy(id128, &id, sizeof id);
+    return 0;
+}
+
+int vlgba_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int vlgba_create(const vlgba_problem *prob, const vlgba_options *opt, vlgba_ctx **out)
+{
+    if (!out) return VLGBA_E_ARG;
+    return ctx_create(prob, opt, out, true, true, false);
+}
+
+void vlgba_destroy(vlgba_ctx *ctx) { ctx_free(ctx); }
+
+int vlgba_set_params(vlgba_ctx *c, const double *a, const double *b)
+{
+    if (!c || !a || !b) return VLGBA_E_ARG;
+    TRY(upload(c->d.a, a, (size_t)c->d.ld, c->d.stream));
+    TRY(upload(c->d.b, b + 3 * (size_t)c->p0, 3 * (size_t)c->d.n, c->d.stream));
+    c->lin_valid = 0;
+    VLGBA_CHECK(hipStreamSynchronize(c->d.stream));
+    return 0;
+}
+
+int vlgba_get_params(vlgba_ctx *c, double *a, double *b)
+{
+    if (!c) return VLGBA_E_ARG;
+    if (a) TRY(download(a, c->d.a, (size_t)c->d.ld, c->d.stream));
+    if (b) {
+        if (c->world > 1) {
+            // every rank returns the full b: all-reduce of a zero-padded copy
+            double *full = nullptr;
+            TRY(dalloc(&full, 3 * (size_t)c->n_global));
+            VLGBA_CHECK(hipMemsetAsync(full, 0, sizeof(double) * 3 * c->n_global, c->d.stream));
+            VLGBA_CHECK(hipMemcpyAsync(full + 3 * (size_t)c->p0, c->d.b,
+                                       sizeof(double) * 3 * c->d.n, hipMemcpyDeviceToDevice,
+                                       c->d.stream));
+            int rc = allreduce(c, full, 3 * (size_t)c->n_global);
+            if (!rc) rc = download(b, full, 3 * (size_t)c->n_global, c->d.stream);
+            (void)hipStreamSynchronize(c->d.stream);
+            (void)hipFree(full);
+            if (rc) return rc;
+        } else {
+            TRY(download(b, c->d.b, 3 * (size_t)c->d.n, c->d.stream));
+        }
+    }
+    VLGBA_CHECK(hipStreamSynchronize(c->d.stream));
+    return 0;
+}
+
+int vlgba_set_timing(vlgba_ctx *c, int on)
+{
+    if (!c) return VLGBA_E_ARG;
+    if (on && !c->ev[0])
+        for (auto &e : c->ev) VLGBA_CHECK(hipEventCreate(&e));
+    c->timing = on;
+    return 0;
+}
+
+int vlgba_phase_ms(vlgba_ctx *c, double *ms7)
+{
+    if (!c || !ms7) return VLGBA_E_ARG;
+    for (int q = 0; q < 7; q++) ms7[q] = c->phase_ms[q];
+    return 0;
+}
+
+int vlgba_sync(vlgba_ctx *c)
+{
+    if (!c) return VLGBA_E_ARG;
+    VLGBA_CHECK(hipStreamSynchronize(c->d.stream));
+    return 0;
+}
+
+int vlgba_step(vlgba_ctx *c, int relinearize, int update_lm, vlgba_step_info *info)
+{
+    if (!c) return VLGBA_E_ARG;
+    vlgba_step_info tmp;
+    if (!info) info = &tmp;
+    TRY(lm_pass(c, relinearize, info));
+    if (update_lm) lm_apply(c, info);
+    return 0;
+}
+
+// bundle_euclid.m:111-249
+int vlgba_run(vlgba_ctx *c, double *error_out, vlgba_stats *stats)
+{
+    if (!c) return VLGBA_E_ARG;
+    auto t0 = std::chrono::steady_clock::now();
+    c->lambda = c->lambda0;
+    c->nu = 2.0;
+    c->lin_valid = 0;
+    std::vector<double> err;   // error_, 1-based in the reference
+    int iter = 1, iter2 = 0, passes = 0, acc = 0;
+    for (;;) {
+        if (!(iter < c->max_iter && iter2 < c->max_iter2)) break;
+        if (iter >= 3) {
+            const double e1 = err[iter - 1], e0 = err[iter - 2];
+            if (!(e1 > 1e-20 && e0 - e1 > 1e-3 * e0)) break;
+        }
+        vlgba_step_info info;
+        TRY(lm_pass(c, 0, &info));
+        passes++;
+        if (info.accepted) {
+            const double olde = info.old_sse / c->num_vis, newe = info.new_sse / c->num_vis;
+            if (c->verbose && c->rank == 0)
+                std::printf("iter %d: error= %.5g -> %.5g\n", iter, olde, newe);
+            if ((int)err.size() < iter) err.push_back(olde);
+            else err[iter - 1] = olde;
+            iter++;
+            err.push_back(newe);
+            iter2 = 0;
+            acc++;
+        } else {
+            iter2++;
+        }
+        lm_apply(c, &info);
+    }
+    VLGBA_CHECK(hipStreamSynchronize(c->d.stream));
+    if (error_out)
+        for (size_t q = 0; q < err.size(); q++) error_out[q] = err[q];
+    if (stats) {
+        stats->iterations = passes;
+        stats->accepted = acc;
+        stats->num_error = (int)err.size();
+        stats->lambda = c->lambda;
+        stats->seconds =
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return 0;
+}
+
+int vlgba_solve(const vlgba_problem *prob, const vlgba_options *opt, double *a, double *b,
+                double *error_out, vlgba_stats *stats)
+{
+    if (!a || !b) return VLGBA_E_ARG;
+    vlgba_ctx *c = nullptr;
+    TRY(vlgba_create(prob, opt, &c));
+    int rc = vlgba_set_params(c, a, b);
+    if (!rc) rc = vlgba_run(c, error_out, stats);
+    if (!rc) rc = vlgba_get_params(c, a, b);
+    vlgba_destroy(c);
+    return rc;
+}
+
+// ---------------------------------------------------------------------------
+// stage entries (MEX layouts)
+// ---------------------------------------------------------------------------
+static void obs_from_vis(int m, int n, const double *vis, std::vector<int> &pt,
+                         std::vector<int> &cam)
+{
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < m; j++)
+            if (vis[i + (size_t)n * j] != 0.0) {
+                pt.push_back(i);
+                cam.push_back(j);
+            }
+}
+
+int vlgba_mex_bundle_1(int m, int n, int num_a, const double *K, const double *a,
+                       const double *b, const double *X, const double *vis, double *X_hat,
+                       double *A, double *B, double *e, double *U, double *V, double *W,
+                       double *eA, double *eB)
+{
+    if (m < 1 || n < 0 || !K || !a || !b || !X || !vis) return VLGBA_E_ARG;
+    std::vector<int> pt, cam;
+    obs_from_vis(m, n, vis, pt, cam);
+    const long long N = (long long)pt.size();
+    std::vector<double> ox(2 * N);
+    for (long long q = 0; q < N; q++) {
+        const size_t p = (size_t)pt[q] + (size_t)n * cam[q];
+        ox[2 * q] = X[2 * p];
+        ox[2 * q + 1] = X[2 * p + 1];
+    }
+    vlgba_problem pr = {m, n, num_a, N, pt.data(), cam.data(), ox.data(), K, 0.0};
+    vlgba_ctx *c = nullptr;
+    TRY(ctx_create(&pr, nullptr, &c, true, true, true));
+    ba_dev &d = c->d;
+    int rc = 0;
+    std::vector<double> jr((size_t)d.js * N), hW((size_t)3 * num_a * N), xh(2 * N), hB(6 * N);
+    do {
+        if ((rc = ctx_alloc(c, &d.xh_out, 2 * (size_t)N))) break;
+        if ((rc = ctx_alloc(c, &d.B_out, 6 * (size_t)N))) break;
+        if ((rc = upload(d.a, a, (size_t)d.ld, d.stream))) break;
+        if ((rc = upload(d.b, b, 3 * (size_t)n, d.stream))) break;
+        ba_flags f = {0, 0, 0};
+        if ((rc = ba_launch_rotations(&d, d.a, d.rot, 1))) break;
+        if ((rc = ba_launch_linearize(&d, f))) break;
+        if ((rc = ba_launch_camera_reduce(&d, f))) break;
+        if ((rc = download(jr.data(), d.jrec, jr.size(), d.stream))) break;
+        if ((rc = download(hW.data(), d.W, hW.size(), d.stream))) break;
+        if ((rc = download(xh.data(), d.xh_out, xh.size(), d.stream))) break;
+        if ((rc = download(hB.data(), d.B_out, hB.size(), d.stream))) break;
+        if ((rc = download(U, d.U, (size_t)num_a * num_a * m, d.stream))) break;
+        if ((rc = download(eA, d.eA, (size_t)num_a * m, d.stream))) break;
+        if ((rc = download(V, d.V, 9 * (size_t)n, d.stream))) break;
+        if ((rc = download(eB, d.eB, 3 * (size_t)n, d.stream))) break;
+        if (hipStreamSynchronize(d.stream) != hipSuccess) { rc = -1; break; }
+    } while (0);
+    ctx_free(c);
+    if (rc) return rc;
+    // scatter to the dense MEX layouts; invisible pairs: X_hat = X, zeros
+    const size_t nm = (size_t)n * m;
+    for (size_t p = 0; p < nm; p++) {
+        X_hat[2 * p] = X[2 * p];
+        X_hat[2 * p + 1] = X[2 * p + 1];
+        e[2 * p] = e[2 * p + 1] = 0.0;
+    }
+    std::memset(A, 0, sizeof(double) * 2 * num_a * nm);
+    std::memset(B, 0, sizeof(double) * 6 * nm);
+    std::memset(W, 0, sizeof(double) * 3 * num_a * nm);
+    const int js = 2 * num_a + 2;
+    for (long long q = 0; q < N; q++) {
+        const size_t p = (size_t)pt[q] + (size_t)n * cam[q];
+        X_hat[2 * p] = xh[2 * q];
+        X_hat[2 * p + 1] = xh[2 * q + 1];
+        std::memcpy(A + 2 * num_a * p, jr.data() + js * q, sizeof(double) * 2 * num_a);
+        e[2 * p] = jr[js * q + 2 * num_a];
+        e[2 * p + 1] = jr[js * q + 2 * num_a + 1];
+        std::memcpy(B + 6 * p, hB.data() + 6 * q, sizeof(double) * 6);
+        std::memcpy(W + 3 * num_a * p, hW.data() + 3 * num_a * q, sizeof(double) * 3 * num_a);
+    }
+    return 0;
+}
+
+int vlgba_mex_bundle_2(int m, int n, int num_a, const double *Y, const double *W,
+                       const double *U, const double *eA, const double *eB, double *S,
+                       double *e_)
+{
+    if (m < 1 || n < 0 || !Y || !W || !U || !eA || !eB || !S || !e_) return VLGBA_E_ARG;
+    const int bs = 3 * num_a;
+    std::vector<int> pt, cam;
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < m; j++) {
+            const size_t p = (size_t)i + (size_t)n * j;
+            bool nz = false;
+            for (int q = 0; q < bs && !nz; q++) nz = (Y[bs * p + q] != 0.0) || (W[bs * p + q] != 0.0);
+            if (nz) {
+                pt.push_back(i);
+                cam.push_back(j);
+            }
+        }
+    const long long N = (long long)pt.size();
+    std::vector<double> ox(2 * N, 0.0), hY((size_t)bs * N), hW((size_t)bs * N);
+    for (long long q = 0; q < N; q++) {
+        const size_t p = (size_t)pt[q] + (size_t)n * cam[q];
+        std::memcpy(hY.data() + bs * q, Y + bs * p, sizeof(double) * bs);
+        std::memcpy(hW.data() + bs * q, W + bs * p, sizeof(double) * bs);
+    }
+    std::vector<double> K(4 * (size_t)m, 1.0);
+    vlgba_problem pr = {m, n, num_a, N, pt.data(), cam.data(), ox.data(), K.data(), 0.0};
+    vlgba_ctx *c = nullptr;
+    TRY(ctx_create(&pr, nullptr, &c, false, true, true));
+    ba_dev &d = c->d;
+    const long long ld = d.ld;
+    int rc = 0;
+    double *Sd = nullptr;
+    do {
+        if ((rc = ctx_alloc(c, &Sd, (size_t)(ld * ld)))) break;
+        if ((rc = upload(d.Y, hY.data(), hY.size(), d.stream))) break;
+        if ((rc = upload(d.W, hW.data(), hW.size(), d.stream))) break;
+        if ((rc = upload(d.U, U, (size_t)num_a * num_a * m, d.stream))) break;
+        if ((rc = upload(d.eA, eA, (size_t)num_a * m, d.stream))) break;
+        if ((rc = upload(d.eB, eB, 3 * (size_t)n, d.stream))) break;
+        if ((rc = ba_launch_yeb(&d))) break;
+        // U is given already damped (bundle_euclid.m:192 passes U_): lambda = 0
+        if ((rc = ba_launch_schur(&d, 0.0))) break;
+        if ((rc = ba_launch_assemble_plain(&d, Sd, ld))) break;
+        if ((rc = download(S, Sd, (size_t)(ld * ld), d.stream))) break;
+        if ((rc = download(e_, d.rhs, (size_t)ld, d.stream))) break;
+        if (hipStreamSynchronize(d.stream) != hipSuccess) { rc = -1; break; }
+    } while (0);
+    ctx_free(c);
+    return rc;
+}
+
+int vlgba_mex_bundle_3(int m, int n, int num_a, const double *W, const double *da,
+                       const double *eB, const double *Vinv, const double *K, const double *a,
+                       const double *b, const double *X, const double *vis, double *db,
+                       double *a_new, double *b_new, double *X_hat)
+{
+    if (m < 1 || n < 0 || !W || !da || !eB || !Vinv || !K || !a || !b || !X || !vis)
+        return VLGBA_E_ARG;
+    const int bs = 3 * num_a;
+    std::vector<int> pt, cam;
+    std::vector<unsigned char> ov;
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < m; j++) {
+            const size_t p = (size_t)i + (size_t)n * j;
+            bool nz = vis[p] != 0.0;
+            const bool v = nz;
+            for (int q = 0; q < bs && !nz; q++) nz = W[bs * p + q] != 0.0;
+            if (nz) {
+                pt.push_back(i);
+                cam.push_back(j);
+                ov.push_back(v ? 1 : 0);
+            }
+        }
+    const long long N = (long long)pt.size();
+    std::vector<double> ox(2 * N), hW((size_t)bs * N), xh(2 * N);
+    for (long long q = 0; q < N; q++) {
+        const size_t p = (size_t)pt[q] + (size_t)n * cam[q];
+        ox[2 * q] = X[2 * p];
+        ox[2 * q + 1] = X[2 * p + 1];
+        std::memcpy(hW.data() + bs * q, W + bs * p, sizeof(double) * bs);
+    }
+    vlgba_problem pr = {m, n, num_a, N, pt.data(), cam.data(), ox.data(), K, 0.0};
+    vlgba_ctx *c = nullptr;
+    TRY(ctx_create(&pr, nullptr, &c, true, true, true));
+    ba_dev &d = c->d;
+    int rc = 0;
+    do {
+        if ((rc = ctx_alloc(c, &d.xh_out, 2 * (size_t)N))) break;
+        if ((rc = ctx_alloc(c, &d.obs_vis, (size_t)N))) break;
+        if ((rc = upload(d.obs_vis, ov.data(), ov.size(), d.stream))) break;
+        if ((rc = upload(d.W, hW.data(), hW.size(), d.stream))) break;
+        if ((rc = upload(d.da, da, (size_t)d.ld, d.stream))) break;
+        if ((rc = upload(d.eB, eB, 3 * (size_t)n, d.stream))) break;
+        if ((rc = upload(d.Vinv, Vinv, 9 * (size_t)n, d.stream))) break;
+        if ((rc = upload(d.a, a, (size_t)d.ld, d.stream))) break;
+        if ((rc = upload(d.b, b, 3 * (size_t)n, d.stream))) break;
+        VLGBA_CHECK(hipMemsetAsync(d.eA, 0, sizeof(double) * d.ld, d.stream));
+        if ((rc = ba_launch_update(&d, 0.0))) break;
+        if ((rc = download(db, d.db, 3 * (size_t)n, d.stream))) break;
+        if ((rc = download(a_new, d.a_new, (size_t)d.ld, d.stream))) break;
+        if ((rc = download(b_new, d.b_new, 3 * (size_t)n, d.stream))) break;
+        if ((rc = download(xh.data(), d.xh_out, xh.size(), d.stream))) break;
+        if (hipStreamSynchronize(d.stream) != hipSuccess) { rc = -1; break; }
+    } while (0);
+    ctx_free(c);
+    if (rc) return rc;
+    const size_t nm = (size_t)n * m;
+    for (size_t p = 0; p < nm; p++) {
+        X_hat[2 * p] = X[2 * p];
+        X_hat[2 * p + 1] = X[2 * p + 1];
+    }
+    for (long long q = 0; q < N; q++) {
+        if (!ov[q]) continue;
+        const size_t p = (size_t)pt[q] + (size_t)n * cam[q];
+        X_hat[2 * p] = xh[2 * q];
+        X_hat[2 * p + 1] = xh[2 * q + 1];
+    }
+    return 0;
+}
+
+}  // extern "C"

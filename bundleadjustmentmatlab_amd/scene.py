@@ -1,0 +1,227 @@
+"""Seeded synthetic scenes for the Euclidean BA path.
+
+The reference generates scenes with unseeded MATLAB randn/rand
+(toolbox/test/generate_scene_and_motion.m:1-122) and perturbs them as in
+toolbox/test/demo_bundle_euclid.m:29-31.  Here every config is seeded
+(numpy PCG64) so runs are reproducible:
+
+* ``mview_scene``  -- a seeded restatement of generate_scene_and_motion.m:36-117
+  (f = 500, c = (250, 250), 500x500 image, random-walk camera motion,
+  tracked / re-detected / new features), used for config 1 (m = 10, <= 200
+  points, the test_mview.m:19-26 setting) and config 5 (test_incremental).
+* ``banded_scene`` -- configs 2-4: every point is seen by ``track`` consecutive
+  cameras (start camera uniform), i.e. video-like banded co-visibility; a damped
+  random-walk camera path keeps each point in front of all its cameras at any
+  sequence length (the reference's undamped walk diverges over 1000 frames).
+
+Both return a :class:`Scene` with ground truth, the observation list sorted
+point-major (point ascending, camera ascending: the order of the reference's
+column-major n x m loops), and the perturbed initial parameters.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+import numpy as np
+
+
+def rodrigues(w):
+    """Rotation matrices for rotation vectors w (3, k) -> (k, 3, 3), numpy/libm.
+
+    Same formula as vl_rodrigues; used only to synthesise
+    scenes, never on the solve path."""
+    w = np.asarray(w, dtype=np.float64).reshape(3, -1)
+    th = np.sqrt((w * w).sum(0))
+    small = th < 1e-6
+    ths = np.where(small, 1.0, th)
+    x, y, z = w / ths
+    s, c = np.sin(th), np.cos(th)
+    mc = 1.0 - c
+    R = np.empty((w.shape[1], 3, 3))
+    R[:, 0, 0] = 1 - mc * (y * y + z * z)
+    R[:, 1, 0] = s * z + mc * x * y
+    R[:, 2, 0] = -s * y + mc * x * z
+    R[:, 0, 1] = -s * z + mc * x * y
+    R[:, 1, 1] = 1 - mc * (z * z + x * x)
+    R[:, 2, 1] = s * x + mc * y * z
+    R[:, 0, 2] = s * y + mc * x * z
+    R[:, 1, 2] = -s * x + mc * y * z
+    R[:, 2, 2] = 1 - mc * (x * x + y * y)
+    R[small] = np.eye(3)
+    return R
+
+
+def project(K, w, T, X, cam, pt):
+    """Pinhole projection of points X[:, pt] in cameras cam -> (k, 2) and depth."""
+    R = rodrigues(w)
+    Xc = np.einsum("kij,jk->ki", R[cam], X[:3, pt]) + T[:, cam].T
+    u = (K[0, cam] * Xc[:, 0] + K[2, cam] * Xc[:, 2]) / Xc[:, 2]
+    v = (K[1, cam] * Xc[:, 1] + K[3, cam] * Xc[:, 2]) / Xc[:, 2]
+    return np.stack([u, v], 1), Xc[:, 2]
+
+
+@dataclass
+class Scene:
+    K: np.ndarray        # (4, m) fx fy cx cy
+    T: np.ndarray        # (3, m) ground-truth translation
+    w: np.ndarray        # (3, m) ground-truth rotation vector
+    X: np.ndarray        # (4, n) ground-truth homogeneous points
+    obs_pt: np.ndarray   # (N,) int32, point-major order
+    obs_cam: np.ndarray  # (N,) int32
+    obs_x: np.ndarray    # (N, 2) measured pixels (noisy)
+    T0: np.ndarray       # (3, m) perturbed initial translation
+    w0: np.ndarray       # (3, m) perturbed initial rotation
+    X0: np.ndarray       # (4, n) perturbed initial points
+
+    @property
+    def m(self):
+        return self.K.shape[1]
+
+    @property
+    def n(self):
+        return self.X.shape[1]
+
+    @property
+    def num_obs(self):
+        return len(self.obs_pt)
+
+    def dense(self):
+        """MATLAB-shaped x (3, n, m) and visibility (n, m), bundle_euclid.m:9,50."""
+        x = np.zeros((3, self.n, self.m), order="F")
+        x[0, self.obs_pt, self.obs_cam] = self.obs_x[:, 0]
+        x[1, self.obs_pt, self.obs_cam] = self.obs_x[:, 1]
+        x[2, self.obs_pt, self.obs_cam] = 1.0
+        vis = np.zeros((self.n, self.m), order="F")
+        vis[self.obs_pt, self.obs_cam] = 1.0
+        return x, vis
+
+
+def _perturb(rng, w, T, X, keep_first_rotation):
+    """demo_bundle_euclid.m:29-31: w + 1e-3 N, T + 1e-4 N, X(1:3) + 1e-3 N."""
+    w0 = w + rng.standard_normal(w.shape) * 1e-3
+    if keep_first_rotation:
+        w0[:, 0] = w[:, 0]       # camera 1 keeps w = 0 (App. A Q2, test_mview path)
+    T0 = T + rng.standard_normal(T.shape) * 1e-4
+    X0 = X.copy()
+    X0[:3] += rng.standard_normal(X[:3].shape) * 1e-3
+    return w0, T0, X0
+
+
+def _sort_point_major(pt, cam, x):
+    order = np.lexsort((cam, pt))
+    return (pt[order].astype(np.int32), cam[order].astype(np.int32),
+            np.ascontiguousarray(x[order]))
+
+
+def mview_scene(m=10, min_n=100, max_n=200, depth=100.0, noise=0.5, seed=1,
+                keep_first_rotation=True):
+    """Seeded restatement of generate_scene_and_motion.m:36-117 (+ noise as
+    test_mview.m:45, perturbation as demo_bundle_euclid.m:29-31)."""
+    rng = np.random.default_rng(seed)
+    width = height = 500.0
+    f, cx, cy = width, width / 2, height / 2
+    K = np.tile(np.array([[f], [f], [cx], [cy]]), (1, m))
+    w = np.zeros((3, m))
+    T = np.zeros((3, m))
+    vw, vT = np.zeros(3), np.zeros(3)
+    for j in range(1, m):
+        vw = vw + 1e-2 * rng.standard_normal(3)
+        vT = vT + 1e-0 * rng.standard_normal(3)
+        w[:, j] = w[:, j - 1] + vw
+        T[:, j] = T[:, j - 1] + vT
+    R = rodrigues(w)
+    Kinv = np.linalg.inv(np.array([[f, 0, cx], [0, f, cy], [0, 0, 1.0]]))
+    Xs, xs = [], {}
+    vis = {}
+
+    def proj(j, i):
+        p = np.array([[f, 0, cx], [0, f, cy], [0, 0, 1.0]]) @ (R[j] @ Xs[i] + T[:, j])
+        return p
+
+    for j in range(m):
+        tracked = 0
+        for i in range(len(Xs)):                   # track previous features (:62-79)
+            if j > 0 and vis.get((i, j - 1), 0):
+                p = proj(j, i)
+                if p[2] > 0.01 * depth and 1 < p[0] / p[2] < width and 1 < p[1] / p[2] < height:
+                    tracked += 1
+                    xs[(i, j)] = p[:2] / p[2]
+                    vis[(i, j)] = 1
+        if tracked < min_n:                         # re-detect stored features (:81-97)
+            for i in range(len(Xs)):
+                if not vis.get((i, j), 0):
+                    p = proj(j, i)
+                    if (tracked < max_n and p[2] > 0.01 * depth and
+                            1 < p[0] / p[2] < width and 1 < p[1] / p[2] < height):
+                        tracked += 1
+                        xs[(i, j)] = p[:2] / p[2]
+                        vis[(i, j)] = 1
+        if tracked < min_n:                         # new features (:99-117)
+            n_new = max_n - tracked
+            xi = rng.random((2, n_new)) * np.array([[width], [height]])
+            d = (1 + 0.5 * rng.standard_normal(n_new)) * depth
+            for k in range(n_new):
+                if d[k] > 0:
+                    Xi = R[j].T @ (d[k] * Kinv @ np.array([xi[0, k], xi[1, k], 1.0]) - T[:, j])
+                    Xs.append(Xi)
+                    i = len(Xs) - 1
+                    xs[(i, j)] = xi[:, k].copy()
+                    vis[(i, j)] = 1
+    n = len(Xs)
+    X = np.vstack([np.array(Xs).T, np.ones((1, n))])
+    keys = sorted(vis.keys())
+    pt = np.array([k[0] for k in keys])
+    cam = np.array([k[1] for k in keys])
+    x = np.array([xs[k] for k in keys]) + rng.standard_normal((len(keys), 2)) * noise
+    pt, cam, x = _sort_point_major(pt, cam, x)
+    w0, T0, X0 = _perturb(rng, w, T, X, keep_first_rotation)
+    return Scene(K, T, w, X, pt, cam, x, T0, w0, X0)
+
+
+def banded_scene(m=50, n=10_000, track=6, depth=(80.0, 120.0), noise=0.5, seed=2,
+                 keep_first_rotation=False):
+    """Configs 2-4: point i is seen by ``track`` consecutive
+    cameras starting at a uniform camera; N = track * n observations."""
+    rng = np.random.default_rng(seed)
+    track = min(track, m)
+    width = height = 500.0
+    f, cx, cy = width, width / 2, height / 2
+    K = np.tile(np.array([[f], [f], [cx], [cy]]), (1, m))
+    w = np.zeros((3, m))
+    T = np.zeros((3, m))
+    vw, vT = np.zeros(3), np.zeros(3)
+    for j in range(1, m):                            # damped random walk
+        vw = 0.8 * vw + 2e-3 * rng.standard_normal(3)
+        vT = 0.8 * vT + 2e-1 * rng.standard_normal(3)
+        w[:, j] = w[:, j - 1] + vw
+        T[:, j] = T[:, j - 1] + vT
+    R = rodrigues(w)
+    start = rng.integers(0, m - track + 1, size=n)
+    # place each point in front of its first camera, then check all cameras
+    uv = rng.random((n, 2)) * np.array([width, height])
+    d = rng.uniform(depth[0], depth[1], size=n)
+    ray = np.stack([(uv[:, 0] - cx) / f, (uv[:, 1] - cy) / f, np.ones(n)], 1) * d[:, None]
+    Xw = np.einsum("kji,kj->ki", R[start], ray - T[:, start].T)   # R^T (ray - T)
+    X = np.vstack([Xw.T, np.ones((1, n))])
+    pt = np.repeat(np.arange(n), track)
+    cam = (start[:, None] + np.arange(track)[None, :]).reshape(-1)
+    x, z = project(K, w, T, X, cam, pt)
+    assert np.all(z > 0.01 * depth[0]), "synthetic point behind a camera"
+    x = x + rng.standard_normal(x.shape) * noise
+    pt, cam, x = _sort_point_major(pt, cam, x)
+    w0, T0, X0 = _perturb(rng, w, T, X, keep_first_rotation)
+    return Scene(K, T, w, X, pt, cam, x, T0, w0, X0)
+
+
+CONFIGS = {
+    # name: (factory, kwargs)   -- BASELINE.json "configs"
+    "cfg1": (mview_scene, dict(m=10, min_n=100, max_n=200, depth=100.0, seed=1)),
+    "cfg2": (banded_scene, dict(m=50, n=10_000, track=6, seed=2)),
+    "cfg3": (banded_scene, dict(m=1000, n=500_000, track=6, seed=3)),
+    "cfg5": (mview_scene, dict(m=50, min_n=100, max_n=200, depth=100.0, seed=5)),
+}
+
+
+def make_config(name, **over):
+    fn, kw = CONFIGS[name]
+    kw = dict(kw, **over)
+    return fn(**kw)

@@ -1,0 +1,148 @@
+/*
+ * vlgba.h -- C ABI of libvlgba, the MI355X (gfx950) Euclidean bundle adjuster.
+ *
+ * Drop-in for the Levenberg-Marquardt path of caomw/BundleAdjustmentMatlab
+ * (VLG toolbox/bundle).  Plain C: pointers and sizes only, no C++ / torch /
+ * HIP types.  All arrays are fp64 column major in the reference's MATLAB
+ * layouts unless stated otherwise; indices are 0-based int32.
+ *
+ * Return codes: 0 on success; VLGBA_E_* (< 0) for argument errors; a
+ * negative hipError_t (-1 .. -999) for device failures.
+ *
+ * Threading: a vlgba_ctx is single-threaded (one HIP stream per context);
+ * distinct contexts may be used from distinct threads.
+ */
+#ifndef VLGBA_H
+#define VLGBA_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VLGBA_E_ARG (-1001)      /* bad size / option                        */
+#define VLGBA_E_NUMA (-1002)     /* num_a not in {6, 7, 10}                  */
+#define VLGBA_E_ORDER (-1003)    /* observation list not point-major / dups  */
+#define VLGBA_E_NOMEM (-1004)    /* host allocation failed                    */
+#define VLGBA_E_COMM (-1005)     /* RCCL failure                              */
+
+/* ------------------------------------------------------------------------
+ * Problem: the reference's packed parameters and a COO observation list.
+ *   a      num_a x m   [w; T; (K)] per camera  (bundle_euclid.m:88-96)
+ *   b      3 x n       Xe(1:3,:)               (bundle_euclid.m:99)
+ *   obs    visible (point, camera) pairs of x(1:2,:,:) / 'visibility'
+ *          (bundle_euclid.m:50,71,102); any order, duplicates rejected.
+ * ------------------------------------------------------------------------ */
+typedef struct {
+    int m;                 /* cameras                                            */
+    int n;                 /* points                                             */
+    int num_a;             /* 6 fix_calibration, 7 fix_principal, 10 variable K  */
+    long long num_obs;     /* visible observations                               */
+    const int *obs_pt;     /* [num_obs] point index                              */
+    const int *obs_cam;    /* [num_obs] camera index                             */
+    const double *obs_x;   /* [2*num_obs] measured (u, v)                        */
+    const double *K;       /* [4*m] fx fy cx cy (mex_bundle_1_XABeUVWeAeB.c:186) */
+    double num_vis;        /* sum of the visibility values (bundle_euclid.m:82);
+                              <= 0 means num_obs                                 */
+} vlgba_problem;
+
+typedef struct {
+    int fix_structure;           /* bundle_euclid.m:58-59                      */
+    int fix_motion;              /* :60-61                                     */
+    const unsigned char *pivot;  /* [m] or NULL: 'fix_pivot', pivot (:62-65)   */
+    int verbose;                 /* 'verbose' (:73-74, printed to stdout)     */
+    int max_iter;                /* 0 -> 20  (:117)                            */
+    int max_iter2;               /* 0 -> 10  (:118)                            */
+    double lambda0;              /* 0 -> 1e-3 (:111)                           */
+    int device;                  /* HIP device ordinal                         */
+    /* point sharding over ranks (one process per GPU); world_size <= 1: none  */
+    int rank;
+    int world_size;
+    const void *comm_id;         /* 128-byte ncclUniqueId from rank 0, or NULL */
+} vlgba_options;
+
+typedef struct {
+    int iterations;        /* LM passes (accepted + rejected)                 */
+    int accepted;          /* accepted steps                                  */
+    int num_error;         /* entries written to error_out                    */
+    double lambda;         /* final damping                                   */
+    double seconds;        /* wall time of the solve (setup excluded)         */
+} vlgba_stats;
+
+/* One LM pass, for benchmarking / custom drivers. */
+typedef struct {
+    double old_sse;        /* e'e before the step (bundle_euclid.m:209)       */
+    double new_sse;        /* e_new'e_new (:210)                              */
+    double dpg;            /* dp'(lambda dp + g) (:217)                       */
+    double rho;
+    double lambda;         /* lambda used by this pass                        */
+    int accepted;
+    int chol_failed;       /* non-positive pivot in the reduced solve         */
+} vlgba_step_info;
+
+typedef struct vlgba_ctx vlgba_ctx;
+
+/* ---- fused solver: the whole bundle_euclid.m LM loop on the GPU -----------
+ * Replaces bundle_euclid.m:111-249 (and its three MEX calls :139,192,204).
+ * a (num_a*m) and b (3*n) are read as the start point and overwritten with
+ * the result.  error_out (>= max_iter+1 doubles, may be NULL) receives
+ * error_ (SSE / num_vis per accepted step, :219-231). */
+int vlgba_solve(const vlgba_problem *prob, const vlgba_options *opt, double *a, double *b,
+                double *error_out, vlgba_stats *stats);
+
+/* ---- handle API -------------------------------------------------------- */
+int vlgba_create(const vlgba_problem *prob, const vlgba_options *opt, vlgba_ctx **out);
+int vlgba_set_params(vlgba_ctx *ctx, const double *a, const double *b);
+int vlgba_get_params(vlgba_ctx *ctx, double *a, double *b);
+/* one LM pass at the context's lambda; relinearize != 0 forces stage 1 even
+ * when the previous pass was rejected (bench: every pass does full work).
+ * update_lm != 0 applies the accept/reject rule (:218-241) to the context. */
+int vlgba_step(vlgba_ctx *ctx, int relinearize, int update_lm, vlgba_step_info *info);
+int vlgba_run(vlgba_ctx *ctx, double *error_out, vlgba_stats *stats);
+int vlgba_sync(vlgba_ctx *ctx);
+void vlgba_destroy(vlgba_ctx *ctx);
+/* device-kernel timing of the last vlgba_step, milliseconds per phase:
+ * [0] linearize [1] camera reduce [2] damp/Y [3] schur [4] assemble
+ * [5] cholesky+solve [6] update; requires vlgba_set_timing(ctx, 1) first. */
+int vlgba_set_timing(vlgba_ctx *ctx, int on);
+int vlgba_phase_ms(vlgba_ctx *ctx, double *ms7);
+
+/* ---- stage entries with the reference MEX argument layouts ---------------
+ * Host pointers in, host pointers out; every output is fully written (zeros
+ * / X for invisible pairs, as the MEX files leave them).  vis is n x m
+ * (non-zero = visible, bundle_euclid.m:81). */
+
+/* [X_hat A B e U V W eA eB] = mex_bundle_1_XABeUVWeAeB(K, a, b, X, visible)
+ * replaces toolbox/bundle/mex_bundle_1_XABeUVWeAeB.c:72-337. */
+int vlgba_mex_bundle_1(int m, int n, int num_a, const double *K, const double *a,
+                       const double *b, const double *X, const double *vis,
+                       double *X_hat, double *A, double *B, double *e, double *U, double *V,
+                       double *W, double *eA, double *eB);
+
+/* [S e_] = mex_bundle_2_Se_(Y, W, U, eA, eB)
+ * replaces toolbox/bundle/mex_bundle_2_Se_.c:15-158.  The co-visibility
+ * pattern is taken from the non-zero W_ij / Y_ij blocks (exact: the
+ * reference adds exact zeros for the others). */
+int vlgba_mex_bundle_2(int m, int n, int num_a, const double *Y, const double *W,
+                       const double *U, const double *eA, const double *eB, double *S,
+                       double *e_);
+
+/* [db a_new b_new X_hat] = mex_bundle_3_db_new(W, da, eB, V_inv, K, a, b, X, visible)
+ * replaces toolbox/bundle/mex_bundle_3_db_new.c:170-328 (db uses da(1:6,j)
+ * only, as the reference does). */
+int vlgba_mex_bundle_3(int m, int n, int num_a, const double *W, const double *da,
+                       const double *eB, const double *Vinv, const double *K, const double *a,
+                       const double *b, const double *X, const double *vis, double *db,
+                       double *a_new, double *b_new, double *X_hat);
+
+/* Multi-GPU: rank 0 creates the 128-byte RCCL unique id, the caller
+ * broadcasts it (e.g. torch.distributed) and passes it as opt->comm_id. */
+int vlgba_get_unique_id(void *id128);
+
+/* Library / device info: writes a NUL-terminated string, returns its length. */
+int vlgba_version(char *buf, int len);
+int vlgba_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VLGBA_H */
