@@ -1,0 +1,117 @@
+"""The C-ABI library: builds, loads without a GPU, exports every symbol that
+include/vlgba.h declares, and the ctypes mirrors match the C struct layouts."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "vlgba.h")
+
+
+def declared_functions():
+    src = open(HDR).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(vlgba_\w+)\s*\(", src)))
+
+
+def test_library_loads_and_exports_all():
+    import bundleadjustmentmatlab_amd as pkg
+    L = pkg.lib()
+    names = declared_functions()
+    assert len(names) >= 15
+    for nm in names:
+        assert hasattr(L, nm), nm
+    from bundleadjustmentmatlab_amd._lib import SIGNATURES
+    assert sorted(SIGNATURES) == names          # the Python binding covers the header
+
+
+def test_version_and_device_count_without_gpu():
+    import bundleadjustmentmatlab_amd as pkg
+    L = pkg.lib()
+    buf = ctypes.create_string_buffer(128)
+    n = L.vlgba_version(buf, 128)
+    assert n > 0 and b"gfx950" in buf.value
+    assert L.vlgba_device_count() >= 0
+
+
+def test_bad_arguments_rejected_before_device_work():
+    import bundleadjustmentmatlab_amd as pkg
+    from bundleadjustmentmatlab_amd._lib import VlgbaProblem
+    L = pkg.lib()
+    h = ctypes.c_void_p()
+    assert L.vlgba_create(None, None, ctypes.byref(h)) == -1001
+    prob = VlgbaProblem(2, 3, 8, 0, None, None, None, None, 0.0)   # num_a = 8 invalid
+    import numpy as np
+    K = np.ones(8)
+    prob.K = K.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    assert L.vlgba_create(ctypes.byref(prob), None, ctypes.byref(h)) == -1002
+
+
+C_LAYOUT = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "vlgba.h"
+#define P(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
+int main(void) {
+  printf("vlgba_problem %zu\nvlgba_options %zu\nvlgba_stats %zu\nvlgba_step_info %zu\n",
+         sizeof(vlgba_problem), sizeof(vlgba_options), sizeof(vlgba_stats),
+         sizeof(vlgba_step_info));
+  P(vlgba_problem, num_obs) P(vlgba_problem, obs_x) P(vlgba_problem, num_vis)
+  P(vlgba_options, pivot) P(vlgba_options, lambda0) P(vlgba_options, comm_id)
+  P(vlgba_stats, lambda) P(vlgba_stats, seconds)
+  P(vlgba_step_info, accepted) P(vlgba_step_info, chol_failed)
+  return 0;
+}
+"""
+
+
+def test_struct_layouts_match_ctypes(tmp_path):
+    from bundleadjustmentmatlab_amd import _lib as B
+    src = tmp_path / "layout.c"
+    src.write_text(C_LAYOUT)
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), str(src), "-o",
+                    str(exe)], check=True)
+    out = dict(l.rsplit(" ", 1) for l in subprocess.check_output([str(exe)]).decode().split("\n")
+               if l)
+    assert int(out["vlgba_problem"]) == ctypes.sizeof(B.VlgbaProblem)
+    assert int(out["vlgba_options"]) == ctypes.sizeof(B.VlgbaOptions)
+    assert int(out["vlgba_stats"]) == ctypes.sizeof(B.VlgbaStats)
+    assert int(out["vlgba_step_info"]) == ctypes.sizeof(B.VlgbaStepInfo)
+    chk = {"vlgba_problem.num_obs": B.VlgbaProblem.num_obs.offset,
+           "vlgba_problem.obs_x": B.VlgbaProblem.obs_x.offset,
+           "vlgba_problem.num_vis": B.VlgbaProblem.num_vis.offset,
+           "vlgba_options.pivot": B.VlgbaOptions.pivot.offset,
+           "vlgba_options.lambda0": B.VlgbaOptions.lambda0.offset,
+           "vlgba_options.comm_id": B.VlgbaOptions.comm_id.offset,
+           "vlgba_stats.lambda": B.VlgbaStats.lambda_.offset,
+           "vlgba_stats.seconds": B.VlgbaStats.seconds.offset,
+           "vlgba_step_info.accepted": B.VlgbaStepInfo.accepted.offset,
+           "vlgba_step_info.chol_failed": B.VlgbaStepInfo.chol_failed.offset}
+    for k, v in chk.items():
+        assert int(out[k]) == v, k
+
+
+def test_header_compiles_as_c_and_cpp(tmp_path):
+    src = tmp_path / "inc.c"
+    src.write_text('#include "vlgba.h"\nint main(void){return 0;}\n')
+    for cc, ext in (("gcc", "c"), ("g++", "cpp")):
+        f = tmp_path / f"inc.{ext}"
+        f.write_text(src.read_text())
+        subprocess.run([cc, "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), "-c",
+                        str(f), "-o", str(tmp_path / f"inc_{ext}.o")], check=True)
+
+
+def test_product_does_not_touch_oracle():
+    """The shipped package never imports / loads anything under oracle/."""
+    pkg_dir = os.path.join(ROOT, "bundleadjustmentmatlab_amd")
+    for dirpath, _, files in os.walk(pkg_dir):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".h", "Makefile")):
+                txt = open(os.path.join(dirpath, f)).read()
+                for bad in ("bundle_euclid_ref", "ba_oracle", "nomex_numpy", "libba_oracle",
+                            "oracle/"):
+                    assert bad not in txt, (f, bad)
