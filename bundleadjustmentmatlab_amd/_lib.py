@@ -28,7 +28,8 @@ class VlgbaOptions(ctypes.Structure):
     _fields_ = [("fix_structure", c_int), ("fix_motion", c_int), ("pivot", c_up),
                 ("verbose", c_int), ("max_iter", c_int), ("max_iter2", c_int),
                 ("lambda0", c_double), ("device", c_int), ("rank", c_int),
-                ("world_size", c_int), ("comm_id", ctypes.c_void_p)]
+                ("world_size", c_int), ("comm_id", ctypes.c_void_p), ("dense_solve", c_int),
+                ("ordered", c_int)]
 
 
 class VlgbaStats(ctypes.Structure):

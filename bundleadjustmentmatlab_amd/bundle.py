@@ -111,7 +111,8 @@ class BundleAdjuster:
 
     def __init__(self, K, obs_pt, obs_cam, obs_x, n, num_a=6, *, fix_structure=False,
                  fix_motion=False, pivot=None, verbose=False, num_vis=0.0, device=0,
-                 rank=0, world_size=1, comm_id=None, max_iter=0, max_iter2=0, lambda0=0.0):
+                 rank=0, world_size=1, comm_id=None, max_iter=0, max_iter2=0, lambda0=0.0,
+                 dense_solve=False, ordered=False):
         L = lib()
         self.K = _F(K)
         self.m = self.K.shape[1]
@@ -135,7 +136,8 @@ class BundleAdjuster:
                            self._pivot.ctypes.data_as(c_up) if self._pivot is not None else None,
                            int(verbose), int(max_iter), int(max_iter2), float(lambda0),
                            int(device), int(rank), int(world_size),
-                           ctypes.cast(self._comm, ctypes.c_void_p) if self._comm else None)
+                           ctypes.cast(self._comm, ctypes.c_void_p) if self._comm else None,
+                           int(dense_solve), int(ordered))
         h = ctypes.c_void_p()
         check(L.vlgba_create(ctypes.byref(prob), ctypes.byref(opt), ctypes.byref(h)),
               "vlgba_create")

@@ -1,42 +1,74 @@
 // ba_chol.hip -- dense reduced-camera solve on gfx950: blocked right-looking
-// Cholesky with fp64 MFMA (v_mfma_f64_16x16x4_f64) + triangular solves.
+// tile Cholesky with fp64 MFMA (v_mfma_f64_16x16x4_f64) + triangular solves.
 //
 // Replaces da = pinv(S) * e_ (toolbox/bundle/bundle_euclid.m:193).  S is
 // symmetric positive definite once its exactly-zero rows (fixed parameters,
-// App. A Q2/Q8) have been replaced by identity rows in k_fix_zero_rows, and on
-// that matrix pinv and the Cholesky solve agree to conditioning-limited
-// rounding.  A non-positive pivot sets *status (the host then treats the step
-// like a rejected one).
+// App. A Q2/Q8) are given a unit diagonal (k_fix_diag), and on that matrix
+// pinv and the Cholesky solve agree to conditioning-limited rounding.  A
+// non-positive pivot sets *status (the host treats the step as rejected).
 //
-// Storage: S column major, leading dimension lds (a multiple of NB = 64),
-// lower triangle used.  Per tile column k:
-//   k_potrf_tile : factor L_kk in LDS, form L_kk^-1 (kept per k for the
-//                  backward solve), y_k = L_kk^-1 r_k  (forward solve folded in)
-//   k_panel      : L_ik = A_ik L_kk^-T as an MFMA GEMM against L_kk^-1, then
-//                  r_i -= L_ik y_k
-//   k_syrk       : A_ij -= L_ik L_jk^T for k < j <= i (MFMA), the bulk
+// Storage: S column major, leading dimension lds (multiple of NB = 64), lower
+// triangle.  Tile envelope: tile row i of S (hence of L: the profile is
+// preserved by Cholesky) is zero left of tile column tfirst[i]; every kernel
+// below visits only tiles inside the envelope, which is exact (the skipped
+// tiles are zero and stay zero).  dense_solve = 1 visits every lower tile.
+//
+// Per tile column k (two launches):
+//   k_factor_panel : WG 0 factors L_kk in registers (one wave), forms
+//                    L_kk^-1 and y_k = L_kk^-1 r_k (forward solve folded in);
+//                    WG b >= 1 redoes that factorisation in LDS and computes
+//                    panel tile L_ik = A_ik L_kk^-T (MFMA), r_i -= L_ik y_k
+//   k_syrk         : A_ij -= L_ik L_jk^T for envelope pairs k < j <= i (MFMA)
 // then per k descending k_backward: x_k = L_kk^-T z_k, z_j -= L_kj^T x_k.
 #include "ba_internal.h"
 
+#include <vector>
+
 #define NB 64
-#define LP 66  // LDS row pitch in doubles: lanes r and r+1 / t and t+1 of a
-               // 16x4 MFMA operand read land on distinct ds_read_b64 banks
+#define LP 66  // LDS row pitch (doubles): conflict-free 16x4 MFMA operand reads
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-// load tile (ti, tj) of S (column major) into LDS row-major T[r][c]
+// S tile (ti, tj) -> LDS row-major T[r][c] (256 threads).  Thread (r = tid&63,
+// c0 = tid>>6) moves column c0 + 4u, u = 0..15: each wave reads whole 512-B
+// columns (coalesced) and all 16 loads are in flight before the LDS writes.
 __device__ __forceinline__ void load_tile(const double *__restrict__ S, long long lds, int ti,
                                           int tj, double *T)
 {
     const double *base = S + (long long)NB * ti + lds * (long long)NB * tj;
-    for (int q = threadIdx.x; q < NB * NB; q += blockDim.x) {
-        const int r = q & (NB - 1), c = q >> 6;
-        T[r * LP + c] = base[r + lds * c];
-    }
+    const int r = threadIdx.x & 63, c0 = threadIdx.x >> 6;
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) v[u] = base[r + lds * (c0 + 4 * u)];
+#pragma unroll
+    for (int u = 0; u < 16; u++) T[r * LP + c0 + 4 * u] = v[u];
 }
 
-// acc(64x64 per workgroup of 256) = As[r][:] . Bs[c][:]  (both row-major, K = 64)
-// wave w owns rows 32*(w>>1) .. +31 and cols 32*(w&1) .. +31 as 2x2 MFMA tiles.
+// row-major 64x64 (src[r*64 + c]) -> LDS T[r][c], loads batched as above
+__device__ __forceinline__ void load_rowmajor(const double *__restrict__ src, double *T)
+{
+    const int c = threadIdx.x & 63, r0 = threadIdx.x >> 6;
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) v[u] = src[(r0 + 4 * u) * NB + c];
+#pragma unroll
+    for (int u = 0; u < 16; u++) T[(r0 + 4 * u) * LP + c] = v[u];
+}
+
+__device__ __forceinline__ void store_tile(double *__restrict__ S, long long lds, int ti, int tj,
+                                           const double *T)
+{
+    double *base = S + (long long)NB * ti + lds * (long long)NB * tj;
+    const int r = threadIdx.x & 63, c0 = threadIdx.x >> 6;
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) v[u] = T[r * LP + c0 + 4 * u];
+#pragma unroll
+    for (int u = 0; u < 16; u++) base[r + lds * (c0 + 4 * u)] = v[u];
+}
+
+// acc = As[r][:] . Bs[c][:] over K = 64 for the 64x64 tile of a 256-thread WG.
+// Wave w owns rows 32*(w>>1) .. +31, cols 32*(w&1) .. +31 as 2x2 MFMA tiles.
 // f64 16x16x4 operand map: A lane l -> A[l&15][l>>4], B lane l -> B[l>>4][l&15];
 // result register q of lane l -> (row (l>>4) + 4q, col l&15).
 __device__ __forceinline__ void mfma_64x64(const double *As, const double *Bs, d4 acc[2][2])
@@ -62,187 +94,312 @@ __device__ __forceinline__ void mfma_64x64(const double *As, const double *Bs, d
     }
 }
 
-// ---------------------------------------------------------------------------
-// diagonal tile: Cholesky in LDS, explicit inverse, forward-solve step
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_potrf_tile(double *__restrict__ S, long long lds, int k,
-                                                    double *__restrict__ linv,
-                                                    const double *__restrict__ rhs,
-                                                    double *__restrict__ y,
-                                                    double *__restrict__ status)
+// write acc (scale * acc + (add ? T : 0)) into LDS tile T in MFMA layout
+__device__ __forceinline__ void acc_to_lds(const d4 acc[2][2], double *T, double scale, bool add)
 {
-    __shared__ double A[NB * LP];
-    __shared__ double Li[NB * LP];
-    __shared__ double piv;
-    const int tid = threadIdx.x;
-    load_tile(S, lds, k, k, A);
-    __syncthreads();
-    for (int c = 0; c < NB; c++) {
-        if (tid == 0) {
-            double d = A[c * LP + c];
-            if (!(d > 0.0)) {
-                status[0] = 1.0;
-                d = 1.0;
-            }
-            piv = sqrt(d);
-            A[c * LP + c] = piv;
-        }
-        __syncthreads();
-        const double p = piv;
-        if (tid > c && tid < NB) A[tid * LP + c] = A[tid * LP + c] / p;
-        __syncthreads();
-        // trailing update of the tile's lower triangle
-        const int rem = NB - 1 - c;
-        for (int q = tid; q < rem * rem; q += blockDim.x) {
-            const int r = c + 1 + q / rem, cc = c + 1 + q % rem;
-            if (cc <= r) A[r * LP + cc] -= A[r * LP + c] * A[cc * LP + c];
-        }
-        __syncthreads();
-    }
-    // write L_kk (lower) back; zero the strict upper part of the tile
-    {
-        double *base = S + (long long)NB * k + lds * (long long)NB * k;
-        for (int q = tid; q < NB * NB; q += blockDim.x) {
-            const int r = q & (NB - 1), c = q >> 6;
-            base[r + lds * c] = (r >= c) ? A[r * LP + c] : 0.0;
-        }
-    }
-    // Li = L^-1 (lower): thread c solves L x = e_c by forward substitution
-    if (tid < NB) {
-        const int c = tid;
-        for (int r = 0; r < c; r++) Li[r * LP + c] = 0.0;
-        Li[c * LP + c] = 1.0 / A[c * LP + c];
-        for (int r = c + 1; r < NB; r++) {
-            double s = 0.0;
-            for (int q = c; q < r; q++) s += A[r * LP + q] * Li[q * LP + c];
-            Li[r * LP + c] = -s / A[r * LP + r];
-        }
-    }
-    __syncthreads();
-    double *lo = linv + (long long)NB * NB * k;
-    for (int q = tid; q < NB * NB; q += blockDim.x) {
-        const int r = q >> 6, c = q & (NB - 1);
-        lo[q] = Li[r * LP + c];  // row-major L^-1
-    }
-    // y_k = L_kk^-1 r_k
-    if (tid < NB) {
-        double s = 0.0;
-        for (int q = 0; q <= tid; q++) s += Li[tid * LP + q] * rhs[(long long)NB * k + q];
-        y[(long long)NB * k + tid] = s;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// panel: L_ik = A_ik L_kk^-T, r_i -= L_ik y_k   (grid: i = k+1 .. nt-1)
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_panel(double *__restrict__ S, long long lds, int k,
-                                               const double *__restrict__ linv,
-                                               double *__restrict__ rhs,
-                                               const double *__restrict__ y)
-{
-    extern __shared__ __attribute__((aligned(16))) double sm[];
-    double *As = sm, *Bs = sm + NB * LP;
-    const int i = k + 1 + blockIdx.x;
-    const int tid = threadIdx.x;
-    load_tile(S, lds, i, k, As);
-    const double *lo = linv + (long long)NB * NB * k;
-    for (int q = tid; q < NB * NB; q += blockDim.x) Bs[(q >> 6) * LP + (q & 63)] = lo[q];
-    __syncthreads();
-    d4 acc[2][2];
-    mfma_64x64(As, Bs, acc);
-    __syncthreads();
-    const int lane = tid & 63, w = tid >> 6;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r0 = 32 * (w >> 1), c0 = 32 * (w & 1);
-    double *base = S + (long long)NB * i + lds * (long long)NB * k;
 #pragma unroll
     for (int x = 0; x < 2; x++)
 #pragma unroll
-        for (int yy = 0; yy < 2; yy++)
+        for (int y = 0; y < 2; y++)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const int r = r0 + 16 * x + (lane >> 4) + 4 * q, c = c0 + 16 * yy + (lane & 15);
-                As[r * LP + c] = acc[x][yy][q];
-                base[r + lds * c] = acc[x][yy][q];
+                const int r = r0 + 16 * x + (lane >> 4) + 4 * q, c = c0 + 16 * y + (lane & 15);
+                const double v = scale * acc[x][y][q];
+                T[r * LP + c] = add ? T[r * LP + c] + v : v;
             }
+}
+
+// The whole 256-thread workgroup factors the 64x64 SPD tile in As (row-major,
+// lower used) and inverts the factor in the same right-looking sweep:
+// thread (r = tid & 63, g = tid >> 6) keeps row r, columns 16g .. 16g+15 of A
+// and of X (X starts as I; solving L X = I row by row gives X = L^-1).
+// Column c of L and row c of X are broadcast through LDS (double-buffered by
+// the parity of c: two barriers per column).  Writes L (zero upper) to As and
+// L^-1 to Li (both row-major).  Returns false on a non-positive pivot.
+__device__ bool block_potrf_inv(double *As, double *Li)
+{
+    __shared__ double colL[2][NB];
+    __shared__ double rowX[2][NB];
+    __shared__ double rpiv[2];
+    __shared__ int bad;
+    const int tid = threadIdx.x, r = tid & 63, g = tid >> 6;
+    double a[16], x[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; jj++) {
+        a[jj] = As[r * LP + 16 * g + jj];
+        x[jj] = (r == 16 * g + jj) ? 1.0 : 0.0;
+    }
+    if (tid == 0) bad = 0;
     __syncthreads();
+    for (int gc = 0; gc < 4; gc++)
+#pragma unroll
+    for (int jc = 0; jc < 16; jc++) {
+        const int c = 16 * gc + jc, b = jc & 1;
+        if (g == gc && r == c) {
+            double d = a[jc];
+            if (!(d > 0.0)) {
+                bad = 1;
+                d = 1.0;
+            }
+            a[jc] = sqrt(d);
+            colL[b][c] = a[jc];
+            rpiv[b] = 1.0 / a[jc];     // one division per column; scale by it
+        }
+        __syncthreads();
+        const double rp = rpiv[b];
+        if (g == gc && r > c) {
+            a[jc] = a[jc] * rp;
+            colL[b][r] = a[jc];
+        }
+        if (r == c) {
+#pragma unroll
+            for (int jj = 0; jj < 16; jj++) {
+                x[jj] = x[jj] * rp;
+                rowX[b][16 * g + jj] = x[jj];
+            }
+        }
+        __syncthreads();
+        if (r > c) {
+            const double lrc = colL[b][r];
+#pragma unroll
+            for (int jj = 0; jj < 16; jj++) {
+                const int q = 16 * g + jj;
+                if (q > c && q <= r) a[jj] = fma(-lrc, colL[b][q], a[jj]);
+                x[jj] = fma(-lrc, rowX[b][q], x[jj]);
+            }
+        }
+    }
+#pragma unroll
+    for (int jj = 0; jj < 16; jj++) {
+        const int q = 16 * g + jj;
+        As[r * LP + q] = (q <= r) ? a[jj] : 0.0;
+        Li[r * LP + q] = x[jj];
+    }
+    __syncthreads();
+    return bad == 0;
+}
+
+// ---------------------------------------------------------------------------
+// factor + panel for tile column k.  blockIdx 0: diagonal; b >= 1: panel tile
+// pan[b-1].
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_factor_panel(double *__restrict__ S, long long lds,
+                                                      int k, const int *__restrict__ pan,
+                                                      double *__restrict__ linv,
+                                                      double *__restrict__ rhs,
+                                                      double *__restrict__ y,
+                                                      double *__restrict__ status)
+{
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double *As = sm, *Bs = sm + NB * LP;
+    __shared__ double yk[NB], rk[NB];
+    const int tid = threadIdx.x;
+    load_tile(S, lds, k, k, As);
+    if (tid < NB) rk[tid] = rhs[(long long)NB * k + tid];
+    __syncthreads();
+    const bool ok = block_potrf_inv(As, Bs);
+    // y_k = L^-1 r_k
     if (tid < NB) {
         double s = 0.0;
-        for (int c = 0; c < NB; c++) s += As[tid * LP + c] * y[(long long)NB * k + c];
+        for (int q = 0; q <= tid; q++) s += Bs[tid * LP + q] * rk[q];
+        yk[tid] = s;
+    }
+    if (blockIdx.x == 0) {
+        store_tile(S, lds, k, k, As);
+        double *lo = linv + (long long)NB * NB * k;
+        for (int q = tid; q < NB * NB; q += blockDim.x) lo[q] = Bs[(q >> 6) * LP + (q & 63)];
+        __syncthreads();
+        if (tid < NB) y[(long long)NB * k + tid] = yk[tid];
+        if (tid == 0 && !ok) status[0] = 1.0;
+        return;
+    }
+    const int i = pan[blockIdx.x - 1];
+    __syncthreads();
+    load_tile(S, lds, i, k, As);
+    __syncthreads();
+    d4 acc[2][2];
+    mfma_64x64(As, Bs, acc);   // L_ik[r][c] = sum_t A_ik[r][t] Li[c][t]
+    __syncthreads();
+    acc_to_lds(acc, As, 1.0, false);
+    __syncthreads();
+    store_tile(S, lds, i, k, As);
+    if (tid < NB) {
+        double s = 0.0;
+        for (int c = 0; c < NB; c++) s += As[tid * LP + c] * yk[c];
         rhs[(long long)NB * i + tid] -= s;
     }
 }
 
 // ---------------------------------------------------------------------------
-// trailing update A_ij -= L_ik L_jk^T, k < j <= i   (grid: lower tiles)
+// trailing update A_ij -= L_ik L_jk^T for pan pairs (jj <= ii)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_syrk(double *__restrict__ S, long long lds, int k, int nt)
+__global__ __launch_bounds__(256) void k_syrk(double *__restrict__ S, long long lds, int k,
+                                              const int *__restrict__ pan, int T)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double *As = sm, *Bs = sm + NB * LP;
-    // blockIdx.x -> (i, j) over the lower triangle of the (nt-k-1)^2 trailing tiles
-    const int T = nt - k - 1;
     int q = blockIdx.x, jj = 0;
-    while (q >= T - jj) { q -= T - jj; jj++; }
-    const int j = k + 1 + jj, i = j + q;
-    (void)T;
+    while (q >= T - jj) {
+        q -= T - jj;
+        jj++;
+    }
+    const int j = pan[jj], i = pan[jj + q];
     load_tile(S, lds, i, k, As);
     load_tile(S, lds, j, k, Bs);
     __syncthreads();
     d4 acc[2][2];
     mfma_64x64(As, Bs, acc);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int r0 = 32 * (w >> 1), c0 = 32 * (w & 1);
-    double *base = S + (long long)NB * i + lds * (long long)NB * j;
-#pragma unroll
-    for (int x = 0; x < 2; x++)
-#pragma unroll
-        for (int yy = 0; yy < 2; yy++)
-#pragma unroll
-            for (int qq = 0; qq < 4; qq++) {
-                const int r = r0 + 16 * x + (lane >> 4) + 4 * qq, c = c0 + 16 * yy + (lane & 15);
-                base[r + lds * c] -= acc[x][yy][qq];
-            }
+    __syncthreads();
+    load_tile(S, lds, i, j, As);
+    __syncthreads();
+    acc_to_lds(acc, As, -1.0, true);
+    __syncthreads();
+    store_tile(S, lds, i, j, As);
 }
 
 // ---------------------------------------------------------------------------
-// backward solve step k: x_k = L_kk^-T z_k; z_j -= L_kj^T x_k (grid j = 0..k)
+// backward solve step k: x_k = L_kk^-T z_k; z_j -= L_kj^T x_k, j in [j0, k)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_backward(const double *__restrict__ S, long long lds,
-                                                  int k, const double *__restrict__ linv,
+                                                  int k, int j0,
+                                                  const double *__restrict__ linv,
                                                   double *__restrict__ z, double *__restrict__ x)
 {
-    __shared__ double xs[NB];
+    __shared__ double xs[NB], zk[NB];
     __shared__ double part[4][NB];
-    const int j = blockIdx.x, tid = threadIdx.x;
+    __shared__ double Lt[NB * LP];
+    const int j = j0 + blockIdx.x, tid = threadIdx.x;
     const double *lo = linv + (long long)NB * NB * k;  // row-major L^-1
-    if (tid < NB) {
+    load_rowmajor(lo, Lt);
+    if (tid < NB) zk[tid] = z[(long long)NB * k + tid];
+    __syncthreads();
+    {   // x_k[c] = sum_{r >= c} Li[r][c] z_k[r]: thread (c, quarter)
+        const int c = tid & 63, qr = tid >> 6;
         double s = 0.0;
-        for (int r = tid; r < NB; r++) s += lo[r * NB + tid] * z[(long long)NB * k + r];
-        xs[tid] = s;
+        for (int r = 16 * qr; r < 16 * qr + 16; r++)
+            if (r >= c) s += Lt[r * LP + c] * zk[r];
+        part[qr][c] = s;
     }
+    __syncthreads();
+    if (tid < NB) xs[tid] = ((part[0][tid] + part[1][tid]) + part[2][tid]) + part[3][tid];
     __syncthreads();
     if (j == k) {
         if (tid < NB) x[(long long)NB * k + tid] = xs[tid];
         return;
     }
-    // z_j[c] -= sum_r L_kj[r][c] x_k[r]; 4 partial sums over row quarters
+    // z_j[c] -= sum_r L_kj[r][c] x_k[r]: stage L_kj (coalesced), thread (c, quarter)
+    load_tile(S, lds, k, j, Lt);
+    __syncthreads();
     const int c = tid & 63, qr = tid >> 6;
-    const double *base = S + (long long)NB * k + lds * (long long)NB * j;
     double s = 0.0;
-    for (int r = 16 * qr; r < 16 * qr + 16; r++) s += base[r + lds * c] * xs[r];
+#pragma unroll
+    for (int r = 16 * qr; r < 16 * qr + 16; r++) s += Lt[r * LP + c] * xs[r];
     part[qr][c] = s;
     __syncthreads();
     if (tid < NB)
         z[(long long)NB * j + tid] -= ((part[0][tid] + part[1][tid]) + part[2][tid]) + part[3][tid];
 }
 
-int ba_chol_solve(ba_dev *d)
+// zero every envelope tile of S (fill from the previous factorisation)
+__global__ void k_zero_env(double *__restrict__ S, long long lds, const int *__restrict__ env)
+{
+    const int i = env[2 * blockIdx.x], k = env[2 * blockIdx.x + 1];
+    double *base = S + (long long)NB * i + lds * (long long)NB * k;
+    for (int q = threadIdx.x; q < NB * NB; q += blockDim.x) {
+        const int r = q & (NB - 1), c = q >> 6;
+        base[r + lds * c] = 0.0;
+    }
+}
+
+// pinv semantics for exactly-zero rows (App. A Q2, Q8): such a row/column of
+// S is exactly zero (its A columns are zero, hence its W and Y rows); give it
+// a unit diagonal and a zero right-hand side so da = 0 there.
+__global__ void k_fix_diag(double *__restrict__ S, double *__restrict__ rhs, long long lds)
+{
+    const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= lds) return;
+    double *d = S + r + lds * r;
+    if (*d == 0.0) {
+        *d = 1.0;
+        rhs[r] = 0.0;
+    }
+}
+
+// ===========================================================================
+int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
 {
     const int nt = (int)(d->lds / NB);
+    d->nt = nt;
+    d->h_tfirst = new int[nt];
+    for (int i = 0; i < nt; i++) d->h_tfirst[i] = d->dense_solve ? 0 : i;
+    if (!d->dense_solve)
+        for (int b = 0; b < nb; b++) {
+            const int j = blk_jk[2 * b], k = blk_jk[2 * b + 1];   // j >= k
+            const long long r0 = (long long)d->na * j, c0 = (long long)d->na * k;
+            for (long long r = r0; r < r0 + d->na; r++) {
+                const int ti = (int)(r / NB);
+                const int tk = (int)(c0 / NB);
+                if (tk < d->h_tfirst[ti]) d->h_tfirst[ti] = tk;
+            }
+        }
+    std::vector<int> ptr(nt + 1, 0), list, env;
+    for (int k = 0; k < nt; k++) {
+        for (int i = k + 1; i < nt; i++)
+            if (d->h_tfirst[i] <= k) list.push_back(i);
+        ptr[k + 1] = (int)list.size();
+    }
+    for (int k = 0; k < nt; k++)
+        for (int i = k; i < nt; i++)
+            if (d->h_tfirst[i] <= k) {
+                env.push_back(i);
+                env.push_back(k);
+            }
+    d->n_env = (int)env.size() / 2;
+    d->pan_ptr_h = new int[nt + 1];
+    for (int k = 0; k <= nt; k++) d->pan_ptr_h[k] = ptr[k];
+    VLGBA_CHECK(hipMalloc(&d->pan_list, sizeof(int) * (list.size() + 1)));
+    VLGBA_CHECK(hipMalloc(&d->env_tiles, sizeof(int) * (env.size() + 1)));
+    if (!list.empty())
+        VLGBA_CHECK(hipMemcpyAsync(d->pan_list, list.data(), sizeof(int) * list.size(),
+                                   hipMemcpyHostToDevice, d->stream));
+    VLGBA_CHECK(hipMemcpyAsync(d->env_tiles, env.data(), sizeof(int) * env.size(),
+                               hipMemcpyHostToDevice, d->stream));
+    VLGBA_CHECK(hipMemsetAsync(d->S, 0, sizeof(double) * d->lds * d->lds, d->stream));
+    VLGBA_CHECK(hipStreamSynchronize(d->stream));
+    return 0;
+}
+
+void ba_chol_free(ba_dev *d)
+{
+    delete[] d->h_tfirst;
+    delete[] d->pan_ptr_h;
+    if (d->pan_list) (void)hipFree(d->pan_list);
+    if (d->env_tiles) (void)hipFree(d->env_tiles);
+    d->h_tfirst = d->pan_ptr_h = nullptr;
+    d->pan_list = d->env_tiles = nullptr;
+}
+
+int ba_chol_prepare(ba_dev *d)
+{
+    k_zero_env<<<d->n_env, 256, 0, d->stream>>>(d->S, d->lds, d->env_tiles);
+    return -(int)hipGetLastError();
+}
+
+int ba_chol_fix_diag(ba_dev *d)
+{
+    k_fix_diag<<<(int)((d->lds + 255) / 256), 256, 0, d->stream>>>(d->S, d->rhs, d->lds);
+    return -(int)hipGetLastError();
+}
+
+int ba_chol_solve(ba_dev *d)
+{
+    const int nt = d->nt;
     const size_t smem = sizeof(double) * 2 * NB * LP;
     static bool attr_done = false;
     if (!attr_done) {
-        VLGBA_CHECK(hipFuncSetAttribute((const void *)k_panel,
+        VLGBA_CHECK(hipFuncSetAttribute((const void *)k_factor_panel,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
         VLGBA_CHECK(hipFuncSetAttribute((const void *)k_syrk,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
@@ -250,15 +407,18 @@ int ba_chol_solve(ba_dev *d)
     }
     VLGBA_CHECK(hipMemsetAsync(d->scal + 4, 0, sizeof(double), d->stream));
     for (int k = 0; k < nt; k++) {
-        k_potrf_tile<<<1, 256, 0, d->stream>>>(d->S, d->lds, k, d->linv, d->rhs, d->ywork,
-                                               d->scal + 4);
-        const int T = nt - k - 1;
-        if (T > 0) {
-            k_panel<<<T, 256, smem, d->stream>>>(d->S, d->lds, k, d->linv, d->rhs, d->ywork);
-            k_syrk<<<T * (T + 1) / 2, 256, smem, d->stream>>>(d->S, d->lds, k, nt);
-        }
+        const int p0 = d->pan_ptr_h[k], T = d->pan_ptr_h[k + 1] - p0;
+        k_factor_panel<<<1 + T, 256, smem, d->stream>>>(d->S, d->lds, k, d->pan_list + p0,
+                                                         d->linv, d->rhs, d->ywork,
+                                                         d->scal + 4);
+        if (T > 0)
+            k_syrk<<<T * (T + 1) / 2, 256, smem, d->stream>>>(d->S, d->lds, k, d->pan_list + p0,
+                                                              T);
     }
-    for (int k = nt - 1; k >= 0; k--)
-        k_backward<<<k + 1, 256, 0, d->stream>>>(d->S, d->lds, k, d->linv, d->ywork, d->da);
+    for (int k = nt - 1; k >= 0; k--) {
+        const int j0 = d->h_tfirst[k];
+        k_backward<<<k - j0 + 1, 256, 0, d->stream>>>(d->S, d->lds, k, j0, d->linv, d->ywork,
+                                                       d->da);
+    }
     return -(int)hipGetLastError();
 }

@@ -56,10 +56,38 @@ struct ba_dev {
     long long lds;     // ld rounded up to the Cholesky tile (padding rows = identity)
     double *linv;      // [lds/64][64*64] inverses of the diagonal Cholesky tiles
     double *ywork;     // [lds] forward-solve result
+    // tile envelope of the reduced system (64 x 64 tiles): tile row i of L is
+    // non-zero only in tile columns >= tfirst[i] (profile is preserved by the
+    // factorisation), so tiles left of it are never touched.
+    int nt;
+    int *h_tfirst;     // host [nt]
+    int *pan_ptr_h;    // host [nt+1]  offsets into pan_list (panel tiles of step k)
+    int *pan_list;     // device: tile rows i > k with tfirst[i] <= k, per k
+    int *env_tiles;    // device [n_env][2] (i, k) tiles inside the envelope
+    int n_env;
+    int dense_solve;   // 1: ignore the envelope (every lower tile, for measurement)
     // reductions: partial sums per block of the reducing kernels, in fixed order
     double *part;      // [3][PART_MAX]
     double *scal;      // [8] : 0 old_sse, 1 new_sse, 2 dpg, 3 chol_status ...
     int *chol_cnt;     // arrival counters for the triangular solves
+    // ---- fast (chunked) Schur path: points in chunks of <= CH_OBS observations;
+    // per chunk the co-visible blocks it touches ("slots") and the cameras it
+    // sees ("e-slots") get one partial each, reduced per block in chunk order.
+    int ordered;       // 1: sequential bit-exact kernels (k_damp_point + k_schur)
+    int nch;           // chunks
+    int *ch_pt;        // [nch+1] local point ranges
+    int *ch_slot;      // [nch+1] slot ranges (slots are numbered chunk-major)
+    int *ch_eslot;     // [nch+1] e-slot ranges
+    int *slot_blk;     // [ns] block id of each slot
+    int *slot_tptr;    // [ns+1] term ranges
+    unsigned short *slot_term;  // [nterm][2] chunk-local obs indices
+    int *eslot_optr;   // [nes+1]
+    unsigned short *eslot_obs;  // [neo] chunk-local obs indices
+    int *blk_sptr, *blk_slots;  // per block: its slots in chunk order
+    int *cam_eptr, *cam_eslots; // per camera: its e-slots in chunk order
+    double *spart;     // [ns][NA*NA]
+    double *epart;     // [nes][NA]
+    int ns, nes;
     // optional outputs / inputs of the MEX-compatible stage entries (else NULL)
     double *xh_out;    // [N][2] projections (stage 1 and stage 3)
     double *B_out;     // [N][6] point Jacobians (stage 1)
@@ -70,6 +98,8 @@ struct ba_dev {
 };
 
 #define BA_PART_MAX 65536
+#define BA_CH_OBS 128      // observations per Schur chunk (LDS budget)
+#define BA_CH_PTS 64       // points per Schur chunk
 
 // ---- ba_kernels.hip ----
 int ba_launch_rotations(ba_dev *d, const double *a, double *rot, int all5);
@@ -80,6 +110,17 @@ int ba_launch_schur(ba_dev *d, double lambda);
 int ba_launch_assemble(ba_dev *d);
 int ba_launch_update(ba_dev *d, double lambda);
 int ba_launch_yeb(ba_dev *d);
+int ba_launch_schur_fast(ba_dev *d, double lambda);   // fused damp + Vinv + Y + S + e_
 int ba_launch_assemble_plain(ba_dev *d, double *S, long long ld);
 // ---- ba_chol.hip ----
+int ba_chol_setup(ba_dev *d, const int *blk_jk_host, int nb);
+void ba_chol_free(ba_dev *d);
+int ba_chol_prepare(ba_dev *d);
+int ba_chol_fix_diag(ba_dev *d);
 int ba_chol_solve(ba_dev *d);
+
+#define TRY_RC(x)                                                                   \
+    do {                                                                            \
+        int rc__ = (x);                                                             \
+        if (rc__) return rc__;                                                      \
+    } while (0)

@@ -336,6 +336,133 @@ __global__ void k_schur(const int *__restrict__ blk_jk, const int *__restrict__ 
     }
 }
 
+// -------------------------------------------------------------------------
+// Fast path: one workgroup per chunk of consecutive points.  The chunk's W
+// rows are one contiguous HBM range (point-major storage): copied to LDS with
+// coalesced loads; per point V* -> V*^-1 (written out for the back
+// substitution); Y = W V*^-1 and t = Y eB formed in LDS (never stored); every
+// co-visible block the chunk touches accumulates sum_i Y_ij W_ik^T over the
+// chunk's points (ascending) into one partial, every camera sum_i Y_ij eB_i.
+// Same per-term expressions as k_damp_point / k_schur; only the grouping of
+// the sums over points differs (chunk partials, reduced in chunk order by
+// k_schur_reduce), so the result is deterministic run to run.
+// -------------------------------------------------------------------------
+template <int NA>
+__global__ __launch_bounds__(256) void k_schur_chunk(
+    const int *__restrict__ ch_pt, const int *__restrict__ ch_slot,
+    const int *__restrict__ ch_eslot, const int *__restrict__ slot_tptr,
+    const unsigned short *__restrict__ slot_term, const int *__restrict__ eslot_optr,
+    const unsigned short *__restrict__ eslot_obs, const int *__restrict__ pt_ptr,
+    const double *__restrict__ V, const double *__restrict__ eB, const double *__restrict__ W,
+    double lambda, double *__restrict__ Vinv, double *__restrict__ spart,
+    double *__restrict__ epart)
+{
+    constexpr int WS = 3 * NA;
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double *Wl = sm;                                // [CH_OBS][WS]
+    double *Yl = Wl + BA_CH_OBS * WS;               // [CH_OBS][WS]
+    double *tl = Yl + BA_CH_OBS * WS;               // [CH_OBS][NA]
+    double *Vl = tl + BA_CH_OBS * NA;               // [CH_PTS][9]
+    double *El = Vl + BA_CH_PTS * 9;                // [CH_PTS][3]
+    int *lpt = (int *)(El + BA_CH_PTS * 3);         // [CH_OBS]
+    const int ch = blockIdx.x, tid = threadIdx.x;
+    const int p0 = ch_pt[ch], p1 = ch_pt[ch + 1], np = p1 - p0;
+    const int obase = pt_ptr[p0], nobs = pt_ptr[p1] - obase;
+    // W rows: one contiguous range (coalesced 8-byte loads)
+    {
+        const double *src = W + (size_t)WS * obase;
+        const int nw = nobs * WS;
+        for (int q = tid; q < nw; q += 256) Wl[q] = src[q];
+    }
+    // per point: V* -> V*^-1, eB, local obs -> point map
+    if (tid < np) {
+        const int i = p0 + tid;
+        double vs[9], vi[9];
+#pragma unroll
+        for (int q = 0; q < 9; q++) vs[q] = V[9 * (size_t)i + q];
+#pragma unroll
+        for (int k = 0; k < 3; k++) vs[4 * k] = (1 + lambda) * vs[4 * k];
+        vlg_pinv3(vs, vi);
+#pragma unroll
+        for (int q = 0; q < 9; q++) {
+            Vl[9 * tid + q] = vi[q];
+            Vinv[9 * (size_t)i + q] = vi[q];
+        }
+#pragma unroll
+        for (int q = 0; q < 3; q++) El[3 * tid + q] = eB[3 * (size_t)i + q];
+        for (int o = pt_ptr[i]; o < pt_ptr[i + 1]; o++) lpt[o - obase] = tid;
+    }
+    __syncthreads();
+    // Y = W V*^-1 (bundle_euclid.m:182)
+    for (int q = tid; q < nobs * WS; q += 256) {
+        const int lo = q / WS, e = q % WS, r = e % NA, c = e / NA;
+        const double *w = Wl + WS * lo;
+        const double *vi = Vl + 9 * lpt[lo];
+        Yl[q] = w[r] * vi[3 * c] + w[r + NA] * vi[1 + 3 * c] + w[r + 2 * NA] * vi[2 + 3 * c];
+    }
+    __syncthreads();
+    // t = Y eB (mex_bundle_2_Se_.c:143-147)
+    for (int q = tid; q < nobs * NA; q += 256) {
+        const int lo = q / NA, r = q % NA;
+        const double *y = Yl + WS * lo;
+        const double *eb = El + 3 * lpt[lo];
+        tl[q] = y[r] * eb[0] + y[r + NA] * eb[1] + y[r + 2 * NA] * eb[2];
+    }
+    __syncthreads();
+    // block partials: sum over the chunk's terms (points ascending)
+    const int s0 = ch_slot[ch], ns = ch_slot[ch + 1] - s0;
+    for (int q = tid; q < ns * NA * NA; q += 256) {
+        const int s = s0 + q / (NA * NA), e = q % (NA * NA), r = e % NA, c = e / NA;
+        double acc = 0.0;
+        for (int u = slot_tptr[s]; u < slot_tptr[s + 1]; u++) {
+            const double *y = Yl + WS * slot_term[2 * u];
+            const double *w = Wl + WS * slot_term[2 * u + 1];
+            acc += y[r] * w[c] + y[r + NA] * w[c + NA] + y[r + 2 * NA] * w[c + 2 * NA];
+        }
+        spart[(size_t)NA * NA * s + e] = acc;
+    }
+    const int e0 = ch_eslot[ch], nes = ch_eslot[ch + 1] - e0;
+    for (int q = tid; q < nes * NA; q += 256) {
+        const int s = e0 + q / NA, r = q % NA;
+        double acc = 0.0;
+        for (int u = eslot_optr[s]; u < eslot_optr[s + 1]; u++) acc += tl[NA * eslot_obs[u] + r];
+        epart[(size_t)NA * s + r] = acc;
+    }
+}
+
+// S blocks and e_ from the chunk partials, in chunk order
+template <int NA>
+__global__ void k_schur_reduce(const int *__restrict__ blk_jk, const int *__restrict__ blk_sptr,
+                               const int *__restrict__ blk_slots,
+                               const int *__restrict__ cam_eptr,
+                               const int *__restrict__ cam_eslots,
+                               const double *__restrict__ spart,
+                               const double *__restrict__ epart, const double *__restrict__ U,
+                               const double *__restrict__ eA, int nb, double lambda, int owner,
+                               double *__restrict__ sblk, double *__restrict__ rhs)
+{
+    const int bk = blockIdx.x, l = threadIdx.x;
+    if (bk >= nb) return;
+    const int j = blk_jk[2 * bk], k = blk_jk[2 * bk + 1];
+    if (l < NA * NA) {
+        const int r = l % NA, c = l / NA;
+        double acc = 0.0;
+        if (j == k && owner) {
+            const double u = U[(size_t)NA * NA * j + r + NA * c];
+            acc = (r == c) ? (1 + lambda) * u : u;
+        }
+        for (int q = blk_sptr[bk]; q < blk_sptr[bk + 1]; q++)
+            acc -= spart[(size_t)NA * NA * blk_slots[q] + l];
+        sblk[(size_t)NA * NA * bk + l] = acc;
+    } else if (j == k && l < NA * NA + NA) {
+        const int r = l - NA * NA;
+        double acc = owner ? eA[(size_t)NA * j + r] : 0.0;
+        for (int q = cam_eptr[j]; q < cam_eptr[j + 1]; q++)
+            acc -= epart[(size_t)NA * cam_eslots[q] + r];
+        rhs[(size_t)NA * j + r] = acc;
+    }
+}
+
 // t_o = Y_o eB_i for given Y (stage-2 entry; k_damp_point forms it otherwise)
 template <int NA>
 __global__ void k_point_yeb(const int *__restrict__ pt_ptr, const double *__restrict__ Y,
@@ -358,29 +485,16 @@ __global__ void k_point_yeb(const int *__restrict__ pt_ptr, const double *__rest
 // -------------------------------------------------------------------------
 template <int NA>
 __global__ void k_assemble(const int *__restrict__ blk_jk, const double *__restrict__ sblk,
-                           int nb, long long lds, double *__restrict__ S)
+                           int nb, long long lds, int lower_only, double *__restrict__ S)
 {
     const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= (long long)nb * NA * NA) return;
     const int bk = (int)(g / (NA * NA)), l = (int)(g % (NA * NA));
     const int j = blk_jk[2 * bk], k = blk_jk[2 * bk + 1];
     const int r = l % NA, c = l / NA;
-    S[(long long)(NA * j + r) + lds * (long long)(NA * k + c)] = sblk[g];
-}
-
-// pinv semantics for exactly-zero rows (App. A Q2, Q8): a zero diagonal entry
-// of S marks a fixed parameter; make its row/column the identity, rhs 0.
-__global__ void k_fix_zero_rows(double *__restrict__ S, double *__restrict__ rhs, long long ld)
-{
-    const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= ld) return;
-    double *d = S + r + ld * r;
-    if (*d == 0.0) {
-        for (long long c = 0; c < r; c++) S[r + ld * c] = 0.0;
-        for (long long q = r + 1; q < ld; q++) S[q + ld * r] = 0.0;
-        *d = 1.0;
-        rhs[r] = 0.0;
-    }
+    const long long row = NA * j + r, col = NA * k + c;
+    if (lower_only && row < col) return;
+    S[row + lds * col] = sblk[g];
 }
 
 // -------------------------------------------------------------------------
@@ -555,6 +669,39 @@ int ba_launch_schur(ba_dev *d, double lambda)
     return -(int)hipGetLastError();
 }
 
+template <int NA>
+static int launch_schur_fast(ba_dev *d, double lambda)
+{
+    const size_t smem = sizeof(double) * (2 * BA_CH_OBS * 3 * NA + BA_CH_OBS * NA +
+                                          BA_CH_PTS * 12) +
+                        sizeof(int) * BA_CH_OBS;
+    static bool attr = false;
+    if (!attr) {
+        VLGBA_CHECK(hipFuncSetAttribute((const void *)k_schur_chunk<NA>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+        attr = true;
+    }
+    if (d->nch > 0)
+        k_schur_chunk<NA><<<d->nch, 256, smem, d->stream>>>(
+            d->ch_pt, d->ch_slot, d->ch_eslot, d->slot_tptr, d->slot_term, d->eslot_optr,
+            d->eslot_obs, d->pt_ptr, d->V, d->eB, d->W, lambda, d->Vinv, d->spart, d->epart);
+    const int bs = (NA * NA + NA) <= 64 ? 64 : 128;
+    k_schur_reduce<NA><<<d->nb, bs, 0, d->stream>>>(
+        d->blk_jk, d->blk_sptr, d->blk_slots, d->cam_eptr, d->cam_eslots, d->spart, d->epart,
+        d->U, d->eA, d->nb, lambda, d->schur_owner, d->sblk, d->rhs);
+    return -(int)hipGetLastError();
+}
+
+int ba_launch_schur_fast(ba_dev *d, double lambda)
+{
+    switch (d->na) {
+    case 6: return launch_schur_fast<6>(d, lambda);
+    case 7: return launch_schur_fast<7>(d, lambda);
+    case 10: return launch_schur_fast<10>(d, lambda);
+    default: return -1000;
+    }
+}
+
 int ba_launch_yeb(ba_dev *d)
 {
     const int g = grid_for(d->n, 256, 1 << 30);
@@ -565,14 +712,15 @@ int ba_launch_yeb(ba_dev *d)
 
 int ba_launch_assemble(ba_dev *d)
 {
-    VLGBA_CHECK(hipMemsetAsync(d->S, 0, sizeof(double) * d->lds * d->lds, d->stream));
-    VLGBA_CHECK(hipMemsetAsync(d->rhs + d->ld, 0, sizeof(double) * (d->lds - d->ld), d->stream));
+    TRY_RC(ba_chol_prepare(d));   // zero the envelope tiles (last factor's fill)
+    if (d->lds > d->ld)
+        VLGBA_CHECK(
+            hipMemsetAsync(d->rhs + d->ld, 0, sizeof(double) * (d->lds - d->ld), d->stream));
     const long long work = (long long)d->nb * d->na * d->na;
     const int g = (int)((work + 255) / 256);
     BA_DISPATCH(d->na, (k_assemble<NA><<<g, 256, 0, d->stream>>>(d->blk_jk, d->sblk, d->nb,
-                                                                   d->lds, d->S)));
-    k_fix_zero_rows<<<(int)((d->lds + 255) / 256), 256, 0, d->stream>>>(d->S, d->rhs, d->lds);
-    return -(int)hipGetLastError();
+                                                                   d->lds, 1, d->S)));
+    return ba_chol_fix_diag(d);
 }
 
 int ba_launch_update(ba_dev *d, double lambda)
@@ -600,6 +748,6 @@ int ba_launch_assemble_plain(ba_dev *d, double *S, long long ld)
     const int g = (int)((work + 255) / 256);
     if (g > 0)
         BA_DISPATCH(d->na, (k_assemble<NA><<<g, 256, 0, d->stream>>>(d->blk_jk, d->sblk, d->nb,
-                                                                       ld, S)));
+                                                                       ld, 0, S)));
     return -(int)hipGetLastError();
 }

@@ -107,42 +107,54 @@ int sort_obs(const vlgba_problem *p, host_obs &h)
 // rank agrees on the packed layout); terms only from observations [o0, o1).
 struct host_blocks {
     std::vector<int> jk, ptr, term;
-};
-
-void build_blocks(int m, const std::vector<int> &pt_ptr_all, const std::vector<int> &cam_all,
-                  int p0, int p1, long long obs_base, bool lower, bool all_diag, host_blocks &hb)
-{
-    const int n = (int)pt_ptr_all.size() - 1;
-    const bool dense_tab = (long long)m * m <= (1LL << 26);
-    std::vector<int> tab;
+    int m = 0;
+    bool dense_tab = true;
+    std::vector<int> tab;                                // m*m block ids (dense)
     std::vector<std::vector<std::pair<int, int>>> rows;  // sparse fallback: (k, id)
-    if (dense_tab) tab.assign((size_t)m * m, -1);
-    else rows.resize(m);
-    auto find = [&](int j, int k) -> int {
+    int find(int j, int k) const
+    {
         if (dense_tab) return tab[(size_t)j * m + k];
-        for (auto &pr : rows[j]) if (pr.first == k) return pr.second;
+        for (auto &pr : rows[j])
+            if (pr.first == k) return pr.second;
         return -1;
-    };
-    auto insert = [&](int j, int k) -> int {
+    }
+    int insert(int j, int k)
+    {
         int id = find(j, k);
         if (id >= 0) return id;
-        id = (int)hb.jk.size() / 2;
-        hb.jk.push_back(j);
-        hb.jk.push_back(k);
+        id = (int)jk.size() / 2;
+        jk.push_back(j);
+        jk.push_back(k);
         if (dense_tab) tab[(size_t)j * m + k] = id;
         else rows[j].push_back({k, id});
         return id;
-    };
+    }
+};
+
+void build_blocks(int m, const std::vector<int> &pt_ptr_all, const std::vector<int> &cam_all,
+                  int p0, int p1, long long obs_base, bool lower, bool all_diag, bool need_terms,
+                  host_blocks &hb)
+{
+    const int n = (int)pt_ptr_all.size() - 1;
+    hb.m = m;
+    hb.dense_tab = (long long)m * m <= (1LL << 26);
+    if (hb.dense_tab) hb.tab.assign((size_t)m * m, -1);
+    else hb.rows.resize(m);
+    auto find = [&](int j, int k) -> int { return hb.find(j, k); };
     if (all_diag)
-        for (int j = 0; j < m; j++) insert(j, j);
+        for (int j = 0; j < m; j++) hb.insert(j, j);
     for (int i = 0; i < n; i++)
         for (int a = pt_ptr_all[i]; a < pt_ptr_all[i + 1]; a++)
             for (int b = pt_ptr_all[i]; b < pt_ptr_all[i + 1]; b++) {
                 const int j = cam_all[a], k = cam_all[b];
                 if (lower && j < k) continue;
-                insert(j, k);
+                hb.insert(j, k);
             }
     const int nb = (int)hb.jk.size() / 2;
+    if (!need_terms) {
+        hb.ptr.assign(nb + 1, 0);
+        return;
+    }
     std::vector<long long> cnt(nb + 1, 0);
     for (int i = p0; i < p1; i++)
         for (int a = pt_ptr_all[i]; a < pt_ptr_all[i + 1]; a++)
@@ -165,6 +177,105 @@ void build_blocks(int m, const std::vector<int> &pt_ptr_all, const std::vector<i
                 hb.term[2 * s] = (int)(a - obs_base);
                 hb.term[2 * s + 1] = (int)(b - obs_base);
             }
+}
+
+// Chunk plan of the fast Schur path for the local points (pt_ptr local,
+// cam local observation cameras).  Returns false when a point has more than
+// BA_CH_OBS observations (the caller then uses the ordered kernels).
+struct host_plan {
+    std::vector<int> ch_pt, ch_slot, ch_eslot, slot_blk, slot_tptr, eslot_optr;
+    std::vector<unsigned short> slot_term, eslot_obs;
+    std::vector<int> blk_sptr, blk_slots, cam_eptr, cam_eslots;
+};
+
+bool build_plan(int m, const std::vector<int> &lptr, const std::vector<int> &lcam,
+                const host_blocks &hb, host_plan &P)
+{
+    const int n = (int)lptr.size() - 1;
+    const int nb = (int)hb.jk.size() / 2;
+    for (int i = 0; i < n; i++)
+        if (lptr[i + 1] - lptr[i] > BA_CH_OBS) return false;
+    std::vector<int> slot_of(nb, -1), eslot_of(m, -1), touched, tcam;
+    std::vector<std::vector<std::pair<int, int>>> terms;   // per local slot
+    std::vector<std::vector<int>> eobs;                     // per local e-slot
+    P.ch_pt.push_back(0);
+    P.ch_slot.push_back(0);
+    P.ch_eslot.push_back(0);
+    P.slot_tptr.push_back(0);
+    P.eslot_optr.push_back(0);
+    int p = 0;
+    while (p < n) {
+        const int obase = lptr[p];
+        int q = p;
+        while (q < n && q - p < BA_CH_PTS && lptr[q + 1] - obase <= BA_CH_OBS) q++;
+        touched.clear();
+        tcam.clear();
+        terms.clear();
+        eobs.clear();
+        for (int i = p; i < q; i++)
+            for (int a = lptr[i]; a < lptr[i + 1]; a++) {
+                const int j = lcam[a];
+                if (eslot_of[j] < 0) {
+                    eslot_of[j] = (int)tcam.size();
+                    tcam.push_back(j);
+                    eobs.emplace_back();
+                }
+                eobs[eslot_of[j]].push_back(a - obase);
+                for (int b = lptr[i]; b < lptr[i + 1]; b++) {
+                    const int k = lcam[b];
+                    if (j < k) continue;
+                    const int blk = hb.find(j, k);
+                    if (slot_of[blk] < 0) {
+                        slot_of[blk] = (int)touched.size();
+                        touched.push_back(blk);
+                        terms.emplace_back();
+                    }
+                    terms[slot_of[blk]].push_back({a - obase, b - obase});
+                }
+            }
+        for (size_t s = 0; s < touched.size(); s++) {
+            P.slot_blk.push_back(touched[s]);
+            for (auto &t : terms[s]) {
+                P.slot_term.push_back((unsigned short)t.first);
+                P.slot_term.push_back((unsigned short)t.second);
+            }
+            P.slot_tptr.push_back((int)P.slot_term.size() / 2);
+            slot_of[touched[s]] = -1;
+        }
+        for (size_t s = 0; s < tcam.size(); s++) {
+            for (int o : eobs[s]) P.eslot_obs.push_back((unsigned short)o);
+            P.eslot_optr.push_back((int)P.eslot_obs.size());
+            eslot_of[tcam[s]] = -1;
+        }
+        // cameras of the chunk, for the per-camera reduction below
+        for (size_t s = 0; s < tcam.size(); s++) P.cam_eslots.push_back(tcam[s]);
+        P.ch_pt.push_back(q);
+        P.ch_slot.push_back((int)P.slot_blk.size());
+        P.ch_eslot.push_back((int)P.eslot_optr.size() - 1);
+        p = q;
+    }
+    // per block: its slots in chunk order (counting sort keeps slot order)
+    const int ns = (int)P.slot_blk.size();
+    P.blk_sptr.assign(nb + 1, 0);
+    for (int s = 0; s < ns; s++) P.blk_sptr[P.slot_blk[s] + 1]++;
+    for (int b = 0; b < nb; b++) P.blk_sptr[b + 1] += P.blk_sptr[b];
+    P.blk_slots.resize(ns);
+    {
+        std::vector<int> pos(P.blk_sptr.begin(), P.blk_sptr.end() - 1);
+        for (int s = 0; s < ns; s++) P.blk_slots[pos[P.slot_blk[s]]++] = s;
+    }
+    // per camera: its e-slots in chunk order (cam_eslots currently = camera of e-slot)
+    const int nes = (int)P.eslot_optr.size() - 1;
+    std::vector<int> ecam(P.cam_eslots);
+    P.cam_eptr.assign(m + 1, 0);
+    for (int s = 0; s < nes; s++) P.cam_eptr[ecam[s] + 1]++;
+    for (int j = 0; j < m; j++) P.cam_eptr[j + 1] += P.cam_eptr[j];
+    P.cam_eslots.assign(nes, 0);
+    {
+        std::vector<int> pos(P.cam_eptr.begin(), P.cam_eptr.end() - 1);
+        for (int s = 0; s < nes; s++) P.cam_eslots[pos[ecam[s]]++] = s;
+    }
+    return true;
 }
 
 }  // namespace
@@ -196,6 +307,7 @@ static void ctx_free(vlgba_ctx *c)
     for (void *p : c->allocs) (void)hipFree(p);
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
+    ba_chol_free(&c->d);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->d.stream) (void)hipStreamDestroy(c->d.stream);
     delete c;
@@ -245,10 +357,16 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         std::vector<int> pos(cptr.begin(), cptr.end() - 1);
         for (int o = 0; o < d.N; o++) cobs[pos[lcam[o]]++] = o;
     }
+    bool fast = !d.ordered && !stage_mode;
+    for (int i = 0; fast && i < d.n; i++)
+        if (lptr[i + 1] - lptr[i] > BA_CH_OBS) fast = false;   // very long track
+    if (!fast) d.ordered = 1;
     host_blocks hb;
-    build_blocks(p->m, pt_ptr_all, h.cam, c->p0, c->p1, o0, lower_blocks, all_diag, hb);
+    build_blocks(p->m, pt_ptr_all, h.cam, c->p0, c->p1, o0, lower_blocks, all_diag, !fast, hb);
     d.nb = (int)hb.jk.size() / 2;
     d.T = (long long)hb.term.size() / 2;
+    host_plan plan;
+    if (fast) build_plan(p->m, lptr, lcam, hb, plan);
 
     TRY(ctx_alloc(c, &d.obs_cam, d.N));
     TRY(ctx_alloc(c, &d.pt_ptr, d.n + 1));
@@ -264,8 +382,41 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
     TRY(ctx_alloc(c, &d.rot_new, 9 * (size_t)p->m));
     TRY(ctx_alloc(c, &d.jrec, (size_t)d.js * d.N));
     TRY(ctx_alloc(c, &d.W, (size_t)3 * na * d.N));
-    TRY(ctx_alloc(c, &d.Y, (size_t)3 * na * d.N));
-    TRY(ctx_alloc(c, &d.t, (size_t)na * d.N));
+    if (!fast) {   // the fast path forms Y and t in LDS only
+        TRY(ctx_alloc(c, &d.Y, (size_t)3 * na * d.N));
+        TRY(ctx_alloc(c, &d.t, (size_t)na * d.N));
+    } else {
+        d.nch = (int)plan.ch_pt.size() - 1;
+        d.ns = (int)plan.slot_blk.size();
+        d.nes = (int)plan.eslot_optr.size() - 1;
+        TRY(ctx_alloc(c, &d.ch_pt, plan.ch_pt.size()));
+        TRY(ctx_alloc(c, &d.ch_slot, plan.ch_slot.size()));
+        TRY(ctx_alloc(c, &d.ch_eslot, plan.ch_eslot.size()));
+        TRY(ctx_alloc(c, &d.slot_blk, plan.slot_blk.size()));
+        TRY(ctx_alloc(c, &d.slot_tptr, plan.slot_tptr.size()));
+        TRY(ctx_alloc(c, &d.slot_term, plan.slot_term.size()));
+        TRY(ctx_alloc(c, &d.eslot_optr, plan.eslot_optr.size()));
+        TRY(ctx_alloc(c, &d.eslot_obs, plan.eslot_obs.size()));
+        TRY(ctx_alloc(c, &d.blk_sptr, plan.blk_sptr.size()));
+        TRY(ctx_alloc(c, &d.blk_slots, plan.blk_slots.size()));
+        TRY(ctx_alloc(c, &d.cam_eptr, plan.cam_eptr.size()));
+        TRY(ctx_alloc(c, &d.cam_eslots, plan.cam_eslots.size()));
+        TRY(ctx_alloc(c, &d.spart, (size_t)na * na * d.ns));
+        TRY(ctx_alloc(c, &d.epart, (size_t)na * d.nes));
+        TRY(upload(d.ch_pt, plan.ch_pt.data(), plan.ch_pt.size(), s));
+        TRY(upload(d.ch_slot, plan.ch_slot.data(), plan.ch_slot.size(), s));
+        TRY(upload(d.ch_eslot, plan.ch_eslot.data(), plan.ch_eslot.size(), s));
+        TRY(upload(d.slot_blk, plan.slot_blk.data(), plan.slot_blk.size(), s));
+        TRY(upload(d.slot_tptr, plan.slot_tptr.data(), plan.slot_tptr.size(), s));
+        TRY(upload(d.slot_term, plan.slot_term.data(), plan.slot_term.size(), s));
+        TRY(upload(d.eslot_optr, plan.eslot_optr.data(), plan.eslot_optr.size(), s));
+        TRY(upload(d.eslot_obs, plan.eslot_obs.data(), plan.eslot_obs.size(), s));
+        TRY(upload(d.blk_sptr, plan.blk_sptr.data(), plan.blk_sptr.size(), s));
+        TRY(upload(d.blk_slots, plan.blk_slots.data(), plan.blk_slots.size(), s));
+        TRY(upload(d.cam_eptr, plan.cam_eptr.data(), plan.cam_eptr.size(), s));
+        TRY(upload(d.cam_eslots, plan.cam_eslots.data(), plan.cam_eslots.size(), s));
+        VLGBA_CHECK(hipStreamSynchronize(s));   // plan vectors are local
+    }
     TRY(ctx_alloc(c, &d.U, (size_t)na * na * p->m + na * (size_t)p->m + 1));
     d.eA = d.U + (size_t)na * na * p->m;     // U | eA | old_sse contiguous: one all-reduce
     TRY(ctx_alloc(c, &d.V, 9 * (size_t)d.n));
@@ -282,6 +433,7 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         TRY(ctx_alloc(c, &d.linv, (size_t)(d.lds / 64) * 64 * 64));
         TRY(ctx_alloc(c, &d.ywork, (size_t)d.lds));
         TRY(ctx_alloc(c, &d.da, (size_t)d.lds));
+        TRY(ba_chol_setup(&d, hb.jk.data(), d.nb));
     } else {
         TRY(ctx_alloc(c, &d.da, (size_t)d.lds));
     }
@@ -363,6 +515,8 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
         c->max_iter2 = o->max_iter2 > 0 ? o->max_iter2 : 10;
         c->lambda0 = c->lambda = o->lambda0 > 0 ? o->lambda0 : 1e-3;
         c->verbose = o->verbose;
+        c->d.dense_solve = o->dense_solve;
+        c->d.ordered = o->ordered;
         rc = ctx_setup(c, p, h, pt_ptr_all, lower_blocks, all_diag, stage_mode);
         if (rc) break;
         if (o->pivot) {
@@ -409,9 +563,14 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
         mark(c, 1);
     }
     mark(c, 2);
-    TRY(ba_launch_damp_point(&d, lam));
-    mark(c, 3);
-    TRY(ba_launch_schur(&d, lam));
+    if (d.ordered) {
+        TRY(ba_launch_damp_point(&d, lam));
+        mark(c, 3);
+        TRY(ba_launch_schur(&d, lam));
+    } else {
+        mark(c, 3);
+        TRY(ba_launch_schur_fast(&d, lam));
+    }
     TRY(allreduce(c, d.sblk, (size_t)d.na * d.na * d.nb + d.ld));
     mark(c, 4);
     TRY(ba_launch_assemble(&d));

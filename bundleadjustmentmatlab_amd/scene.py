@@ -195,7 +195,9 @@ def banded_scene(m=50, n=10_000, track=6, depth=(80.0, 120.0), noise=0.5, seed=2
         w[:, j] = w[:, j - 1] + vw
         T[:, j] = T[:, j - 1] + vT
     R = rodrigues(w)
-    start = rng.integers(0, m - track + 1, size=n)
+    # points numbered in order of creation (first camera), as
+    # generate_scene_and_motion.m:99-116 appends new features frame by frame
+    start = np.sort(rng.integers(0, m - track + 1, size=n))
     # place each point in front of its first camera, then check all cameras
     uv = rng.random((n, 2)) * np.array([width, height])
     d = rng.uniform(depth[0], depth[1], size=n)

@@ -58,6 +58,15 @@ typedef struct {
     int rank;
     int world_size;
     const void *comm_id;         /* 128-byte ncclUniqueId from rank 0, or NULL */
+    /* 1: factor every lower tile of the reduced system; 0 (default): skip the
+     * tiles outside its envelope, which are exactly zero (same result)       */
+    int dense_solve;
+    /* 1: "ordered" (parity) mode -- every sum over points runs sequentially in
+     * ascending point order exactly as the reference loops do, making the
+     * reduced system bit-identical to the reference arithmetic; 0 (default):
+     * the fused chunked Schur path (same terms, sums grouped per chunk of
+     * points, deterministic run to run)                                      */
+    int ordered;
 } vlgba_options;
 
 typedef struct {
