@@ -111,71 +111,189 @@ __device__ __forceinline__ void acc_to_lds(const d4 acc[2][2], double *T, double
             }
 }
 
-// The whole 256-thread workgroup factors the 64x64 SPD tile in As (row-major,
-// lower used) and inverts the factor in the same right-looking sweep:
-// thread (r = tid & 63, g = tid >> 6) keeps row r, columns 16g .. 16g+15 of A
-// and of X (X starts as I; solving L X = I row by row gives X = L^-1).
-// Column c of L and row c of X are broadcast through LDS (double-buffered by
-// the parity of c: two barriers per column).  Writes L (zero upper) to As and
-// L^-1 to Li (both row-major).  Returns false on a non-positive pivot.
-__device__ bool block_potrf_inv(double *As, double *Li)
+// ---- 16x16 MFMA helpers on LDS row-major tiles (pitch LP), one wave each ----
+// nt: acc[r][c] += sum_t A[ra+r][ka+t] * Bt[cb+c][kb+t]   (B given transposed)
+// nn: acc[r][c] += sum_t A[ra+r][ka+t] * Bn[kb+t][cb+c]
+__device__ __forceinline__ d4 mfma16_nt(const double *A, int ra, int ka, const double *Bt, int cb,
+                                        int kb, d4 acc)
 {
-    __shared__ double colL[2][NB];
-    __shared__ double rowX[2][NB];
-    __shared__ double rpiv[2];
-    __shared__ int bad;
-    const int tid = threadIdx.x, r = tid & 63, g = tid >> 6;
-    double a[16], x[16];
+    const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
 #pragma unroll
-    for (int jj = 0; jj < 16; jj++) {
-        a[jj] = As[r * LP + 16 * g + jj];
-        x[jj] = (r == 16 * g + jj) ? 1.0 : 0.0;
+    for (int s = 0; s < 4; s++)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(ra + li) * LP + ka + 4 * s + lk],
+                                                   Bt[(cb + li) * LP + kb + 4 * s + lk], acc,
+                                                   0, 0, 0);
+    return acc;
+}
+
+__device__ __forceinline__ d4 mfma16_nn(const double *A, int ra, int ka, const double *Bn, int kb,
+                                        int cb, d4 acc)
+{
+    const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+#pragma unroll
+    for (int s = 0; s < 4; s++)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(ra + li) * LP + ka + 4 * s + lk],
+                                                   Bn[(kb + 4 * s + lk) * LP + cb + li], acc,
+                                                   0, 0, 0);
+    return acc;
+}
+
+// T[r0 + row][c0 + col] = scale * acc (+ T if add): 16x16 result layout
+__device__ __forceinline__ void put16(double *T, int r0, int c0, d4 acc, double scale, bool add)
+{
+    const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        double *p = T + (r0 + lk + 4 * q) * LP + c0 + li;
+        *p = add ? *p + scale * acc[q] : scale * acc[q];
     }
+}
+
+// out = scale * M v for a 64x64 LDS tile (row-major, pitch LP) and a 64-vector
+// in LDS, by all 256 threads: thread (row, quarter) sums 16 columns, the four
+// quarters are added in fixed order.  Result to LDS out[] (if non-null) and to
+// reg[0] of threads 0..63 (if non-null).  Ends with a barrier.
+__device__ __forceinline__ void gemv64(const double *M, const double *v, double (*part)[NB],
+                                       double *out, double scale, double *reg = nullptr)
+{
+    const int tid = threadIdx.x, row = tid & 63, qq = tid >> 6;
+    double s = 0.0;
+#pragma unroll
+    for (int c = 16 * qq; c < 16 * qq + 16; c++) s = fma(M[row * LP + c], v[c], s);
+    part[qq][row] = s;
+    __syncthreads();
+    if (tid < NB) {
+        const double t = scale * (((part[0][tid] + part[1][tid]) + part[2][tid]) + part[3][tid]);
+        if (out) out[tid] = t;
+        if (reg) reg[0] = t;
+    }
+    __syncthreads();
+}
+
+static __device__ __forceinline__ double rdlane(double v, int l)
+{
+    const long long u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffffLL), l);
+    const int hi = __builtin_amdgcn_readlane((int)(u >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// One wave: Cholesky of the 16x16 diagonal block at (o, o) of As and its
+// inverse (lane r keeps row r of L, then column r of L^-1, in registers;
+// broadcasts by readlane).  L (zero upper) -> As, L^-1 (zero upper) -> Bs.
+__device__ __forceinline__ bool wave_factor16(double *As, double *Bs, int o)
+{
+    const int r = threadIdx.x & 63;
+    double d[16], rd[16];
+#pragma unroll
+    for (int c = 0; c < 16; c++) d[c] = (r < 16) ? As[(o + r) * LP + o + c] : 0.0;
+    bool ok = true;
+    // 1/sqrt of a pivot: hardware estimate + two Newton steps (full fp64)
+    auto rsq = [&](double piv) {
+        if (!(piv > 0.0)) {
+            ok = false;
+            piv = 1.0;
+        }
+        double y = __builtin_amdgcn_rsq(piv);
+        const double hp = 0.5 * piv;
+        y = y * fma(-hp * y, y, 1.5);
+        y = y * fma(-hp * y, y, 1.5);
+        return y;
+    };
+    double pv = rdlane(d[0], 0);
+    double y = rsq(pv);
+#pragma unroll
+    for (int c = 0; c < 16; c++) {
+        rd[c] = y;
+        d[c] = (r == c) ? pv * y : ((r > c) ? d[c] * y : 0.0);
+        // look-ahead: column c+1 first, so the next pivot's rsqrt chain can
+        // overlap the rest of this column's rank-1 update.  Unpredicated:
+        // lanes r < q only touch their upper part (zeroed below), lanes r < c
+        // hold d[c] = 0 and are unchanged.
+        if (c + 1 < 16) {
+            d[c + 1] = fma(-d[c], rdlane(d[c], c + 1), d[c + 1]);
+            pv = rdlane(d[c + 1], c + 1);
+            y = rsq(pv);
+        }
+#pragma unroll
+        for (int q = c + 2; q < 16; q++) d[q] = fma(-d[c], rdlane(d[c], q), d[q]);
+    }
+    if (r < 16) {
+#pragma unroll
+        for (int c = 0; c < 16; c++) As[(o + r) * LP + o + c] = (c <= r) ? d[c] : 0.0;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed
+    __builtin_amdgcn_wave_barrier();
+    // column r of the inverse, right-looking: x_t /= L_tt, x_q -= L_qt x_t
+    double x[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) x[q] = (q == r) ? 1.0 : 0.0;
+#pragma unroll
+    for (int t = 0; t < 16; t++) {
+        x[t] = x[t] * rd[t];
+#pragma unroll
+        for (int q = t + 1; q < 16; q++) x[q] = fma(-As[(o + q) * LP + o + t], x[t], x[q]);
+    }
+    if (r < 16) {
+#pragma unroll
+        for (int c = 0; c < 16; c++) Bs[(o + c) * LP + o + r] = x[c];
+    }
+    return ok;
+}
+
+// The 256-thread workgroup factors the 64x64 SPD tile in As (row-major, lower
+// used) and inverts the factor, blocked by 16: per 16-column step one wave
+// factors the diagonal block, three waves form the panel blocks with MFMA
+// against its inverse, and the four waves apply the trailing MFMA updates; the
+// off-diagonal blocks of L^-1 follow as Li_ij = -Li_ii sum_t L_it Li_tj.
+// Writes L (zero upper) to As and L^-1 (zero upper) to Li.  Returns false on a
+// non-positive pivot.
+__device__ __forceinline__ bool block_potrf_inv(double *As, double *Li)
+{
+    __shared__ double Xs[4][16 * LP];
+    __shared__ __attribute__((aligned(16))) int bad;   // keeps the static LDS a
+                                                       // multiple of 16 B (G17)
+    const int tid = threadIdx.x, w = tid >> 6;
+    for (int q = tid; q < NB * LP; q += blockDim.x) Li[q] = 0.0;
     if (tid == 0) bad = 0;
     __syncthreads();
-    for (int gc = 0; gc < 4; gc++)
-#pragma unroll
-    for (int jc = 0; jc < 16; jc++) {
-        const int c = 16 * gc + jc, b = jc & 1;
-        if (g == gc && r == c) {
-            double d = a[jc];
-            if (!(d > 0.0)) {
-                bad = 1;
-                d = 1.0;
-            }
-            a[jc] = sqrt(d);
-            colL[b][c] = a[jc];
-            rpiv[b] = 1.0 / a[jc];     // one division per column; scale by it
+    for (int kb = 0; kb < 4; kb++) {
+        const int o = 16 * kb;
+        if (w == 0 && !wave_factor16(As, Li, o) && (tid & 63) == 0) bad = 1;
+        __syncthreads();
+        if (w >= 1 && kb + w <= 3) {   // panel block L_i = A_i,kb Dinv^T
+            const int i = kb + w;
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
+            acc = mfma16_nt(As, 16 * i, o, Li, o, o, acc);
+            put16(As, 16 * i, o, acc, 1.0, false);
         }
         __syncthreads();
-        const double rp = rpiv[b];
-        if (g == gc && r > c) {
-            a[jc] = a[jc] * rp;
-            colL[b][r] = a[jc];
-        }
-        if (r == c) {
-#pragma unroll
-            for (int jj = 0; jj < 16; jj++) {
-                x[jj] = x[jj] * rp;
-                rowX[b][16 * g + jj] = x[jj];
-            }
-        }
+        // trailing blocks (i, j), kb < j <= i <= 3, dealt round-robin to the waves
+        int pidx = 0;
+        for (int j = kb + 1; j < 4; j++)
+            for (int i = j; i < 4; i++, pidx++)
+                if ((pidx & 3) == w) {
+                    d4 acc = {0.0, 0.0, 0.0, 0.0};
+                    acc = mfma16_nt(As, 16 * i, o, As, 16 * j, o, acc);
+                    put16(As, 16 * i, 16 * j, acc, -1.0, true);
+                }
         __syncthreads();
-        if (r > c) {
-            const double lrc = colL[b][r];
-#pragma unroll
-            for (int jj = 0; jj < 16; jj++) {
-                const int q = 16 * g + jj;
-                if (q > c && q <= r) a[jj] = fma(-lrc, colL[b][q], a[jj]);
-                x[jj] = fma(-lrc, rowX[b][q], x[jj]);
-            }
-        }
     }
-#pragma unroll
-    for (int jj = 0; jj < 16; jj++) {
-        const int q = 16 * g + jj;
-        As[r * LP + q] = (q <= r) ? a[jj] : 0.0;
-        Li[r * LP + q] = x[jj];
+    for (int i = 1; i < 4; i++) {   // block rows of L^-1, one wave per block
+        if (w < i) {
+            const int j = w;
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
+            for (int t = j; t < i; t++) acc = mfma16_nn(As, 16 * i, 16 * t, Li, 16 * t, 16 * j, acc);
+            put16(Xs[w], 0, 0, acc, 1.0, false);
+            d4 acc2 = {0.0, 0.0, 0.0, 0.0};
+            acc2 = mfma16_nn(Li, 16 * i, 16 * i, Xs[w], 0, 0, acc2);
+            put16(Li, 16 * i, 16 * j, acc2, -1.0, false);
+        }
+        __syncthreads();
+    }
+    for (int q = tid; q < NB * NB; q += blockDim.x) {   // zero the upper triangle of L
+        const int r = q >> 6, c = q & 63;
+        if (c > r) As[r * LP + c] = 0.0;
     }
     __syncthreads();
     return bad == 0;
@@ -190,33 +308,28 @@ __global__ __launch_bounds__(256) void k_factor_panel(double *__restrict__ S, lo
                                                       double *__restrict__ linv,
                                                       double *__restrict__ rhs,
                                                       double *__restrict__ y,
-                                                      double *__restrict__ status)
+                                                      double *__restrict__ status,
+                                                      int fuse_diag)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    double *As = sm, *Bs = sm + NB * LP;
+    double *As = sm, *Bs = sm + NB * LP, *Cs = sm + 2 * NB * LP;
     __shared__ double yk[NB], rk[NB];
+    __shared__ double part[4][NB];
     const int tid = threadIdx.x;
     load_tile(S, lds, k, k, As);
     if (tid < NB) rk[tid] = rhs[(long long)NB * k + tid];
     __syncthreads();
     const bool ok = block_potrf_inv(As, Bs);
-    // y_k = L^-1 r_k
-    if (tid < NB) {
-        double s = 0.0;
-        for (int q = 0; q <= tid; q++) s += Bs[tid * LP + q] * rk[q];
-        yk[tid] = s;
-    }
+    gemv64(Bs, rk, part, yk, 1.0);            // y_k = L^-1 r_k
     if (blockIdx.x == 0) {
         store_tile(S, lds, k, k, As);
         double *lo = linv + (long long)NB * NB * k;
         for (int q = tid; q < NB * NB; q += blockDim.x) lo[q] = Bs[(q >> 6) * LP + (q & 63)];
-        __syncthreads();
         if (tid < NB) y[(long long)NB * k + tid] = yk[tid];
         if (tid == 0 && !ok) status[0] = 1.0;
         return;
     }
     const int i = pan[blockIdx.x - 1];
-    __syncthreads();
     load_tile(S, lds, i, k, As);
     __syncthreads();
     d4 acc[2][2];
@@ -225,10 +338,17 @@ __global__ __launch_bounds__(256) void k_factor_panel(double *__restrict__ S, lo
     acc_to_lds(acc, As, 1.0, false);
     __syncthreads();
     store_tile(S, lds, i, k, As);
-    if (tid < NB) {
-        double s = 0.0;
-        for (int c = 0; c < NB; c++) s += As[tid * LP + c] * yk[c];
-        rhs[(long long)NB * i + tid] -= s;
+    double ri[1];
+    gemv64(As, yk, part, nullptr, 1.0, ri);   // (L_ik y_k)[tid] for tid < 64
+    if (tid < NB) rhs[(long long)NB * i + tid] -= ri[0];
+    if (fuse_diag) {
+        // the only panel tile of this step: apply A_ii -= L_ik L_ik^T here
+        mfma_64x64(As, As, acc);
+        load_tile(S, lds, i, i, Cs);
+        __syncthreads();
+        acc_to_lds(acc, Cs, -1.0, true);
+        __syncthreads();
+        store_tile(S, lds, i, i, Cs);
     }
 }
 
@@ -397,10 +517,11 @@ int ba_chol_solve(ba_dev *d)
 {
     const int nt = d->nt;
     const size_t smem = sizeof(double) * 2 * NB * LP;
+    const size_t smem3 = sizeof(double) * 3 * NB * LP;
     static bool attr_done = false;
     if (!attr_done) {
         VLGBA_CHECK(hipFuncSetAttribute((const void *)k_factor_panel,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem3));
         VLGBA_CHECK(hipFuncSetAttribute((const void *)k_syrk,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
         attr_done = true;
@@ -408,10 +529,12 @@ int ba_chol_solve(ba_dev *d)
     VLGBA_CHECK(hipMemsetAsync(d->scal + 4, 0, sizeof(double), d->stream));
     for (int k = 0; k < nt; k++) {
         const int p0 = d->pan_ptr_h[k], T = d->pan_ptr_h[k + 1] - p0;
-        k_factor_panel<<<1 + T, 256, smem, d->stream>>>(d->S, d->lds, k, d->pan_list + p0,
-                                                         d->linv, d->rhs, d->ywork,
-                                                         d->scal + 4);
-        if (T > 0)
+        // a single panel tile (narrow envelope) applies its own trailing update
+        const int fuse = (T == 1);
+        k_factor_panel<<<1 + T, 256, smem3, d->stream>>>(d->S, d->lds, k, d->pan_list + p0,
+                                                          d->linv, d->rhs, d->ywork,
+                                                          d->scal + 4, fuse);
+        if (T > 0 && !fuse)
             k_syrk<<<T * (T + 1) / 2, 256, smem, d->stream>>>(d->S, d->lds, k, d->pan_list + p0,
                                                               T);
     }
