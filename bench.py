@@ -87,12 +87,16 @@ def main():
     for _ in range(args.warmup):
         ba.step(relinearize=True, update_lm=False)
     ba.sync()
-    # per-phase device timing (HIP events on the library stream), untimed pass
+    # per-phase and per-kernel device timing (HIP events around every launch on
+    # the library stream), in untimed passes
     ba.set_timing(True)
+    ba.kernel_ms(reset=True)
     phases = []
-    for _ in range(max(1, min(3, args.steps))):
+    n_timed = max(1, min(3, args.steps))
+    for _ in range(n_timed):
         ba.step(relinearize=True, update_lm=False)
         phases.append(ba.phase_ms())
+    kms = ba.kernel_ms(reset=True)
     ba.set_timing(False)
     ph = {k: float(np.median([p[k] for p in phases])) for k in phases[0]}
 
@@ -117,28 +121,16 @@ def main():
     log(f"[bench] last pass: old_sse={info.old_sse:.9g} new_sse={info.new_sse:.9g} "
         f"rho={info.rho:.4g}")
 
-    # ---- roofline of the dominant phase -----------------------------------
-    n_s = num_a * sc.m
-    dom = max(ph, key=ph.get)
     N = sc.num_obs
-    if dom == "cholesky_solve":
-        flops = n_s ** 3 / 3.0 + 2.0 * n_s ** 2
-        roof = dict(bound="mfma", achieved=flops / (ph[dom] * 1e-3) / 1e12,
-                    peak=PEAK_F64_TFLOPS, unit="TFLOP/s")
-    else:
-        # algorithmic HBM bytes of the phase (DESIGN.md "Roofline")
-        per_obs = {"linearize": 16 + 4 + 8 * (2 * num_a + 2) + 8 * 3 * num_a,
-                   "camera_reduce": 8 * (2 * num_a + 2) + 4,
-                   "damp_y": 8 * 3 * num_a * 2 + 8 * num_a,
-                   "schur": 8 * 3 * num_a * 2,
-                   "update": 8 * 3 * num_a + 16 + 4,
-                   "assemble": 0}.get(dom, 0)
-        nbytes = per_obs * N
-        roof = dict(bound="hbm", achieved=nbytes / (ph[dom] * 1e-3) / 1e9,
-                    peak=PEAK_HBM_GBS, unit="GB/s")
-    roof["frac"] = roof["achieved"] / roof["peak"]
-    roof["traffic"] = None
-    roof["kernel"] = dom
+    # ---- roofline of the dominant kernel -----------------------------------
+    roofs = {k: kernel_roofline(k, tot, calls, sc, num_a, world) for k, (tot, calls) in
+             kms.items()}
+    dom = max(kms, key=lambda k: kms[k][0])
+    roof = roofs[dom]
+    log("[bench] kernels (avg us/launch, launches/pass, roofline frac): " +
+        "  ".join(f"{k}={1e3 * t / c:.1f}us x{c / n_timed:.0f} "
+                  f"{roofs[k]['frac']:.3f}" for k, (t, c) in
+                  sorted(kms.items(), key=lambda kv: -kv[1][0])))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -171,6 +163,64 @@ def main():
     ba.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def envelope_panels(sc, num_a):
+    """Panel tiles per Cholesky step of the tile envelope (ba_chol.hip)."""
+    NB = 64
+    n_s = num_a * sc.m
+    nt = (n_s + NB - 1) // NB
+    tfirst = np.arange(nt)
+    ptr = np.concatenate([[0], np.cumsum(np.bincount(sc.obs_pt, minlength=sc.n))])
+    cnt = np.diff(ptr)
+    cmin = np.minimum.reduceat(sc.obs_cam, ptr[:-1][cnt > 0])
+    lo = np.repeat(cmin, cnt[cnt > 0])           # smallest camera of each obs' point
+    for r in range(num_a):                        # every row of camera j couples with it
+        np.minimum.at(tfirst, (num_a * sc.obs_cam + r) // NB, (num_a * lo) // NB)
+    T = np.array([(tfirst[k + 1:] <= k).sum() for k in range(nt)])
+    return nt, T
+
+
+def kernel_roofline(name, tot_ms, calls, sc, num_a, world):
+    """Algorithmic bytes (HBM-bound kernels) or flops (MFMA kernels) per launch
+    divided by the measured average launch time (DESIGN.md 'Roofline')."""
+    N = sc.num_obs / world
+    n = sc.n / world
+    avg_s = tot_ms * 1e-3 / calls
+    NB = 64
+    if name in ("k_factor_panel", "k_syrk", "k_backward"):
+        nt, T = envelope_panels(sc, num_a)
+        if name == "k_factor_panel":
+            # potrf + trtri of the diagonal tile, T panel GEMMs, fused syrk if T == 1
+            fl = sum(2 * NB ** 3 / 3 + t * 2 * NB ** 3 + (NB ** 3 if t == 1 else 0) for t in T)
+        elif name == "k_syrk":
+            fl = sum(t * (t + 1) / 2 * 2 * NB ** 3 for t in T if t > 1)
+        else:
+            fl = sum(2 * NB * NB * (1 + t) for t in T)
+        passes = calls / max(1, (len(T) if name != "k_syrk" else sum(1 for t in T if t > 1)))
+        per = fl / (calls / passes)                 # flops per launch
+        achieved = per / avg_s / 1e12
+        return dict(bound="mfma", achieved=achieved, peak=PEAK_F64_TFLOPS, unit="TFLOP/s",
+                    frac=achieved / PEAK_F64_TFLOPS, traffic=None, kernel=name,
+                    per_launch=f"{per:.3g} flop")
+    JS = 8 * (2 * num_a + 2)
+    WS = 8 * 3 * num_a
+    per_obs = {"k_linearize": 16 + 4 + JS + WS,          # obs (x, cam) in; jrec, W out
+               "k_camera_reduce": JS + 4,                 # jrec + cam_obs in
+               "k_damp_point": 2 * WS + 8 * num_a,        # W in; Y, t out
+               "k_schur": 2 * WS,                         # Y, W per term (>= once)
+               "k_schur_chunk": WS,                       # W in (once, contiguous)
+               "k_point_update": WS + 16 + 4}.get(name, 0)
+    per_pt = {"k_linearize": 24 + 72 + 24 + 4,           # b in; V, eB out
+              "k_damp_point": 72 + 24 + 72,
+              "k_schur_chunk": 72 + 24 + 72,             # V, eB in; V*^-1 out
+              "k_point_update": 24 + 72 + 24 + 48 + 4}.get(name, 0)
+    # every such kernel runs once per pass: bytes per launch = bytes per pass
+    nbytes = per_obs * N + per_pt * n
+    achieved = nbytes / avg_s / 1e9 if nbytes else 0.0
+    return dict(bound="hbm", achieved=achieved, peak=PEAK_HBM_GBS, unit="GB/s",
+                frac=achieved / PEAK_HBM_GBS, traffic=None, kernel=name,
+                per_launch=f"{nbytes:.3g} B")
 
 
 def cpu_baseline(sc, a0, b0, num_a, sample_points):

@@ -191,6 +191,16 @@ class BundleAdjuster:
     def set_timing(self, on=True):
         check(self._L.vlgba_set_timing(self._h, int(on)), "vlgba_set_timing")
 
+    def kernel_ms(self, reset=True):
+        """{kernel: (total ms, launches)} accumulated since the last reset over
+        the passes run with set_timing(True)."""
+        n = 13
+        ms = np.zeros(n)
+        calls = (ctypes.c_longlong * n)()
+        check(self._L.vlgba_kernel_ms(self._h, _dp(ms), calls, int(reset)), "vlgba_kernel_ms")
+        return {self._L.vlgba_kernel_name(k).decode(): (float(ms[k]), int(calls[k]))
+                for k in range(n) if calls[k] > 0}
+
     def phase_ms(self):
         ms = np.zeros(7)
         check(self._L.vlgba_phase_ms(self._h, _dp(ms)), "vlgba_phase_ms")

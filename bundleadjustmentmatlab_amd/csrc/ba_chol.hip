@@ -531,17 +531,24 @@ int ba_chol_solve(ba_dev *d)
         const int p0 = d->pan_ptr_h[k], T = d->pan_ptr_h[k + 1] - p0;
         // a single panel tile (narrow envelope) applies its own trailing update
         const int fuse = (T == 1);
+        KT_B(d);
         k_factor_panel<<<1 + T, 256, smem3, d->stream>>>(d->S, d->lds, k, d->pan_list + p0,
                                                           d->linv, d->rhs, d->ywork,
                                                           d->scal + 4, fuse);
-        if (T > 0 && !fuse)
+        KT_E(d, KT_FACTOR);
+        if (T > 0 && !fuse) {
+            KT_B(d);
             k_syrk<<<T * (T + 1) / 2, 256, smem, d->stream>>>(d->S, d->lds, k, d->pan_list + p0,
                                                               T);
+            KT_E(d, KT_SYRK);
+        }
     }
     for (int k = nt - 1; k >= 0; k--) {
         const int j0 = d->h_tfirst[k];
+        KT_B(d);
         k_backward<<<k - j0 + 1, 256, 0, d->stream>>>(d->S, d->lds, k, j0, d->linv, d->ywork,
                                                        d->da);
+        KT_E(d, KT_BACKWARD);
     }
     return -(int)hipGetLastError();
 }

@@ -28,6 +28,25 @@
         if (err__ != hipSuccess) return -(int)err__;                                \
     } while (0)
 
+// Per-kernel HIP-event timing (diagnostic passes only): every launch of a
+// tracked kernel is bracketed by two events on the library stream; after the
+// pass the elapsed times are summed per kernel.
+enum {
+    KT_ROT, KT_LIN, KT_CAMRED, KT_DAMP, KT_SCHUR, KT_SCHUR_CHUNK, KT_SCHUR_RED,
+    KT_ASSEMBLE, KT_FACTOR, KT_SYRK, KT_BACKWARD, KT_CAMUPD, KT_PTUPD, KT_N
+};
+#define KT_MAX_EV 8192
+struct ba_ktimer {
+    int on;
+    int nev;
+    hipEvent_t ev[KT_MAX_EV];
+    int kid[KT_MAX_EV / 2];
+    double ms[KT_N];
+    long long calls[KT_N];
+};
+void kt_begin(struct ba_ktimer *t, hipStream_t s);
+void kt_end(struct ba_ktimer *t, hipStream_t s, int kid);
+
 struct ba_flags {
     int fix_structure;  // V, W, eB = 0       (bundle_euclid.m:140-144)
     int fix_motion;     // U, W, eA = 0       (:145-149)
@@ -94,8 +113,14 @@ struct ba_dev {
     unsigned char *obs_vis;  // [N] stage 3: 0 = structural-only pair (no projection)
     int schur_owner;   // this rank adds U* / eA into the reduced system
     double scal_host[8];
+    struct ba_ktimer *kt;   // NULL unless kernel timing is enabled
     hipStream_t stream;
 };
+
+#define KT_B(d) \
+    do { if ((d)->kt && (d)->kt->on) kt_begin((d)->kt, (d)->stream); } while (0)
+#define KT_E(d, id) \
+    do { if ((d)->kt && (d)->kt->on) kt_end((d)->kt, (d)->stream, (id)); } while (0)
 
 #define BA_PART_MAX 65536
 #define BA_CH_OBS 128      // observations per Schur chunk (LDS budget)

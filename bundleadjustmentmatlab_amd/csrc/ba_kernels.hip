@@ -629,17 +629,21 @@ int ba_launch_rotations(ba_dev *d, const double *a, double *rot, int all5)
 {
     (void)all5;
     const int g = grid_for(d->m, 64, 1 << 30);
+    KT_B(d);
     BA_DISPATCH(d->na, (k_rotations<NA><<<g, 64, 0, d->stream>>>(a, rot, d->m)));
+    KT_E(d, KT_ROT);
     return -(int)hipGetLastError();
 }
 
 int ba_launch_linearize(ba_dev *d, ba_flags f)
 {
     const int g = grid_for(d->n, 256, PT_GRID_CAP);
+    KT_B(d);
     BA_DISPATCH(d->na, (k_linearize<NA><<<g, 256, 0, d->stream>>>(
                            d->pt_ptr, d->obs_cam, d->obs_x, d->K4, d->a, d->rot, d->b, d->n, f,
                            d->pivot, d->jrec, d->W, d->V, d->eB, d->part, d->xh_out,
                            d->B_out)));
+    KT_E(d, KT_LIN);
     k_sum_parts<<<1, 256, 0, d->stream>>>(d->part, g, d->scal + 0);
     return -(int)hipGetLastError();
 }
@@ -647,25 +651,31 @@ int ba_launch_linearize(ba_dev *d, ba_flags f)
 int ba_launch_camera_reduce(ba_dev *d, ba_flags f)
 {
     const int bs = (d->na * (d->na + 1) / 2 + d->na) <= 64 ? 64 : 128;
+    KT_B(d);
     BA_DISPATCH(d->na, (k_camera_reduce<NA><<<d->m, bs, 0, d->stream>>>(
                            d->cam_ptr, d->cam_obs, d->jrec, d->m, f, d->pivot, d->U, d->eA)));
+    KT_E(d, KT_CAMRED);
     return -(int)hipGetLastError();
 }
 
 int ba_launch_damp_point(ba_dev *d, double lambda)
 {
     const int g = grid_for(d->n, 256, PT_GRID_CAP);
+    KT_B(d);
     BA_DISPATCH(d->na, (k_damp_point<NA><<<g, 256, 0, d->stream>>>(
                            d->pt_ptr, d->V, d->eB, d->W, d->n, lambda, d->Vinv, d->Y, d->t)));
+    KT_E(d, KT_DAMP);
     return -(int)hipGetLastError();
 }
 
 int ba_launch_schur(ba_dev *d, double lambda)
 {
     const int bs = (d->na * d->na + d->na) <= 64 ? 64 : 128;
+    KT_B(d);
     BA_DISPATCH(d->na, (k_schur<NA><<<d->nb, bs, 0, d->stream>>>(
                            d->blk_jk, d->blk_ptr, d->term, d->Y, d->W, d->t, d->U, d->eA, d->nb,
                            lambda, d->schur_owner, d->sblk, d->rhs)));
+    KT_E(d, KT_SCHUR);
     return -(int)hipGetLastError();
 }
 
@@ -681,14 +691,18 @@ static int launch_schur_fast(ba_dev *d, double lambda)
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
         attr = true;
     }
+    KT_B(d);
     if (d->nch > 0)
         k_schur_chunk<NA><<<d->nch, 256, smem, d->stream>>>(
             d->ch_pt, d->ch_slot, d->ch_eslot, d->slot_tptr, d->slot_term, d->eslot_optr,
             d->eslot_obs, d->pt_ptr, d->V, d->eB, d->W, lambda, d->Vinv, d->spart, d->epart);
+    KT_E(d, KT_SCHUR_CHUNK);
     const int bs = (NA * NA + NA) <= 64 ? 64 : 128;
+    KT_B(d);
     k_schur_reduce<NA><<<d->nb, bs, 0, d->stream>>>(
         d->blk_jk, d->blk_sptr, d->blk_slots, d->cam_eptr, d->cam_eslots, d->spart, d->epart,
         d->U, d->eA, d->nb, lambda, d->schur_owner, d->sblk, d->rhs);
+    KT_E(d, KT_SCHUR_RED);
     return -(int)hipGetLastError();
 }
 
@@ -726,15 +740,19 @@ int ba_launch_assemble(ba_dev *d)
 int ba_launch_update(ba_dev *d, double lambda)
 {
     const int gc = grid_for(d->m, 256, 1 << 30);
+    KT_B(d);
     BA_DISPATCH(d->na, (k_camera_update<NA><<<gc, 256, 0, d->stream>>>(
                            d->a, d->da, d->eA, d->m, lambda, d->a_new, d->rot_new, d->part)));
+    KT_E(d, KT_CAMUPD);
     k_sum_parts<<<1, 256, 0, d->stream>>>(d->part, gc, d->scal + 2);
     const int g = grid_for(d->n, 256, PT_GRID_CAP);
+    KT_B(d);
     BA_DISPATCH(d->na, (k_point_update<NA><<<g, 256, 0, d->stream>>>(
                            d->pt_ptr, d->obs_cam, d->obs_x, d->K4, d->W, d->da, d->eB, d->Vinv,
                            d->b, d->a_new, d->rot_new, d->n, lambda, d->db, d->b_new,
                            d->part + BA_PART_MAX, d->part + 2 * BA_PART_MAX, d->obs_vis,
                            d->xh_out)));
+    KT_E(d, KT_PTUPD);
     k_sum_parts<<<1, 256, 0, d->stream>>>(d->part + BA_PART_MAX, g, d->scal + 1);
     k_sum_parts<<<1, 256, 0, d->stream>>>(d->part + 2 * BA_PART_MAX, g, d->scal + 3);
     return -(int)hipGetLastError();

@@ -280,6 +280,20 @@ bool build_plan(int m, const std::vector<int> &lptr, const std::vector<int> &lca
 
 }  // namespace
 
+void kt_begin(ba_ktimer *t, hipStream_t s)
+{
+    if (t->nev + 2 > KT_MAX_EV) return;
+    (void)hipEventRecord(t->ev[t->nev], s);
+}
+
+void kt_end(ba_ktimer *t, hipStream_t s, int kid)
+{
+    if (t->nev + 2 > KT_MAX_EV) return;
+    (void)hipEventRecord(t->ev[t->nev + 1], s);
+    t->kid[t->nev / 2] = kid;
+    t->nev += 2;
+}
+
 // =========================================================================
 struct vlgba_ctx {
     ba_dev d;
@@ -307,6 +321,10 @@ static void ctx_free(vlgba_ctx *c)
     for (void *p : c->allocs) (void)hipFree(p);
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
+    if (c->d.kt) {
+        for (auto &e : c->d.kt->ev) (void)hipEventDestroy(e);
+        delete c->d.kt;
+    }
     ba_chol_free(&c->d);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->d.stream) (void)hipStreamDestroy(c->d.stream);
@@ -598,6 +616,13 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
             (void)hipEventElapsedTime(&ms, c->ev[map[q][0]], c->ev[map[q][1]]);
             c->phase_ms[q] = ms;
         }
+        ba_ktimer *kt = d.kt;
+        for (int q = 0; kt && q + 1 < kt->nev; q += 2) {
+            (void)hipEventElapsedTime(&ms, kt->ev[q], kt->ev[q + 1]);
+            kt->ms[kt->kid[q / 2]] += ms;
+            kt->calls[kt->kid[q / 2]]++;
+        }
+        if (kt) kt->nev = 0;
     }
     info->old_sse = hs[0];
     info->new_sse = hs[1];
@@ -706,8 +731,37 @@ int vlgba_set_timing(vlgba_ctx *c, int on)
     if (!c) return VLGBA_E_ARG;
     if (on && !c->ev[0])
         for (auto &e : c->ev) VLGBA_CHECK(hipEventCreate(&e));
+    if (on && !c->d.kt) {
+        c->d.kt = new (std::nothrow) ba_ktimer();
+        if (!c->d.kt) return VLGBA_E_NOMEM;
+        for (auto &e : c->d.kt->ev) VLGBA_CHECK(hipEventCreate(&e));
+    }
     c->timing = on;
+    if (c->d.kt) c->d.kt->on = on;
     return 0;
+}
+
+int vlgba_kernel_ms(vlgba_ctx *c, double *ms, long long *calls, int reset)
+{
+    if (!c || !c->d.kt) return VLGBA_E_ARG;
+    for (int k = 0; k < KT_N; k++) {
+        if (ms) ms[k] = c->d.kt->ms[k];
+        if (calls) calls[k] = c->d.kt->calls[k];
+        if (reset) {
+            c->d.kt->ms[k] = 0.0;
+            c->d.kt->calls[k] = 0;
+        }
+    }
+    return 0;
+}
+
+const char *vlgba_kernel_name(int k)
+{
+    static const char *names[KT_N] = {
+        "k_rotations", "k_linearize", "k_camera_reduce", "k_damp_point", "k_schur",
+        "k_schur_chunk", "k_schur_reduce", "k_assemble", "k_factor_panel", "k_syrk",
+        "k_backward", "k_camera_update", "k_point_update"};
+    return (k >= 0 && k < KT_N) ? names[k] : "";
 }
 
 int vlgba_phase_ms(vlgba_ctx *c, double *ms7)

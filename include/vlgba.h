@@ -114,6 +114,12 @@ void vlgba_destroy(vlgba_ctx *ctx);
  * [5] cholesky+solve [6] update; requires vlgba_set_timing(ctx, 1) first. */
 int vlgba_set_timing(vlgba_ctx *ctx, int on);
 int vlgba_phase_ms(vlgba_ctx *ctx, double *ms7);
+/* per-kernel device time accumulated over the passes run with timing on
+ * (HIP events around every launch): ms[k], calls[k] for k < VLGBA_NKERNELS,
+ * named by vlgba_kernel_name(k); reset = 1 clears the accumulators. */
+#define VLGBA_NKERNELS 13
+int vlgba_kernel_ms(vlgba_ctx *ctx, double *ms, long long *calls, int reset);
+const char *vlgba_kernel_name(int k);
 
 /* ---- stage entries with the reference MEX argument layouts ---------------
  * Host pointers in, host pointers out; every output is fully written (zeros
