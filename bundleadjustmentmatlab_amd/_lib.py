@@ -29,7 +29,12 @@ class VlgbaOptions(ctypes.Structure):
                 ("verbose", c_int), ("max_iter", c_int), ("max_iter2", c_int),
                 ("lambda0", c_double), ("device", c_int), ("rank", c_int),
                 ("world_size", c_int), ("comm_id", ctypes.c_void_p), ("dense_solve", c_int),
-                ("ordered", c_int)]
+                ("ordered", c_int), ("allreduce", ctypes.c_void_p),
+                ("allreduce_user", ctypes.c_void_p)]
+
+
+# int (*allreduce)(double *buf, long long count, void *user)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, c_dp, c_ll, ctypes.c_void_p)
 
 
 class VlgbaStats(ctypes.Structure):

@@ -21,8 +21,8 @@ from __future__ import annotations
 import ctypes
 import numpy as np
 
-from ._lib import (VlgbaOptions, VlgbaProblem, VlgbaStats, VlgbaStepInfo, c_dp, c_ip, c_up,
-                   check, lib)
+from ._lib import (ALLREDUCE_FN, VlgbaOptions, VlgbaProblem, VlgbaStats, VlgbaStepInfo, c_dp,
+                   c_ip, c_up, check, lib)
 
 __all__ = ["bundle_euclid", "bundle_euclid_obs", "BundleAdjuster", "parse_options",
            "mex_bundle_1_XABeUVWeAeB", "mex_bundle_2_Se_", "mex_bundle_3_db_new"]
@@ -112,7 +112,7 @@ class BundleAdjuster:
     def __init__(self, K, obs_pt, obs_cam, obs_x, n, num_a=6, *, fix_structure=False,
                  fix_motion=False, pivot=None, verbose=False, num_vis=0.0, device=0,
                  rank=0, world_size=1, comm_id=None, max_iter=0, max_iter2=0, lambda0=0.0,
-                 dense_solve=False, ordered=False):
+                 dense_solve=False, ordered=False, allreduce=None):
         L = lib()
         self.K = _F(K)
         self.m = self.K.shape[1]
@@ -132,12 +132,23 @@ class BundleAdjuster:
         self._comm = None
         if comm_id is not None:
             self._comm = ctypes.create_string_buffer(bytes(comm_id), 128)
+        self._ar = None
+        if allreduce is not None:
+            # host collective: allreduce(np.ndarray) sums in place over ranks
+            def _cb(buf, count, _user, fn=allreduce):
+                try:
+                    fn(np.ctypeslib.as_array(buf, shape=(count,)))
+                    return 0
+                except Exception:   # noqa: BLE001 -- reported to the library as failure
+                    return 1
+            self._ar = ALLREDUCE_FN(_cb)
         opt = VlgbaOptions(int(fix_structure), int(fix_motion),
                            self._pivot.ctypes.data_as(c_up) if self._pivot is not None else None,
                            int(verbose), int(max_iter), int(max_iter2), float(lambda0),
                            int(device), int(rank), int(world_size),
                            ctypes.cast(self._comm, ctypes.c_void_p) if self._comm else None,
-                           int(dense_solve), int(ordered))
+                           int(dense_solve), int(ordered),
+                           ctypes.cast(self._ar, ctypes.c_void_p) if self._ar else None, None)
         h = ctypes.c_void_p()
         check(L.vlgba_create(ctypes.byref(prob), ctypes.byref(opt), ctypes.byref(h)),
               "vlgba_create")

@@ -300,6 +300,8 @@ struct vlgba_ctx {
     ba_flags flags;
     int rank = 0, world = 1;
     ncclComm_t comm = nullptr;
+    int (*host_allreduce)(double *, long long, void *) = nullptr;
+    void *host_user = nullptr;
     int p0 = 0, p1 = 0;          // global point range of this rank
     int n_global = 0;
     long long N_global = 0;
@@ -342,8 +344,20 @@ static int ctx_alloc(vlgba_ctx *c, T **p, size_t count)
 static int allreduce(vlgba_ctx *c, double *buf, size_t count)
 {
     if (c->world <= 1 || count == 0) return 0;
-    ncclResult_t r = ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c->comm, c->d.stream);
-    return r == ncclSuccess ? 0 : VLGBA_E_COMM;
+    if (c->comm) {
+        ncclResult_t r =
+            ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c->comm, c->d.stream);
+        return r == ncclSuccess ? 0 : VLGBA_E_COMM;
+    }
+    // host collective (vlgba_options.allreduce): device -> host, sum, host -> device
+    c->hb_tmp.resize(count);
+    TRY(download(c->hb_tmp.data(), buf, count, c->d.stream));
+    VLGBA_CHECK(hipStreamSynchronize(c->d.stream));
+    if (c->host_allreduce(c->hb_tmp.data(), (long long)count, c->host_user) != 0)
+        return VLGBA_E_COMM;
+    TRY(upload(buf, c->hb_tmp.data(), count, c->d.stream));
+    VLGBA_CHECK(hipStreamSynchronize(c->d.stream));
+    return 0;
 }
 
 // Device buffers + host-side structure for the observations of points [p0, p1).
@@ -512,10 +526,17 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
             };
             c->p0 = c->rank == 0 ? 0 : std::min(bound(c->rank), p->n);
             c->p1 = c->rank == c->world - 1 ? p->n : std::min(bound(c->rank + 1), p->n);
-            if (!o->comm_id) { rc = VLGBA_E_COMM; break; }
-            ncclUniqueId id;
-            std::memcpy(&id, o->comm_id, sizeof id);
-            if (ncclCommInitRank(&c->comm, c->world, id, c->rank) != ncclSuccess) {
+            if (o->comm_id) {
+                ncclUniqueId id;
+                std::memcpy(&id, o->comm_id, sizeof id);
+                if (ncclCommInitRank(&c->comm, c->world, id, c->rank) != ncclSuccess) {
+                    rc = VLGBA_E_COMM;
+                    break;
+                }
+            } else if (o->allreduce) {
+                c->host_allreduce = o->allreduce;
+                c->host_user = o->allreduce_user;
+            } else {
                 rc = VLGBA_E_COMM;
                 break;
             }

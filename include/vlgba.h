@@ -67,6 +67,12 @@ typedef struct {
      * the fused chunked Schur path (same terms, sums grouped per chunk of
      * points, deterministic run to run)                                      */
     int ordered;
+    /* world_size > 1 without comm_id: a host collective instead of RCCL.  The
+     * library copies the buffer to host memory, calls allreduce(buf, count,
+     * user), which must leave the element-wise sum over ranks in buf and
+     * return 0, and copies it back (e.g. gloo via torch.distributed). */
+    int (*allreduce)(double *buf, long long count, void *user);
+    void *allreduce_user;
 } vlgba_options;
 
 typedef struct {

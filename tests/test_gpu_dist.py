@@ -1,0 +1,88 @@
+"""Point-sharded solver on 2 ranks sharing one GPU (gloo host collective).
+
+Exercises every piece of libvlgba's multi-GPU data path -- contiguous point
+ranges, the owner rule for U* / eA, the all-reduce of U | eA | SSE, of the
+packed reduced system and of the scalars, the replicated solve, the full-b
+gather -- with the collective routed through vlgba_options.allreduce
+(torch.distributed gloo) instead of RCCL, so it runs on a 1-GPU box.  Result:
+equal to the 1-rank solve to summation-order rounding, and identical on both
+ranks.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(ba, a, b, steps=3):
+    ba.set_params(a, b)
+    infos = [ba.step(relinearize=True, update_lm=True) for _ in range(steps)]
+    return infos, ba.get_params()
+
+
+def _worker(rank, world, port, outdir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    torch.cuda.set_device(0)
+    import bundleadjustmentmatlab_amd as pkg
+    from bundleadjustmentmatlab_amd.scene import make_config
+    sc = make_config("cfg2", m=40, n=5000, seed=21)
+    a = np.zeros((6, sc.m), order="F")
+    a[0:3], a[3:6] = sc.w0, sc.T0
+    b = np.asfortranarray(sc.X0[:3])
+
+    def ar(arr):
+        t = torch.from_numpy(arr)
+        dist.all_reduce(t)
+
+    ba = pkg.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, 6, rank=rank,
+                            world_size=world, allreduce=ar)
+    infos, (a2, b2) = _run(ba, a, b)
+    ba.close()
+    res = dict(old=[i.old_sse for i in infos], new=[i.new_sse for i in infos],
+               acc=[i.accepted for i in infos], a=a2, b=b2)
+    if rank == 0:
+        ba1 = pkg.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, 6)
+        infos1, (a1, b1) = _run(ba1, a, b)
+        ba1.close()
+        res.update(old1=[i.old_sse for i in infos1], new1=[i.new_sse for i in infos1],
+                   acc1=[i.accepted for i in infos1], a1=a1, b1=b1)
+    np.savez(os.path.join(outdir, f"rank{rank}.npz"), **res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_sharded_solve_matches_single(tmp_path):
+    import torch.multiprocessing as mp
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    r0 = np.load(tmp_path / "rank0.npz")
+    r1 = np.load(tmp_path / "rank1.npz")
+    # both ranks: identical decisions and parameters (replicated solve)
+    assert np.array_equal(r0["acc"], r1["acc"])
+    assert np.array_equal(r0["a"], r1["a"]) and np.array_equal(r0["b"], r1["b"])
+    # vs the single-rank solve: the first pass differs by summation order only;
+    # later passes inherit the FD-Jacobian amplification of those differences
+    # (measured ~5e-6 relative on pass 3), as in tests/test_gpu_parity.py
+    assert np.array_equal(r0["acc"], r0["acc1"])
+    assert abs(r0["old"][0] - r0["old1"][0]) <= 1e-11 * r0["old1"][0]
+    assert abs(r0["new"][0] - r0["new1"][0]) <= 1e-7 * r0["new1"][0]
+    assert np.allclose(r0["old"], r0["old1"], rtol=1e-4, atol=0)
+    assert np.allclose(r0["new"], r0["new1"], rtol=1e-4, atol=0)
+    # parameters are compared through the cost above: they drift along the
+    # 7-dof similarity gauge that only the damping constrains (~1e-3 here)
