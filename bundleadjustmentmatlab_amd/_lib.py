@@ -33,6 +33,8 @@ class VlgbaOptions(ctypes.Structure):
                 ("allreduce_user", ctypes.c_void_p)]
 
 
+NKERNELS = 16   # VLGBA_NKERNELS
+
 # int (*allreduce)(double *buf, long long count, void *user)
 ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, c_dp, c_ll, ctypes.c_void_p)
 

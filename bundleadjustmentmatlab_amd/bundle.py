@@ -21,8 +21,8 @@ from __future__ import annotations
 import ctypes
 import numpy as np
 
-from ._lib import (ALLREDUCE_FN, VlgbaOptions, VlgbaProblem, VlgbaStats, VlgbaStepInfo, c_dp,
-                   c_ip, c_up, check, lib)
+from ._lib import (ALLREDUCE_FN, NKERNELS, VlgbaOptions, VlgbaProblem, VlgbaStats,
+                   VlgbaStepInfo, c_dp, c_ip, c_up, check, lib)
 
 __all__ = ["bundle_euclid", "bundle_euclid_obs", "BundleAdjuster", "parse_options",
            "mex_bundle_1_XABeUVWeAeB", "mex_bundle_2_Se_", "mex_bundle_3_db_new"]
@@ -106,14 +106,19 @@ class BundleAdjuster:
 
     obs_pt / obs_cam (0-based) and obs_x (N, 2) describe the visible
     observations; K is 4 x m; num_a is 6 (fix_calibration), 7 (fix_principal)
-    or 10 (variable K).  Options follow bundle_euclid.m's names.
+    or 10 (variable K).  Options follow bundle_euclid.m's names.  ``solver``
+    picks the reduced-camera solve: "auto" (cyclic reduction when S is
+    tile-tridiagonal, else envelope Cholesky), "envelope" or "dense";
+    ``dense_solve=True`` is the same as solver="dense".
     """
+    SOLVERS = {"auto": 0, "dense": 1, "envelope": 2}
 
     def __init__(self, K, obs_pt, obs_cam, obs_x, n, num_a=6, *, fix_structure=False,
                  fix_motion=False, pivot=None, verbose=False, num_vis=0.0, device=0,
                  rank=0, world_size=1, comm_id=None, max_iter=0, max_iter2=0, lambda0=0.0,
-                 dense_solve=False, ordered=False, allreduce=None):
+                 dense_solve=False, ordered=False, allreduce=None, solver=None):
         L = lib()
+        solve_mode = self.SOLVERS[solver] if solver is not None else int(bool(dense_solve))
         self.K = _F(K)
         self.m = self.K.shape[1]
         self.n = int(n)
@@ -147,7 +152,7 @@ class BundleAdjuster:
                            int(verbose), int(max_iter), int(max_iter2), float(lambda0),
                            int(device), int(rank), int(world_size),
                            ctypes.cast(self._comm, ctypes.c_void_p) if self._comm else None,
-                           int(dense_solve), int(ordered),
+                           solve_mode, int(ordered),
                            ctypes.cast(self._ar, ctypes.c_void_p) if self._ar else None, None)
         h = ctypes.c_void_p()
         check(L.vlgba_create(ctypes.byref(prob), ctypes.byref(opt), ctypes.byref(h)),
@@ -205,7 +210,7 @@ class BundleAdjuster:
     def kernel_ms(self, reset=True):
         """{kernel: (total ms, launches)} accumulated since the last reset over
         the passes run with set_timing(True)."""
-        n = 13
+        n = NKERNELS
         ms = np.zeros(n)
         calls = (ctypes.c_longlong * n)()
         check(self._L.vlgba_kernel_ms(self._h, _dp(ms), calls, int(reset)), "vlgba_kernel_ms")

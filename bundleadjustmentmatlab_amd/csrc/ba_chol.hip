@@ -44,6 +44,30 @@ __device__ __forceinline__ void load_tile(const double *__restrict__ S, long lon
     for (int u = 0; u < 16; u++) T[r * LP + c0 + 4 * u] = v[u];
 }
 
+// S tile (ti, tj) transposed -> LDS T[c][r] = tile[r][c] (LDS writes contiguous in r)
+__device__ __forceinline__ void load_tile_t(const double *__restrict__ S, long long lds, int ti,
+                                            int tj, double *T)
+{
+    const double *base = S + (long long)NB * ti + lds * (long long)NB * tj;
+    const int r = threadIdx.x & 63, c0 = threadIdx.x >> 6;
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) v[u] = base[r + lds * (c0 + 4 * u)];
+#pragma unroll
+    for (int u = 0; u < 16; u++) T[(c0 + 4 * u) * LP + r] = v[u];
+}
+
+// LDS T[r][c] -> row-major 64x64 dst[r*64 + c]
+__device__ __forceinline__ void store_rowmajor(double *__restrict__ dst, const double *T)
+{
+    const int c = threadIdx.x & 63, r0 = threadIdx.x >> 6;
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) v[u] = T[(r0 + 4 * u) * LP + c];
+#pragma unroll
+    for (int u = 0; u < 16; u++) dst[(r0 + 4 * u) * NB + c] = v[u];
+}
+
 // row-major 64x64 (src[r*64 + c]) -> LDS T[r][c], loads batched as above
 __device__ __forceinline__ void load_rowmajor(const double *__restrict__ src, double *T)
 {
@@ -71,15 +95,11 @@ __device__ __forceinline__ void store_tile(double *__restrict__ S, long long lds
 // Wave w owns rows 32*(w>>1) .. +31, cols 32*(w&1) .. +31 as 2x2 MFMA tiles.
 // f64 16x16x4 operand map: A lane l -> A[l&15][l>>4], B lane l -> B[l>>4][l&15];
 // result register q of lane l -> (row (l>>4) + 4q, col l&15).
-__device__ __forceinline__ void mfma_64x64(const double *As, const double *Bs, d4 acc[2][2])
+__device__ __forceinline__ void mfma_64x64_acc(const double *As, const double *Bs, d4 acc[2][2])
 {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r0 = 32 * (w >> 1), c0 = 32 * (w & 1);
     const int li = lane & 15, lk = lane >> 4;
-#pragma unroll
-    for (int x = 0; x < 2; x++)
-#pragma unroll
-        for (int y = 0; y < 2; y++) acc[x][y] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll 4
     for (int s = 0; s < NB / 4; s++) {
         const int kk = 4 * s + lk;
@@ -92,6 +112,15 @@ __device__ __forceinline__ void mfma_64x64(const double *As, const double *Bs, d
         acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
         acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
     }
+}
+
+__device__ __forceinline__ void mfma_64x64(const double *As, const double *Bs, d4 acc[2][2])
+{
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) acc[x][y] = d4{0.0, 0.0, 0.0, 0.0};
+    mfma_64x64_acc(As, Bs, acc);
 }
 
 // write acc (scale * acc + (add ? T : 0)) into LDS tile T in MFMA layout
@@ -167,6 +196,20 @@ __device__ __forceinline__ void gemv64(const double *M, const double *v, double 
         if (out) out[tid] = t;
         if (reg) reg[0] = t;
     }
+    __syncthreads();
+}
+
+// out[c] = scale * sum_r M[r][c] v[r] (M^T v), same thread split and order as gemv64
+__device__ __forceinline__ void gemv64_t(const double *M, const double *v, double (*part)[NB],
+                                         double *out, double scale)
+{
+    const int tid = threadIdx.x, c = tid & 63, qq = tid >> 6;
+    double s = 0.0;
+#pragma unroll
+    for (int r = 16 * qq; r < 16 * qq + 16; r++) s = fma(M[r * LP + c], v[r], s);
+    part[qq][c] = s;
+    __syncthreads();
+    if (tid < NB) out[tid] = scale * (((part[0][tid] + part[1][tid]) + part[2][tid]) + part[3][tid]);
     __syncthreads();
 }
 
@@ -422,6 +465,147 @@ __global__ __launch_bounds__(256) void k_backward(const double *__restrict__ S, 
         z[(long long)NB * j + tid] -= ((part[0][tid] + part[1][tid]) + part[2][tid]) + part[3][tid];
 }
 
+// ---------------------------------------------------------------------------
+// Block cyclic reduction for a tile-tridiagonal S (co-visibility band narrower
+// than one tile: tile row i couples only with tiles i-1, i+1).  This is the
+// Cholesky factorisation of S in odd-even (nested-dissection) order: at each
+// level the even positions e of the active tile list are eliminated in
+// parallel; their neighbours p < e < q are kept and coupled through e.  Per
+// eliminated tile e (L_e = chol(D_e)):
+//     Lp_e = L(p, e) = C(p, e) L_e^-T,   Lq_e = L(q, e) = C(q, e) L_e^-T,
+//     y_e  = L_e^-1 r_e
+// per kept tile k with eliminated neighbours e- < k < e+ and next kept k2:
+//     D_k -= Lq_{e-} Lq_{e-}^T + Lp_{e+} Lp_{e+}^T,
+//     r_k -= Lq_{e-} y_{e-} + Lp_{e+} y_{e+},
+//     C(k2, k) = -Lq_{e+} Lp_{e+}^T          (fill between the kept tiles)
+// log2(nt) levels instead of nt sequential tile steps.  Back substitution in
+// reverse level order: x_e = L_e^-T (y_e - Lp_e^T x_p - Lq_e^T x_q).
+// C(i, j), i > j, lives in S tile (i, j); Lp / Lq in crL[2][nt][64*64].
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_cr_factor(double *__restrict__ S, long long lds,
+                                                   const int *__restrict__ elim, int nt,
+                                                   double *__restrict__ linv,
+                                                   double *__restrict__ crL,
+                                                   const double *__restrict__ rhs,
+                                                   double *__restrict__ y,
+                                                   double *__restrict__ status)
+{
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double *As = sm, *Bs = sm + NB * LP, *Cs = sm + 2 * NB * LP;
+    __shared__ double rk[NB];
+    __shared__ double part[4][NB];
+    const int tid = threadIdx.x;
+    const int e = elim[3 * blockIdx.x], p = elim[3 * blockIdx.x + 1], q = elim[3 * blockIdx.x + 2];
+    load_tile(S, lds, e, e, As);
+    if (tid < NB) rk[tid] = rhs[(long long)NB * e + tid];
+    __syncthreads();
+    const bool ok = block_potrf_inv(As, Bs);
+    gemv64(Bs, rk, part, y + (long long)NB * e, 1.0);
+    store_rowmajor(linv + (long long)NB * NB * e, Bs);
+    if (tid == 0 && !ok) status[0] = 1.0;
+    d4 acc[2][2];
+    if (p >= 0) {   // C(p, e) = tile(e, p)^T
+        load_tile_t(S, lds, e, p, Cs);
+        __syncthreads();
+        mfma_64x64(Cs, Bs, acc);
+        __syncthreads();
+        acc_to_lds(acc, Cs, 1.0, false);
+        __syncthreads();
+        store_rowmajor(crL + (long long)NB * NB * e, Cs);
+        __syncthreads();
+    }
+    if (q >= 0) {   // C(q, e) = tile(q, e)
+        load_tile(S, lds, q, e, Cs);
+        __syncthreads();
+        mfma_64x64(Cs, Bs, acc);
+        __syncthreads();
+        acc_to_lds(acc, Cs, 1.0, false);
+        __syncthreads();
+        store_rowmajor(crL + (long long)NB * NB * (nt + e), Cs);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_cr_update(double *__restrict__ S, long long lds,
+                                                   const int *__restrict__ keep, int nt,
+                                                   const double *__restrict__ crL,
+                                                   double *__restrict__ rhs,
+                                                   const double *__restrict__ y)
+{
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double *As = sm, *Bs = sm + NB * LP, *Cs = sm + 2 * NB * LP;
+    __shared__ double ym[NB], yp[NB], um[NB], up[NB];
+    __shared__ double part[4][NB];
+    const int tid = threadIdx.x;
+    const int *kp = keep + 4 * blockIdx.x;
+    const int k = kp[0], em = kp[1], ep = kp[2], k2 = kp[3];
+    const long long T2 = (long long)NB * NB;
+    load_tile(S, lds, k, k, As);
+    load_rowmajor(crL + T2 * (nt + em), Bs);   // Lq_{e-} = L(k, e-)
+    if (ep >= 0) load_rowmajor(crL + T2 * ep, Cs);   // Lp_{e+} = L(k, e+)
+    if (tid < NB) {
+        ym[tid] = y[(long long)NB * em + tid];
+        yp[tid] = (ep >= 0) ? y[(long long)NB * ep + tid] : 0.0;
+    }
+    __syncthreads();
+    d4 acc[2][2];
+    mfma_64x64(Bs, Bs, acc);
+    if (ep >= 0) mfma_64x64_acc(Cs, Cs, acc);
+    acc_to_lds(acc, As, -1.0, true);   // each thread updates the elements it owns
+    gemv64(Bs, ym, part, um, 1.0);
+    if (ep >= 0) gemv64(Cs, yp, part, up, 1.0);
+    if (tid < NB) {
+        double r = rhs[(long long)NB * k + tid] - um[tid];
+        if (ep >= 0) r -= up[tid];
+        rhs[(long long)NB * k + tid] = r;
+    }
+    __syncthreads();
+    store_tile(S, lds, k, k, As);
+    if (k2 >= 0) {   // C(k2, k) = -Lq_{e+} Lp_{e+}^T
+        __syncthreads();
+        load_rowmajor(crL + T2 * (nt + ep), Bs);
+        __syncthreads();
+        mfma_64x64(Bs, Cs, acc);
+        __syncthreads();
+        acc_to_lds(acc, As, -1.0, false);
+        __syncthreads();
+        store_tile(S, lds, k2, k, As);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_cr_back(const int *__restrict__ elim, int nt,
+                                                 const double *__restrict__ linv,
+                                                 const double *__restrict__ crL,
+                                                 const double *__restrict__ y,
+                                                 double *__restrict__ x)
+{
+    __shared__ double Ls[NB * LP];
+    __shared__ double t[NB], u[NB];
+    __shared__ double part[4][NB];
+    const int tid = threadIdx.x;
+    const int e = elim[3 * blockIdx.x], p = elim[3 * blockIdx.x + 1], q = elim[3 * blockIdx.x + 2];
+    const long long T2 = (long long)NB * NB;
+    if (tid < NB) t[tid] = y[(long long)NB * e + tid];
+    if (p >= 0) {
+        load_rowmajor(crL + T2 * e, Ls);
+        if (tid < NB) u[tid] = x[(long long)NB * p + tid];
+        __syncthreads();
+        gemv64_t(Ls, u, part, u, 1.0);
+        if (tid < NB) t[tid] -= u[tid];
+        __syncthreads();
+    }
+    if (q >= 0) {
+        load_rowmajor(crL + T2 * (nt + e), Ls);
+        if (tid < NB) u[tid] = x[(long long)NB * q + tid];
+        __syncthreads();
+        gemv64_t(Ls, u, part, u, 1.0);
+        if (tid < NB) t[tid] -= u[tid];
+        __syncthreads();
+    }
+    load_rowmajor(linv + T2 * e, Ls);
+    __syncthreads();
+    gemv64_t(Ls, t, part, x + (long long)NB * e, 1.0);
+}
+
 // zero every envelope tile of S (fill from the previous factorisation)
 __global__ void k_zero_env(double *__restrict__ S, long long lds, const int *__restrict__ env)
 {
@@ -477,6 +661,48 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
                 env.push_back(k);
             }
     d->n_env = (int)env.size() / 2;
+    // cyclic reduction when S is tile-tridiagonal (dense_solve 0 = auto)
+    bool tridiag = d->dense_solve == 0 && nt > 1;
+    for (int i = 1; tridiag && i < nt; i++)
+        if (d->h_tfirst[i] < i - 1) tridiag = false;
+    d->cr_nlev = 0;
+    if (tridiag) {
+        std::vector<int> act(nt), elim, keep, eptr{0}, kptr{0};
+        for (int i = 0; i < nt; i++) act[i] = i;
+        while (!act.empty()) {
+            const int len = (int)act.size();
+            std::vector<int> next;
+            for (int t = 0; t < len; t++) {
+                if ((t & 1) == 0) {
+                    elim.push_back(act[t]);
+                    elim.push_back(t > 0 ? act[t - 1] : -1);
+                    elim.push_back(t + 1 < len ? act[t + 1] : -1);
+                } else {
+                    keep.push_back(act[t]);
+                    keep.push_back(act[t - 1]);
+                    keep.push_back(t + 1 < len ? act[t + 1] : -1);
+                    keep.push_back(t + 2 < len ? act[t + 2] : -1);
+                    next.push_back(act[t]);
+                }
+            }
+            eptr.push_back((int)elim.size() / 3);
+            kptr.push_back((int)keep.size() / 4);
+            act.swap(next);
+        }
+        d->cr_nlev = (int)eptr.size() - 1;
+        d->cr_eptr_h = new int[eptr.size()];
+        d->cr_kptr_h = new int[kptr.size()];
+        for (size_t q = 0; q < eptr.size(); q++) d->cr_eptr_h[q] = eptr[q];
+        for (size_t q = 0; q < kptr.size(); q++) d->cr_kptr_h[q] = kptr[q];
+        VLGBA_CHECK(hipMalloc(&d->cr_elim, sizeof(int) * elim.size()));
+        VLGBA_CHECK(hipMalloc(&d->cr_keep, sizeof(int) * (keep.size() + 1)));
+        VLGBA_CHECK(hipMalloc(&d->crL, sizeof(double) * 2 * (size_t)nt * NB * NB));
+        VLGBA_CHECK(hipMemcpyAsync(d->cr_elim, elim.data(), sizeof(int) * elim.size(),
+                                   hipMemcpyHostToDevice, d->stream));
+        if (!keep.empty())
+            VLGBA_CHECK(hipMemcpyAsync(d->cr_keep, keep.data(), sizeof(int) * keep.size(),
+                                       hipMemcpyHostToDevice, d->stream));
+    }
     d->pan_ptr_h = new int[nt + 1];
     for (int k = 0; k <= nt; k++) d->pan_ptr_h[k] = ptr[k];
     VLGBA_CHECK(hipMalloc(&d->pan_list, sizeof(int) * (list.size() + 1)));
@@ -495,6 +721,15 @@ void ba_chol_free(ba_dev *d)
 {
     delete[] d->h_tfirst;
     delete[] d->pan_ptr_h;
+    delete[] d->cr_eptr_h;
+    delete[] d->cr_kptr_h;
+    d->cr_eptr_h = d->cr_kptr_h = nullptr;
+    if (d->cr_elim) (void)hipFree(d->cr_elim);
+    if (d->cr_keep) (void)hipFree(d->cr_keep);
+    if (d->crL) (void)hipFree(d->crL);
+    d->cr_elim = d->cr_keep = nullptr;
+    d->crL = nullptr;
+    d->cr_nlev = 0;
     if (d->pan_list) (void)hipFree(d->pan_list);
     if (d->env_tiles) (void)hipFree(d->env_tiles);
     d->h_tfirst = d->pan_ptr_h = nullptr;
@@ -522,11 +757,40 @@ int ba_chol_solve(ba_dev *d)
     if (!attr_done) {
         VLGBA_CHECK(hipFuncSetAttribute((const void *)k_factor_panel,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem3));
+        VLGBA_CHECK(hipFuncSetAttribute((const void *)k_cr_factor,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem3));
+        VLGBA_CHECK(hipFuncSetAttribute((const void *)k_cr_update,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem3));
         VLGBA_CHECK(hipFuncSetAttribute((const void *)k_syrk,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
         attr_done = true;
     }
     VLGBA_CHECK(hipMemsetAsync(d->scal + 4, 0, sizeof(double), d->stream));
+    if (d->cr_nlev > 0) {
+        for (int l = 0; l < d->cr_nlev; l++) {
+            const int e0 = d->cr_eptr_h[l], ne = d->cr_eptr_h[l + 1] - e0;
+            const int k0 = d->cr_kptr_h[l], nk = d->cr_kptr_h[l + 1] - k0;
+            KT_B(d);
+            k_cr_factor<<<ne, 256, smem3, d->stream>>>(d->S, d->lds, d->cr_elim + 3 * e0, nt,
+                                                       d->linv, d->crL, d->rhs, d->ywork,
+                                                       d->scal + 4);
+            KT_E(d, KT_CR_FACTOR);
+            if (nk > 0) {
+                KT_B(d);
+                k_cr_update<<<nk, 256, smem3, d->stream>>>(d->S, d->lds, d->cr_keep + 4 * k0, nt,
+                                                           d->crL, d->rhs, d->ywork);
+                KT_E(d, KT_CR_UPDATE);
+            }
+        }
+        for (int l = d->cr_nlev - 1; l >= 0; l--) {
+            const int e0 = d->cr_eptr_h[l], ne = d->cr_eptr_h[l + 1] - e0;
+            KT_B(d);
+            k_cr_back<<<ne, 256, 0, d->stream>>>(d->cr_elim + 3 * e0, nt, d->linv, d->crL,
+                                                 d->ywork, d->da);
+            KT_E(d, KT_CR_BACK);
+        }
+        return -(int)hipGetLastError();
+    }
     for (int k = 0; k < nt; k++) {
         const int p0 = d->pan_ptr_h[k], T = d->pan_ptr_h[k + 1] - p0;
         // a single panel tile (narrow envelope) applies its own trailing update

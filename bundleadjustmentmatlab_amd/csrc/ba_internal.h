@@ -33,7 +33,8 @@
 // pass the elapsed times are summed per kernel.
 enum {
     KT_ROT, KT_LIN, KT_CAMRED, KT_DAMP, KT_SCHUR, KT_SCHUR_CHUNK, KT_SCHUR_RED,
-    KT_ASSEMBLE, KT_FACTOR, KT_SYRK, KT_BACKWARD, KT_CAMUPD, KT_PTUPD, KT_N
+    KT_ASSEMBLE, KT_FACTOR, KT_SYRK, KT_BACKWARD, KT_CAMUPD, KT_PTUPD, KT_CR_FACTOR,
+    KT_CR_UPDATE, KT_CR_BACK, KT_N
 };
 #define KT_MAX_EV 8192
 struct ba_ktimer {
@@ -84,7 +85,13 @@ struct ba_dev {
     int *pan_list;     // device: tile rows i > k with tfirst[i] <= k, per k
     int *env_tiles;    // device [n_env][2] (i, k) tiles inside the envelope
     int n_env;
-    int dense_solve;   // 1: ignore the envelope (every lower tile, for measurement)
+    int dense_solve;   // 0 auto, 1: every lower tile (measurement), 2: envelope, no CR
+    // block cyclic reduction (tile-tridiagonal S): per level, eliminated tiles
+    // (e, p, q) and kept tiles (k, e-, e+, k2); -1 = none
+    int cr_nlev;
+    int *cr_eptr_h, *cr_kptr_h;   // host [nlev+1]
+    int *cr_elim, *cr_keep;       // device [3 * ne], [4 * nk]
+    double *crL;                  // [2][nt][64*64] L(p, e) | L(q, e)
     // reductions: partial sums per block of the reducing kernels, in fixed order
     double *part;      // [3][PART_MAX]
     double *scal;      // [8] : 0 old_sse, 1 new_sse, 2 dpg, 3 chol_status ...
@@ -106,7 +113,10 @@ struct ba_dev {
     int *cam_eptr, *cam_eslots; // per camera: its e-slots in chunk order
     double *spart;     // [ns][NA*NA]
     double *epart;     // [nes][NA]
+    double *upart;     // [nes][NA(NA+1)/2 + NA] per-chunk U_j (lower) | eA_j partials
+    double *chsse;     // [nch] per-chunk SSE partials of the linearisation
     int ns, nes;
+    int ch_max_terms, ch_max_slots;   // per-chunk maxima: LDS staging of the term lists
     // optional outputs / inputs of the MEX-compatible stage entries (else NULL)
     double *xh_out;    // [N][2] projections (stage 1 and stage 3)
     double *B_out;     // [N][6] point Jacobians (stage 1)
@@ -125,6 +135,8 @@ struct ba_dev {
 #define BA_PART_MAX 65536
 #define BA_CH_OBS 128      // observations per Schur chunk (LDS budget)
 #define BA_CH_PTS 64       // points per Schur chunk
+#define BA_CH_TERMS 4096   // (obs, obs) terms per chunk: a track of <= 90 observations
+#define BA_CH_SLOTS 1024   // co-visible blocks touched per chunk
 
 // ---- ba_kernels.hip ----
 int ba_launch_rotations(ba_dev *d, const double *a, double *rot, int all5);

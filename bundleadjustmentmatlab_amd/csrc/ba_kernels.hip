@@ -184,6 +184,184 @@ __global__ __launch_bounds__(256) void k_linearize(
 }
 
 // -------------------------------------------------------------------------
+// Fast-path linearisation, one workgroup per Schur chunk (<= 128 observations
+// of consecutive points), two lanes per observation: lane 0 projects the base
+// point and the first HA camera columns, lane 1 the base point, the remaining
+// camera columns and the three point columns (same expressions as
+// k_linearize).  A, B, e go to LDS; then per observation W_ij (one contiguous,
+// coalesced HBM range per chunk), per point V_i / eB_i (sequential over the
+// point's cameras, as k_linearize), per camera of the chunk one partial of
+// U_j / eA_j (sequential over the chunk's points), reduced per camera in chunk
+// order by k_camera_reduce_chunks.  jrec is never written.
+// -------------------------------------------------------------------------
+template <int NA>
+__global__ __launch_bounds__(256) void k_linearize_chunk(
+    const int *__restrict__ ch_pt, const int *__restrict__ ch_eslot,
+    const int *__restrict__ eslot_optr, const unsigned short *__restrict__ eslot_obs,
+    const int *__restrict__ pt_ptr, const int *__restrict__ obs_cam,
+    const double *__restrict__ obs_x, const double *__restrict__ K4,
+    const double *__restrict__ a, const double *__restrict__ rot,
+    const double *__restrict__ b, ba_flags f, const unsigned char *__restrict__ pivot,
+    double *__restrict__ W, double *__restrict__ V, double *__restrict__ eB,
+    double *__restrict__ upart, double *__restrict__ part_sse)
+{
+    constexpr int NVK = NA - 6;
+    constexpr int HA = (NA + 4) / 2;        // lane 0: base + A[0, HA)
+    constexpr int RS = 2 * NA + 8;          // LDS row: A (2 NA), B (6), e (2)
+    constexpr int NU = NA * (NA + 1) / 2;
+    __shared__ double rows[BA_CH_OBS * RS];
+    __shared__ int lpt[BA_CH_OBS];
+    __shared__ int eoff[BA_CH_OBS + 1];
+    __shared__ unsigned short eobl[BA_CH_OBS];
+    const int ch = blockIdx.x, tid = threadIdx.x;
+    const int p0 = ch_pt[ch], p1 = ch_pt[ch + 1], np = p1 - p0;
+    const int obase = pt_ptr[p0], nobs = pt_ptr[p1] - obase;
+    const int e0 = ch_eslot[ch], nes = ch_eslot[ch + 1] - e0;
+    if (tid < np)
+        for (int o = pt_ptr[p0 + tid]; o < pt_ptr[p0 + tid + 1]; o++) lpt[o - obase] = tid;
+    {
+        const int u0 = eslot_optr[e0], nu = eslot_optr[e0 + nes] - u0;
+        for (int q = tid; q < nu; q += 256) eobl[q] = eslot_obs[u0 + q];
+        for (int q = tid; q <= nes; q += 256) eoff[q] = eslot_optr[e0 + q] - u0;
+    }
+    __syncthreads();
+    double sse = 0.0;
+    {
+        const int lo = tid >> 1, half = tid & 1;
+        if (lo < nobs) {
+            const int o = obase + lo, j = obs_cam[o], i = p0 + lpt[lo];
+            const double bi[3] = {b[3 * (size_t)i], b[3 * (size_t)i + 1],
+                                  b[3 * (size_t)i + 2]};
+            double a0[NA], k4[4], Rl[9];
+#pragma unroll
+            for (int c = 0; c < NA; c++) a0[c] = a[(size_t)NA * j + c];
+#pragma unroll
+            for (int c = 0; c < 4; c++) k4[c] = K4[4 * (size_t)j + c];
+            const double *R = rot + 45 * (size_t)j;
+#pragma unroll
+            for (int q = 0; q < 9; q++) Rl[q] = R[q];
+            double Kc[9], xh[2];
+            vlg_calib(Kc, k4, a0, NVK);
+            vlg_project(Kc, Rl, a0 + 3, bi, xh);
+            double *row = rows + RS * lo;
+            const int k0 = half ? HA : 0, k1 = half ? NA : HA;
+            for (int k = k0; k < k1; k++) {   // camera columns (mex_bundle_1 :201-209)
+                double a1[NA], Kc1[9], Rk[9], x1[2];
+#pragma unroll
+                for (int c = 0; c < NA; c++) a1[c] = a0[c] + H_FD * ((c == k) ? 1.0 : 0.0);
+                vlg_calib(Kc1, k4, a1, NVK);
+                const double *Rs = R + 9 * ((k < 3) ? (1 + k) : 4);
+#pragma unroll
+                for (int q = 0; q < 9; q++) Rk[q] = Rs[q];
+                vlg_project(Kc1, Rk, a1 + 3, bi, x1);
+                row[2 * k] = (x1[0] - xh[0]) / H_FD;
+                row[2 * k + 1] = (x1[1] - xh[1]) / H_FD;
+            }
+            if (half) {
+#pragma unroll
+                for (int k = 0; k < 3; k++) {   // point columns (:211-219)
+                    double b1[3], x1[2];
+#pragma unroll
+                    for (int c = 0; c < 3; c++) b1[c] = bi[c] + H_FD * ((c == k) ? 1.0 : 0.0);
+                    vlg_project(Kc, Rl, a0 + 3, b1, x1);
+                    row[2 * NA + 2 * k] = (x1[0] - xh[0]) / H_FD;
+                    row[2 * NA + 2 * k + 1] = (x1[1] - xh[1]) / H_FD;
+                }
+            } else {
+                const double e0 = obs_x[2 * (size_t)o] - xh[0];
+                const double e1 = obs_x[2 * (size_t)o + 1] - xh[1];
+                row[2 * NA + 6] = e0;
+                row[2 * NA + 7] = e1;
+                sse = e0 * e0 + e1 * e1;
+            }
+        }
+    }
+    __syncthreads();
+    // W_ij = A^T B onto a zeroed output (:305-314): the chunk's rows are contiguous
+    {
+        double *wdst = W + (size_t)3 * NA * obase;
+        for (int q = tid; q < nobs * 3 * NA; q += 256) {
+            const int lo = q / (3 * NA), e = q % (3 * NA), r = e % NA, c = e / NA;
+            const int j = obs_cam[obase + lo];
+            const bool wzero = f.fix_structure || f.fix_motion || (f.has_pivot && pivot[j]);
+            const double *row = rows + RS * lo;
+            const double *B = row + 2 * NA;
+            wdst[q] = wzero ? 0.0 : 0.0 + (row[2 * r] * B[2 * c] + row[2 * r + 1] * B[2 * c + 1]);
+        }
+    }
+    // V_i += B^T B, eB_i += B^T e over the point's cameras (:293-302, :326-332)
+    for (int q = tid; q < np * 12; q += 256) {
+        const int pl = q / 12, e = q % 12, i = p0 + pl;
+        const int lo0 = pt_ptr[i] - obase, lo1 = pt_ptr[i + 1] - obase;
+        double acc = 0.0;
+        if (e < 9) {
+            const int r = e % 3, c = e / 3;
+            for (int lo = lo0; lo < lo1; lo++) {
+                const double *B = rows + RS * lo + 2 * NA;
+                acc += B[2 * r] * B[2 * c] + B[2 * r + 1] * B[2 * c + 1];
+            }
+        } else {
+            const int r = e - 9;
+            for (int lo = lo0; lo < lo1; lo++) {
+                const double *B = rows + RS * lo + 2 * NA;
+                acc += B[2 * r] * B[6] + B[2 * r + 1] * B[7];
+            }
+        }
+        if (f.fix_structure) acc = 0.0;
+        if (e < 9) V[9 * (size_t)i + e] = acc;
+        else eB[3 * (size_t)i + e - 9] = acc;
+    }
+    // U_j (lower triangle) / eA_j partials per camera of the chunk
+    for (int q = tid; q < nes * (NU + NA); q += 256) {
+        const int s = q / (NU + NA), l = q % (NU + NA);
+        int r, c;
+        if (l < NU) {
+            int t = l;
+            c = 0;
+            while (t >= NA - c) { t -= NA - c; c++; }
+            r = c + t;
+        } else {
+            r = l - NU;
+            c = NA;   // e occupies the column after B: row[2 NA + 6]
+        }
+        const int cc = (c < NA) ? 2 * c : 2 * NA + 6;
+        double acc = 0.0;
+        for (int u = eoff[s]; u < eoff[s + 1]; u++) {
+            const double *row = rows + RS * eobl[u];
+            acc += row[2 * r] * row[cc] + row[2 * r + 1] * row[cc + 1];
+        }
+        upart[(size_t)(NU + NA) * (e0 + s) + l] = acc;
+    }
+    block_sum_to<256>(sse, part_sse + blockIdx.x);
+}
+
+// U_j, eA_j from the per-chunk partials, in chunk order (fast path)
+template <int NA>
+__global__ void k_camera_reduce_chunks(const int *__restrict__ cam_eptr,
+                                       const int *__restrict__ cam_eslots,
+                                       const double *__restrict__ upart, int m, ba_flags f,
+                                       const unsigned char *__restrict__ pivot,
+                                       double *__restrict__ U, double *__restrict__ eA)
+{
+    constexpr int NU = NA * (NA + 1) / 2;
+    const int j = blockIdx.x, l = threadIdx.x;
+    if (j >= m || l >= NU + NA) return;
+    double acc = 0.0;
+    for (int q = cam_eptr[j]; q < cam_eptr[j + 1]; q++)
+        acc += upart[(size_t)(NU + NA) * cam_eslots[q] + l];
+    if (f.fix_motion || (f.has_pivot && pivot[j])) acc = 0.0;
+    if (l < NU) {
+        int t = l, c = 0;
+        while (t >= NA - c) { t -= NA - c; c++; }
+        const int r = c + t;
+        U[(size_t)NA * NA * j + r + NA * c] = acc;
+        U[(size_t)NA * NA * j + c + NA * r] = acc;
+    } else {
+        eA[(size_t)NA * j + l - NU] = acc;
+    }
+}
+
+// -------------------------------------------------------------------------
 // U_j, eA_j: one workgroup per camera, each output owned by one lane and
 // summed sequentially over the camera's observations in ascending point order
 // (= mex_bundle_1_XABeUVWeAeB.c:266-323 with the exact zeros skipped).
@@ -354,7 +532,7 @@ __global__ __launch_bounds__(256) void k_schur_chunk(
     const unsigned short *__restrict__ slot_term, const int *__restrict__ eslot_optr,
     const unsigned short *__restrict__ eslot_obs, const int *__restrict__ pt_ptr,
     const double *__restrict__ V, const double *__restrict__ eB, const double *__restrict__ W,
-    double lambda, double *__restrict__ Vinv, double *__restrict__ spart,
+    double lambda, int tcap, int scap, double *__restrict__ Vinv, double *__restrict__ spart,
     double *__restrict__ epart)
 {
     constexpr int WS = 3 * NA;
@@ -365,14 +543,31 @@ __global__ __launch_bounds__(256) void k_schur_chunk(
     double *Vl = tl + BA_CH_OBS * NA;               // [CH_PTS][9]
     double *El = Vl + BA_CH_PTS * 9;                // [CH_PTS][3]
     int *lpt = (int *)(El + BA_CH_PTS * 3);         // [CH_OBS]
+    unsigned *terml = (unsigned *)(lpt + BA_CH_OBS);   // [tcap] (y obs | w obs << 16)
+    int *soff = (int *)(terml + tcap);                  // [scap+1] slot term offsets
+    int *eoff = soff + scap + 1;                        // [CH_OBS+1] e-slot obs offsets
+    unsigned short *eobl = (unsigned short *)(eoff + BA_CH_OBS + 1);   // [CH_OBS]
     const int ch = blockIdx.x, tid = threadIdx.x;
     const int p0 = ch_pt[ch], p1 = ch_pt[ch + 1], np = p1 - p0;
     const int obase = pt_ptr[p0], nobs = pt_ptr[p1] - obase;
+    const int s0 = ch_slot[ch], ns = ch_slot[ch + 1] - s0;
+    const int e0 = ch_eslot[ch], nes = ch_eslot[ch + 1] - e0;
     // W rows: one contiguous range (coalesced 8-byte loads)
     {
         const double *src = W + (size_t)WS * obase;
         const int nw = nobs * WS;
         for (int q = tid; q < nw; q += 256) Wl[q] = src[q];
+    }
+    // the chunk's term and e-slot lists (contiguous: slots are numbered chunk-major),
+    // so the accumulation loops below touch LDS only
+    {
+        const int t0 = slot_tptr[s0], nt = slot_tptr[s0 + ns] - t0;
+        const unsigned *src = (const unsigned *)slot_term + t0;
+        for (int q = tid; q < nt; q += 256) terml[q] = src[q];
+        for (int q = tid; q <= ns; q += 256) soff[q] = slot_tptr[s0 + q] - t0;
+        const int u0 = eslot_optr[e0], nu = eslot_optr[e0 + nes] - u0;
+        for (int q = tid; q < nu; q += 256) eobl[q] = eslot_obs[u0 + q];
+        for (int q = tid; q <= nes; q += 256) eoff[q] = eslot_optr[e0 + q] - u0;
     }
     // per point: V* -> V*^-1, eB, local obs -> point map
     if (tid < np) {
@@ -409,24 +604,43 @@ __global__ __launch_bounds__(256) void k_schur_chunk(
         tl[q] = y[r] * eb[0] + y[r + NA] * eb[1] + y[r + 2 * NA] * eb[2];
     }
     __syncthreads();
-    // block partials: sum over the chunk's terms (points ascending)
-    const int s0 = ch_slot[ch], ns = ch_slot[ch + 1] - s0;
-    for (int q = tid; q < ns * NA * NA; q += 256) {
-        const int s = s0 + q / (NA * NA), e = q % (NA * NA), r = e % NA, c = e / NA;
-        double acc = 0.0;
-        for (int u = slot_tptr[s]; u < slot_tptr[s + 1]; u++) {
-            const double *y = Yl + WS * slot_term[2 * u];
-            const double *w = Wl + WS * slot_term[2 * u + 1];
-            acc += y[r] * w[c] + y[r + NA] * w[c + NA] + y[r + 2 * NA] * w[c + 2 * NA];
+    // block partials: sum over the chunk's terms (points ascending).  One lane
+    // per (slot, column pair): the term's Y row block is read once for 2 NA
+    // outputs (LDS-instruction bound otherwise); every entry keeps the
+    // per-term expression and the term order of k_schur.
+    constexpr int NCP = (NA + 1) / 2;
+    for (int q = tid; q < ns * NCP; q += 256) {
+        const int s = q / NCP, c0 = 2 * (q % NCP);
+        const bool two = c0 + 1 < NA;
+        double acc0[NA], acc1[NA];
+#pragma unroll
+        for (int r = 0; r < NA; r++) acc0[r] = acc1[r] = 0.0;
+        for (int u = soff[s]; u < soff[s + 1]; u++) {
+            const unsigned tw = terml[u];
+            const double *y = Yl + WS * (tw & 0xffffu);
+            const double *w = Wl + WS * (tw >> 16);
+            const double wa0 = w[c0], wa1 = w[c0 + NA], wa2 = w[c0 + 2 * NA];
+            const int c1 = two ? c0 + 1 : c0;
+            const double wb0 = w[c1], wb1 = w[c1 + NA], wb2 = w[c1 + 2 * NA];
+#pragma unroll
+            for (int r = 0; r < NA; r++) {
+                const double y0 = y[r], y1 = y[r + NA], y2 = y[r + 2 * NA];
+                acc0[r] += y0 * wa0 + y1 * wa1 + y2 * wa2;
+                acc1[r] += y0 * wb0 + y1 * wb1 + y2 * wb2;
+            }
         }
-        spart[(size_t)NA * NA * s + e] = acc;
+        double *dst = spart + (size_t)NA * NA * (s0 + s);
+#pragma unroll
+        for (int r = 0; r < NA; r++) {
+            dst[r + NA * c0] = acc0[r];
+            if (two) dst[r + NA * (c0 + 1)] = acc1[r];
+        }
     }
-    const int e0 = ch_eslot[ch], nes = ch_eslot[ch + 1] - e0;
     for (int q = tid; q < nes * NA; q += 256) {
-        const int s = e0 + q / NA, r = q % NA;
+        const int s = q / NA, r = q % NA;
         double acc = 0.0;
-        for (int u = eslot_optr[s]; u < eslot_optr[s + 1]; u++) acc += tl[NA * eslot_obs[u] + r];
-        epart[(size_t)NA * s + r] = acc;
+        for (int u = eoff[s]; u < eoff[s + 1]; u++) acc += tl[NA * eobl[u] + r];
+        epart[(size_t)NA * (e0 + s) + r] = acc;
     }
 }
 
@@ -637,6 +851,17 @@ int ba_launch_rotations(ba_dev *d, const double *a, double *rot, int all5)
 
 int ba_launch_linearize(ba_dev *d, ba_flags f)
 {
+    if (!d->ordered) {
+        KT_B(d);
+        if (d->nch > 0)
+            BA_DISPATCH(d->na, (k_linearize_chunk<NA><<<d->nch, 256, 0, d->stream>>>(
+                                   d->ch_pt, d->ch_eslot, d->eslot_optr, d->eslot_obs,
+                                   d->pt_ptr, d->obs_cam, d->obs_x, d->K4, d->a, d->rot, d->b,
+                                   f, d->pivot, d->W, d->V, d->eB, d->upart, d->chsse)));
+        KT_E(d, KT_LIN);
+        k_sum_parts<<<1, 256, 0, d->stream>>>(d->chsse, d->nch, d->scal + 0);
+        return -(int)hipGetLastError();
+    }
     const int g = grid_for(d->n, 256, PT_GRID_CAP);
     KT_B(d);
     BA_DISPATCH(d->na, (k_linearize<NA><<<g, 256, 0, d->stream>>>(
@@ -651,6 +876,14 @@ int ba_launch_linearize(ba_dev *d, ba_flags f)
 int ba_launch_camera_reduce(ba_dev *d, ba_flags f)
 {
     const int bs = (d->na * (d->na + 1) / 2 + d->na) <= 64 ? 64 : 128;
+    if (!d->ordered) {
+        KT_B(d);
+        BA_DISPATCH(d->na, (k_camera_reduce_chunks<NA><<<d->m, bs, 0, d->stream>>>(
+                               d->cam_eptr, d->cam_eslots, d->upart, d->m, f, d->pivot, d->U,
+                               d->eA)));
+        KT_E(d, KT_CAMRED);
+        return -(int)hipGetLastError();
+    }
     KT_B(d);
     BA_DISPATCH(d->na, (k_camera_reduce<NA><<<d->m, bs, 0, d->stream>>>(
                            d->cam_ptr, d->cam_obs, d->jrec, d->m, f, d->pivot, d->U, d->eA)));
@@ -682,20 +915,23 @@ int ba_launch_schur(ba_dev *d, double lambda)
 template <int NA>
 static int launch_schur_fast(ba_dev *d, double lambda)
 {
-    const size_t smem = sizeof(double) * (2 * BA_CH_OBS * 3 * NA + BA_CH_OBS * NA +
-                                          BA_CH_PTS * 12) +
-                        sizeof(int) * BA_CH_OBS;
-    static bool attr = false;
-    if (!attr) {
+    const int tcap = (d->ch_max_terms + 1) & ~1, scap = d->ch_max_slots;
+    size_t smem = sizeof(double) * (2 * BA_CH_OBS * 3 * NA + BA_CH_OBS * NA + BA_CH_PTS * 12) +
+                  sizeof(int) * BA_CH_OBS + sizeof(unsigned) * tcap +
+                  sizeof(int) * (scap + 1 + BA_CH_OBS + 1) + sizeof(unsigned short) * BA_CH_OBS;
+    smem = (smem + 15) & ~(size_t)15;
+    static size_t attr = 0;
+    if (smem > attr) {
         VLGBA_CHECK(hipFuncSetAttribute((const void *)k_schur_chunk<NA>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-        attr = true;
+        attr = smem;
     }
     KT_B(d);
     if (d->nch > 0)
         k_schur_chunk<NA><<<d->nch, 256, smem, d->stream>>>(
             d->ch_pt, d->ch_slot, d->ch_eslot, d->slot_tptr, d->slot_term, d->eslot_optr,
-            d->eslot_obs, d->pt_ptr, d->V, d->eB, d->W, lambda, d->Vinv, d->spart, d->epart);
+            d->eslot_obs, d->pt_ptr, d->V, d->eB, d->W, lambda, tcap, scap, d->Vinv, d->spart,
+            d->epart);
     KT_E(d, KT_SCHUR_CHUNK);
     const int bs = (NA * NA + NA) <= 64 ? 64 : 128;
     KT_B(d);

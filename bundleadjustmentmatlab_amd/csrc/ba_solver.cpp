@@ -186,6 +186,7 @@ struct host_plan {
     std::vector<int> ch_pt, ch_slot, ch_eslot, slot_blk, slot_tptr, eslot_optr;
     std::vector<unsigned short> slot_term, eslot_obs;
     std::vector<int> blk_sptr, blk_slots, cam_eptr, cam_eslots;
+    int max_terms = 0, max_slots = 0;   // per chunk (LDS staging size)
 };
 
 bool build_plan(int m, const std::vector<int> &lptr, const std::vector<int> &lcam,
@@ -193,8 +194,13 @@ bool build_plan(int m, const std::vector<int> &lptr, const std::vector<int> &lca
 {
     const int n = (int)lptr.size() - 1;
     const int nb = (int)hb.jk.size() / 2;
+    auto pt_terms = [&](int i) {
+        const long long k = lptr[i + 1] - lptr[i];
+        return k * (k + 1) / 2;
+    };
     for (int i = 0; i < n; i++)
-        if (lptr[i + 1] - lptr[i] > BA_CH_OBS) return false;
+        if (lptr[i + 1] - lptr[i] > BA_CH_OBS || pt_terms(i) > BA_CH_TERMS) return false;
+    P.max_terms = P.max_slots = 0;
     std::vector<int> slot_of(nb, -1), eslot_of(m, -1), touched, tcam;
     std::vector<std::vector<std::pair<int, int>>> terms;   // per local slot
     std::vector<std::vector<int>> eobs;                     // per local e-slot
@@ -207,7 +213,11 @@ bool build_plan(int m, const std::vector<int> &lptr, const std::vector<int> &lca
     while (p < n) {
         const int obase = lptr[p];
         int q = p;
-        while (q < n && q - p < BA_CH_PTS && lptr[q + 1] - obase <= BA_CH_OBS) q++;
+        long long nterm = 0;
+        while (q < n && q - p < BA_CH_PTS && lptr[q + 1] - obase <= BA_CH_OBS &&
+               nterm + pt_terms(q) <= BA_CH_TERMS)
+            nterm += pt_terms(q++);
+        P.max_terms = std::max(P.max_terms, (int)nterm);
         touched.clear();
         tcam.clear();
         terms.clear();
@@ -233,6 +243,7 @@ bool build_plan(int m, const std::vector<int> &lptr, const std::vector<int> &lca
                     terms[slot_of[blk]].push_back({a - obase, b - obase});
                 }
             }
+        P.max_slots = std::max(P.max_slots, (int)touched.size());
         for (size_t s = 0; s < touched.size(); s++) {
             P.slot_blk.push_back(touched[s]);
             for (auto &t : terms[s]) {
@@ -390,15 +401,21 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         for (int o = 0; o < d.N; o++) cobs[pos[lcam[o]]++] = o;
     }
     bool fast = !d.ordered && !stage_mode;
-    for (int i = 0; fast && i < d.n; i++)
-        if (lptr[i + 1] - lptr[i] > BA_CH_OBS) fast = false;   // very long track
-    if (!fast) d.ordered = 1;
+    for (int i = 0; fast && i < d.n; i++) {   // very long track: sequential kernels
+        const long long k = lptr[i + 1] - lptr[i];
+        if (k > BA_CH_OBS || k * (k + 1) / 2 > BA_CH_TERMS) fast = false;
+    }
     host_blocks hb;
+    host_plan plan;
     build_blocks(p->m, pt_ptr_all, h.cam, c->p0, c->p1, o0, lower_blocks, all_diag, !fast, hb);
+    if (fast && !build_plan(p->m, lptr, lcam, hb, plan)) {
+        fast = false;
+        hb = host_blocks();
+        build_blocks(p->m, pt_ptr_all, h.cam, c->p0, c->p1, o0, lower_blocks, all_diag, true, hb);
+    }
+    if (!fast) d.ordered = 1;
     d.nb = (int)hb.jk.size() / 2;
     d.T = (long long)hb.term.size() / 2;
-    host_plan plan;
-    if (fast) build_plan(p->m, lptr, lcam, hb, plan);
 
     TRY(ctx_alloc(c, &d.obs_cam, d.N));
     TRY(ctx_alloc(c, &d.pt_ptr, d.n + 1));
@@ -412,15 +429,17 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
     TRY(ctx_alloc(c, &d.b_new, 3 * (size_t)d.n));
     TRY(ctx_alloc(c, &d.rot, 45 * (size_t)p->m));
     TRY(ctx_alloc(c, &d.rot_new, 9 * (size_t)p->m));
-    TRY(ctx_alloc(c, &d.jrec, (size_t)d.js * d.N));
     TRY(ctx_alloc(c, &d.W, (size_t)3 * na * d.N));
-    if (!fast) {   // the fast path forms Y and t in LDS only
+    if (!fast) {   // the fast path forms A, e, Y and t in LDS only
+        TRY(ctx_alloc(c, &d.jrec, (size_t)d.js * d.N));
         TRY(ctx_alloc(c, &d.Y, (size_t)3 * na * d.N));
         TRY(ctx_alloc(c, &d.t, (size_t)na * d.N));
     } else {
         d.nch = (int)plan.ch_pt.size() - 1;
         d.ns = (int)plan.slot_blk.size();
         d.nes = (int)plan.eslot_optr.size() - 1;
+        d.ch_max_terms = plan.max_terms;
+        d.ch_max_slots = plan.max_slots;
         TRY(ctx_alloc(c, &d.ch_pt, plan.ch_pt.size()));
         TRY(ctx_alloc(c, &d.ch_slot, plan.ch_slot.size()));
         TRY(ctx_alloc(c, &d.ch_eslot, plan.ch_eslot.size()));
@@ -435,6 +454,8 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         TRY(ctx_alloc(c, &d.cam_eslots, plan.cam_eslots.size()));
         TRY(ctx_alloc(c, &d.spart, (size_t)na * na * d.ns));
         TRY(ctx_alloc(c, &d.epart, (size_t)na * d.nes));
+        TRY(ctx_alloc(c, &d.upart, (size_t)(na * (na + 1) / 2 + na) * d.nes));
+        TRY(ctx_alloc(c, &d.chsse, (size_t)d.nch));
         TRY(upload(d.ch_pt, plan.ch_pt.data(), plan.ch_pt.size(), s));
         TRY(upload(d.ch_slot, plan.ch_slot.data(), plan.ch_slot.size(), s));
         TRY(upload(d.ch_eslot, plan.ch_eslot.data(), plan.ch_eslot.size(), s));
@@ -781,7 +802,8 @@ const char *vlgba_kernel_name(int k)
     static const char *names[KT_N] = {
         "k_rotations", "k_linearize", "k_camera_reduce", "k_damp_point", "k_schur",
         "k_schur_chunk", "k_schur_reduce", "k_assemble", "k_factor_panel", "k_syrk",
-        "k_backward", "k_camera_update", "k_point_update"};
+        "k_backward", "k_camera_update", "k_point_update", "k_cr_factor", "k_cr_update",
+        "k_cr_back"};
     return (k >= 0 && k < KT_N) ? names[k] : "";
 }
 

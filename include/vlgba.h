@@ -58,8 +58,13 @@ typedef struct {
     int rank;
     int world_size;
     const void *comm_id;         /* 128-byte ncclUniqueId from rank 0, or NULL */
-    /* 1: factor every lower tile of the reduced system; 0 (default): skip the
-     * tiles outside its envelope, which are exactly zero (same result)       */
+    /* reduced-camera solve (replaces pinv(S)*e_, bundle_euclid.m:193):
+     * 0 (default) automatic -- block cyclic reduction (odd-even nested
+     *   dissection, log2 depth) when S is tile-tridiagonal (co-visibility
+     *   band narrower than 64 rows), else the envelope tile Cholesky;
+     * 1: tile Cholesky over every lower tile (measurement);
+     * 2: envelope tile Cholesky (tiles outside the envelope are exactly zero,
+     *   so 1 and 2 give identical results)                                   */
     int dense_solve;
     /* 1: "ordered" (parity) mode -- every sum over points runs sequentially in
      * ascending point order exactly as the reference loops do, making the
@@ -123,7 +128,7 @@ int vlgba_phase_ms(vlgba_ctx *ctx, double *ms7);
 /* per-kernel device time accumulated over the passes run with timing on
  * (HIP events around every launch): ms[k], calls[k] for k < VLGBA_NKERNELS,
  * named by vlgba_kernel_name(k); reset = 1 clears the accumulators. */
-#define VLGBA_NKERNELS 13
+#define VLGBA_NKERNELS 16
 int vlgba_kernel_ms(vlgba_ctx *ctx, double *ms, long long *calls, int reset);
 const char *vlgba_kernel_name(int k);
 
