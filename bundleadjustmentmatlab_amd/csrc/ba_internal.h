@@ -111,12 +111,23 @@ struct ba_dev {
     unsigned short *eslot_obs;  // [neo] chunk-local obs indices
     int *blk_sptr, *blk_slots;  // per block: its slots in chunk order
     int *cam_eptr, *cam_eslots; // per camera: its e-slots in chunk order
-    double *spart;     // [ns][NA*NA]
-    double *epart;     // [nes][NA]
+    double *spart;     // [ngs][NA*NA] per group slot
+    double *epart;     // [nge][NA] per group e-slot
     double *upart;     // [nes][NA(NA+1)/2 + NA] per-chunk U_j (lower) | eA_j partials
     double *chsse;     // [nch] per-chunk SSE partials of the linearisation
     int ns, nes;
     int ch_max_terms, ch_max_slots;   // per-chunk maxima: LDS staging of the term lists
+    // Schur groups (consecutive chunks, one workgroup): block / camera partials
+    // accumulate in LDS over the group's chunks and are written once per group
+    int ngrp, ngs, nge;
+    int grp_max_s, grp_max_e;         // LDS accumulator sizes (largest non-direct group)
+    unsigned *blob;                   // per-chunk metadata records (see build_plan)
+    int *ch_blob, *ch_obase;          // [nch+1] record offsets (words), first local obs
+    int max_blob;
+    int *grp_ch, *grp_gs, *grp_ge;    // [ngrp+1] chunk / group-slot / group-eslot ranges
+    unsigned short *cs_g, *ce_g;      // chunk slot / chunk e-slot -> group-local id
+    int *blk_gptr, *blk_gslots;       // per block: its group slots in group order
+    int *cam_gptr, *cam_gslots;       // per camera: its group e-slots in group order
     // optional outputs / inputs of the MEX-compatible stage entries (else NULL)
     double *xh_out;    // [N][2] projections (stage 1 and stage 3)
     double *B_out;     // [N][6] point Jacobians (stage 1)
@@ -136,7 +147,10 @@ struct ba_dev {
 #define BA_CH_OBS 128      // observations per Schur chunk (LDS budget)
 #define BA_CH_PTS 64       // points per Schur chunk
 #define BA_CH_TERMS 4096   // (obs, obs) terms per chunk: a track of <= 90 observations
-#define BA_CH_SLOTS 1024   // co-visible blocks touched per chunk
+#define BA_GACC 4096       // max doubles of LDS block accumulators per Schur group
+#define BA_GE_CAP 128      // cameras per Schur group
+#define BA_GROUPS 2048     // target number of Schur groups (workgroups)
+#define BA_GROUP_CH 64     // max chunks per Schur group
 
 // ---- ba_kernels.hip ----
 int ba_launch_rotations(ba_dev *d, const double *a, double *rot, int all5);

@@ -7,6 +7,8 @@
 //   k_camera_reduce    the per-camera half of :266-334 (U_j, eA_j)
 //   k_damp_point       bundle_euclid.m:168-184 (V* = damp(V), pinv, Y = W V*^-1)
 //   k_schur            mex_bundle_2_Se_.c:72-155 (S_jk, e_) on the co-visible blocks
+//   k_linearize_chunk  fast path: linearisation per chunk of points + U/eA partials
+//   k_schur_group      fast path: damp + V*^-1 + Y + S / e_ partials per group of chunks
 //   k_assemble         dense S for the reduced solve (bundle_euclid.m:193)
 //   k_camera_update    mex_bundle_3_db_new.c:294-298 (a_new) + rotations of a_new
 //   k_point_update     mex_bundle_3_db_new.c:257-324 (db, b_new, new projections)
@@ -515,132 +517,208 @@ __global__ void k_schur(const int *__restrict__ blk_jk, const int *__restrict__ 
 }
 
 // -------------------------------------------------------------------------
-// Fast path: one workgroup per chunk of consecutive points.  The chunk's W
-// rows are one contiguous HBM range (point-major storage): copied to LDS with
-// coalesced loads; per point V* -> V*^-1 (written out for the back
-// substitution); Y = W V*^-1 and t = Y eB formed in LDS (never stored); every
-// co-visible block the chunk touches accumulates sum_i Y_ij W_ik^T over the
-// chunk's points (ascending) into one partial, every camera sum_i Y_ij eB_i.
-// Same per-term expressions as k_damp_point / k_schur; only the grouping of
-// the sums over points differs (chunk partials, reduced in chunk order by
-// k_schur_reduce), so the result is deterministic run to run.
+// Schur groups: one workgroup per group of consecutive chunks (<= BA_CH_OBS
+// observations of consecutive points each).  Software-pipelined: while chunk
+// k is being reduced, chunk k+1's W rows, V / eB and metadata record (one
+// contiguous blob) are in flight into registers.  Per chunk:
+//   V*^-1 per point (bundle_euclid.m:168-180; written for the back substitution)
+//   Y = W V*^-1 in LDS (:182, never stored)
+//   block sums: lane (chunk slot, row half, column pair) sums the chunk's terms
+//     (points ascending) and adds them to the group accumulator of the block
+//   e_ sums per camera: t_o = Y_o eB_i (mex_bundle_2_Se_.c:143-147)
+// Accumulation order per entry: chunks ascending, terms ascending ->
+// deterministic.  A "direct" group (one chunk touching more blocks than the LDS
+// accumulators hold) writes its sums straight to HBM.
 // -------------------------------------------------------------------------
 template <int NA>
-__global__ __launch_bounds__(256) void k_schur_chunk(
-    const int *__restrict__ ch_pt, const int *__restrict__ ch_slot,
-    const int *__restrict__ ch_eslot, const int *__restrict__ slot_tptr,
-    const unsigned short *__restrict__ slot_term, const int *__restrict__ eslot_optr,
-    const unsigned short *__restrict__ eslot_obs, const int *__restrict__ pt_ptr,
-    const double *__restrict__ V, const double *__restrict__ eB, const double *__restrict__ W,
-    double lambda, int tcap, int scap, double *__restrict__ Vinv, double *__restrict__ spart,
+__global__ __launch_bounds__(256) void k_schur_group(
+    const int *__restrict__ grp_ch, const int *__restrict__ grp_gs,
+    const int *__restrict__ grp_ge, const int *__restrict__ ch_pt,
+    const int *__restrict__ ch_obase, const int *__restrict__ ch_blob,
+    const unsigned *__restrict__ blob, const double *__restrict__ V,
+    const double *__restrict__ eB, const double *__restrict__ W, double lambda, int bcap,
+    int gcap, int ecap, double *__restrict__ Vinv, double *__restrict__ spart,
     double *__restrict__ epart)
 {
     constexpr int WS = 3 * NA;
+    constexpr int NR = (NA + 1) / 2;          // rows per half
+    constexpr int NCP = (NA + 1) / 2;         // column pairs
+    constexpr int IT = 2 * NCP;               // lanes per slot
+    constexpr int GS_CAP = BA_GACC / (NA * NA);
+    constexpr int WREG = (BA_CH_OBS * WS + 255) / 256;
+    constexpr int BREG = 4;                   // blob words per lane in registers
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    double *Wl = sm;                                // [CH_OBS][WS]
-    double *Yl = Wl + BA_CH_OBS * WS;               // [CH_OBS][WS]
-    double *tl = Yl + BA_CH_OBS * WS;               // [CH_OBS][NA]
-    double *Vl = tl + BA_CH_OBS * NA;               // [CH_PTS][9]
-    double *El = Vl + BA_CH_PTS * 9;                // [CH_PTS][3]
-    int *lpt = (int *)(El + BA_CH_PTS * 3);         // [CH_OBS]
-    unsigned *terml = (unsigned *)(lpt + BA_CH_OBS);   // [tcap] (y obs | w obs << 16)
-    int *soff = (int *)(terml + tcap);                  // [scap+1] slot term offsets
-    int *eoff = soff + scap + 1;                        // [CH_OBS+1] e-slot obs offsets
-    unsigned short *eobl = (unsigned short *)(eoff + BA_CH_OBS + 1);   // [CH_OBS]
-    const int ch = blockIdx.x, tid = threadIdx.x;
-    const int p0 = ch_pt[ch], p1 = ch_pt[ch + 1], np = p1 - p0;
-    const int obase = pt_ptr[p0], nobs = pt_ptr[p1] - obase;
-    const int s0 = ch_slot[ch], ns = ch_slot[ch + 1] - s0;
-    const int e0 = ch_eslot[ch], nes = ch_eslot[ch + 1] - e0;
-    // W rows: one contiguous range (coalesced 8-byte loads)
-    {
-        const double *src = W + (size_t)WS * obase;
-        const int nw = nobs * WS;
-        for (int q = tid; q < nw; q += 256) Wl[q] = src[q];
+    double *Wl = sm;                                 // [CH_OBS][WS]
+    double *Yl = Wl + BA_CH_OBS * WS;                // [CH_OBS][WS]
+    double *Vl = Yl + BA_CH_OBS * WS;                // [CH_PTS][9]  V*^-1
+    double *El = Vl + BA_CH_PTS * 9;                 // [CH_PTS][3]
+    double *gacc = El + BA_CH_PTS * 3;               // [gcap][NA*NA]
+    double *geacc = gacc + gcap * NA * NA;           // [ecap][NA]
+    unsigned *bl = (unsigned *)(geacc + ecap * NA);  // [bcap] metadata record
+    __shared__ int gp0[BA_GROUP_CH + 1], gob[BA_GROUP_CH + 1], gbo[BA_GROUP_CH + 1];
+    const int g = blockIdx.x, tid = threadIdx.x;
+    const int c0 = grp_ch[g], nc = grp_ch[g + 1] - c0;
+    const int gs0 = grp_gs[g], ngs = grp_gs[g + 1] - gs0;
+    const int ge0 = grp_ge[g], nge = grp_ge[g + 1] - ge0;
+    const bool direct = ngs > GS_CAP;
+    if (!direct) {
+        for (int q = tid; q < ngs * NA * NA; q += 256) gacc[q] = 0.0;
+        for (int q = tid; q < nge * NA; q += 256) geacc[q] = 0.0;
     }
-    // the chunk's term and e-slot lists (contiguous: slots are numbered chunk-major),
-    // so the accumulation loops below touch LDS only
-    {
-        const int t0 = slot_tptr[s0], nt = slot_tptr[s0 + ns] - t0;
-        const unsigned *src = (const unsigned *)slot_term + t0;
-        for (int q = tid; q < nt; q += 256) terml[q] = src[q];
-        for (int q = tid; q <= ns; q += 256) soff[q] = slot_tptr[s0 + q] - t0;
-        const int u0 = eslot_optr[e0], nu = eslot_optr[e0 + nes] - u0;
-        for (int q = tid; q < nu; q += 256) eobl[q] = eslot_obs[u0 + q];
-        for (int q = tid; q <= nes; q += 256) eoff[q] = eslot_optr[e0 + q] - u0;
+    for (int q = tid; q <= nc; q += 256) {
+        gp0[q] = ch_pt[c0 + q];
+        gob[q] = ch_obase[c0 + q];
+        gbo[q] = ch_blob[c0 + q];
     }
-    // per point: V* -> V*^-1, eB, local obs -> point map
-    if (tid < np) {
-        const int i = p0 + tid;
-        double vs[9], vi[9];
+    __syncthreads();
+    double wreg[WREG], vreg[9], ereg[3];
+    unsigned breg[BREG];
+    auto fetch = [&](int k) {
+        const int ob = gob[k], nw = (gob[k + 1] - ob) * WS;
+        const double *src = W + (size_t)WS * ob;
 #pragma unroll
-        for (int q = 0; q < 9; q++) vs[q] = V[9 * (size_t)i + q];
+        for (int u = 0; u < WREG; u++) {
+            const int q = tid + 256 * u;
+            wreg[u] = (q < nw) ? src[q] : 0.0;
+        }
+        const int i = gp0[k] + tid;
+        if (i < gp0[k + 1]) {
 #pragma unroll
-        for (int k = 0; k < 3; k++) vs[4 * k] = (1 + lambda) * vs[4 * k];
-        vlg_pinv3(vs, vi);
+            for (int q = 0; q < 9; q++) vreg[q] = V[9 * (size_t)i + q];
 #pragma unroll
-        for (int q = 0; q < 9; q++) {
-            Vl[9 * tid + q] = vi[q];
-            Vinv[9 * (size_t)i + q] = vi[q];
+            for (int q = 0; q < 3; q++) ereg[q] = eB[3 * (size_t)i + q];
+        }
+        const unsigned *bs = blob + gbo[k];
+        const int nbw = gbo[k + 1] - gbo[k];
+#pragma unroll
+        for (int u = 0; u < BREG; u++) {
+            const int q = tid + 256 * u;
+            breg[u] = (q < nbw) ? bs[q] : 0u;
+        }
+    };
+    fetch(0);
+    for (int k = 0; k < nc; k++) {
+        const int p0 = gp0[k], np = gp0[k + 1] - p0;
+        const int obase = gob[k], nobs = gob[k + 1] - obase;
+        const int nbw = gbo[k + 1] - gbo[k];
+        // stage chunk k from registers
+#pragma unroll
+        for (int u = 0; u < WREG; u++) {
+            const int q = tid + 256 * u;
+            if (q < nobs * WS) Wl[q] = wreg[u];
         }
 #pragma unroll
-        for (int q = 0; q < 3; q++) El[3 * tid + q] = eB[3 * (size_t)i + q];
-        for (int o = pt_ptr[i]; o < pt_ptr[i + 1]; o++) lpt[o - obase] = tid;
-    }
-    __syncthreads();
-    // Y = W V*^-1 (bundle_euclid.m:182)
-    for (int q = tid; q < nobs * WS; q += 256) {
-        const int lo = q / WS, e = q % WS, r = e % NA, c = e / NA;
-        const double *w = Wl + WS * lo;
-        const double *vi = Vl + 9 * lpt[lo];
-        Yl[q] = w[r] * vi[3 * c] + w[r + NA] * vi[1 + 3 * c] + w[r + 2 * NA] * vi[2 + 3 * c];
-    }
-    __syncthreads();
-    // t = Y eB (mex_bundle_2_Se_.c:143-147)
-    for (int q = tid; q < nobs * NA; q += 256) {
-        const int lo = q / NA, r = q % NA;
-        const double *y = Yl + WS * lo;
-        const double *eb = El + 3 * lpt[lo];
-        tl[q] = y[r] * eb[0] + y[r + NA] * eb[1] + y[r + 2 * NA] * eb[2];
-    }
-    __syncthreads();
-    // block partials: sum over the chunk's terms (points ascending).  One lane
-    // per (slot, column pair): the term's Y row block is read once for 2 NA
-    // outputs (LDS-instruction bound otherwise); every entry keeps the
-    // per-term expression and the term order of k_schur.
-    constexpr int NCP = (NA + 1) / 2;
-    for (int q = tid; q < ns * NCP; q += 256) {
-        const int s = q / NCP, c0 = 2 * (q % NCP);
-        const bool two = c0 + 1 < NA;
-        double acc0[NA], acc1[NA];
+        for (int u = 0; u < BREG; u++) {
+            const int q = tid + 256 * u;
+            if (q < nbw) bl[q] = breg[u];
+        }
+        for (int q = tid + 256 * BREG; q < nbw; q += 256) bl[q] = blob[gbo[k] + q];
+        if (tid < np) {   // V* -> V*^-1 from this lane's own registers
+            const int i = p0 + tid;
+            double vs[9], vi[9];
 #pragma unroll
-        for (int r = 0; r < NA; r++) acc0[r] = acc1[r] = 0.0;
-        for (int u = soff[s]; u < soff[s + 1]; u++) {
-            const unsigned tw = terml[u];
-            const double *y = Yl + WS * (tw & 0xffffu);
-            const double *w = Wl + WS * (tw >> 16);
-            const double wa0 = w[c0], wa1 = w[c0 + NA], wa2 = w[c0 + 2 * NA];
-            const int c1 = two ? c0 + 1 : c0;
-            const double wb0 = w[c1], wb1 = w[c1 + NA], wb2 = w[c1 + 2 * NA];
+            for (int q = 0; q < 9; q++) vs[q] = vreg[q];
 #pragma unroll
-            for (int r = 0; r < NA; r++) {
-                const double y0 = y[r], y1 = y[r + NA], y2 = y[r + 2 * NA];
-                acc0[r] += y0 * wa0 + y1 * wa1 + y2 * wa2;
-                acc1[r] += y0 * wb0 + y1 * wb1 + y2 * wb2;
+            for (int c = 0; c < 3; c++) vs[4 * c] = (1 + lambda) * vs[4 * c];
+            vlg_pinv3(vs, vi);
+#pragma unroll
+            for (int q = 0; q < 9; q++) {
+                Vl[9 * tid + q] = vi[q];
+                Vinv[9 * (size_t)i + q] = vi[q];
+            }
+#pragma unroll
+            for (int q = 0; q < 3; q++) El[3 * tid + q] = ereg[q];
+        }
+        __syncthreads();
+        if (k + 1 < nc) fetch(k + 1);   // in flight during the work below
+        const unsigned h1 = bl[1];
+        const int ns = (int)(h1 & 0xffffu), nes = (int)(h1 >> 16), nt = (int)bl[2];
+        const unsigned *soff = bl + 4;
+        const unsigned *eoff = soff + ns + 1;
+        const unsigned *sgl = eoff + nes + 1;
+        const unsigned *egl = sgl + ns;
+        const unsigned *lpt = egl + nes;
+        const unsigned *terml = lpt + nobs;
+        const unsigned *eobl = terml + nt;
+        // Y = W V*^-1 (bundle_euclid.m:182): lane (obs, row) forms the row's 3 entries
+        for (int q = tid; q < nobs * NA; q += 256) {
+            const int lo = q / NA, r = q % NA;
+            const double *w = Wl + WS * lo;
+            const double *vi = Vl + 9 * lpt[lo];
+            const double w0 = w[r], w1 = w[r + NA], w2 = w[r + 2 * NA];
+            double *y = Yl + WS * lo + r;
+#pragma unroll
+            for (int c = 0; c < 3; c++)
+                y[NA * c] = fma(w2, vi[2 + 3 * c], fma(w1, vi[1 + 3 * c], w0 * vi[3 * c]));
+        }
+        __syncthreads();
+        // block sums over the chunk's terms: lane (slot, row half, column pair,
+        // term parity); the two parities are combined by a lane shuffle
+        for (int q = tid; q < ns * IT * 2; q += 256) {
+            const int par = q & 1, qq = q >> 1;
+            const int s = qq / IT, rh = (qq % IT) / NCP, c0c = 2 * (qq % NCP);
+            const int r0 = rh * NR, nr = (rh == 0) ? NR : NA - NR;
+            const bool two = c0c + 1 < NA;
+            const int c1c = two ? c0c + 1 : c0c;
+            double acc0[NR], acc1[NR];
+#pragma unroll
+            for (int r = 0; r < NR; r++) acc0[r] = acc1[r] = 0.0;
+            const int u1 = (int)soff[s + 1];
+            for (int u = (int)soff[s] + par; u < u1; u += 2) {
+                const unsigned tw = terml[u];
+                const double *y = Yl + WS * (tw & 0xffffu) + r0;
+                const double *w = Wl + WS * (tw >> 16);
+                const double wa0 = w[c0c], wa1 = w[c0c + NA], wa2 = w[c0c + 2 * NA];
+                const double wb0 = w[c1c], wb1 = w[c1c + NA], wb2 = w[c1c + 2 * NA];
+#pragma unroll
+                for (int r = 0; r < NR; r++) {
+                    if (r < nr) {
+                        const double y0 = y[r], y1 = y[r + NA], y2 = y[r + 2 * NA];
+                        acc0[r] = fma(y2, wa2, fma(y1, wa1, fma(y0, wa0, acc0[r])));
+                        acc1[r] = fma(y2, wb2, fma(y1, wb1, fma(y0, wb0, acc1[r])));
+                    }
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < NR; r++) {
+                acc0[r] += __shfl_xor(acc0[r], 1, 64);
+                acc1[r] += __shfl_xor(acc1[r], 1, 64);
+            }
+            if (par) continue;
+            double *dst = direct ? spart + (size_t)NA * NA * (gs0 + s)
+                                 : gacc + NA * NA * sgl[s];
+#pragma unroll
+            for (int r = 0; r < NR; r++) {
+                if (r < nr) {
+                    double *d0 = dst + (r0 + r) + NA * c0c;
+                    *d0 = direct ? acc0[r] : *d0 + acc0[r];
+                    if (two) {
+                        double *d1 = dst + (r0 + r) + NA * (c0c + 1);
+                        *d1 = direct ? acc1[r] : *d1 + acc1[r];
+                    }
+                }
             }
         }
-        double *dst = spart + (size_t)NA * NA * (s0 + s);
-#pragma unroll
-        for (int r = 0; r < NA; r++) {
-            dst[r + NA * c0] = acc0[r];
-            if (two) dst[r + NA * (c0 + 1)] = acc1[r];
+        // e_ sums: t_o = Y_o eB_i (mex_bundle_2_Se_.c:143-147) summed per camera,
+        // on the lanes the block sums leave idle (highest thread ids first)
+        for (int q = 255 - tid; q < nes * NA; q += 256) {
+            const int s = q / NA, r = q % NA;
+            double acc = 0.0;
+            const int u1 = (int)eoff[s + 1];
+            for (int u = (int)eoff[s]; u < u1; u++) {
+                const int lo = (int)eobl[u];
+                const double *y = Yl + WS * lo;
+                const double *eb = El + 3 * lpt[lo];
+                acc = fma(y[r + 2 * NA], eb[2], fma(y[r + NA], eb[1], fma(y[r], eb[0], acc)));
+            }
+            if (direct) epart[(size_t)NA * (ge0 + s) + r] = acc;
+            else geacc[NA * egl[s] + r] += acc;
         }
+        __syncthreads();
     }
-    for (int q = tid; q < nes * NA; q += 256) {
-        const int s = q / NA, r = q % NA;
-        double acc = 0.0;
-        for (int u = eoff[s]; u < eoff[s + 1]; u++) acc += tl[NA * eobl[u] + r];
-        epart[(size_t)NA * (e0 + s) + r] = acc;
+    if (!direct) {
+        for (int q = tid; q < ngs * NA * NA; q += 256) spart[(size_t)NA * NA * gs0 + q] = gacc[q];
+        for (int q = tid; q < nge * NA; q += 256) epart[(size_t)NA * ge0 + q] = geacc[q];
     }
 }
 
@@ -915,28 +993,27 @@ int ba_launch_schur(ba_dev *d, double lambda)
 template <int NA>
 static int launch_schur_fast(ba_dev *d, double lambda)
 {
-    const int tcap = (d->ch_max_terms + 1) & ~1, scap = d->ch_max_slots;
-    size_t smem = sizeof(double) * (2 * BA_CH_OBS * 3 * NA + BA_CH_OBS * NA + BA_CH_PTS * 12) +
-                  sizeof(int) * BA_CH_OBS + sizeof(unsigned) * tcap +
-                  sizeof(int) * (scap + 1 + BA_CH_OBS + 1) + sizeof(unsigned short) * BA_CH_OBS;
+    const int gcap = d->grp_max_s, ecap = d->grp_max_e, bcap = d->max_blob;
+    size_t smem = sizeof(double) * (2 * BA_CH_OBS * 3 * NA + BA_CH_PTS * 12 + gcap * NA * NA +
+                                    ecap * NA) +
+                  sizeof(unsigned) * bcap;
     smem = (smem + 15) & ~(size_t)15;
     static size_t attr = 0;
     if (smem > attr) {
-        VLGBA_CHECK(hipFuncSetAttribute((const void *)k_schur_chunk<NA>,
+        VLGBA_CHECK(hipFuncSetAttribute((const void *)k_schur_group<NA>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
         attr = smem;
     }
     KT_B(d);
-    if (d->nch > 0)
-        k_schur_chunk<NA><<<d->nch, 256, smem, d->stream>>>(
-            d->ch_pt, d->ch_slot, d->ch_eslot, d->slot_tptr, d->slot_term, d->eslot_optr,
-            d->eslot_obs, d->pt_ptr, d->V, d->eB, d->W, lambda, tcap, scap, d->Vinv, d->spart,
-            d->epart);
+    if (d->ngrp > 0)
+        k_schur_group<NA><<<d->ngrp, 256, smem, d->stream>>>(
+            d->grp_ch, d->grp_gs, d->grp_ge, d->ch_pt, d->ch_obase, d->ch_blob, d->blob, d->V,
+            d->eB, d->W, lambda, bcap, gcap, ecap, d->Vinv, d->spart, d->epart);
     KT_E(d, KT_SCHUR_CHUNK);
     const int bs = (NA * NA + NA) <= 64 ? 64 : 128;
     KT_B(d);
     k_schur_reduce<NA><<<d->nb, bs, 0, d->stream>>>(
-        d->blk_jk, d->blk_sptr, d->blk_slots, d->cam_eptr, d->cam_eslots, d->spart, d->epart,
+        d->blk_jk, d->blk_gptr, d->blk_gslots, d->cam_gptr, d->cam_gslots, d->spart, d->epart,
         d->U, d->eA, d->nb, lambda, d->schur_owner, d->sblk, d->rhs);
     KT_E(d, KT_SCHUR_RED);
     return -(int)hipGetLastError();

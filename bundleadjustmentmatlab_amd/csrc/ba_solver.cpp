@@ -187,9 +187,34 @@ struct host_plan {
     std::vector<unsigned short> slot_term, eslot_obs;
     std::vector<int> blk_sptr, blk_slots, cam_eptr, cam_eslots;
     int max_terms = 0, max_slots = 0;   // per chunk (LDS staging size)
+    // Schur groups: consecutive chunks whose co-visible blocks ("group slots")
+    // and cameras ("group e-slots") are accumulated in LDS across the group
+    std::vector<int> grp_ch, grp_gs, grp_ge;      // [ngrp+1] ranges
+    std::vector<unsigned short> cs_g, ce_g;        // chunk slot / e-slot -> group-local id
+    std::vector<int> gslot_blk, gecam;             // [ngs], [nge]
+    std::vector<int> blk_gptr, blk_gslots, cam_gptr, cam_gslots;
+    int grp_max_s = 0, grp_max_e = 0;             // largest accumulated group
+    // per chunk one contiguous metadata record (one coalesced prefetch):
+    //   [np | nobs << 16][ns | nes << 16][nterm][neobs] soff[ns+1] eoff[nes+1]
+    //   sgl[ns] egl[nes] lpt[nobs] term[nterm] (y | w << 16) eobl[neobs]
+    std::vector<unsigned> blob;
+    std::vector<int> ch_blob, ch_obase;            // [nch+1]
+    int max_blob = 0;
 };
 
-bool build_plan(int m, const std::vector<int> &lptr, const std::vector<int> &lcam,
+// counting sort of ids by key: ptr[nkey+1], list of ids in ascending id order per key
+static void bucket(const std::vector<int> &key, int nkey, std::vector<int> &ptr,
+                   std::vector<int> &list)
+{
+    ptr.assign(nkey + 1, 0);
+    for (int k : key) ptr[k + 1]++;
+    for (int q = 0; q < nkey; q++) ptr[q + 1] += ptr[q];
+    list.resize(key.size());
+    std::vector<int> pos(ptr.begin(), ptr.end() - 1);
+    for (size_t s = 0; s < key.size(); s++) list[pos[key[s]]++] = (int)s;
+}
+
+bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<int> &lcam,
                 const host_blocks &hb, host_plan &P)
 {
     const int n = (int)lptr.size() - 1;
@@ -285,6 +310,95 @@ bool build_plan(int m, const std::vector<int> &lptr, const std::vector<int> &lca
     {
         std::vector<int> pos(P.cam_eptr.begin(), P.cam_eptr.end() - 1);
         for (int s = 0; s < nes; s++) P.cam_eslots[pos[ecam[s]]++] = s;
+    }
+    // Schur groups (greedy): at most gs_cap distinct blocks (LDS accumulators),
+    // BA_GE_CAP cameras and gmax chunks (>= ~2048 groups keep the chip busy).
+    // A chunk with more than gs_cap blocks forms a group of its own whose
+    // partials go straight to HBM ("direct" group).
+    const int nch = (int)P.ch_pt.size() - 1;
+    const int gs_cap = BA_GACC / (na * na);
+    const int gmax = std::min(BA_GROUP_CH, std::max(1, (nch + BA_GROUPS - 1) / BA_GROUPS));
+    std::vector<int> gslot_of(nb, -1), gcam_of(m, -1);
+    P.cs_g.assign(ns, 0);
+    P.ce_g.assign(nes, 0);
+    P.grp_ch.assign(1, 0);
+    P.grp_gs.assign(1, 0);
+    P.grp_ge.assign(1, 0);
+    for (int c = 0; c < nch;) {
+        std::vector<int> gs, ge;
+        int d = c;
+        for (; d < nch && d - c < gmax; d++) {
+            int new_s = 0, new_e = 0;
+            for (int s = P.ch_slot[d]; s < P.ch_slot[d + 1]; s++) new_s += gslot_of[P.slot_blk[s]] < 0;
+            for (int e = P.ch_eslot[d]; e < P.ch_eslot[d + 1]; e++) new_e += gcam_of[ecam[e]] < 0;
+            if (d > c && ((int)gs.size() + new_s > gs_cap || (int)ge.size() + new_e > BA_GE_CAP))
+                break;
+            for (int s = P.ch_slot[d]; s < P.ch_slot[d + 1]; s++) {
+                const int b = P.slot_blk[s];
+                if (gslot_of[b] < 0) {
+                    gslot_of[b] = (int)gs.size();
+                    gs.push_back(b);
+                }
+                P.cs_g[s] = (unsigned short)gslot_of[b];
+            }
+            for (int e = P.ch_eslot[d]; e < P.ch_eslot[d + 1]; e++) {
+                const int j = ecam[e];
+                if (gcam_of[j] < 0) {
+                    gcam_of[j] = (int)ge.size();
+                    ge.push_back(j);
+                }
+                P.ce_g[e] = (unsigned short)gcam_of[j];
+            }
+            if ((int)gs.size() > gs_cap) {   // direct group: this chunk alone
+                d++;
+                break;
+            }
+        }
+        for (int b : gs) {
+            P.gslot_blk.push_back(b);
+            gslot_of[b] = -1;
+        }
+        for (int j : ge) {
+            P.gecam.push_back(j);
+            gcam_of[j] = -1;
+        }
+        if ((int)gs.size() <= gs_cap) {   // LDS accumulators actually needed
+            P.grp_max_s = std::max(P.grp_max_s, (int)gs.size());
+            P.grp_max_e = std::max(P.grp_max_e, (int)ge.size());
+        }
+        P.grp_ch.push_back(d);
+        P.grp_gs.push_back((int)P.gslot_blk.size());
+        P.grp_ge.push_back((int)P.gecam.size());
+        c = d;
+    }
+    bucket(P.gslot_blk, nb, P.blk_gptr, P.blk_gslots);
+    bucket(P.gecam, m, P.cam_gptr, P.cam_gslots);
+    P.ch_blob.assign(1, 0);
+    P.ch_obase.assign(1, lptr[0]);
+    for (int c = 0; c < nch; c++) {
+        const int p0 = P.ch_pt[c], p1 = P.ch_pt[c + 1];
+        const int nobs = lptr[p1] - lptr[p0];
+        const int s0 = P.ch_slot[c], s1 = P.ch_slot[c + 1];
+        const int e0 = P.ch_eslot[c], e1 = P.ch_eslot[c + 1];
+        const int t0 = P.slot_tptr[s0], t1 = P.slot_tptr[s1];
+        const int u0 = P.eslot_optr[e0], u1 = P.eslot_optr[e1];
+        std::vector<unsigned> &B = P.blob;
+        B.push_back((unsigned)(p1 - p0) | ((unsigned)nobs << 16));
+        B.push_back((unsigned)(s1 - s0) | ((unsigned)(e1 - e0) << 16));
+        B.push_back((unsigned)(t1 - t0));
+        B.push_back((unsigned)(u1 - u0));
+        for (int s = s0; s <= s1; s++) B.push_back((unsigned)(P.slot_tptr[s] - t0));
+        for (int e = e0; e <= e1; e++) B.push_back((unsigned)(P.eslot_optr[e] - u0));
+        for (int s = s0; s < s1; s++) B.push_back(P.cs_g[s]);
+        for (int e = e0; e < e1; e++) B.push_back(P.ce_g[e]);
+        for (int i = p0; i < p1; i++)
+            for (int o = lptr[i]; o < lptr[i + 1]; o++) B.push_back((unsigned)(i - p0));
+        for (int t = t0; t < t1; t++)
+            B.push_back((unsigned)P.slot_term[2 * t] | ((unsigned)P.slot_term[2 * t + 1] << 16));
+        for (int u = u0; u < u1; u++) B.push_back(P.eslot_obs[u]);
+        P.ch_blob.push_back((int)B.size());
+        P.ch_obase.push_back(lptr[p1]);
+        P.max_blob = std::max(P.max_blob, P.ch_blob[c + 1] - P.ch_blob[c]);
     }
     return true;
 }
@@ -408,7 +522,7 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
     host_blocks hb;
     host_plan plan;
     build_blocks(p->m, pt_ptr_all, h.cam, c->p0, c->p1, o0, lower_blocks, all_diag, !fast, hb);
-    if (fast && !build_plan(p->m, lptr, lcam, hb, plan)) {
+    if (fast && !build_plan(p->m, na, lptr, lcam, hb, plan)) {
         fast = false;
         hb = host_blocks();
         build_blocks(p->m, pt_ptr_all, h.cam, c->p0, c->p1, o0, lower_blocks, all_diag, true, hb);
@@ -452,8 +566,38 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         TRY(ctx_alloc(c, &d.blk_slots, plan.blk_slots.size()));
         TRY(ctx_alloc(c, &d.cam_eptr, plan.cam_eptr.size()));
         TRY(ctx_alloc(c, &d.cam_eslots, plan.cam_eslots.size()));
-        TRY(ctx_alloc(c, &d.spart, (size_t)na * na * d.ns));
-        TRY(ctx_alloc(c, &d.epart, (size_t)na * d.nes));
+        d.ngrp = (int)plan.grp_ch.size() - 1;
+        d.max_blob = plan.max_blob;
+        TRY(ctx_alloc(c, &d.blob, plan.blob.size()));
+        TRY(ctx_alloc(c, &d.ch_blob, plan.ch_blob.size()));
+        TRY(ctx_alloc(c, &d.ch_obase, plan.ch_obase.size()));
+        TRY(upload(d.blob, plan.blob.data(), plan.blob.size(), s));
+        TRY(upload(d.ch_blob, plan.ch_blob.data(), plan.ch_blob.size(), s));
+        TRY(upload(d.ch_obase, plan.ch_obase.data(), plan.ch_obase.size(), s));
+        d.grp_max_s = plan.grp_max_s;
+        d.grp_max_e = plan.grp_max_e;
+        d.ngs = (int)plan.gslot_blk.size();
+        d.nge = (int)plan.gecam.size();
+        TRY(ctx_alloc(c, &d.spart, (size_t)na * na * d.ngs));
+        TRY(ctx_alloc(c, &d.epart, (size_t)na * d.nge));
+        TRY(ctx_alloc(c, &d.grp_ch, plan.grp_ch.size()));
+        TRY(ctx_alloc(c, &d.grp_gs, plan.grp_gs.size()));
+        TRY(ctx_alloc(c, &d.grp_ge, plan.grp_ge.size()));
+        TRY(ctx_alloc(c, &d.cs_g, plan.cs_g.size()));
+        TRY(ctx_alloc(c, &d.ce_g, plan.ce_g.size()));
+        TRY(ctx_alloc(c, &d.blk_gptr, plan.blk_gptr.size()));
+        TRY(ctx_alloc(c, &d.blk_gslots, plan.blk_gslots.size()));
+        TRY(ctx_alloc(c, &d.cam_gptr, plan.cam_gptr.size()));
+        TRY(ctx_alloc(c, &d.cam_gslots, plan.cam_gslots.size()));
+        TRY(upload(d.grp_ch, plan.grp_ch.data(), plan.grp_ch.size(), s));
+        TRY(upload(d.grp_gs, plan.grp_gs.data(), plan.grp_gs.size(), s));
+        TRY(upload(d.grp_ge, plan.grp_ge.data(), plan.grp_ge.size(), s));
+        TRY(upload(d.cs_g, plan.cs_g.data(), plan.cs_g.size(), s));
+        TRY(upload(d.ce_g, plan.ce_g.data(), plan.ce_g.size(), s));
+        TRY(upload(d.blk_gptr, plan.blk_gptr.data(), plan.blk_gptr.size(), s));
+        TRY(upload(d.blk_gslots, plan.blk_gslots.data(), plan.blk_gslots.size(), s));
+        TRY(upload(d.cam_gptr, plan.cam_gptr.data(), plan.cam_gptr.size(), s));
+        TRY(upload(d.cam_gslots, plan.cam_gslots.data(), plan.cam_gslots.size(), s));
         TRY(ctx_alloc(c, &d.upart, (size_t)(na * (na + 1) / 2 + na) * d.nes));
         TRY(ctx_alloc(c, &d.chsse, (size_t)d.nch));
         TRY(upload(d.ch_pt, plan.ch_pt.data(), plan.ch_pt.size(), s));
@@ -801,7 +945,7 @@ const char *vlgba_kernel_name(int k)
 {
     static const char *names[KT_N] = {
         "k_rotations", "k_linearize", "k_camera_reduce", "k_damp_point", "k_schur",
-        "k_schur_chunk", "k_schur_reduce", "k_assemble", "k_factor_panel", "k_syrk",
+        "k_schur_group", "k_schur_reduce", "k_assemble", "k_factor_panel", "k_syrk",
         "k_backward", "k_camera_update", "k_point_update", "k_cr_factor", "k_cr_update",
         "k_cr_back"};
     return (k >= 0 && k < KT_N) ? names[k] : "";
