@@ -60,6 +60,7 @@ SIGNATURES = {
     "vlgba_get_params": (c_int, [ctypes.c_void_p, c_dp, c_dp]),
     "vlgba_step": (c_int, [ctypes.c_void_p, c_int, c_int, ctypes.POINTER(VlgbaStepInfo)]),
     "vlgba_run": (c_int, [ctypes.c_void_p, c_dp, ctypes.POINTER(VlgbaStats)]),
+    "vlgba_get_linearization": (c_int, [ctypes.c_void_p, c_dp, c_dp, c_dp, c_dp, c_dp]),
     "vlgba_sync": (c_int, [ctypes.c_void_p]),
     "vlgba_destroy": (None, [ctypes.c_void_p]),
     "vlgba_set_timing": (c_int, [ctypes.c_void_p, c_int]),

@@ -204,6 +204,20 @@ class BundleAdjuster:
     def sync(self):
         check(self._L.vlgba_sync(self._h), "vlgba_sync")
 
+    def linearization(self):
+        """Stage 1 at the current parameters: dict of U (na, na, m), eA (na, m),
+        V (3, 3, n), eB (3, n) and W (na, 3, N) with observations point-major
+        (points ascending, cameras ascending within a point)."""
+        na, m, n, N = self.num_a, self.m, self.n, self.num_obs
+        U = np.zeros((na, na, m), order="F")
+        eA = np.zeros((na, m), order="F")
+        V = np.zeros((3, 3, n), order="F")
+        eB = np.zeros((3, n), order="F")
+        W = np.zeros((na, 3, N), order="F")
+        check(self._L.vlgba_get_linearization(self._h, _dp(U), _dp(eA), _dp(V), _dp(eB),
+                                              _dp(W)), "vlgba_get_linearization")
+        return dict(U=U, eA=eA, V=V, eB=eB, W=W)
+
     def set_timing(self, on=True):
         check(self._L.vlgba_set_timing(self._h, int(on)), "vlgba_set_timing")
 

@@ -26,6 +26,33 @@
 
 #define H_FD VLG_FD_H
 
+// Diagnostic build only (make stamps): thread 0 of every workgroup adds the
+// s_memtime cycles of each phase of the fast-path kernels to g_stamp.
+#ifdef BA_STAMPS
+__device__ unsigned long long g_stamp[32];
+#define STAMP_DECL unsigned long long st_prev_ = __builtin_amdgcn_s_memtime()
+#define STAMP(i)                                                                    \
+    do {                                                                            \
+        if (threadIdx.x == 0) {                                                     \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();             \
+            atomicAdd(&g_stamp[i], t_ - st_prev_);                                  \
+            st_prev_ = t_;                                                          \
+        }                                                                           \
+    } while (0)
+extern "C" int vlgba_debug_stamps(unsigned long long *out, int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamp), sizeof(g_stamp)) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[32] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#else
+#define STAMP_DECL
+#define STAMP(i)
+#endif
+
 // -------------------------------------------------------------------------
 // block reduction of one double per thread -> partial[blockIdx.x]
 // -------------------------------------------------------------------------
@@ -561,6 +588,7 @@ __global__ __launch_bounds__(256) void k_schur_group(
     const int gs0 = grp_gs[g], ngs = grp_gs[g + 1] - gs0;
     const int ge0 = grp_ge[g], nge = grp_ge[g + 1] - ge0;
     const bool direct = ngs > GS_CAP;
+    STAMP_DECL;
     if (!direct) {
         for (int q = tid; q < ngs * NA * NA; q += 256) gacc[q] = 0.0;
         for (int q = tid; q < nge * NA; q += 256) geacc[q] = 0.0;
@@ -573,30 +601,30 @@ __global__ __launch_bounds__(256) void k_schur_group(
     __syncthreads();
     double wreg[WREG], vreg[9], ereg[3];
     unsigned breg[BREG];
+    // unconditional loads from clamped addresses: a load under a lane
+    // condition becomes a branch + vmcnt(0) per element (cdna_hip_programming.md)
     auto fetch = [&](int k) {
         const int ob = gob[k], nw = (gob[k + 1] - ob) * WS;
         const double *src = W + (size_t)WS * ob;
+        const int wl = nw > 0 ? nw - 1 : 0;
+        if (nw == 0) src = W;
 #pragma unroll
-        for (int u = 0; u < WREG; u++) {
-            const int q = tid + 256 * u;
-            wreg[u] = (q < nw) ? src[q] : 0.0;
-        }
-        const int i = gp0[k] + tid;
-        if (i < gp0[k + 1]) {
+        for (int u = 0; u < WREG; u++) wreg[u] = src[min(tid + 256 * u, wl)];
+        const int i0 = gp0[k], np = gp0[k + 1] - i0;
+        const size_t i = (size_t)i0 + (np > 0 ? min(tid, np - 1) : 0);
+        const double *vs = np > 0 ? V + 9 * i : V;
+        const double *es = np > 0 ? eB + 3 * i : eB;
 #pragma unroll
-            for (int q = 0; q < 9; q++) vreg[q] = V[9 * (size_t)i + q];
+        for (int q = 0; q < 9; q++) vreg[q] = vs[q];
 #pragma unroll
-            for (int q = 0; q < 3; q++) ereg[q] = eB[3 * (size_t)i + q];
-        }
+        for (int q = 0; q < 3; q++) ereg[q] = es[q];
         const unsigned *bs = blob + gbo[k];
-        const int nbw = gbo[k + 1] - gbo[k];
+        const int bl1 = gbo[k + 1] - gbo[k] - 1;   // a record is never empty
 #pragma unroll
-        for (int u = 0; u < BREG; u++) {
-            const int q = tid + 256 * u;
-            breg[u] = (q < nbw) ? bs[q] : 0u;
-        }
+        for (int u = 0; u < BREG; u++) breg[u] = bs[min(tid + 256 * u, bl1)];
     };
     fetch(0);
+    STAMP(0);
     for (int k = 0; k < nc; k++) {
         const int p0 = gp0[k], np = gp0[k + 1] - p0;
         const int obase = gob[k], nobs = gob[k + 1] - obase;
@@ -630,6 +658,7 @@ __global__ __launch_bounds__(256) void k_schur_group(
             for (int q = 0; q < 3; q++) El[3 * tid + q] = ereg[q];
         }
         __syncthreads();
+        STAMP(1);
         if (k + 1 < nc) fetch(k + 1);   // in flight during the work below
         const unsigned h1 = bl[1];
         const int ns = (int)(h1 & 0xffffu), nes = (int)(h1 >> 16), nt = (int)bl[2];
@@ -652,6 +681,7 @@ __global__ __launch_bounds__(256) void k_schur_group(
                 y[NA * c] = fma(w2, vi[2 + 3 * c], fma(w1, vi[1 + 3 * c], w0 * vi[3 * c]));
         }
         __syncthreads();
+        STAMP(2);
         // block sums over the chunk's terms: lane (slot, row half, column pair,
         // term parity); the two parities are combined by a lane shuffle
         for (int q = tid; q < ns * IT * 2; q += 256) {
@@ -714,11 +744,20 @@ __global__ __launch_bounds__(256) void k_schur_group(
             if (direct) epart[(size_t)NA * (ge0 + s) + r] = acc;
             else geacc[NA * egl[s] + r] += acc;
         }
+        STAMP(3);
         __syncthreads();
+        STAMP(4);
     }
     if (!direct) {
         for (int q = tid; q < ngs * NA * NA; q += 256) spart[(size_t)NA * NA * gs0 + q] = gacc[q];
         for (int q = tid; q < nge * NA; q += 256) epart[(size_t)NA * ge0 + q] = geacc[q];
+    }
+    STAMP(5);
+    if (tid == 0) {
+#ifdef BA_STAMPS
+        atomicAdd(&g_stamp[6], (unsigned long long)nc);
+        atomicAdd(&g_stamp[7], 1ull);
+#endif
     }
 }
 

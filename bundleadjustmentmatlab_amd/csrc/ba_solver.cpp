@@ -912,6 +912,27 @@ int vlgba_get_params(vlgba_ctx *c, double *a, double *b)
     return 0;
 }
 
+int vlgba_get_linearization(vlgba_ctx *c, double *U, double *eA, double *V, double *eB,
+                            double *W)
+{
+    if (!c) return VLGBA_E_ARG;
+    ba_dev &d = c->d;
+    TRY(ba_launch_rotations(&d, d.a, d.rot, 1));
+    TRY(ba_launch_linearize(&d, c->flags));
+    TRY(ba_launch_camera_reduce(&d, c->flags));
+    VLGBA_CHECK(hipMemcpyAsync(d.eA + d.ld, d.scal + 0, sizeof(double), hipMemcpyDeviceToDevice,
+                               d.stream));
+    TRY(allreduce(c, d.U, (size_t)d.na * d.na * d.m + d.ld + 1));
+    c->lin_valid = 1;
+    if (U) TRY(download(U, d.U, (size_t)d.na * d.na * d.m, d.stream));
+    if (eA) TRY(download(eA, d.eA, (size_t)d.ld, d.stream));
+    if (V) TRY(download(V, d.V, 9 * (size_t)d.n, d.stream));
+    if (eB) TRY(download(eB, d.eB, 3 * (size_t)d.n, d.stream));
+    if (W) TRY(download(W, d.W, (size_t)3 * d.na * d.N, d.stream));
+    VLGBA_CHECK(hipStreamSynchronize(d.stream));
+    return 0;
+}
+
 int vlgba_set_timing(vlgba_ctx *c, int on)
 {
     if (!c) return VLGBA_E_ARG;

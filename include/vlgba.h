@@ -117,6 +117,14 @@ int vlgba_get_params(vlgba_ctx *ctx, double *a, double *b);
  * when the previous pass was rejected (bench: every pass does full work).
  * update_lm != 0 applies the accept/reject rule (:218-241) to the context. */
 int vlgba_step(vlgba_ctx *ctx, int relinearize, int update_lm, vlgba_step_info *info);
+/* stage 1 at the current parameters (mex_bundle_1_XABeUVWeAeB.c outputs, the
+ * reduced forms of bundle_euclid.m:139-154): U (num_a x num_a x m), eA
+ * (num_a x m) summed over all ranks; V (3 x 3 x n_local), eB (3 x n_local) and
+ * W (num_a x 3 per observation, observations point-major: points ascending,
+ * cameras ascending within a point) for this rank's points.  Any pointer may
+ * be NULL.  Also marks the linearisation valid for the next vlgba_step. */
+int vlgba_get_linearization(vlgba_ctx *ctx, double *U, double *eA, double *V, double *eB,
+                            double *W);
 int vlgba_run(vlgba_ctx *ctx, double *error_out, vlgba_stats *stats);
 int vlgba_sync(vlgba_ctx *ctx);
 void vlgba_destroy(vlgba_ctx *ctx);

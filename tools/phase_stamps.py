@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Per-phase cycle split of the fast-path kernels (diagnostic build).
+
+Build ``make -C bundleadjustmentmatlab_amd/csrc stamps`` (libvlgba_stamps.so,
+-DBA_STAMPS), then run on the GPU box:  python tools/phase_stamps.py [cfg]
+Prints, per stamped phase, the s_memtime cycles summed over workgroups and
+per chunk (thread 0 of each workgroup stamps at its phase boundaries).
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bundleadjustmentmatlab_amd._lib as L  # noqa: E402
+
+L.LIB_PATH = os.path.join(ROOT, "bundleadjustmentmatlab_amd", "libvlgba_stamps.so")
+from bundleadjustmentmatlab_amd import BundleAdjuster  # noqa: E402
+from bundleadjustmentmatlab_amd.scene import make_config  # noqa: E402
+
+PHASES = {"k_schur_group": ["prologue", "stage+pinv", "Y", "slots+e", "barrier", "epilogue"]}
+
+
+def main():
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "cfg3"
+    sc = make_config(cfg)
+    lib = L.lib()
+    fn = lib.vlgba_debug_stamps
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    a = np.zeros((6, sc.m), order="F")
+    a[0:3], a[3:6] = sc.w0, sc.T0
+    b = np.asfortranarray(sc.X0[:3])
+    ba = BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, 6)
+    ba.set_params(a, b)
+    st = (ctypes.c_ulonglong * 32)()
+    ba.step(relinearize=True, update_lm=False)
+    ba.sync()
+    fn(st, 1)
+    reps = 5
+    for _ in range(reps):
+        ba.step(relinearize=True, update_lm=False)
+    ba.sync()
+    fn(st, 1)
+    v = [st[i] / reps for i in range(32)]
+    chunks, wgs = v[6], v[7]
+    print(f"k_schur_group: {wgs:.0f} workgroups, {chunks:.0f} chunks per pass")
+    tot = sum(v[:6])
+    for i, name in enumerate(PHASES["k_schur_group"]):
+        print(f"  {name:12s} {v[i] / 1e6:9.2f} Mcycles  {100 * v[i] / tot:5.1f}%  "
+              f"{v[i] / max(chunks, 1):9.0f} cycles/chunk")
+    ba.close()
+
+
+if __name__ == "__main__":
+    main()
