@@ -123,8 +123,12 @@ def main():
 
     N = sc.num_obs
     # ---- roofline of the dominant kernel -----------------------------------
-    roofs = {k: kernel_roofline(k, tot, calls, sc, num_a, world) for k, (tot, calls) in
+    plan = ba.plan_info()
+    roofs = {k: kernel_roofline(k, tot, calls, plan, n_timed) for k, (tot, calls) in
              kms.items()}
+    traffic = pmc_traffic(args.config, plan)
+    for k, r in roofs.items():
+        r["traffic"] = traffic.get(k)
     dom = max(kms, key=lambda k: kms[k][0])
     roof = roofs[dom]
     log("[bench] kernels (avg us/launch, launches/pass, roofline frac): " +
@@ -165,62 +169,90 @@ def main():
         dist.destroy_process_group()
 
 
-def envelope_panels(sc, num_a):
-    """Panel tiles per Cholesky step of the tile envelope (ba_chol.hip)."""
-    NB = 64
-    n_s = num_a * sc.m
-    nt = (n_s + NB - 1) // NB
-    tfirst = np.arange(nt)
-    ptr = np.concatenate([[0], np.cumsum(np.bincount(sc.obs_pt, minlength=sc.n))])
-    cnt = np.diff(ptr)
-    cmin = np.minimum.reduceat(sc.obs_cam, ptr[:-1][cnt > 0])
-    lo = np.repeat(cmin, cnt[cnt > 0])           # smallest camera of each obs' point
-    for r in range(num_a):                        # every row of camera j couples with it
-        np.minimum.at(tfirst, (num_a * sc.obs_cam + r) // NB, (num_a * lo) // NB)
-    T = np.array([(tfirst[k + 1:] <= k).sum() for k in range(nt)])
-    return nt, T
+# timer name (vlgba_kernel_name) -> device kernel base name in rocprofv3 output
+PMC_ALIAS = {"k_linearize": "k_linearize_chunk", "k_camera_reduce": "k_camera_reduce_chunks"}
 
 
-def kernel_roofline(name, tot_ms, calls, sc, num_a, world):
-    """Algorithmic bytes (HBM-bound kernels) or flops (MFMA kernels) per launch
-    divided by the measured average launch time (DESIGN.md 'Roofline')."""
-    N = sc.num_obs / world
-    n = sc.n / world
+def pmc_traffic(config, plan):
+    """HBM bytes per launch of each kernel from the committed PMC passes
+    (profiles/pmc_traffic_<config>.json, tools/pmc_traffic.py: FETCH_SIZE x 2 +
+    WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), or {} if absent.
+    Valid for the fast (chunked) single-rank path it was collected on."""
+    path = os.path.join(ROOT, "profiles", f"pmc_traffic_{config}.json")
+    if plan.get("ordered") or not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        kern = json.load(f)["kernels"]
+    out = {}
+    for name in list(PMC_ALIAS) + [k for k in kern if k.startswith("k_")]:
+        base = PMC_ALIAS.get(name, name)
+        if base in kern:
+            out[name] = kern[base]["bytes"]
+    return out
+
+
+def kernel_roofline(name, tot_ms, calls, plan, n_passes):
+    """Algorithmic bytes (HBM-bound kernels) or flops (MFMA / VALU kernels) per
+    launch divided by the measured average launch duration.
+    Sizes come from the library's own execution plan (vlgba_plan_info), so the
+    figures follow the chunk / group / tile counts actually launched."""
+    NA = plan["num_a"]
+    N, n, m = plan["obs"], plan["points"], plan["cameras"]
+    NU = NA * (NA + 1) // 2
+    WS = 8 * 3 * NA                         # W_ij, NA x 3 fp64
     avg_s = tot_ms * 1e-3 / calls
-    NB = 64
-    if name in ("k_factor_panel", "k_syrk", "k_backward"):
-        nt, T = envelope_panels(sc, num_a)
-        if name == "k_factor_panel":
-            # potrf + trtri of the diagonal tile, T panel GEMMs, fused syrk if T == 1
-            fl = sum(2 * NB ** 3 / 3 + t * 2 * NB ** 3 + (NB ** 3 if t == 1 else 0) for t in T)
-        elif name == "k_syrk":
-            fl = sum(t * (t + 1) / 2 * 2 * NB ** 3 for t in T if t > 1)
-        else:
-            fl = sum(2 * NB * NB * (1 + t) for t in T)
-        passes = calls / max(1, (len(T) if name != "k_syrk" else sum(1 for t in T if t > 1)))
-        per = fl / (calls / passes)                 # flops per launch
-        achieved = per / avg_s / 1e12
-        return dict(bound="mfma", achieved=achieved, peak=PEAK_F64_TFLOPS, unit="TFLOP/s",
-                    frac=achieved / PEAK_F64_TFLOPS, traffic=None, kernel=name,
-                    per_launch=f"{per:.3g} flop")
-    JS = 8 * (2 * num_a + 2)
-    WS = 8 * 3 * num_a
-    per_obs = {"k_linearize": 16 + 4 + JS + WS,          # obs (x, cam) in; jrec, W out
-               "k_camera_reduce": JS + 4,                 # jrec + cam_obs in
-               "k_damp_point": 2 * WS + 8 * num_a,        # W in; Y, t out
-               "k_schur": 2 * WS,                         # Y, W per term (>= once)
-               "k_schur_chunk": WS,                       # W in (once, contiguous)
-               "k_point_update": WS + 16 + 4}.get(name, 0)
-    per_pt = {"k_linearize": 24 + 72 + 24 + 4,           # b in; V, eB out
-              "k_damp_point": 72 + 24 + 72,
-              "k_schur_chunk": 72 + 24 + 72,             # V, eB in; V*^-1 out
-              "k_point_update": 24 + 72 + 24 + 48 + 4}.get(name, 0)
-    # every such kernel runs once per pass: bytes per launch = bytes per pass
-    nbytes = per_obs * N + per_pt * n
-    achieved = nbytes / avg_s / 1e9 if nbytes else 0.0
-    return dict(bound="hbm", achieved=achieved, peak=PEAK_HBM_GBS, unit="GB/s",
-                frac=achieved / PEAK_HBM_GBS, traffic=None, kernel=name,
-                per_launch=f"{nbytes:.3g} B")
+    per_pass = calls / n_passes             # launches per LM pass
+    nbytes, flops = 0.0, 0.0
+    if name == "k_linearize":
+        # obs (cam, u, v) + chunk-local ids in; W out; b in; V, eB out; U / eA partials out
+        nbytes = (N * (4 + 16 + 2 + WS) + n * (4 + 24 + 72 + 24) +
+                  plan["chunk_eslots"] * (8 * (NU + NA) + 4) + plan["chunks"] * 20)
+        # 1 + NA + 3 projections per observation (~53 flop each) + 2(NA+3) FD divides
+        flops = N * ((1 + NA + 3) * 53 + 2 * (NA + 3) * 2 + 3 * NA * 3)
+    elif name == "k_camera_reduce":
+        nbytes = plan["chunk_eslots"] * (8 * (NU + NA) + 4) + m * 8 * (NA * NA + NA)
+    elif name == "k_schur_group":
+        # W, V, eB, metadata in; V*^-1 out; LDS-accumulated block / camera partials out
+        nbytes = (N * WS + n * (72 + 24 + 72) + 4 * plan["blob_words"] +
+                  8 * NA * NA * plan["group_slots"] + 8 * NA * plan["group_eslots"])
+        # S terms (NA x NA x 3 fma each), Y = W V*^-1, e_ terms
+        flops = 2 * (plan["schur_terms"] * NA * NA * 3 + N * NA * 9 + N * NA * 3)
+    elif name == "k_schur_reduce":
+        nbytes = (8 * NA * NA * plan["group_slots"] + 8 * NA * plan["group_eslots"] +
+                  8 * (NA * NA + 1) * plan["blocks"] + 8 * NA * m)
+    elif name == "k_point_update":
+        nbytes = N * (WS + 4 + 16) + n * (4 + 24 + 72 + 24 + 24 + 24)
+    elif name == "k_rotations":
+        nbytes = m * 8 * (NA + 45)
+    elif name == "k_camera_update":
+        nbytes = m * 8 * (3 * NA + 9)
+    elif name in ("k_cr_factor", "k_cr_update", "k_cr_back") and plan["cr_levels"]:
+        T = 64
+        if name == "k_cr_factor":     # potrf + trtri of L_e, two panel products
+            flops = plan["cr_elim"] * (2 * T ** 3 / 3 + 2 * 2 * T ** 3 + 2 * T * T)
+        elif name == "k_cr_update":   # two SYRK-shaped products + the fill product
+            flops = plan["cr_keep"] * (3 * 2 * T ** 3 + 4 * T * T)
+        else:                         # three tile GEMVs
+            flops = plan["cr_elim"] * 3 * 2 * T * T
+        flops /= per_pass
+        nbytes = 0.0
+    else:
+        nbytes = 0.0
+    if name not in ("k_cr_factor", "k_cr_update", "k_cr_back"):
+        nbytes /= per_pass                  # once-per-pass kernels: bytes per launch
+        flops /= per_pass
+    gbs = nbytes / avg_s / 1e9 if nbytes else 0.0
+    tfs = flops / avg_s / 1e12 if flops else 0.0
+    hbm = dict(bound="hbm", achieved=gbs, peak=PEAK_HBM_GBS, unit="GB/s",
+               frac=gbs / PEAK_HBM_GBS, traffic=None, kernel=name,
+               per_launch=f"{nbytes:.4g} B", avg_launch_us=avg_s * 1e6)
+    fl = dict(bound="mfma", achieved=tfs, peak=PEAK_F64_TFLOPS, unit="TFLOP/s",
+              frac=tfs / PEAK_F64_TFLOPS, traffic=None, kernel=name,
+              per_launch=f"{flops:.4g} flop", avg_launch_us=avg_s * 1e6)
+    if name.startswith("k_cr_"):
+        return fl
+    # a kernel with both figures is reported against the roof it is closer to
+    return hbm if hbm["frac"] >= fl["frac"] else fl
 
 
 def cpu_baseline(sc, a0, b0, num_a, sample_points):

@@ -231,6 +231,19 @@ class BundleAdjuster:
         return {self._L.vlgba_kernel_name(k).decode(): (float(ms[k]), int(calls[k]))
                 for k in range(n) if calls[k] > 0}
 
+    PLAN_KEYS = ("obs", "points", "cameras", "num_a", "chunks", "chunk_slots",
+                 "chunk_eslots", "groups", "group_slots", "group_eslots", "blocks",
+                 "tiles", "cr_levels", "cr_elim", "cr_keep", "ordered", "schur_terms",
+                 "blob_words")
+
+    def plan_info(self):
+        """Execution-plan sizes of this rank (vlgba_plan_info)."""
+        n = len(self.PLAN_KEYS)
+        buf = (ctypes.c_longlong * n)()
+        rc = self._L.vlgba_plan_info(self._h, buf, n)
+        check(min(rc, 0), "vlgba_plan_info")
+        return dict(zip(self.PLAN_KEYS, [int(v) for v in buf]))
+
     def phase_ms(self):
         ms = np.zeros(7)
         check(self._L.vlgba_phase_ms(self._h, _dp(ms)), "vlgba_phase_ms")

@@ -117,6 +117,8 @@ struct ba_dev {
     double *chsse;     // [nch] per-chunk SSE partials of the linearisation
     int ns, nes;
     int ch_max_terms, ch_max_slots;   // per-chunk maxima: LDS staging of the term lists
+    long long nterm_fast;             // (obs, obs) Schur terms of the chunk plan
+    long long blob_words;             // metadata words of the chunk plan
     // Schur groups (consecutive chunks, one workgroup): block / camera partials
     // accumulate in LDS over the group's chunks and are written once per group
     int ngrp, ngs, nge;

@@ -554,6 +554,8 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         d.nes = (int)plan.eslot_optr.size() - 1;
         d.ch_max_terms = plan.max_terms;
         d.ch_max_slots = plan.max_slots;
+        d.nterm_fast = (long long)plan.slot_term.size() / 2;
+        d.blob_words = (long long)plan.blob.size();
         TRY(ctx_alloc(c, &d.ch_pt, plan.ch_pt.size()));
         TRY(ctx_alloc(c, &d.ch_slot, plan.ch_slot.size()));
         TRY(ctx_alloc(c, &d.ch_eslot, plan.ch_eslot.size()));
@@ -970,6 +972,20 @@ const char *vlgba_kernel_name(int k)
         "k_backward", "k_camera_update", "k_point_update", "k_cr_factor", "k_cr_update",
         "k_cr_back"};
     return (k >= 0 && k < KT_N) ? names[k] : "";
+}
+
+int vlgba_plan_info(vlgba_ctx *c, long long *info, int len)
+{
+    if (!c || !info) return VLGBA_E_ARG;
+    const ba_dev &d = c->d;
+    const long long ne = d.cr_nlev ? d.cr_eptr_h[d.cr_nlev] : 0;
+    const long long nk = d.cr_nlev ? d.cr_kptr_h[d.cr_nlev] : 0;
+    const long long v[VLGBA_NPLAN] = {d.N,   d.n,    d.m,   d.na,         d.nch,  d.ns,
+                                      d.nes, d.ngrp, d.ngs, d.nge,        d.nb,   d.nt,
+                                      d.cr_nlev, ne, nk,    d.ordered,    d.ordered ? d.T : d.nterm_fast,
+                                      d.blob_words};
+    for (int k = 0; k < len && k < VLGBA_NPLAN; k++) info[k] = v[k];
+    return VLGBA_NPLAN;
 }
 
 int vlgba_phase_ms(vlgba_ctx *c, double *ms7)

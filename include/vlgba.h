@@ -139,6 +139,16 @@ int vlgba_phase_ms(vlgba_ctx *ctx, double *ms7);
 #define VLGBA_NKERNELS 16
 int vlgba_kernel_ms(vlgba_ctx *ctx, double *ms, long long *calls, int reset);
 const char *vlgba_kernel_name(int k);
+/* execution-plan sizes of this rank (roofline accounting in bench.py):
+ * [0] observations [1] points [2] cameras [3] num_a [4] Schur chunks
+ * [5] chunk block slots [6] chunk camera slots [7] Schur groups [8] group
+ * block slots [9] group camera slots [10] co-visible blocks (j >= k)
+ * [11] 64-row tiles of S [12] cyclic-reduction levels (0: tile Cholesky)
+ * [13] eliminated tiles [14] kept-tile updates [15] ordered mode
+ * [16] Schur (obs, obs) terms [17] chunk metadata words.
+ * Writes min(len, VLGBA_NPLAN) entries, returns VLGBA_NPLAN. */
+#define VLGBA_NPLAN 18
+int vlgba_plan_info(vlgba_ctx *ctx, long long *info, int len);
 
 /* ---- stage entries with the reference MEX argument layouts ---------------
  * Host pointers in, host pointers out; every output is fully written (zeros
