@@ -124,6 +124,7 @@ def main():
     N = sc.num_obs
     # ---- roofline of the dominant kernel -----------------------------------
     plan = ba.plan_info()
+    log("[bench] plan: " + " ".join(f"{k}={v}" for k, v in plan.items()))
     roofs = {k: kernel_roofline(k, tot, calls, plan, n_timed) for k, (tot, calls) in
              kms.items()}
     traffic = pmc_traffic(args.config, plan)

@@ -109,14 +109,18 @@ class BundleAdjuster:
     or 10 (variable K).  Options follow bundle_euclid.m's names.  ``solver``
     picks the reduced-camera solve: "auto" (cyclic reduction when S is
     tile-tridiagonal, else envelope Cholesky), "envelope" or "dense";
-    ``dense_solve=True`` is the same as solver="dense".
+    ``dense_solve=True`` is the same as solver="dense".  ``schur_kernel``
+    picks the fast-path Schur complement kernel: "auto" (dense per-chunk
+    products on fp64 MFMA when the tracks fit) or "terms" (per-term sums).
     """
     SOLVERS = {"auto": 0, "dense": 1, "envelope": 2}
+    SCHUR_KERNELS = {"auto": 0, "terms": 1}
 
     def __init__(self, K, obs_pt, obs_cam, obs_x, n, num_a=6, *, fix_structure=False,
                  fix_motion=False, pivot=None, verbose=False, num_vis=0.0, device=0,
                  rank=0, world_size=1, comm_id=None, max_iter=0, max_iter2=0, lambda0=0.0,
-                 dense_solve=False, ordered=False, allreduce=None, solver=None):
+                 dense_solve=False, ordered=False, allreduce=None, solver=None,
+                 schur_kernel="auto"):
         L = lib()
         solve_mode = self.SOLVERS[solver] if solver is not None else int(bool(dense_solve))
         self.K = _F(K)
@@ -153,7 +157,8 @@ class BundleAdjuster:
                            int(device), int(rank), int(world_size),
                            ctypes.cast(self._comm, ctypes.c_void_p) if self._comm else None,
                            solve_mode, int(ordered),
-                           ctypes.cast(self._ar, ctypes.c_void_p) if self._ar else None, None)
+                           ctypes.cast(self._ar, ctypes.c_void_p) if self._ar else None, None,
+                           self.SCHUR_KERNELS[schur_kernel])
         h = ctypes.c_void_p()
         check(L.vlgba_create(ctypes.byref(prob), ctypes.byref(opt), ctypes.byref(h)),
               "vlgba_create")
@@ -234,7 +239,7 @@ class BundleAdjuster:
     PLAN_KEYS = ("obs", "points", "cameras", "num_a", "chunks", "chunk_slots",
                  "chunk_eslots", "groups", "group_slots", "group_eslots", "blocks",
                  "tiles", "cr_levels", "cr_elim", "cr_keep", "ordered", "schur_terms",
-                 "blob_words")
+                 "blob_words", "mfma")
 
     def plan_info(self):
         """Execution-plan sizes of this rank (vlgba_plan_info)."""

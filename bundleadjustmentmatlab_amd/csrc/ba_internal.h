@@ -94,12 +94,14 @@ struct ba_dev {
     double *crL;                  // [2][nt][64*64] L(p, e) | L(q, e)
     // reductions: partial sums per block of the reducing kernels, in fixed order
     double *part;      // [3][PART_MAX]
-    double *scal;      // [8] : 0 old_sse, 1 new_sse, 2 dpg, 3 chol_status ...
+    double *scal;      // [8] : 0 old_sse, 1 new_sse, 2 dpg cams, 3 dpg pts, 4 chol status
     int *chol_cnt;     // arrival counters for the triangular solves
     // ---- fast (chunked) Schur path: points in chunks of <= CH_OBS observations;
     // per chunk the co-visible blocks it touches ("slots") and the cameras it
     // sees ("e-slots") get one partial each, reduced per block in chunk order.
     int ordered;       // 1: sequential bit-exact kernels (k_damp_point + k_schur)
+    int mfma;          // fast path: 1 = MFMA Schur chunks (k_schur_mfma), 0 = term lists
+    int no_mfma;       // option: force the term-list Schur kernel
     int nch;           // chunks
     int *ch_pt;        // [nch+1] local point ranges
     int *ch_slot;      // [nch+1] slot ranges (slots are numbered chunk-major)
@@ -153,6 +155,13 @@ struct ba_dev {
 #define BA_GE_CAP 128      // cameras per Schur group
 #define BA_GROUPS 2048     // target number of Schur groups (workgroups)
 #define BA_GROUP_CH 64     // max chunks per Schur group
+// MFMA Schur path (k_schur_mfma): a chunk is 4 K-blocks of 5 points (one per
+// wave), its cameras span NA * cameras <= 16 * BA_MF_RT slab columns
+#define BA_MF_PTS 20
+#define BA_MF_RT(na) ((na) == 6 ? 3 : 4)
+#define BA_MF_CMAX(na) ((16 * BA_MF_RT(na)) / (na))
+#define BA_MF_GACC 1536    // doubles of LDS block accumulators per MFMA Schur group
+#define BA_MF_GE_CAP 24    // cameras per MFMA Schur group (LDS budget: 2 groups per CU)
 
 // ---- ba_kernels.hip ----
 int ba_launch_rotations(ba_dev *d, const double *a, double *rot, int all5);

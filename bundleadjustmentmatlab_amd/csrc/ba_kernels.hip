@@ -26,6 +26,8 @@
 
 #define H_FD VLG_FD_H
 
+typedef double d4 __attribute__((ext_vector_type(4)));
+
 // Diagnostic build only (make stamps): thread 0 of every workgroup adds the
 // s_memtime cycles of each phase of the fast-path kernels to g_stamp.
 #ifdef BA_STAMPS
@@ -761,6 +763,225 @@ __global__ __launch_bounds__(256) void k_schur_group(
     }
 }
 
+// -------------------------------------------------------------------------
+// V*^-1 per point (bundle_euclid.m:168-180) for the MFMA Schur path
+// -------------------------------------------------------------------------
+template <int NA>
+__global__ __launch_bounds__(256) void k_point_vinv(const double *__restrict__ V, int n,
+                                                    double lambda, double *__restrict__ Vinv)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    double vs[9], vi[9];
+#pragma unroll
+    for (int q = 0; q < 9; q++) vs[q] = V[9 * (size_t)i + q];
+#pragma unroll
+    for (int c = 0; c < 3; c++) vs[4 * c] = (1 + lambda) * vs[4 * c];
+    vlg_pinv3(vs, vi);
+#pragma unroll
+    for (int q = 0; q < 9; q++) Vinv[9 * (size_t)i + q] = vi[q];
+}
+
+// -------------------------------------------------------------------------
+// Schur complement on fp64 MFMA, operands register-resident (default fast
+// path when every track fits).  A chunk holds <= BA_MF_PTS = 4 x 5 consecutive
+// points seeing <= BA_MF_CMAX cameras; wave w owns the chunk's points
+// 5w .. 5w + 4, i.e. rows k = 3 p' + q (p' < 5, q < 3; row 15 zero) of the
+// 16-row K-block w of the dense chunk slabs
+//     Wk[k][NA cs + r] = W_o[r][q],   Yk = D Wk,   D[3p'+q][3p'+t] = V*^-1_p[t][q]
+// (o = observation of point p in camera slot cs, cameras ascending; zero where
+// p does not see cs).  Yk holds Y_o = W_o V*^-1_p (bundle_euclid.m:182).
+// Per 4-row K step s the lane (li = l & 15, lk = l >> 4) holds the B fragment
+// Wk[4s + lk][16 t + li] of every column tile t (gathered straight from the
+// point-major W in HBM) and the A fragment D[li][4s + lk]; then
+//     Y tile t   = sum_s mfma(D frag s, W frag s t)         (K = 16)
+//     S(ti, tj) += sum_s mfma(Y tile ti reg s, W frag s tj)  (lower tiles)
+// The Y accumulator's register s IS the A fragment of K step s
+// (v_mfma_f64_16x16x4f64: C row = lk + 4 reg, col = li; A lane = [li][lk]),
+// so Y never leaves the registers and no LDS or barrier is needed per chunk.
+//     S_chunk[NA cs_j + r][NA cs_k + c] = sum_i Y_ij[r] . W_ik[c]
+// over the chunk's points (mex_bundle_2_Se_.c:80-118; the pairs a point does
+// not see add exact zeros); e_ partials sum_k Yk[k][.] eB[k] (:132-155).
+// Consecutive chunks with one camera list (a run of video-like tracks) keep
+// accumulating in the registers; at a change of cameras ("flush") the four
+// waves add their sums of each lower entry of each co-visible block to the
+// group accumulator in LDS in wave order.  Every sum runs in a fixed order ->
+// deterministic run to run; only the grouping differs from the term kernel.
+// -------------------------------------------------------------------------
+#define BA_MF_KB 5   // points per K-block (one wave)
+template <int NA>
+__global__ __launch_bounds__(256, (NA == 6) ? 2 : 1) void k_schur_mfma(
+    const int *__restrict__ grp_ch, const int *__restrict__ grp_gs,
+    const int *__restrict__ grp_ge, const int *__restrict__ ch_pt,
+    const int *__restrict__ ch_obase, const int *__restrict__ ch_blob,
+    const unsigned *__restrict__ blob, const double *__restrict__ W,
+    const double *__restrict__ Vinv, const double *__restrict__ eB, int nobs_all, int n_all,
+    int gcap, int ecap, double *__restrict__ spart, double *__restrict__ epart)
+{
+    constexpr int WS = 3 * NA;
+    constexpr int RT = BA_MF_RT(NA);
+    constexpr int NTL = RT * (RT + 1) / 2;
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double *gacc = sm;                                   // [gcap][NA*NA]
+    double *geacc = gacc + gcap * NA * NA;               // [ecap][NA]
+    unsigned *rec = (unsigned *)(geacc + ecap * NA);     // the group's chunk records
+    __shared__ int gp0[BA_GROUP_CH + 1], gob[BA_GROUP_CH + 1], gbo[BA_GROUP_CH + 1];
+    const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    const int c0 = grp_ch[g], nc = grp_ch[g + 1] - c0;
+    const int gs0 = grp_gs[g], ngs = grp_gs[g + 1] - gs0;
+    const int ge0 = grp_ge[g], nge = grp_ge[g + 1] - ge0;
+    const int rb0 = ch_blob[c0], nrw = ch_blob[c0 + nc] - rb0;
+    for (int q = tid; q < ngs * NA * NA; q += 256) gacc[q] = 0.0;
+    for (int q = tid; q < nge * NA; q += 256) geacc[q] = 0.0;
+    for (int q = tid; q < nrw; q += 256) rec[q] = blob[rb0 + q];
+    for (int q = tid; q <= nc; q += 256) {
+        gp0[q] = ch_pt[c0 + q];
+        gob[q] = ch_obase[c0 + q];
+        gbo[q] = ch_blob[c0 + q] - rb0;
+    }
+    __syncthreads();
+    // lane constants: K rows of its fragments, slab columns of its tiles
+    int kp[4], kq[4], ccs[RT], crr[RT];
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+        const int k = 4 * s + lk;
+        kp[s] = k < 3 * BA_MF_KB ? k / 3 : -1;
+        kq[s] = k % 3;
+    }
+#pragma unroll
+    for (int t = 0; t < RT; t++) {
+        ccs[t] = (16 * t + li) / NA;
+        crr[t] = (16 * t + li) % NA;
+    }
+    const int dp = li < 3 * BA_MF_KB ? li / 3 : -2, dq = li % 3;
+    // fragments of one chunk, unconditional loads from clamped addresses
+    // Absent entries read the exact zeros of the row past the end of W / V*^-1 /
+    // eB (no select after a load: its wait lands at the MFMA that consumes it);
+    // addresses are a uniform chunk base plus a 32-bit lane offset.
+    auto load = [&](int k, double (&wf)[4][RT], double (&df)[4], double (&ef)[4]) {
+        const unsigned *r = rec + gbo[k];
+        const int np = gp0[k + 1] - gp0[k], i0 = gp0[k], ob = gob[k];
+        const int C = (int)(r[1] & 0xffu);
+        const unsigned char *tab = (const unsigned char *)(r + 2 + C + C * (C + 1) / 2);
+        const double *wbase = W + (size_t)WS * ob;
+        const double *vbase = Vinv + 9 * (size_t)i0;
+        const double *ebase = eB + 3 * (size_t)i0;
+        const int wz = WS * (nobs_all - ob), vz = 9 * (n_all - i0), ez = 3 * (n_all - i0);
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const int p = BA_MF_KB * wv + kp[s];
+            const bool pv = kp[s] >= 0 && p < np;
+#pragma unroll
+            for (int t = 0; t < RT; t++) {
+                const bool cv = pv && ccs[t] < C;
+                const int idx = cv ? (int)tab[p * C + ccs[t]] : 0xff;
+                wf[s][t] = wbase[idx != 0xff ? WS * idx + crr[t] + NA * kq[s] : wz];
+            }
+            const bool dv = pv && kp[s] == dp;
+            df[s] = vbase[dv ? 9 * p + kq[s] + 3 * dq : vz];
+            ef[s] = ebase[pv ? 3 * p + kq[s] : ez];
+        }
+    };
+    d4 accS[NTL];
+    double eacc[RT];
+#pragma unroll
+    for (int u = 0; u < NTL; u++) accS[u] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int t = 0; t < RT; t++) eacc[t] = 0.0;
+    // one chunk: Y tiles, e_ sums, lower S tiles; flush at a change of cameras
+    auto process = [&](int k, const double (&wc)[4][RT], const double (&dc)[4],
+                       const double (&ec)[4]) {
+        const unsigned *r = rec + gbo[k];
+        const unsigned h1 = r[1];
+        const int C = (int)(h1 & 0xffu), fl = (int)((h1 >> 8) & 0xffu), Rc = NA * C;
+        const int nt = (Rc + 15) >> 4;
+        // row tile by row tile: one Y tile live at a time.  Every tile runs (tiles
+        // past the chunk's columns multiply exact zeros): no branch between the
+        // next chunk's loads and the MFMAs, so their waits stay precise
+        (void)nt;
+#pragma unroll
+        for (int ti = 0; ti < RT; ti++) {
+            {
+                d4 y = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int s = 0; s < 4; s++)
+                    y = __builtin_amdgcn_mfma_f64_16x16x4f64(dc[s], wc[s][ti], y, 0, 0, 0);
+                eacc[ti] = fma(y[3], ec[3], fma(y[2], ec[2], fma(y[1], ec[1],
+                                                                 fma(y[0], ec[0], eacc[ti]))));
+#pragma unroll
+                for (int tj = 0; tj <= ti; tj++) {
+#pragma unroll
+                    for (int s = 0; s < 4; s++)
+                        accS[ti * (ti + 1) / 2 + tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+                            y[s], wc[s][tj], accS[ti * (ti + 1) / 2 + tj], 0, 0, 0);
+                }
+            }
+        }
+        if (fl & 2) {   // flush: wave by wave into the group accumulators
+            const unsigned *ge = r + 2;
+            const unsigned *pair = ge + C;
+            double ecol[RT];
+#pragma unroll
+            for (int t = 0; t < RT; t++) {   // e_ column sums over the lane quarters
+                const double v0 = __shfl(eacc[t], li, 64), v1 = __shfl(eacc[t], li + 16, 64);
+                const double v2 = __shfl(eacc[t], li + 32, 64), v3 = __shfl(eacc[t], li + 48, 64);
+                ecol[t] = ((v0 + v1) + v2) + v3;
+                eacc[t] = 0.0;
+            }
+            for (int w = 0; w < 4; w++) {
+                if (wv == w) {
+#pragma unroll
+                    for (int ti = 0; ti < RT; ti++)
+#pragma unroll
+                        for (int tj = 0; tj <= ti; tj++) {
+                            const int col = 16 * tj + li;
+#pragma unroll
+                            for (int q = 0; q < 4; q++) {
+                                const int rr = 16 * ti + lk + 4 * q;
+                                if (rr < Rc && col < Rc && rr >= col) {
+                                    const int cr = rr / NA, cc = col / NA;
+                                    const unsigned gsl = pair[cr * (cr + 1) / 2 + cc];
+                                    if (gsl != 0xffffffffu)
+                                        gacc[gsl * (NA * NA) + (rr - NA * cr) +
+                                             NA * (col - NA * cc)] +=
+                                            accS[ti * (ti + 1) / 2 + tj][q];
+                                }
+                            }
+                        }
+                    if (lk == 0) {
+#pragma unroll
+                        for (int t = 0; t < RT; t++) {
+                            const int col = 16 * t + li;
+                            if (col < Rc) {
+                                const int cs = col / NA;
+                                geacc[ge[cs] * NA + col - NA * cs] += ecol[t];
+                            }
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+#pragma unroll
+            for (int u = 0; u < NTL; u++) accS[u] = d4{0.0, 0.0, 0.0, 0.0};
+        }
+    };
+    // two register sets, software pipelined: the next chunk's fragments are in
+    // flight while this chunk's MFMAs run (no register copies between sets)
+    double wa[4][RT], da[4], ea[4], wb[4][RT], db[4], eb[4];
+    load(0, wa, da, ea);
+    for (int k = 0; k < nc; k += 2) {
+        load(min(k + 1, nc - 1), wb, db, eb);   // unconditional: a clamped reload at the end
+        process(k, wa, da, ea);
+        if (k + 1 >= nc) break;
+        load(min(k + 2, nc - 1), wa, da, ea);
+        process(k + 1, wb, db, eb);
+    }
+    __syncthreads();
+    for (int q = tid; q < ngs * NA * NA; q += 256) spart[(size_t)NA * NA * gs0 + q] = gacc[q];
+    for (int q = tid; q < nge * NA; q += 256) epart[(size_t)NA * ge0 + q] = geacc[q];
+}
+
 // S blocks and e_ from the chunk partials, in chunk order
 template <int NA>
 __global__ void k_schur_reduce(const int *__restrict__ blk_jk, const int *__restrict__ blk_sptr,
@@ -1033,6 +1254,26 @@ template <int NA>
 static int launch_schur_fast(ba_dev *d, double lambda)
 {
     const int gcap = d->grp_max_s, ecap = d->grp_max_e, bcap = d->max_blob;
+    if (d->mfma) {
+        KT_B(d);
+        k_point_vinv<NA><<<(d->n + 255) / 256, 256, 0, d->stream>>>(d->V, d->n, lambda, d->Vinv);
+        KT_E(d, KT_DAMP);
+        const size_t sm2 = sizeof(double) * (gcap * NA * NA + ecap * NA) +
+                           sizeof(unsigned) * (size_t)bcap;
+        static size_t attr2 = 0;
+        if (sm2 > attr2) {
+            VLGBA_CHECK(hipFuncSetAttribute((const void *)k_schur_mfma<NA>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)sm2));
+            attr2 = sm2;
+        }
+        KT_B(d);
+        if (d->ngrp > 0)
+            k_schur_mfma<NA><<<d->ngrp, 256, sm2, d->stream>>>(
+                d->grp_ch, d->grp_gs, d->grp_ge, d->ch_pt, d->ch_obase, d->ch_blob, d->blob,
+                d->W, d->Vinv, d->eB, d->N, d->n, gcap, ecap, d->spart, d->epart);
+        KT_E(d, KT_SCHUR_CHUNK);
+    } else {
     size_t smem = sizeof(double) * (2 * BA_CH_OBS * 3 * NA + BA_CH_PTS * 12 + gcap * NA * NA +
                                     ecap * NA) +
                   sizeof(unsigned) * bcap;
@@ -1049,6 +1290,7 @@ static int launch_schur_fast(ba_dev *d, double lambda)
             d->grp_ch, d->grp_gs, d->grp_ge, d->ch_pt, d->ch_obase, d->ch_blob, d->blob, d->V,
             d->eB, d->W, lambda, bcap, gcap, ecap, d->Vinv, d->spart, d->epart);
     KT_E(d, KT_SCHUR_CHUNK);
+    }
     const int bs = (NA * NA + NA) <= 64 ? 64 : 128;
     KT_B(d);
     k_schur_reduce<NA><<<d->nb, bs, 0, d->stream>>>(

@@ -214,8 +214,12 @@ static void bucket(const std::vector<int> &key, int nkey, std::vector<int> &ptr,
     for (size_t s = 0; s < key.size(); s++) list[pos[key[s]]++] = (int)s;
 }
 
+// cmax > 0: chunks for the MFMA Schur kernel (k_schur_mfma): at most
+// BA_MF_PTS points and cmax cameras per chunk (the chunk's dense Y / W fit
+// one K = 64 slab of 16 * BA_MF_RT(na) rows); its metadata records are the
+// dense-layout ones described at build of P.blob below.
 bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<int> &lcam,
-                const host_blocks &hb, host_plan &P)
+                const host_blocks &hb, host_plan &P, int cmax)
 {
     const int n = (int)lptr.size() - 1;
     const int nb = (int)hb.jk.size() / 2;
@@ -224,7 +228,11 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
         return k * (k + 1) / 2;
     };
     for (int i = 0; i < n; i++)
-        if (lptr[i + 1] - lptr[i] > BA_CH_OBS || pt_terms(i) > BA_CH_TERMS) return false;
+        if (lptr[i + 1] - lptr[i] > BA_CH_OBS || pt_terms(i) > BA_CH_TERMS ||
+            (cmax > 0 && lptr[i + 1] - lptr[i] > cmax))
+            return false;
+    const int pts_max = cmax > 0 ? BA_MF_PTS : BA_CH_PTS;
+    std::vector<int> cam_stamp(m, -1);   // chunk camera set (MFMA chunking)
     P.max_terms = P.max_slots = 0;
     std::vector<int> slot_of(nb, -1), eslot_of(m, -1), touched, tcam;
     std::vector<std::vector<std::pair<int, int>>> terms;   // per local slot
@@ -239,9 +247,30 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
         const int obase = lptr[p];
         int q = p;
         long long nterm = 0;
-        while (q < n && q - p < BA_CH_PTS && lptr[q + 1] - obase <= BA_CH_OBS &&
-               nterm + pt_terms(q) <= BA_CH_TERMS)
+        int ncam = 0;
+        bool uniform = true;   // every point so far sees exactly the first point's cameras
+        auto same_cams = [&](int i1, int i2) {
+            if (lptr[i1 + 1] - lptr[i1] != lptr[i2 + 1] - lptr[i2]) return false;
+            for (int a = 0; a < lptr[i1 + 1] - lptr[i1]; a++)
+                if (lcam[lptr[i1] + a] != lcam[lptr[i2] + a]) return false;
+            return true;
+        };
+        while (q < n && q - p < pts_max && lptr[q + 1] - obase <= BA_CH_OBS &&
+               nterm + pt_terms(q) <= BA_CH_TERMS) {
+            if (cmax > 0) {
+                // a run of points with one camera list (video-like tracks) keeps its
+                // chunks to itself: its MFMA sums stay in registers across chunks
+                const bool same = q == p || same_cams(p, q);
+                if (uniform && !same && q - p >= 4) break;
+                uniform = uniform && same;
+                int add = 0;
+                for (int a = lptr[q]; a < lptr[q + 1]; a++) add += cam_stamp[lcam[a]] != p;
+                if (ncam + add > cmax) break;
+                for (int a = lptr[q]; a < lptr[q + 1]; a++) cam_stamp[lcam[a]] = p;
+                ncam += add;
+            }
             nterm += pt_terms(q++);
+        }
         P.max_terms = std::max(P.max_terms, (int)nterm);
         touched.clear();
         tcam.clear();
@@ -316,8 +345,11 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
     // A chunk with more than gs_cap blocks forms a group of its own whose
     // partials go straight to HBM ("direct" group).
     const int nch = (int)P.ch_pt.size() - 1;
-    const int gs_cap = BA_GACC / (na * na);
+    // the MFMA kernel has no direct mode: one chunk's blocks must always fit
+    const int gs_cap = cmax > 0 ? std::max(BA_MF_GACC / (na * na), cmax * (cmax + 1) / 2)
+                                : BA_GACC / (na * na);
     const int gmax = std::min(BA_GROUP_CH, std::max(1, (nch + BA_GROUPS - 1) / BA_GROUPS));
+    const int ge_cap = cmax > 0 ? std::max(BA_MF_GE_CAP, cmax) : BA_GE_CAP;
     std::vector<int> gslot_of(nb, -1), gcam_of(m, -1);
     P.cs_g.assign(ns, 0);
     P.ce_g.assign(nes, 0);
@@ -331,7 +363,7 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
             int new_s = 0, new_e = 0;
             for (int s = P.ch_slot[d]; s < P.ch_slot[d + 1]; s++) new_s += gslot_of[P.slot_blk[s]] < 0;
             for (int e = P.ch_eslot[d]; e < P.ch_eslot[d + 1]; e++) new_e += gcam_of[ecam[e]] < 0;
-            if (d > c && ((int)gs.size() + new_s > gs_cap || (int)ge.size() + new_e > BA_GE_CAP))
+            if (d > c && ((int)gs.size() + new_s > gs_cap || (int)ge.size() + new_e > ge_cap))
                 break;
             for (int s = P.ch_slot[d]; s < P.ch_slot[d + 1]; s++) {
                 const int b = P.slot_blk[s];
@@ -375,6 +407,90 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
     bucket(P.gecam, m, P.cam_gptr, P.cam_gslots);
     P.ch_blob.assign(1, 0);
     P.ch_obase.assign(1, lptr[0]);
+    if (cmax > 0) {
+        // dense-layout record per chunk (k_schur_mfma):
+        //   [np | nobs << 16]
+        //   [C | flags << 8 | Kc << 16]  C cameras ascending, Kc = 3 np rounded to 4;
+        //        flags: 1 dense (every point sees every camera of the chunk),
+        //               2 flush (the next chunk of the group has other cameras, or
+        //                 this is the group's last chunk: the register-held MFMA
+        //                 tiles and e_ sums go to the group accumulators)
+        //   ge[C]       group e-slot of each camera slot
+        //   pair[C(C+1)/2]  group slot of block (cam[cr], cam[cc]), cr >= cc, index
+        //                   cr (cr + 1) / 2 + cc; 0xffffffff: not in the group
+        //   idx[ceil(np C / 4)]  byte p C + cs: local observation index of chunk
+        //                        point p in camera slot cs, 0xff if p does not see it
+        std::vector<int> cslot(m, -1), gsl_of(nb, -1), gel_of(m, -1);
+        std::vector<int> ch_grp(nch);
+        for (int g = 0; g + 1 < (int)P.grp_ch.size(); g++)
+            for (int c = P.grp_ch[g]; c < P.grp_ch[g + 1]; c++) ch_grp[c] = g;
+        auto cams_of = [&](int c) {
+            std::vector<int> cams;
+            for (int e = P.ch_eslot[c]; e < P.ch_eslot[c + 1]; e++) cams.push_back(ecam[e]);
+            std::sort(cams.begin(), cams.end());
+            return cams;
+        };
+        std::vector<int> cams = nch > 0 ? cams_of(0) : std::vector<int>();
+        for (int c = 0; c < nch; c++) {
+            const int g = ch_grp[c];
+            if (c == P.grp_ch[g]) {   // group-local slot / camera ids
+                for (int q = P.grp_gs[g]; q < P.grp_gs[g + 1]; q++)
+                    gsl_of[P.gslot_blk[q]] = q - P.grp_gs[g];
+                for (int q = P.grp_ge[g]; q < P.grp_ge[g + 1]; q++)
+                    gel_of[P.gecam[q]] = q - P.grp_ge[g];
+            }
+            const int p0 = P.ch_pt[c], p1 = P.ch_pt[c + 1];
+            const int nobs = lptr[p1] - lptr[p0];
+            const int C = (int)cams.size();
+            std::vector<int> next;
+            bool flush = true;
+            if (c + 1 < nch) {
+                next = cams_of(c + 1);
+                flush = ch_grp[c + 1] != g || next != cams;
+            }
+            for (int q = 0; q < C; q++) cslot[cams[q]] = q;
+            const bool dense = nobs == (p1 - p0) * C;
+            std::vector<unsigned> &B = P.blob;
+            const int kc = (3 * (p1 - p0) + 3) & ~3;
+            B.push_back((unsigned)(p1 - p0) | ((unsigned)nobs << 16));
+            B.push_back((unsigned)C | ((unsigned)(dense ? 1 : 0) << 8) |
+                        ((unsigned)(flush ? 2 : 0) << 8) | ((unsigned)kc << 16));
+            for (int q = 0; q < C; q++) B.push_back((unsigned)gel_of[cams[q]]);
+            for (int cr = 0; cr < C; cr++)
+                for (int cc = 0; cc <= cr; cc++) {
+                    const int blk = hb.find(cams[cr], cams[cc]);
+                    const int sl = blk >= 0 ? gsl_of[blk] : -1;
+                    B.push_back(sl >= 0 ? (unsigned)sl : 0xffffffffu);
+                }
+            {
+                std::vector<unsigned char> tab((size_t)(p1 - p0) * C, 0xff);
+                for (int i = p0; i < p1; i++)
+                    for (int o = lptr[i]; o < lptr[i + 1]; o++)
+                        tab[(size_t)(i - p0) * C + cslot[lcam[o]]] =
+                            (unsigned char)(o - lptr[p0]);
+                for (size_t q = 0; q < tab.size(); q += 4) {
+                    unsigned w = 0;
+                    for (size_t u = 0; u < 4; u++)
+                        w |= (unsigned)(q + u < tab.size() ? tab[q + u] : 0xff) << (8 * u);
+                    B.push_back(w);
+                }
+            }
+            for (int q = 0; q < C; q++) cslot[cams[q]] = -1;
+            if (c + 1 == P.grp_ch[g + 1]) {
+                for (int q = P.grp_gs[g]; q < P.grp_gs[g + 1]; q++) gsl_of[P.gslot_blk[q]] = -1;
+                for (int q = P.grp_ge[g]; q < P.grp_ge[g + 1]; q++) gel_of[P.gecam[q]] = -1;
+            }
+            P.ch_blob.push_back((int)B.size());
+            P.ch_obase.push_back(lptr[p1]);
+            P.max_blob = std::max(P.max_blob, P.ch_blob[c + 1] - P.ch_blob[c]);
+            cams.swap(next);
+        }
+        P.max_blob = 0;   // MFMA path: largest group's record block (staged in LDS)
+        for (int g = 0; g + 1 < (int)P.grp_ch.size(); g++)
+            P.max_blob = std::max(P.max_blob,
+                                  P.ch_blob[P.grp_ch[g + 1]] - P.ch_blob[P.grp_ch[g]]);
+        return true;
+    }
     for (int c = 0; c < nch; c++) {
         const int p0 = P.ch_pt[c], p1 = P.ch_pt[c + 1];
         const int nobs = lptr[p1] - lptr[p0];
@@ -522,10 +638,18 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
     host_blocks hb;
     host_plan plan;
     build_blocks(p->m, pt_ptr_all, h.cam, c->p0, c->p1, o0, lower_blocks, all_diag, !fast, hb);
-    if (fast && !build_plan(p->m, na, lptr, lcam, hb, plan)) {
-        fast = false;
-        hb = host_blocks();
-        build_blocks(p->m, pt_ptr_all, h.cam, c->p0, c->p1, o0, lower_blocks, all_diag, true, hb);
+    // MFMA Schur chunks when every point fits the dense slab, else the term path
+    d.mfma = 0;
+    if (fast && !d.no_mfma && build_plan(p->m, na, lptr, lcam, hb, plan, BA_MF_CMAX(na))) {
+        d.mfma = 1;
+    } else if (fast) {
+        plan = host_plan();
+        if (!build_plan(p->m, na, lptr, lcam, hb, plan, 0)) {
+            fast = false;
+            hb = host_blocks();
+            build_blocks(p->m, pt_ptr_all, h.cam, c->p0, c->p1, o0, lower_blocks, all_diag, true,
+                         hb);
+        }
     }
     if (!fast) d.ordered = 1;
     d.nb = (int)hb.jk.size() / 2;
@@ -543,7 +667,10 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
     TRY(ctx_alloc(c, &d.b_new, 3 * (size_t)d.n));
     TRY(ctx_alloc(c, &d.rot, 45 * (size_t)p->m));
     TRY(ctx_alloc(c, &d.rot_new, 9 * (size_t)p->m));
-    TRY(ctx_alloc(c, &d.W, (size_t)3 * na * d.N));
+    // W, eB, V*^-1 carry one zero row past the end: the MFMA Schur kernel points
+    // the fragment loads of absent (point, camera) pairs at it
+    TRY(ctx_alloc(c, &d.W, (size_t)3 * na * (d.N + 1)));
+    VLGBA_CHECK(hipMemsetAsync(d.W + (size_t)3 * na * d.N, 0, sizeof(double) * 3 * na, s));
     if (!fast) {   // the fast path forms A, e, Y and t in LDS only
         TRY(ctx_alloc(c, &d.jrec, (size_t)d.js * d.N));
         TRY(ctx_alloc(c, &d.Y, (size_t)3 * na * d.N));
@@ -619,8 +746,10 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
     TRY(ctx_alloc(c, &d.U, (size_t)na * na * p->m + na * (size_t)p->m + 1));
     d.eA = d.U + (size_t)na * na * p->m;     // U | eA | old_sse contiguous: one all-reduce
     TRY(ctx_alloc(c, &d.V, 9 * (size_t)d.n));
-    TRY(ctx_alloc(c, &d.eB, 3 * (size_t)d.n));
-    TRY(ctx_alloc(c, &d.Vinv, 9 * (size_t)d.n));
+    TRY(ctx_alloc(c, &d.eB, 3 * (size_t)(d.n + 1)));
+    TRY(ctx_alloc(c, &d.Vinv, 9 * (size_t)(d.n + 1)));
+    VLGBA_CHECK(hipMemsetAsync(d.eB + 3 * (size_t)d.n, 0, sizeof(double) * 3, s));
+    VLGBA_CHECK(hipMemsetAsync(d.Vinv + 9 * (size_t)d.n, 0, sizeof(double) * 9, s));
     TRY(ctx_alloc(c, &d.db, 3 * (size_t)d.n));
     TRY(ctx_alloc(c, &d.blk_jk, 2 * (size_t)d.nb));
     TRY(ctx_alloc(c, &d.blk_ptr, (size_t)d.nb + 1));
@@ -723,6 +852,7 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
         c->verbose = o->verbose;
         c->d.dense_solve = o->dense_solve;
         c->d.ordered = o->ordered;
+        c->d.no_mfma = o->schur_kernel == 1;
         rc = ctx_setup(c, p, h, pt_ptr_all, lower_blocks, all_diag, stage_mode);
         if (rc) break;
         if (o->pivot) {
@@ -983,7 +1113,7 @@ int vlgba_plan_info(vlgba_ctx *c, long long *info, int len)
     const long long v[VLGBA_NPLAN] = {d.N,   d.n,    d.m,   d.na,         d.nch,  d.ns,
                                       d.nes, d.ngrp, d.ngs, d.nge,        d.nb,   d.nt,
                                       d.cr_nlev, ne, nk,    d.ordered,    d.ordered ? d.T : d.nterm_fast,
-                                      d.blob_words};
+                                      d.blob_words, d.mfma};
     for (int k = 0; k < len && k < VLGBA_NPLAN; k++) info[k] = v[k];
     return VLGBA_NPLAN;
 }

@@ -78,6 +78,11 @@ typedef struct {
      * return 0, and copies it back (e.g. gloo via torch.distributed). */
     int (*allreduce)(double *buf, long long count, void *user);
     void *allreduce_user;
+    /* fast-path Schur complement kernel (ordered = 0): 0 (default) automatic --
+     * dense per-chunk Y W^T products on fp64 MFMA when every point has at most
+     * 16 * (num_a == 6 ? 3 : 4) / num_a observations, else per-term sums;
+     * 1: per-term sums (measurement / cross-check).  Same terms either way. */
+    int schur_kernel;
 } vlgba_options;
 
 typedef struct {
@@ -145,9 +150,10 @@ const char *vlgba_kernel_name(int k);
  * block slots [9] group camera slots [10] co-visible blocks (j >= k)
  * [11] 64-row tiles of S [12] cyclic-reduction levels (0: tile Cholesky)
  * [13] eliminated tiles [14] kept-tile updates [15] ordered mode
- * [16] Schur (obs, obs) terms [17] chunk metadata words.
+ * [16] Schur (obs, obs) terms [17] chunk metadata words [18] MFMA Schur
+ * chunks in use.
  * Writes min(len, VLGBA_NPLAN) entries, returns VLGBA_NPLAN. */
-#define VLGBA_NPLAN 18
+#define VLGBA_NPLAN 19
 int vlgba_plan_info(vlgba_ctx *ctx, long long *info, int len);
 
 /* ---- stage entries with the reference MEX argument layouts ---------------

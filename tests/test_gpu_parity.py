@@ -261,18 +261,48 @@ def test_fast_path_matches_ordered(gpu, num_a):
     elif num_a == 10:
         a[6:10] = sc.K
     b = np.asfortranarray(sc.X0[:3])
-    res = []
-    for ordered in (True, False):
+    res, plans = [], []
+    for ordered, kern in ((True, "auto"), (False, "terms"), (False, "auto")):
         ba = gpu.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, num_a,
-                                ordered=ordered)
+                                ordered=ordered, schur_kernel=kern)
         ba.set_params(a, b)
         info = ba.step(relinearize=True, update_lm=False)
         res.append(info)
+        plans.append(ba.plan_info())
         ba.close()
-    o, f = res
-    assert abs(o.old_sse - f.old_sse) <= 1e-13 * o.old_sse, (o.old_sse, f.old_sse)
-    assert abs(o.new_sse - f.new_sse) <= 1e-8 * o.new_sse, (o.new_sse, f.new_sse)
-    assert abs(o.dpg - f.dpg) <= 1e-8 * abs(o.dpg), (o.dpg, f.dpg)
+    assert [p["mfma"] for p in plans] == [0, 0, 1]
+    o = res[0]
+    for f in res[1:]:
+        assert abs(o.old_sse - f.old_sse) <= 1e-13 * o.old_sse, (o.old_sse, f.old_sse)
+        assert abs(o.new_sse - f.new_sse) <= 1e-8 * o.new_sse, (o.new_sse, f.new_sse)
+        assert abs(o.dpg - f.dpg) <= 1e-8 * abs(o.dpg), (o.dpg, f.dpg)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_mfma_schur_on_banded_scene(gpu, seed):
+    """Video-like banded tracks (config-3 shape, scaled down): the MFMA Schur
+    chunks and the per-term kernel give the same reduced system to rounding,
+    on accepted and rejected (re-damped, no relinearisation) passes."""
+    from bundleadjustmentmatlab_amd.scene import make_config
+    sc = make_config("cfg3", m=120, n=30000, seed=seed)
+    a = np.zeros((6, sc.m), order="F")
+    a[0:3], a[3:6] = sc.w0, sc.T0
+    b = np.asfortranarray(sc.X0[:3])
+    out = {}
+    for kern in ("terms", "auto"):
+        ba = gpu.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, 6,
+                                schur_kernel=kern)
+        ba.set_params(a, b)
+        i1 = ba.step(relinearize=True, update_lm=False)
+        i2 = ba.step(relinearize=False, update_lm=False)
+        out[kern] = (i1, i2, ba.plan_info()["mfma"])
+        ba.close()
+    assert out["terms"][2] == 0 and out["auto"][2] == 1
+    for t, f in zip(out["terms"][:2], out["auto"][:2]):
+        # SSE partials are summed per chunk, and the two plans chunk differently
+        assert abs(t.old_sse - f.old_sse) <= 1e-13 * t.old_sse, (t.old_sse, f.old_sse)
+        assert abs(t.new_sse - f.new_sse) <= 1e-9 * t.new_sse, (t.new_sse, f.new_sse)
+        assert abs(t.dpg - f.dpg) <= 1e-9 * abs(t.dpg), (t.dpg, f.dpg)
 
 
 def test_single_pass_config2(gpu, oracle):

@@ -20,7 +20,9 @@ L.LIB_PATH = os.path.join(ROOT, "bundleadjustmentmatlab_amd", "libvlgba_stamps.s
 from bundleadjustmentmatlab_amd import BundleAdjuster  # noqa: E402
 from bundleadjustmentmatlab_amd.scene import make_config  # noqa: E402
 
-PHASES = {"k_schur_group": ["prologue", "stage+pinv", "Y", "slots+e", "barrier", "epilogue"]}
+PHASES = {"k_schur_group": ["prologue", "stage+pinv", "Y", "slots+e", "barrier", "epilogue"],
+          "k_schur_mfma": ["prologue", "stage+pinv", "W scatter", "Y", "mfma+e+flush",
+                           "final barrier", "epilogue"]}
 
 
 def main():
@@ -45,12 +47,20 @@ def main():
     ba.sync()
     fn(st, 1)
     v = [st[i] / reps for i in range(32)]
-    chunks, wgs = v[6], v[7]
-    print(f"k_schur_group: {wgs:.0f} workgroups, {chunks:.0f} chunks per pass")
-    tot = sum(v[:6])
-    for i, name in enumerate(PHASES["k_schur_group"]):
+    kern = "k_schur_mfma" if ba.plan_info()["mfma"] else "k_schur_group"
+    names = PHASES[kern]
+    chunks, wgs = (v[8], v[9]) if kern == "k_schur_mfma" else (v[6], v[7])
+    print(f"{kern}: {wgs:.0f} workgroups, {chunks:.0f} chunks per pass")
+    tot = sum(v[:len(names)])
+    for i, name in enumerate(names):
         print(f"  {name:12s} {v[i] / 1e6:9.2f} Mcycles  {100 * v[i] / tot:5.1f}%  "
               f"{v[i] / max(chunks, 1):9.0f} cycles/chunk")
+    if kern == "k_schur_mfma" and v[11] > 0:
+        # s_memrealtime runs at 100 MHz: calibrates s_memtime and the WG lifetime
+        ghz = v[10] / v[11] * 0.1
+        life_us = v[11] / wgs / 100.0
+        print(f"  s_memtime clock {ghz:.2f} GHz; mean workgroup lifetime {life_us:.1f} us; "
+              f"sum of lifetimes {v[11] / 100.0:.0f} us")
     ba.close()
 
 
