@@ -5,7 +5,8 @@ Drop-in for the Levenberg-Marquardt path of caomw/BundleAdjustmentMatlab
 hand-written gfx950 HIP kernels behind the C ABI in include/vlgba.h
 (libvlgba.so, built in-tree).
 """
-from .bundle import (BundleAdjuster, bundle_euclid, bundle_euclid_obs,  # noqa: F401
+from .bundle import (BundleAdjuster, bundle_euclid, bundle_euclid_nomex,  # noqa: F401
+                     bundle_euclid_obs,
                      mex_bundle_1_XABeUVWeAeB, mex_bundle_2_Se_, mex_bundle_3_db_new,
                      parse_options)
 from ._lib import LIB_PATH, VlgbaError, lib  # noqa: F401

@@ -30,7 +30,8 @@ class VlgbaOptions(ctypes.Structure):
                 ("lambda0", c_double), ("device", c_int), ("rank", c_int),
                 ("world_size", c_int), ("comm_id", ctypes.c_void_p), ("dense_solve", c_int),
                 ("ordered", c_int), ("allreduce", ctypes.c_void_p),
-                ("allreduce_user", ctypes.c_void_p), ("schur_kernel", c_int)]
+                ("allreduce_user", ctypes.c_void_p), ("schur_kernel", c_int),
+                ("semantics", c_int)]
 
 
 NKERNELS = 16   # VLGBA_NKERNELS

@@ -13,6 +13,10 @@ LM loop (bundle_euclid.m:111-249) runs on the GPU through ``vlgba_solve``.
 form that scales to the 1000-camera / 500k-point configs (a dense x at that
 size is 12 GB).
 
+``bundle_euclid_nomex`` is the same drop-in for the reference's pure-MATLAB
+twin toolbox/bundle/bundle_euclid_nomex.m (full-da back substitution, no
+'fix_pivot', Xe_(4,:) = 1).
+
 ``mex_bundle_1_XABeUVWeAeB`` / ``mex_bundle_2_Se_`` / ``mex_bundle_3_db_new``
 mirror the three MEX stages with their exact argument layouts.
 """
@@ -24,7 +28,8 @@ import numpy as np
 from ._lib import (ALLREDUCE_FN, NKERNELS, VlgbaOptions, VlgbaProblem, VlgbaStats,
                    VlgbaStepInfo, c_dp, c_ip, c_up, check, lib)
 
-__all__ = ["bundle_euclid", "bundle_euclid_obs", "BundleAdjuster", "parse_options",
+__all__ = ["bundle_euclid", "bundle_euclid_nomex", "bundle_euclid_obs", "BundleAdjuster",
+           "parse_options",
            "mex_bundle_1_XABeUVWeAeB", "mex_bundle_2_Se_", "mex_bundle_3_db_new"]
 
 
@@ -39,9 +44,11 @@ def _dp(a):
 # ---------------------------------------------------------------------------
 # options (bundle_euclid.m:44-82)
 # ---------------------------------------------------------------------------
-def parse_options(m, n, varargin, x=None):
+def parse_options(m, n, varargin, x=None, nomex=False):
     """Name/value options of bundle_euclid.m:53-78.  Unknown names are
-    ignored, as the reference's switch statement ignores them."""
+    ignored, as the reference's switch statement ignores them.  nomex=True
+    parses bundle_euclid_nomex.m:50-70 instead, which has no 'fix_pivot': the
+    name and its argument fall through its switch and are ignored."""
     o = dict(fix_structure=False, fix_motion=False, fix_pivot=False,
              pivot=np.zeros(m, dtype=bool), num_variableK=4, visible=None, verbose=False)
     k = 0
@@ -54,8 +61,9 @@ def parse_options(m, n, varargin, x=None):
         elif name == "fix_motion":
             o["fix_motion"] = True
         elif name == "fix_pivot":
-            o["fix_pivot"] = True
-            o["pivot"] = np.asarray(varargin[k + 1], dtype=bool).reshape(-1)
+            if not nomex:
+                o["fix_pivot"] = True
+                o["pivot"] = np.asarray(varargin[k + 1], dtype=bool).reshape(-1)
             k += 1
         elif name == "fix_calibration":
             o["num_variableK"] = 0
@@ -112,15 +120,17 @@ class BundleAdjuster:
     ``dense_solve=True`` is the same as solver="dense".  ``schur_kernel``
     picks the fast-path Schur complement kernel: "auto" (dense per-chunk
     products on fp64 MFMA when the tracks fit) or "terms" (per-term sums).
+    ``semantics`` is "mex" (bundle_euclid.m) or "nomex" (bundle_euclid_nomex.m).
     """
     SOLVERS = {"auto": 0, "dense": 1, "envelope": 2}
     SCHUR_KERNELS = {"auto": 0, "terms": 1}
+    SEMANTICS = {"mex": 0, "nomex": 1}
 
     def __init__(self, K, obs_pt, obs_cam, obs_x, n, num_a=6, *, fix_structure=False,
                  fix_motion=False, pivot=None, verbose=False, num_vis=0.0, device=0,
                  rank=0, world_size=1, comm_id=None, max_iter=0, max_iter2=0, lambda0=0.0,
                  dense_solve=False, ordered=False, allreduce=None, solver=None,
-                 schur_kernel="auto"):
+                 schur_kernel="auto", semantics="mex"):
         L = lib()
         solve_mode = self.SOLVERS[solver] if solver is not None else int(bool(dense_solve))
         self.K = _F(K)
@@ -158,7 +168,7 @@ class BundleAdjuster:
                            ctypes.cast(self._comm, ctypes.c_void_p) if self._comm else None,
                            solve_mode, int(ordered),
                            ctypes.cast(self._ar, ctypes.c_void_p) if self._ar else None, None,
-                           self.SCHUR_KERNELS[schur_kernel])
+                           self.SCHUR_KERNELS[schur_kernel], self.SEMANTICS[semantics])
         h = ctypes.c_void_p()
         check(L.vlgba_create(ctypes.byref(prob), ctypes.byref(opt), ctypes.byref(h)),
               "vlgba_create")
@@ -260,11 +270,13 @@ class BundleAdjuster:
 # drop-in drivers
 # ---------------------------------------------------------------------------
 def bundle_euclid_obs(K, Te, w, Xe, obs_pt, obs_cam, obs_x, *varargin, num_vis=0.0, device=0,
-                      rank=0, world_size=1, comm_id=None, return_stats=False):
+                      rank=0, world_size=1, comm_id=None, return_stats=False,
+                      semantics="mex"):
     """bundle_euclid on a COO observation list (0-based point / camera ids)."""
     K, Te, w, Xe = _F(K), _F(Te), _F(w), _F(Xe)
     m, n = w.shape[1], Xe.shape[1]
-    o = parse_options(m, n, varargin)
+    nomex = semantics == "nomex"
+    o = parse_options(m, n, varargin, nomex=nomex)
     nvk = o["num_variableK"]
     num_a = 6 + nvk
     a = pack_a(K, Te, w, nvk)
@@ -273,19 +285,20 @@ def bundle_euclid_obs(K, Te, w, Xe, obs_pt, obs_cam, obs_x, *varargin, num_vis=0
                         fix_structure=o["fix_structure"], fix_motion=o["fix_motion"],
                         pivot=o["pivot"] if o["fix_pivot"] else None, verbose=o["verbose"],
                         num_vis=num_vis, device=device, rank=rank, world_size=world_size,
-                        comm_id=comm_id) as ba:
+                        comm_id=comm_id, semantics=semantics) as ba:
         ba.set_params(a, b)
         err, st = ba.run()
         a, b = ba.get_params()
-    out = unpack(K, a, b, Xe[3:4], nvk) + (err,)
+    # Xe_(4,:): the input's (bundle_euclid.m:267) or ones (bundle_euclid_nomex.m:364)
+    out = unpack(K, a, b, np.ones((1, n)) if nomex else Xe[3:4], nvk) + (err,)
     return out + (st,) if return_stats else out
 
 
-def bundle_euclid(K, Te, w, Xe, x, *varargin, device=0, return_stats=False):
+def bundle_euclid(K, Te, w, Xe, x, *varargin, device=0, return_stats=False, semantics="mex"):
     """[K_ Te_ w_ Xe_ error_] = bundle_euclid(K, Te, w, Xe, x, ...)  (bundle_euclid.m:1)."""
     x = _F(x)
     m, n = np.shape(w)[1], x.shape[1]
-    o = parse_options(m, n, varargin, x=x)
+    o = parse_options(m, n, varargin, x=x, nomex=semantics == "nomex")
     vis = o["visible"]
     num_vis = float(vis.sum())                                     # bundle_euclid.m:82
     pt, cam = np.nonzero(vis)                                      # point-major
@@ -304,7 +317,15 @@ def bundle_euclid(K, Te, w, Xe, x, *varargin, device=0, return_stats=False):
         rest.append(varargin[k])
         k += 1
     return bundle_euclid_obs(K, Te, w, Xe, pt, cam, obs_x, *rest, num_vis=num_vis,
-                             device=device, return_stats=return_stats)
+                             device=device, return_stats=return_stats, semantics=semantics)
+
+
+def bundle_euclid_nomex(K, Te, w, Xe, x, *varargin, device=0, return_stats=False):
+    """[K_ Te_ w_ Xe_ error_] = bundle_euclid_nomex(K, Te, w, Xe, x, ...)
+    (bundle_euclid_nomex.m:1): the same LM loop with the twin's semantics --
+    db from every camera parameter (:268-277), no 'fix_pivot', Xe_(4,:) = 1."""
+    return bundle_euclid(K, Te, w, Xe, x, *varargin, device=device,
+                         return_stats=return_stats, semantics="nomex")
 
 
 # ---------------------------------------------------------------------------

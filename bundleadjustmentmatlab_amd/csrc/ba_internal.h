@@ -102,6 +102,8 @@ struct ba_dev {
     int ordered;       // 1: sequential bit-exact kernels (k_damp_point + k_schur)
     int mfma;          // fast path: 1 = MFMA Schur chunks (k_schur_mfma), 0 = term lists
     int no_mfma;       // option: force the term-list Schur kernel
+    int ndb;           // camera parameters in the back substitution: 6 (MEX, App. A
+                       // Q3) or NA (bundle_euclid_nomex.m semantics)
     int nch;           // chunks
     int *ch_pt;        // [nch+1] local point ranges
     int *ch_slot;      // [nch+1] slot ranges (slots are numbered chunk-major)

@@ -1079,7 +1079,8 @@ __global__ __launch_bounds__(256) void k_camera_update(
 }
 
 // -------------------------------------------------------------------------
-// point update: db_i (only da[0..5] per camera, App. A Q3), b_new, new
+// point update: db_i (da[0 .. ndb) per camera: ndb = 6 as the MEX file,
+// App. A Q3, or NA for bundle_euclid_nomex.m:268-277), b_new, new
 // projections of the point's observations, new SSE and the point part of
 // dp'(lambda dp + g)
 // -------------------------------------------------------------------------
@@ -1090,7 +1091,7 @@ __global__ __launch_bounds__(256) void k_point_update(
     const double *__restrict__ W, const double *__restrict__ da,
     const double *__restrict__ eB, const double *__restrict__ Vinv,
     const double *__restrict__ b, const double *__restrict__ a_new,
-    const double *__restrict__ rot_new, int n, double lambda, double *__restrict__ db,
+    const double *__restrict__ rot_new, int n, int ndb, double lambda, double *__restrict__ db,
     double *__restrict__ b_new, double *__restrict__ part_sse, double *__restrict__ part_dpg,
     const unsigned char *__restrict__ obs_vis, double *__restrict__ xh_out)
 {
@@ -1102,14 +1103,18 @@ __global__ __launch_bounds__(256) void k_point_update(
         for (int o = o0; o < o1; o++) {
             const double *w = W + (size_t)3 * NA * o;
             const double *d = da + (size_t)NA * obs_cam[o];
-            double dl[6];
+            double dl[NA];
 #pragma unroll
-            for (int k = 0; k < 6; k++) dl[k] = d[k];
+            for (int k = 0; k < NA; k++) dl[k] = k < ndb ? d[k] : 0.0;
 #pragma unroll
             for (int r = 0; r < 3; r++) {
                 const double *wr = w + NA * r;
-                rhs[r] -= wr[0] * dl[0] + wr[1] * dl[1] + wr[2] * dl[2] + wr[3] * dl[3] +
-                          wr[4] * dl[4] + wr[5] * dl[5];
+                double t = wr[0] * dl[0] + wr[1] * dl[1] + wr[2] * dl[2] + wr[3] * dl[3] +
+                           wr[4] * dl[4] + wr[5] * dl[5];
+#pragma unroll
+                for (int k = 6; k < NA; k++)   // nomex semantics only (ndb = NA)
+                    if (k < ndb) t = t + wr[k] * dl[k];
+                rhs[r] -= t;
             }
         }
         const double *vi = Vinv + 9 * (size_t)i;
@@ -1343,7 +1348,7 @@ int ba_launch_update(ba_dev *d, double lambda)
     KT_B(d);
     BA_DISPATCH(d->na, (k_point_update<NA><<<g, 256, 0, d->stream>>>(
                            d->pt_ptr, d->obs_cam, d->obs_x, d->K4, d->W, d->da, d->eB, d->Vinv,
-                           d->b, d->a_new, d->rot_new, d->n, lambda, d->db, d->b_new,
+                           d->b, d->a_new, d->rot_new, d->n, d->ndb, lambda, d->db, d->b_new,
                            d->part + BA_PART_MAX, d->part + 2 * BA_PART_MAX, d->obs_vis,
                            d->xh_out)));
     KT_E(d, KT_PTUPD);

@@ -845,7 +845,9 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
         c->num_vis = p->num_vis > 0 ? p->num_vis : (double)p->num_obs;
         c->flags.fix_structure = o->fix_structure;
         c->flags.fix_motion = o->fix_motion;
-        c->flags.has_pivot = o->pivot != nullptr;
+        if (o->semantics != 0 && o->semantics != 1) { rc = VLGBA_E_ARG; break; }
+        // bundle_euclid_nomex.m has no fix_pivot option: the pivot is ignored there
+        c->flags.has_pivot = o->pivot != nullptr && o->semantics == 0;
         c->max_iter = o->max_iter > 0 ? o->max_iter : 20;
         c->max_iter2 = o->max_iter2 > 0 ? o->max_iter2 : 10;
         c->lambda0 = c->lambda = o->lambda0 > 0 ? o->lambda0 : 1e-3;
@@ -853,9 +855,10 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
         c->d.dense_solve = o->dense_solve;
         c->d.ordered = o->ordered;
         c->d.no_mfma = o->schur_kernel == 1;
+        c->d.ndb = o->semantics == 1 ? p->num_a : 6;
         rc = ctx_setup(c, p, h, pt_ptr_all, lower_blocks, all_diag, stage_mode);
         if (rc) break;
-        if (o->pivot) {
+        if (c->flags.has_pivot) {
             rc = ctx_alloc(c, &c->d.pivot, (size_t)p->m);
             if (rc) break;
             rc = upload(c->d.pivot, o->pivot, (size_t)p->m, c->d.stream);

@@ -83,6 +83,12 @@ typedef struct {
      * 16 * (num_a == 6 ? 3 : 4) / num_a observations, else per-term sums;
      * 1: per-term sums (measurement / cross-check).  Same terms either way. */
     int schur_kernel;
+    /* driver semantics: 0 (default) bundle_euclid.m (MEX-backed: the back
+     * substitution uses da(1:6,j) only, mex_bundle_3_db_new.c:113-120, App. A
+     * Q3; 'fix_pivot' honoured); 1 bundle_euclid_nomex.m (the pure-MATLAB
+     * twin: db uses all num_a rows of da, bundle_euclid_nomex.m:268-277; no
+     * fix_pivot -- pivot is ignored) */
+    int semantics;
 } vlgba_options;
 
 typedef struct {

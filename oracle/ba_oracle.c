@@ -357,11 +357,15 @@ void oracle_sp_schur(int m, int n, int num_a, const int *pt_ptr, const int *obs_
 
 /* mex_3 on the observation list: db, a_new, b_new and the new projections of
  * the (visible) observations.  Returns sum of squared new residuals. */
-double oracle_sp_update(int m, int n, int num_a, const int *pt_ptr, const int *obs_cam,
-                        const double *obs_x, const double *W, const double *da,
-                        const double *eB, const double *Vinv, const double *K4,
-                        const double *a, const double *b, double *db, double *a_new,
-                        double *b_new, double *obs_xhat)
+/* ndb: camera parameters used in the back substitution -- 6 as
+ * mex_bundle_3_db_new.c:113-120 (App. A Q3), or num_a for the pure-MATLAB twin
+ * bundle_euclid_nomex.m:268-277 (W(:,:,i,j)' * da(k:k+num_a-1), summed here
+ * left to right after the first six terms). */
+double oracle_sp_update_nd(int m, int n, int num_a, int ndb, const int *pt_ptr,
+                           const int *obs_cam, const double *obs_x, const double *W,
+                           const double *da, const double *eB, const double *Vinv,
+                           const double *K4, const double *a, const double *b, double *db,
+                           double *a_new, double *b_new, double *obs_xhat)
 {
     int i, o, r, k;
     double sse = 0.0;
@@ -375,8 +379,11 @@ double oracle_sp_update(int m, int n, int num_a, const int *pt_ptr, const int *o
             const double *d = da + (size_t)num_a * obs_cam[o];
             for (r = 0; r < 3; r++) {
                 const double *wr = w + num_a * r;
-                rhs[r] -= wr[0] * d[0] + wr[1] * d[1] + wr[2] * d[2] + wr[3] * d[3] +
-                          wr[4] * d[4] + wr[5] * d[5];
+                double t = wr[0] * d[0] + wr[1] * d[1] + wr[2] * d[2] + wr[3] * d[3] +
+                           wr[4] * d[4] + wr[5] * d[5];
+                for (k = 6; k < ndb; k++)
+                    t = t + wr[k] * d[k];
+                rhs[r] -= t;
             }
         }
         for (r = 0; r < 3; r++)
@@ -397,4 +404,15 @@ double oracle_sp_update(int m, int n, int num_a, const int *pt_ptr, const int *o
             sse += d0 * d0 + d1 * d1;
         }
     return sse;
+}
+
+/* mex_bundle_3_db_new.c:99-166 on the observation list (6-term db, App. A Q3) */
+double oracle_sp_update(int m, int n, int num_a, const int *pt_ptr, const int *obs_cam,
+                        const double *obs_x, const double *W, const double *da,
+                        const double *eB, const double *Vinv, const double *K4,
+                        const double *a, const double *b, double *db, double *a_new,
+                        double *b_new, double *obs_xhat)
+{
+    return oracle_sp_update_nd(m, n, num_a, 6, pt_ptr, obs_cam, obs_x, W, da, eB, Vinv, K4, a,
+                               b, db, a_new, b_new, obs_xhat);
 }

@@ -40,6 +40,7 @@ def _lib(variant: str = ""):
             subprocess.run(["make", "-C", _HERE], check=True, capture_output=True)
         lib = ctypes.CDLL(path)
         lib.oracle_sp_update.restype = ctypes.c_double
+        lib.oracle_sp_update_nd.restype = ctypes.c_double
         lib.oracle_sin.restype = ctypes.c_double
         lib.oracle_cos.restype = ctypes.c_double
         lib.oracle_sin.argtypes = [ctypes.c_double]
@@ -221,15 +222,17 @@ def sp_schur(pb, Y, W, Us, eA, eB, num_a, lib=None):
     return S, e_
 
 
-def sp_update(pb, W, da, eB, Vinv, a, b, num_a, lib=None):
+def sp_update(pb, W, da, eB, Vinv, a, b, num_a, lib=None, ndb=6):
+    """mex_bundle_3_db_new.c:99-166 on the observation list; ndb = num_a gives
+    the back substitution of bundle_euclid_nomex.m:268-277 instead."""
     lib = lib or _lib()
     db = np.zeros((3, pb.n), order="F")
     a_new = np.zeros((num_a, pb.m), order="F")
     b_new = np.zeros((3, pb.n), order="F")
     xh = np.zeros((pb.N, 2))
-    sse = lib.oracle_sp_update(pb.m, pb.n, num_a, P(pb.pt_ptr), P(pb.obs_cam), P(pb.obs_x),
-                               P(W), P(F(da)), P(F(eB)), P(F(Vinv)), P(pb.K), P(F(a)),
-                               P(F(b)), P(db), P(a_new), P(b_new), P(xh))
+    sse = lib.oracle_sp_update_nd(pb.m, pb.n, num_a, ndb, P(pb.pt_ptr), P(pb.obs_cam),
+                                  P(pb.obs_x), P(W), P(F(da)), P(F(eB)), P(F(Vinv)), P(pb.K),
+                                  P(F(a)), P(F(b)), P(db), P(a_new), P(b_new), P(xh))
     return db, a_new, b_new, xh, sse
 
 
@@ -292,17 +295,23 @@ def unpack(K, a, b, Xe, nvk):
 
 
 def bundle_euclid_ref(K, Te, w, Xe, x, *varargin, form="dense", vinv="pinv", solve="pinv",
-                      lib=None, trace=None):
+                      lib=None, trace=None, semantics="mex"):
     """[K_ Te_ w_ Xe_ error_] = bundle_euclid(K, Te, w, Xe, x, ...) restated.
 
     trace: optional list; per iteration a dict (lambda, accepted, old, new, rho)
-    is appended.
+    is appended.  semantics="nomex" restates bundle_euclid_nomex.m instead: the
+    back substitution uses every camera parameter (:268-277), 'fix_pivot' is
+    not an option (ignored), Xe_(4,:) = 1 (:364); requires form="sparse".
     """
+    nomex = semantics == "nomex"
+    assert semantics in ("mex", "nomex") and (form == "sparse" or not nomex)
     lib = lib or _lib()
     K, Te, w, Xe, x = F(K), F(Te), F(w), F(Xe), F(x)
     m = w.shape[1]
     n = x.shape[1]
     o = parse_options(m, n, x, varargin)
+    if nomex:
+        o["fix_pivot"] = False
     nvk = o["num_variableK"]
     vis = F(o["visible"])
     num_vis = vis.sum()
@@ -370,7 +379,8 @@ def bundle_euclid_ref(K, Te, w, Xe, x, *varargin, form="dense", vinv="pinv", sol
             old_error = float(e.reshape(-1, order="F") @ e.reshape(-1, order="F"))
             new_error = float(e_new.reshape(-1, order="F") @ e_new.reshape(-1, order="F"))
         else:
-            db, a_new, b_new, xh, _ = sp_update(pb, W, da, eB, Vinv, a, b, num_a, lib)
+            db, a_new, b_new, xh, _ = sp_update(pb, W, da, eB, Vinv, a, b, num_a, lib,
+                                                ndb=num_a if nomex else 6)
             en = pb.obs_x - xh
             old_error = float(e.reshape(-1) @ e.reshape(-1))
             new_error = float(en.reshape(-1) @ en.reshape(-1))
@@ -402,4 +412,6 @@ def bundle_euclid_ref(K, Te, w, Xe, x, *varargin, form="dense", vinv="pinv", sol
             nu = 2.0 * nu
             it2 += 1
     K_, Te_, w_, Xe_ = unpack(K, a, b, Xe, nvk)
+    if nomex:
+        Xe_[3] = 1.0
     return K_, Te_, w_, Xe_, np.array(err)

@@ -152,6 +152,32 @@ def test_lm_fix_pivot(gpu, oracle):
     assert np.array_equal(res[1][:, :2], sc.T0[:, :2])
 
 
+@pytest.mark.parametrize("opts,final_rtol", [(("fix_calibration",), 1e-4), ((), 3e-2)])
+def test_lm_nomex_semantics(gpu, oracle, opts, final_rtol):
+    """bundle_euclid_nomex (the pure-MATLAB twin's semantics: full-da back
+    substitution, no fix_pivot, Xe_(4,:) = 1) vs the oracle with the same
+    semantics: first error_ entry to summation order, first accepted step to
+    rounding, final cost inside the oracle variants' spread."""
+    from bundleadjustmentmatlab_amd.scene import make_config
+    sc = make_config("cfg1", m=6, min_n=30, max_n=60, seed=7)
+    x, vis = sc.dense()
+    pv = np.zeros(sc.m, dtype=bool)
+    pv[:2] = True
+    res = gpu.bundle_euclid_nomex(sc.K, sc.T0, sc.w0, sc.X0, x, "visibility", vis, *opts,
+                                  "fix_pivot", pv)                 # ignored by the twin
+    refs = [oracle.bundle_euclid_ref(sc.K, sc.T0, sc.w0, sc.X0, x, "visibility", vis, *opts,
+                                     form="sparse", vinv=vinv, solve=solve, semantics="nomex")
+            for vinv, solve in VARIANTS]
+    err = res[4]
+    assert abs(err[0] - refs[0][4][0]) <= 1e-12 * refs[0][4][0]
+    e1 = [r[4][1] for r in refs]
+    assert min(e1) * (1 - 1e-7) <= err[1] <= max(e1) * (1 + 1e-7), (err, e1)
+    finals = [r[4][-1] for r in refs]
+    assert min(finals) * (1 - final_rtol) <= err[-1] <= max(finals) * (1 + final_rtol)
+    assert np.all(res[3][3] == 1.0)
+    assert not np.array_equal(res[2][:, :2], sc.w0[:, :2])      # pivot cameras moved
+
+
 def test_envelope_equals_dense_solve(gpu):
     """Skipping the tiles outside the envelope of S is exact: every result of a
     pass is bit-identical to factoring all lower tiles (sequential tile
