@@ -9,6 +9,9 @@ from .bundle import (BundleAdjuster, bundle_euclid, bundle_euclid_nomex,  # noqa
                      bundle_euclid_obs,
                      mex_bundle_1_XABeUVWeAeB, mex_bundle_2_Se_, mex_bundle_3_db_new,
                      parse_options)
+from .projective import (bundle_projective, bundle_projective_nomex,  # noqa: F401
+                         bundle_projective_obs, mex_bundle_proj_1_XABeUVWeAeB,
+                         mex_bundle_proj_2_Se_, mex_bundle_proj_3_db_new)
 from ._lib import LIB_PATH, VlgbaError, lib  # noqa: F401
 
 __version__ = "0.1.0"

@@ -21,7 +21,10 @@ c_up = ctypes.POINTER(ctypes.c_ubyte)
 class VlgbaProblem(ctypes.Structure):
     _fields_ = [("m", c_int), ("n", c_int), ("num_a", c_int), ("num_obs", c_ll),
                 ("obs_pt", c_ip), ("obs_cam", c_ip), ("obs_x", c_dp), ("K", c_dp),
-                ("num_vis", c_double)]
+                ("num_vis", c_double), ("model", c_int)]
+
+
+MODEL_EUCLIDEAN, MODEL_PROJECTIVE = 0, 1   # VLGBA_MODEL_*
 
 
 class VlgbaOptions(ctypes.Structure):
@@ -72,12 +75,16 @@ SIGNATURES = {
     "vlgba_mex_bundle_1": (c_int, [c_int, c_int, c_int] + [c_dp] * 14),
     "vlgba_mex_bundle_2": (c_int, [c_int, c_int, c_int] + [c_dp] * 7),
     "vlgba_mex_bundle_3": (c_int, [c_int, c_int, c_int] + [c_dp] * 13),
+    "vlgba_mex_bundle_proj_1": (c_int, [c_int, c_int] + [c_dp] * 13),
+    "vlgba_mex_bundle_proj_2": (c_int, [c_int, c_int] + [c_dp] * 7),
+    "vlgba_mex_bundle_proj_3": (c_int, [c_int, c_int] + [c_dp] * 12),
     "vlgba_version": (c_int, [ctypes.c_char_p, c_int]),
     "vlgba_get_unique_id": (c_int, [ctypes.c_void_p]),
     "vlgba_device_count": (c_int, []),
 }
 
-ERRORS = {-1001: "bad argument", -1002: "num_a must be 6, 7 or 10",
+ERRORS = {-1001: "bad argument",
+          -1002: "num_a must be 6, 7 or 10 (Euclidean) or 12 (projective)",
           -1003: "duplicate (point, camera) observation", -1004: "out of host memory",
           -1005: "RCCL communicator failure"}
 

@@ -25,7 +25,8 @@ from __future__ import annotations
 import ctypes
 import numpy as np
 
-from ._lib import (ALLREDUCE_FN, NKERNELS, VlgbaOptions, VlgbaProblem, VlgbaStats,
+from ._lib import (ALLREDUCE_FN, MODEL_EUCLIDEAN, MODEL_PROJECTIVE, NKERNELS, VlgbaOptions,
+                   VlgbaProblem, VlgbaStats,
                    VlgbaStepInfo, c_dp, c_ip, c_up, check, lib)
 
 __all__ = ["bundle_euclid", "bundle_euclid_nomex", "bundle_euclid_obs", "BundleAdjuster",
@@ -121,20 +122,23 @@ class BundleAdjuster:
     picks the fast-path Schur complement kernel: "auto" (dense per-chunk
     products on fp64 MFMA when the tracks fit) or "terms" (per-term sums).
     ``semantics`` is "mex" (bundle_euclid.m) or "nomex" (bundle_euclid_nomex.m).
+    ``model="projective"`` solves bundle_projective.m instead: num_a = 12
+    (a = P(:) per camera), K is None and ``m`` gives the camera count.
     """
     SOLVERS = {"auto": 0, "dense": 1, "envelope": 2}
     SCHUR_KERNELS = {"auto": 0, "terms": 1}
     SEMANTICS = {"mex": 0, "nomex": 1}
+    MODELS = {"euclidean": MODEL_EUCLIDEAN, "projective": MODEL_PROJECTIVE}
 
     def __init__(self, K, obs_pt, obs_cam, obs_x, n, num_a=6, *, fix_structure=False,
                  fix_motion=False, pivot=None, verbose=False, num_vis=0.0, device=0,
                  rank=0, world_size=1, comm_id=None, max_iter=0, max_iter2=0, lambda0=0.0,
                  dense_solve=False, ordered=False, allreduce=None, solver=None,
-                 schur_kernel="auto", semantics="mex"):
+                 schur_kernel="auto", semantics="mex", model="euclidean", m=None):
         L = lib()
         solve_mode = self.SOLVERS[solver] if solver is not None else int(bool(dense_solve))
-        self.K = _F(K)
-        self.m = self.K.shape[1]
+        self.K = _F(K) if K is not None else None
+        self.m = int(m) if m is not None else self.K.shape[1]
         self.n = int(n)
         self.num_a = int(num_a)
         self._pt = np.ascontiguousarray(obs_pt, dtype=np.int32)
@@ -143,7 +147,8 @@ class BundleAdjuster:
         self.num_obs = len(self._pt)
         prob = VlgbaProblem(self.m, self.n, self.num_a, self.num_obs,
                             self._pt.ctypes.data_as(c_ip), self._cam.ctypes.data_as(c_ip),
-                            _dp(self._x), _dp(self.K), float(num_vis))
+                            _dp(self._x), _dp(self.K) if self.K is not None else None,
+                            float(num_vis), self.MODELS[model])
         self._pivot = None
         if pivot is not None:
             self._pivot = np.ascontiguousarray(np.asarray(pivot, dtype=bool).reshape(-1),

@@ -2,7 +2,8 @@
 //
 // One ba_dev per (problem, GPU).  Everything lives in HBM for the whole solve;
 // only scalars cross PCIe per LM iteration.  Layout (N = visible observations,
-// NA = num_a = 6 / 7 / 10 camera parameters, m cameras, n points):
+// NA = num_a = 6 / 7 / 10 Euclidean camera parameters or 12 for the projective
+// camera P(:) of bundle_projective.m, m cameras, n points):
 //
 //   observations, point-major (points ascending, cameras ascending inside a
 //   point = the reference's column-major (i + n*j) visiting order per point):
@@ -47,6 +48,11 @@ struct ba_ktimer {
 };
 void kt_begin(struct ba_ktimer *t, hipStream_t s);
 void kt_end(struct ba_ktimer *t, hipStream_t s, int kid);
+
+// camera model: NA == BA_PROJ_NA is the projective camera (a = P(:), 3 x 4,
+// bundle_projective.m:70-73, projection mex_bundle_proj_1_XABeUVWeAeB.c:13-32;
+// no K, no rotations); NA = 6 / 7 / 10 the Euclidean [w; T; (K)]
+#define BA_PROJ_NA 12
 
 struct ba_flags {
     int fix_structure;  // V, W, eB = 0       (bundle_euclid.m:140-144)

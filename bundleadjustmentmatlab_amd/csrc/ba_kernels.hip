@@ -1,4 +1,6 @@
-// ba_kernels.hip -- gfx950 kernels of one Euclidean LM iteration (fp64).
+// ba_kernels.hip -- gfx950 kernels of one LM iteration (fp64), Euclidean
+// (NA = 6 / 7 / 10) and projective (NA = BA_PROJ_NA = 12: the camera is P(:),
+// mex_bundle_proj_{1,3}*.c -- the same loops with reproject_projective_point).
 //
 // Reference path (toolbox/bundle/):
 //   k_rotations        vl_rodrigues per camera, hoisted out of reproject_point.h:44
@@ -76,6 +78,107 @@ __device__ __forceinline__ void block_sum_to(double v, double *out)
 }
 
 // -------------------------------------------------------------------------
+// camera j as the projections see it.  Euclidean (NA = 6 / 7 / 10): a0, the
+// calibration of reproject_point.h:26-41 and the hoisted rotations
+// R(w), R(w + h e_k), R(w + 0) (k_rotations); projective (NA = BA_PROJ_NA):
+// P = a0 (mex_bundle_proj_1_XABeUVWeAeB.c:21-22), K4 / rot unused.
+//   project(b, x)         x = proj(a0, b)
+//   project_dcam(k, b, x) x = proj(a0 + h e_k, b), a1 formed component-wise
+//                         as a0 + h * da (mex_bundle_1 :30-33, proj :47-51)
+//   project_col(c, b, x)  column c of [A | B]: c < NA as project_dcam, else
+//                         proj(a0, b + h e_{c-NA}) (mex_bundle_1 :59-66)
+// -------------------------------------------------------------------------
+template <int NA, bool PROJ = (NA == BA_PROJ_NA)>
+struct cam_view;
+
+template <int NA>
+struct cam_view<NA, false> {
+    double a0[NA], k4[4], Kc[9], Rl[9];
+    const double *R;
+    __device__ __forceinline__ cam_view(const double *__restrict__ a,
+                                        const double *__restrict__ K4,
+                                        const double *__restrict__ rot, int j)
+    {
+#pragma unroll
+        for (int c = 0; c < NA; c++) a0[c] = a[(size_t)NA * j + c];
+#pragma unroll
+        for (int c = 0; c < 4; c++) k4[c] = K4[4 * (size_t)j + c];
+        R = rot + 45 * (size_t)j;
+#pragma unroll
+        for (int q = 0; q < 9; q++) Rl[q] = R[q];
+        vlg_calib(Kc, k4, a0, NA - 6);
+    }
+    __device__ __forceinline__ void project(const double b[3], double x[2]) const
+    {
+        vlg_project(Kc, Rl, a0 + 3, b, x);
+    }
+    __device__ __forceinline__ void project_dcam(int k, const double b[3], double x[2]) const
+    {
+        double a1[NA], Kc1[9], Rk[9];
+#pragma unroll
+        for (int c = 0; c < NA; c++) a1[c] = a0[c] + H_FD * ((c == k) ? 1.0 : 0.0);
+        vlg_calib(Kc1, k4, a1, NA - 6);
+        const double *Rs = R + 9 * ((k < 3) ? (1 + k) : 4);
+#pragma unroll
+        for (int q = 0; q < 9; q++) Rk[q] = Rs[q];
+        vlg_project(Kc1, Rk, a1 + 3, b, x);
+    }
+    // FD column col of [A | B] without a branch: col < NA perturbs camera
+    // component col (as project_dcam), col >= NA point component col - NA
+    // with the unperturbed camera (mex_bundle_1 :43-70: K, R(w), T of a)
+    __device__ __forceinline__ void project_col(int col, const double b[3], double x[2]) const
+    {
+        const bool cam = col < NA;
+        double a1[NA], b1[3], Kc1[9], Rk[9];
+#pragma unroll
+        for (int c = 0; c < NA; c++)
+            a1[c] = cam ? a0[c] + H_FD * ((c == col) ? 1.0 : 0.0) : a0[c];
+#pragma unroll
+        for (int c = 0; c < 3; c++)
+            b1[c] = cam ? b[c] : b[c] + H_FD * ((c == col - NA) ? 1.0 : 0.0);
+        vlg_calib(Kc1, k4, a1, NA - 6);
+        const double *Rs = R + 9 * ((col < 3) ? (1 + col) : (cam ? 4 : 0));
+#pragma unroll
+        for (int q = 0; q < 9; q++) Rk[q] = Rs[q];
+        vlg_project(Kc1, Rk, a1 + 3, b1, x);
+    }
+};
+
+template <int NA>
+struct cam_view<NA, true> {
+    double a0[NA];
+    __device__ __forceinline__ cam_view(const double *__restrict__ a, const double *, const double *,
+                                        int j)
+    {
+#pragma unroll
+        for (int c = 0; c < NA; c++) a0[c] = a[(size_t)NA * j + c];
+    }
+    __device__ __forceinline__ void project(const double b[3], double x[2]) const
+    {
+        vlg_project_proj(a0, b, x);
+    }
+    __device__ __forceinline__ void project_dcam(int k, const double b[3], double x[2]) const
+    {
+        double a1[NA];
+#pragma unroll
+        for (int c = 0; c < NA; c++) a1[c] = a0[c] + H_FD * ((c == k) ? 1.0 : 0.0);
+        vlg_project_proj(a1, b, x);
+    }
+    __device__ __forceinline__ void project_col(int col, const double b[3], double x[2]) const
+    {
+        const bool cam = col < NA;
+        double a1[NA], b1[3];
+#pragma unroll
+        for (int c = 0; c < NA; c++)
+            a1[c] = cam ? a0[c] + H_FD * ((c == col) ? 1.0 : 0.0) : a0[c];
+#pragma unroll
+        for (int c = 0; c < 3; c++)
+            b1[c] = cam ? b[c] : b[c] + H_FD * ((c == col - NA) ? 1.0 : 0.0);
+        vlg_project_proj(a1, b1, x);
+    }
+};
+
+// -------------------------------------------------------------------------
 // rotations: R(a), R(a + h e_k) k = 0..2, R(a + 0) per camera (5 x 9)
 // -------------------------------------------------------------------------
 template <int NA>
@@ -117,7 +220,6 @@ __global__ __launch_bounds__(256) void k_linearize(
     double *__restrict__ B_out)
 {
     constexpr int JS = 2 * NA + 2;
-    constexpr int NVK = NA - 6;
     double sse = 0.0;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const double bi[3] = {b[3 * (size_t)i], b[3 * (size_t)i + 1], b[3 * (size_t)i + 2]};
@@ -128,42 +230,28 @@ __global__ __launch_bounds__(256) void k_linearize(
         const int o_end = pt_ptr[i + 1];
         for (int o = pt_ptr[i]; o < o_end; o++) {
             const int j = obs_cam[o];
-            double a0[NA], k4[4];
-#pragma unroll
-            for (int c = 0; c < NA; c++) a0[c] = a[(size_t)NA * j + c];
-#pragma unroll
-            for (int c = 0; c < 4; c++) k4[c] = K4[4 * (size_t)j + c];
-            const double *R = rot + 45 * (size_t)j;
-            double Rl[9];
-#pragma unroll
-            for (int q = 0; q < 9; q++) Rl[q] = R[q];
-            double Kc[9], xh[2];
-            vlg_calib(Kc, k4, a0, NVK);
-            vlg_project(Kc, Rl, a0 + 3, bi, xh);
+            cam_view<NA> cv(a, K4, rot, j);
+            double xh[2];
+            cv.project(bi, xh);
             double A[2 * NA], B[6];
             // camera derivatives, mex_bundle_1_XABeUVWeAeB.c:201-209, 14-41
+            // (mex_bundle_proj_1_XABeUVWeAeB.c:204-211, 34-59)
 #pragma unroll
             for (int k = 0; k < NA; k++) {
-                double a1[NA], Kc1[9], Rk[9], x1[2];
-#pragma unroll
-                for (int c = 0; c < NA; c++) a1[c] = a0[c] + H_FD * ((c == k) ? 1.0 : 0.0);
-                vlg_calib(Kc1, k4, a1, NVK);
-                const double *Rs = R + 9 * ((k < 3) ? (1 + k) : 4);
-#pragma unroll
-                for (int q = 0; q < 9; q++) Rk[q] = Rs[q];
-                vlg_project(Kc1, Rk, a1 + 3, bi, x1);
-                A[2 * k] = (x1[0] - xh[0]) / H_FD;
-                A[2 * k + 1] = (x1[1] - xh[1]) / H_FD;
+                double x1[2];
+                cv.project_dcam(k, bi, x1);
+                A[2 * k] = vlg_fd_quot(x1[0] - xh[0]);
+                A[2 * k + 1] = vlg_fd_quot(x1[1] - xh[1]);
             }
-            // point derivatives, :211-219, 43-70
+            // point derivatives, :211-219, 43-70 (proj :214-221, 61-86)
 #pragma unroll
             for (int k = 0; k < 3; k++) {
                 double b1[3], x1[2];
 #pragma unroll
                 for (int c = 0; c < 3; c++) b1[c] = bi[c] + H_FD * ((c == k) ? 1.0 : 0.0);
-                vlg_project(Kc, Rl, a0 + 3, b1, x1);
-                B[2 * k] = (x1[0] - xh[0]) / H_FD;
-                B[2 * k + 1] = (x1[1] - xh[1]) / H_FD;
+                cv.project(b1, x1);
+                B[2 * k] = vlg_fd_quot(x1[0] - xh[0]);
+                B[2 * k + 1] = vlg_fd_quot(x1[1] - xh[1]);
             }
             const double e0 = obs_x[2 * (size_t)o] - xh[0];
             const double e1 = obs_x[2 * (size_t)o + 1] - xh[1];
@@ -216,10 +304,11 @@ __global__ __launch_bounds__(256) void k_linearize(
 
 // -------------------------------------------------------------------------
 // Fast-path linearisation, one workgroup per Schur chunk (<= 128 observations
-// of consecutive points), two lanes per observation: lane 0 projects the base
-// point and the first HA camera columns, lane 1 the base point, the remaining
-// camera columns and the three point columns (same expressions as
-// k_linearize).  A, B, e go to LDS; then per observation W_ij (one contiguous,
+// of consecutive points), two lanes per observation: both project the base
+// point, then lane 0 the first NC0 of the NA + 3 FD columns of [A | B] and
+// lane 1 the rest, through one branch-free column routine (same expressions
+// as k_linearize), so the wave runs 1 + NC0 projections, not 1 + NA + 3.
+// A, B, e go to LDS; then per observation W_ij (one contiguous,
 // coalesced HBM range per chunk), per point V_i / eB_i (sequential over the
 // point's cameras, as k_linearize), per camera of the chunk one partial of
 // U_j / eA_j (sequential over the chunk's points), reduced per camera in chunk
@@ -236,8 +325,7 @@ __global__ __launch_bounds__(256) void k_linearize_chunk(
     double *__restrict__ W, double *__restrict__ V, double *__restrict__ eB,
     double *__restrict__ upart, double *__restrict__ part_sse)
 {
-    constexpr int NVK = NA - 6;
-    constexpr int HA = (NA + 4) / 2;        // lane 0: base + A[0, HA)
+    constexpr int NC0 = (NA + 4) / 2;       // lane 0: base + FD columns [0, NC0)
     constexpr int RS = 2 * NA + 8;          // LDS row: A (2 NA), B (6), e (2)
     constexpr int NU = NA * (NA + 1) / 2;
     __shared__ double rows[BA_CH_OBS * RS];
@@ -263,42 +351,24 @@ __global__ __launch_bounds__(256) void k_linearize_chunk(
             const int o = obase + lo, j = obs_cam[o], i = p0 + lpt[lo];
             const double bi[3] = {b[3 * (size_t)i], b[3 * (size_t)i + 1],
                                   b[3 * (size_t)i + 2]};
-            double a0[NA], k4[4], Rl[9];
-#pragma unroll
-            for (int c = 0; c < NA; c++) a0[c] = a[(size_t)NA * j + c];
-#pragma unroll
-            for (int c = 0; c < 4; c++) k4[c] = K4[4 * (size_t)j + c];
-            const double *R = rot + 45 * (size_t)j;
-#pragma unroll
-            for (int q = 0; q < 9; q++) Rl[q] = R[q];
-            double Kc[9], xh[2];
-            vlg_calib(Kc, k4, a0, NVK);
-            vlg_project(Kc, Rl, a0 + 3, bi, xh);
+            cam_view<NA> cv(a, K4, rot, j);
+            double xh[2];
+            cv.project(bi, xh);
             double *row = rows + RS * lo;
-            const int k0 = half ? HA : 0, k1 = half ? NA : HA;
-            for (int k = k0; k < k1; k++) {   // camera columns (mex_bundle_1 :201-209)
-                double a1[NA], Kc1[9], Rk[9], x1[2];
-#pragma unroll
-                for (int c = 0; c < NA; c++) a1[c] = a0[c] + H_FD * ((c == k) ? 1.0 : 0.0);
-                vlg_calib(Kc1, k4, a1, NVK);
-                const double *Rs = R + 9 * ((k < 3) ? (1 + k) : 4);
-#pragma unroll
-                for (int q = 0; q < 9; q++) Rk[q] = Rs[q];
-                vlg_project(Kc1, Rk, a1 + 3, bi, x1);
-                row[2 * k] = (x1[0] - xh[0]) / H_FD;
-                row[2 * k + 1] = (x1[1] - xh[1]) / H_FD;
-            }
-            if (half) {
-#pragma unroll
-                for (int k = 0; k < 3; k++) {   // point columns (:211-219)
-                    double b1[3], x1[2];
-#pragma unroll
-                    for (int c = 0; c < 3; c++) b1[c] = bi[c] + H_FD * ((c == k) ? 1.0 : 0.0);
-                    vlg_project(Kc, Rl, a0 + 3, b1, x1);
-                    row[2 * NA + 2 * k] = (x1[0] - xh[0]) / H_FD;
-                    row[2 * NA + 2 * k + 1] = (x1[1] - xh[1]) / H_FD;
+            // the NA + 3 FD columns of [A | B] (mex_bundle_1 :201-219) split
+            // evenly: lane 0 columns [0, NC0), lane 1 [NC0, NA + 3), one
+            // instruction stream for both (project_col has no branch)
+#pragma unroll 1
+            for (int t = 0; t < NC0; t++) {
+                const int col = half ? NC0 + t : t;
+                if (col < NA + 3) {
+                    double x1[2];
+                    cv.project_col(col, bi, x1);
+                    row[2 * col] = vlg_fd_quot(x1[0] - xh[0]);
+                    row[2 * col + 1] = vlg_fd_quot(x1[1] - xh[1]);
                 }
-            } else {
+            }
+            if (!half) {
                 const double e0 = obs_x[2 * (size_t)o] - xh[0];
                 const double e1 = obs_x[2 * (size_t)o + 1] - xh[1];
                 row[2 * NA + 6] = e0;
@@ -1070,10 +1140,12 @@ __global__ __launch_bounds__(256) void k_camera_update(
             a_new[(size_t)NA * j + c] = an[c];
             acc += d * (lambda * d + eA[(size_t)NA * j + c]);
         }
-        double R[9];
-        vlg_rodrigues(R, an);
+        if constexpr (NA != BA_PROJ_NA) {
+            double R[9];
+            vlg_rodrigues(R, an);
 #pragma unroll
-        for (int q = 0; q < 9; q++) rot_new[9 * (size_t)j + q] = R[q];
+            for (int q = 0; q < 9; q++) rot_new[9 * (size_t)j + q] = R[q];
+        }
     }
     block_sum_to<256>(acc, part + blockIdx.x);
 }
@@ -1095,7 +1167,6 @@ __global__ __launch_bounds__(256) void k_point_update(
     double *__restrict__ b_new, double *__restrict__ part_sse, double *__restrict__ part_dpg,
     const unsigned char *__restrict__ obs_vis, double *__restrict__ xh_out)
 {
-    constexpr int NVK = NA - 6;
     double sse = 0.0, dpg = 0.0;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         double rhs[3] = {eB[3 * (size_t)i], eB[3 * (size_t)i + 1], eB[3 * (size_t)i + 2]};
@@ -1130,15 +1201,20 @@ __global__ __launch_bounds__(256) void k_point_update(
         for (int o = o0; o < o1; o++) {
             if (obs_vis && !obs_vis[o]) continue;
             const int j = obs_cam[o];
-            double an[NA], k4[4], Kc[9], R[9], xh[2];
+            double an[NA], xh[2];
 #pragma unroll
             for (int c = 0; c < NA; c++) an[c] = a_new[(size_t)NA * j + c];
+            if constexpr (NA == BA_PROJ_NA) {   // mex_bundle_proj_3_db_new.c:160-165
+                vlg_project_proj(an, bn, xh);
+            } else {
+                double k4[4], Kc[9], R[9];
 #pragma unroll
-            for (int c = 0; c < 4; c++) k4[c] = K4[4 * (size_t)j + c];
+                for (int c = 0; c < 4; c++) k4[c] = K4[4 * (size_t)j + c];
 #pragma unroll
-            for (int q = 0; q < 9; q++) R[q] = rot_new[9 * (size_t)j + q];
-            vlg_calib(Kc, k4, an, NVK);
-            vlg_project(Kc, R, an + 3, bn, xh);
+                for (int q = 0; q < 9; q++) R[q] = rot_new[9 * (size_t)j + q];
+                vlg_calib(Kc, k4, an, NA - 6);
+                vlg_project(Kc, R, an + 3, bn, xh);
+            }
             const double d0 = obs_x[2 * (size_t)o] - xh[0];
             const double d1 = obs_x[2 * (size_t)o + 1] - xh[1];
             sse += d0 * d0 + d1 * d1;
@@ -1153,12 +1229,23 @@ __global__ __launch_bounds__(256) void k_point_update(
     block_sum_to<256>(dpg, part_dpg + blockIdx.x);
 }
 
-// fixed-order sum of nparts partials -> out (one block)
-__global__ void k_sum_parts(const double *__restrict__ part, int nparts, double *__restrict__ out)
+// fixed-order sum of nparts partials -> out (one 1024-thread block; four
+// independent loads in flight per lane, so the latency of ~25 dependent
+// rounds of HBM loads does not set the time)
+#define BA_SUM_BS 1024
+__global__ __launch_bounds__(BA_SUM_BS) void k_sum_parts(const double *__restrict__ part,
+                                                         int nparts, double *__restrict__ out)
 {
-    double v = 0.0;
-    for (int q = threadIdx.x; q < nparts; q += 256) v += part[q];
-    block_sum_to<256>(v, out);
+    double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+    int q = threadIdx.x;
+    for (; q + 3 * BA_SUM_BS < nparts; q += 4 * BA_SUM_BS) {
+        v0 += part[q];
+        v1 += part[q + BA_SUM_BS];
+        v2 += part[q + 2 * BA_SUM_BS];
+        v3 += part[q + 3 * BA_SUM_BS];
+    }
+    for (; q < nparts; q += BA_SUM_BS) v0 += part[q];
+    block_sum_to<BA_SUM_BS>((v0 + v1) + (v2 + v3), out);
 }
 
 // =========================================================================
@@ -1177,6 +1264,7 @@ static inline int grid_for(long long work, int bs, int cap)
     case 6: { constexpr int NA = 6; CALL; } break;                                  \
     case 7: { constexpr int NA = 7; CALL; } break;                                  \
     case 10: { constexpr int NA = 10; CALL; } break;                                \
+    case BA_PROJ_NA: { constexpr int NA = BA_PROJ_NA; CALL; } break;                \
     default: return -1000;                                                          \
     }
 
@@ -1185,6 +1273,7 @@ static const int PT_GRID_CAP = 8192;  // partial-sum slots used by per-point ker
 int ba_launch_rotations(ba_dev *d, const double *a, double *rot, int all5)
 {
     (void)all5;
+    if (d->na == BA_PROJ_NA) return 0;   // projective camera: no rotations
     const int g = grid_for(d->m, 64, 1 << 30);
     KT_B(d);
     BA_DISPATCH(d->na, (k_rotations<NA><<<g, 64, 0, d->stream>>>(a, rot, d->m)));
@@ -1202,7 +1291,7 @@ int ba_launch_linearize(ba_dev *d, ba_flags f)
                                    d->pt_ptr, d->obs_cam, d->obs_x, d->K4, d->a, d->rot, d->b,
                                    f, d->pivot, d->W, d->V, d->eB, d->upart, d->chsse)));
         KT_E(d, KT_LIN);
-        k_sum_parts<<<1, 256, 0, d->stream>>>(d->chsse, d->nch, d->scal + 0);
+        k_sum_parts<<<1, BA_SUM_BS, 0, d->stream>>>(d->chsse, d->nch, d->scal + 0);
         return -(int)hipGetLastError();
     }
     const int g = grid_for(d->n, 256, PT_GRID_CAP);
@@ -1212,13 +1301,13 @@ int ba_launch_linearize(ba_dev *d, ba_flags f)
                            d->pivot, d->jrec, d->W, d->V, d->eB, d->part, d->xh_out,
                            d->B_out)));
     KT_E(d, KT_LIN);
-    k_sum_parts<<<1, 256, 0, d->stream>>>(d->part, g, d->scal + 0);
+    k_sum_parts<<<1, BA_SUM_BS, 0, d->stream>>>(d->part, g, d->scal + 0);
     return -(int)hipGetLastError();
 }
 
 int ba_launch_camera_reduce(ba_dev *d, ba_flags f)
 {
-    const int bs = (d->na * (d->na + 1) / 2 + d->na) <= 64 ? 64 : 128;
+    const int bs = ((d->na * (d->na + 1) / 2 + d->na) + 63) / 64 * 64;
     if (!d->ordered) {
         KT_B(d);
         BA_DISPATCH(d->na, (k_camera_reduce_chunks<NA><<<d->m, bs, 0, d->stream>>>(
@@ -1246,7 +1335,7 @@ int ba_launch_damp_point(ba_dev *d, double lambda)
 
 int ba_launch_schur(ba_dev *d, double lambda)
 {
-    const int bs = (d->na * d->na + d->na) <= 64 ? 64 : 128;
+    const int bs = ((d->na * d->na + d->na) + 63) / 64 * 64;
     KT_B(d);
     BA_DISPATCH(d->na, (k_schur<NA><<<d->nb, bs, 0, d->stream>>>(
                            d->blk_jk, d->blk_ptr, d->term, d->Y, d->W, d->t, d->U, d->eA, d->nb,
@@ -1296,7 +1385,7 @@ static int launch_schur_fast(ba_dev *d, double lambda)
             d->eB, d->W, lambda, bcap, gcap, ecap, d->Vinv, d->spart, d->epart);
     KT_E(d, KT_SCHUR_CHUNK);
     }
-    const int bs = (NA * NA + NA) <= 64 ? 64 : 128;
+    const int bs = ((NA * NA + NA) + 63) / 64 * 64;
     KT_B(d);
     k_schur_reduce<NA><<<d->nb, bs, 0, d->stream>>>(
         d->blk_jk, d->blk_gptr, d->blk_gslots, d->cam_gptr, d->cam_gslots, d->spart, d->epart,
@@ -1311,6 +1400,7 @@ int ba_launch_schur_fast(ba_dev *d, double lambda)
     case 6: return launch_schur_fast<6>(d, lambda);
     case 7: return launch_schur_fast<7>(d, lambda);
     case 10: return launch_schur_fast<10>(d, lambda);
+    case BA_PROJ_NA: return launch_schur_fast<BA_PROJ_NA>(d, lambda);
     default: return -1000;
     }
 }
@@ -1343,7 +1433,7 @@ int ba_launch_update(ba_dev *d, double lambda)
     BA_DISPATCH(d->na, (k_camera_update<NA><<<gc, 256, 0, d->stream>>>(
                            d->a, d->da, d->eA, d->m, lambda, d->a_new, d->rot_new, d->part)));
     KT_E(d, KT_CAMUPD);
-    k_sum_parts<<<1, 256, 0, d->stream>>>(d->part, gc, d->scal + 2);
+    k_sum_parts<<<1, BA_SUM_BS, 0, d->stream>>>(d->part, gc, d->scal + 2);
     const int g = grid_for(d->n, 256, PT_GRID_CAP);
     KT_B(d);
     BA_DISPATCH(d->na, (k_point_update<NA><<<g, 256, 0, d->stream>>>(
@@ -1352,8 +1442,8 @@ int ba_launch_update(ba_dev *d, double lambda)
                            d->part + BA_PART_MAX, d->part + 2 * BA_PART_MAX, d->obs_vis,
                            d->xh_out)));
     KT_E(d, KT_PTUPD);
-    k_sum_parts<<<1, 256, 0, d->stream>>>(d->part + BA_PART_MAX, g, d->scal + 1);
-    k_sum_parts<<<1, 256, 0, d->stream>>>(d->part + 2 * BA_PART_MAX, g, d->scal + 3);
+    k_sum_parts<<<1, BA_SUM_BS, 0, d->stream>>>(d->part + BA_PART_MAX, g, d->scal + 1);
+    k_sum_parts<<<1, BA_SUM_BS, 0, d->stream>>>(d->part + 2 * BA_PART_MAX, g, d->scal + 3);
     return -(int)hipGetLastError();
 }
 

@@ -549,6 +549,7 @@ struct vlgba_ctx {
     double num_vis = 0;
     int max_iter = 20, max_iter2 = 10, verbose = 0;
     double lambda = 1e-3, lambda0 = 1e-3, nu = 2.0;
+    int model = VLGBA_MODEL_EUCLIDEAN;
     int lin_valid = 0;
     int timing = 0;
     hipEvent_t ev[8] = {};
@@ -773,7 +774,8 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         TRY(upload(d.cam_ptr, cptr.data(), p->m + 1, s));
         TRY(upload(d.cam_obs, cobs.data(), d.N, s));
         TRY(upload(d.obs_x, h.x.data() + 2 * o0, 2 * (size_t)d.N, s));
-        TRY(upload(d.K4, p->K, 4 * (size_t)p->m, s));
+        if (p->K) TRY(upload(d.K4, p->K, 4 * (size_t)p->m, s));
+        else VLGBA_CHECK(hipMemsetAsync(d.K4, 0, sizeof(double) * 4 * p->m, s));
         TRY(upload(d.blk_jk, hb.jk.data(), hb.jk.size(), s));
         TRY(upload(d.blk_ptr, hb.ptr.data(), hb.ptr.size(), s));
         TRY(upload(d.term, hb.term.data(), hb.term.size(), s));
@@ -788,8 +790,15 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
                       std::vector<int> *pt_ptr_out = nullptr, host_obs *h_out = nullptr)
 {
     *out = nullptr;
-    if (!p || p->m < 1 || p->n < 0 || p->num_obs < 0 || !p->K) return VLGBA_E_ARG;
-    if (p->num_a != 6 && p->num_a != 7 && p->num_a != 10) return VLGBA_E_NUMA;
+    if (!p || p->m < 1 || p->n < 0 || p->num_obs < 0) return VLGBA_E_ARG;
+    if (p->model == VLGBA_MODEL_EUCLIDEAN) {
+        if (!p->K) return VLGBA_E_ARG;
+        if (p->num_a != 6 && p->num_a != 7 && p->num_a != 10) return VLGBA_E_NUMA;
+    } else if (p->model == VLGBA_MODEL_PROJECTIVE) {
+        if (p->num_a != BA_PROJ_NA) return VLGBA_E_NUMA;
+    } else {
+        return VLGBA_E_ARG;
+    }
     if (p->num_obs > 0x7fffffffLL) return VLGBA_E_ARG;
     vlgba_ctx *c = new (std::nothrow) vlgba_ctx();
     if (!c) return VLGBA_E_NOMEM;
@@ -847,7 +856,10 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
         c->flags.fix_motion = o->fix_motion;
         if (o->semantics != 0 && o->semantics != 1) { rc = VLGBA_E_ARG; break; }
         // bundle_euclid_nomex.m has no fix_pivot option: the pivot is ignored there
-        c->flags.has_pivot = o->pivot != nullptr && o->semantics == 0;
+        // (nor has bundle_projective.m, :46-56)
+        c->flags.has_pivot = o->pivot != nullptr && o->semantics == 0 &&
+                             p->model == VLGBA_MODEL_EUCLIDEAN;
+        c->model = p->model;
         c->max_iter = o->max_iter > 0 ? o->max_iter : 20;
         c->max_iter2 = o->max_iter2 > 0 ? o->max_iter2 : 10;
         c->lambda0 = c->lambda = o->lambda0 > 0 ? o->lambda0 : 1e-3;
@@ -951,20 +963,29 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
     info->lambda = lam;
     info->chol_failed = hs[4] != 0.0;
     info->rho = (hs[0] - hs[1]) / info->dpg;
-    info->accepted = (hs[0] - hs[1]) > 0 && !info->chol_failed;
+    if (c->model == VLGBA_MODEL_PROJECTIVE)   // bundle_projective.m:182-188 (normalised first)
+        info->accepted = 1 / c->num_vis * hs[1] < 1 / c->num_vis * hs[0] && !info->chol_failed;
+    else                                      // bundle_euclid.m:218
+        info->accepted = (hs[0] - hs[1]) > 0 && !info->chol_failed;
     return 0;
 }
 
-// bundle_euclid.m:218-241 applied to the context
+// bundle_euclid.m:218-241 (bundle_projective.m:188-207) applied to the context
 static void lm_apply(vlgba_ctx *c, const vlgba_step_info *info)
 {
     ba_dev &d = c->d;
+    const bool proj = c->model == VLGBA_MODEL_PROJECTIVE;
     if (info->accepted) {
         std::swap(d.a, d.a_new);
         std::swap(d.b, d.b_new);
-        c->lambda = c->lambda * std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * info->rho - 1.0, 3));
+        if (proj)
+            c->lambda = c->lambda / 10;
+        else
+            c->lambda = c->lambda * std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * info->rho - 1.0, 3));
         c->nu = 2.0;
         c->lin_valid = 0;
+    } else if (proj) {
+        c->lambda = c->lambda * 10;
     } else {
         c->lambda = c->lambda * c->nu;
         c->nu = 2.0 * c->nu;
@@ -1165,7 +1186,10 @@ int vlgba_run(vlgba_ctx *c, double *error_out, vlgba_stats *stats)
         TRY(lm_pass(c, 0, &info));
         passes++;
         if (info.accepted) {
-            const double olde = info.old_sse / c->num_vis, newe = info.new_sse / c->num_vis;
+            const bool proj = c->model == VLGBA_MODEL_PROJECTIVE;
+            // bundle_euclid.m:219-220 divide; bundle_projective.m:182-183 scale by 1/num_vis
+            const double olde = proj ? 1 / c->num_vis * info.old_sse : info.old_sse / c->num_vis;
+            const double newe = proj ? 1 / c->num_vis * info.new_sse : info.new_sse / c->num_vis;
             if (c->verbose && c->rank == 0)
                 std::printf("iter %d: error= %.5g -> %.5g\n", iter, olde, newe);
             if ((int)err.size() < iter) err.push_back(olde);
@@ -1220,12 +1244,13 @@ static void obs_from_vis(int m, int n, const double *vis, std::vector<int> &pt,
             }
 }
 
-int vlgba_mex_bundle_1(int m, int n, int num_a, const double *K, const double *a,
-                       const double *b, const double *X, const double *vis, double *X_hat,
-                       double *A, double *B, double *e, double *U, double *V, double *W,
-                       double *eA, double *eB)
+static int mex1_impl(int model, int m, int n, int num_a, const double *K, const double *a,
+                     const double *b, const double *X, const double *vis, double *X_hat,
+                     double *A, double *B, double *e, double *U, double *V, double *W,
+                     double *eA, double *eB)
 {
-    if (m < 1 || n < 0 || !K || !a || !b || !X || !vis) return VLGBA_E_ARG;
+    if (m < 1 || n < 0 || (!K && model == VLGBA_MODEL_EUCLIDEAN) || !a || !b || !X || !vis)
+        return VLGBA_E_ARG;
     std::vector<int> pt, cam;
     obs_from_vis(m, n, vis, pt, cam);
     const long long N = (long long)pt.size();
@@ -1235,7 +1260,7 @@ int vlgba_mex_bundle_1(int m, int n, int num_a, const double *K, const double *a
         ox[2 * q] = X[2 * p];
         ox[2 * q + 1] = X[2 * p + 1];
     }
-    vlgba_problem pr = {m, n, num_a, N, pt.data(), cam.data(), ox.data(), K, 0.0};
+    vlgba_problem pr = {m, n, num_a, N, pt.data(), cam.data(), ox.data(), K, 0.0, model};
     vlgba_ctx *c = nullptr;
     TRY(ctx_create(&pr, nullptr, &c, true, true, true));
     ba_dev &d = c->d;
@@ -1286,9 +1311,9 @@ int vlgba_mex_bundle_1(int m, int n, int num_a, const double *K, const double *a
     return 0;
 }
 
-int vlgba_mex_bundle_2(int m, int n, int num_a, const double *Y, const double *W,
-                       const double *U, const double *eA, const double *eB, double *S,
-                       double *e_)
+static int mex2_impl(int model, int m, int n, int num_a, const double *Y, const double *W,
+                     const double *U, const double *eA, const double *eB, double *S,
+                     double *e_)
 {
     if (m < 1 || n < 0 || !Y || !W || !U || !eA || !eB || !S || !e_) return VLGBA_E_ARG;
     const int bs = 3 * num_a;
@@ -1311,7 +1336,7 @@ int vlgba_mex_bundle_2(int m, int n, int num_a, const double *Y, const double *W
         std::memcpy(hW.data() + bs * q, W + bs * p, sizeof(double) * bs);
     }
     std::vector<double> K(4 * (size_t)m, 1.0);
-    vlgba_problem pr = {m, n, num_a, N, pt.data(), cam.data(), ox.data(), K.data(), 0.0};
+    vlgba_problem pr = {m, n, num_a, N, pt.data(), cam.data(), ox.data(), K.data(), 0.0, model};
     vlgba_ctx *c = nullptr;
     TRY(ctx_create(&pr, nullptr, &c, false, true, true));
     ba_dev &d = c->d;
@@ -1337,12 +1362,13 @@ int vlgba_mex_bundle_2(int m, int n, int num_a, const double *Y, const double *W
     return rc;
 }
 
-int vlgba_mex_bundle_3(int m, int n, int num_a, const double *W, const double *da,
-                       const double *eB, const double *Vinv, const double *K, const double *a,
-                       const double *b, const double *X, const double *vis, double *db,
-                       double *a_new, double *b_new, double *X_hat)
+static int mex3_impl(int model, int m, int n, int num_a, const double *W, const double *da,
+                     const double *eB, const double *Vinv, const double *K, const double *a,
+                     const double *b, const double *X, const double *vis, double *db,
+                     double *a_new, double *b_new, double *X_hat)
 {
-    if (m < 1 || n < 0 || !W || !da || !eB || !Vinv || !K || !a || !b || !X || !vis)
+    if (m < 1 || n < 0 || !W || !da || !eB || !Vinv ||
+        (!K && model == VLGBA_MODEL_EUCLIDEAN) || !a || !b || !X || !vis)
         return VLGBA_E_ARG;
     const int bs = 3 * num_a;
     std::vector<int> pt, cam;
@@ -1367,7 +1393,7 @@ int vlgba_mex_bundle_3(int m, int n, int num_a, const double *W, const double *d
         ox[2 * q + 1] = X[2 * p + 1];
         std::memcpy(hW.data() + bs * q, W + bs * p, sizeof(double) * bs);
     }
-    vlgba_problem pr = {m, n, num_a, N, pt.data(), cam.data(), ox.data(), K, 0.0};
+    vlgba_problem pr = {m, n, num_a, N, pt.data(), cam.data(), ox.data(), K, 0.0, model};
     vlgba_ctx *c = nullptr;
     TRY(ctx_create(&pr, nullptr, &c, true, true, true));
     ba_dev &d = c->d;
@@ -1404,6 +1430,58 @@ int vlgba_mex_bundle_3(int m, int n, int num_a, const double *W, const double *d
         X_hat[2 * p + 1] = xh[2 * q + 1];
     }
     return 0;
+}
+
+int vlgba_mex_bundle_1(int m, int n, int num_a, const double *K, const double *a,
+                       const double *b, const double *X, const double *vis, double *X_hat,
+                       double *A, double *B, double *e, double *U, double *V, double *W,
+                       double *eA, double *eB)
+{
+    if (num_a == BA_PROJ_NA) return VLGBA_E_NUMA;   // the projective stage has its own entry
+    return mex1_impl(VLGBA_MODEL_EUCLIDEAN, m, n, num_a, K, a, b, X, vis, X_hat, A, B, e, U, V,
+                     W, eA, eB);
+}
+
+int vlgba_mex_bundle_2(int m, int n, int num_a, const double *Y, const double *W,
+                       const double *U, const double *eA, const double *eB, double *S,
+                       double *e_)
+{
+    // mex_bundle_2_Se_.c reads num_a = rows(Y) (:57); 12 is the projective twin's
+    return mex2_impl(num_a == BA_PROJ_NA ? VLGBA_MODEL_PROJECTIVE : VLGBA_MODEL_EUCLIDEAN, m, n,
+                     num_a, Y, W, U, eA, eB, S, e_);
+}
+
+int vlgba_mex_bundle_3(int m, int n, int num_a, const double *W, const double *da,
+                       const double *eB, const double *Vinv, const double *K, const double *a,
+                       const double *b, const double *X, const double *vis, double *db,
+                       double *a_new, double *b_new, double *X_hat)
+{
+    if (num_a == BA_PROJ_NA) return VLGBA_E_NUMA;
+    return mex3_impl(VLGBA_MODEL_EUCLIDEAN, m, n, num_a, W, da, eB, Vinv, K, a, b, X, vis, db,
+                     a_new, b_new, X_hat);
+}
+
+int vlgba_mex_bundle_proj_1(int m, int n, const double *a, const double *b, const double *X,
+                            const double *vis, double *X_hat, double *A, double *B, double *e,
+                            double *U, double *V, double *W, double *eA, double *eB)
+{
+    return mex1_impl(VLGBA_MODEL_PROJECTIVE, m, n, BA_PROJ_NA, nullptr, a, b, X, vis, X_hat, A,
+                     B, e, U, V, W, eA, eB);
+}
+
+int vlgba_mex_bundle_proj_2(int m, int n, const double *Y, const double *W, const double *U,
+                            const double *eA, const double *eB, double *S, double *e_)
+{
+    return mex2_impl(VLGBA_MODEL_PROJECTIVE, m, n, BA_PROJ_NA, Y, W, U, eA, eB, S, e_);
+}
+
+int vlgba_mex_bundle_proj_3(int m, int n, const double *W, const double *da, const double *eB,
+                            const double *Vinv, const double *a, const double *b,
+                            const double *X, const double *vis, double *db, double *a_new,
+                            double *b_new, double *X_hat)
+{
+    return mex3_impl(VLGBA_MODEL_PROJECTIVE, m, n, BA_PROJ_NA, W, da, eB, Vinv, nullptr, a, b, X,
+                     vis, db, a_new, b_new, X_hat);
 }
 
 }  // extern "C"

@@ -20,6 +20,8 @@
  *                           rotation supplied by the caller (so a kernel can
  *                           hoist the per-camera Rodrigues out of the
  *                           per-observation loop without changing a bit)
+ *   vlg_project_proj        reproject_projective_point of
+ *                           toolbox/bundle/mex_bundle_proj_1_XABeUVWeAeB.c:13-32
  *
  * Every expression keeps the reference's evaluation order.
  * Include from C99, C++ or HIP.  Define VLG_ORACLE_LIBM to make the oracle use
@@ -225,8 +227,43 @@ VLG_HD void vlg_project(const double Kc[9], const double R[9], const double t[3]
     x[1] = x1 / x2;
 }
 
+/* Projective camera (a = P(:), 3 x 4 column major, num_a = 12):
+ * x_ = P [b; 1], x = x_(1:2) / x_(3), each row summed left to right
+ * (mex_bundle_proj_1_XABeUVWeAeB.c:13-32, identical in
+ * mex_bundle_proj_3_db_new.c:13-31). */
+VLG_HD void vlg_project_proj(const double P[12], const double b[3], double x[2])
+{
+    double x0 = P[0] * b[0] + P[3] * b[1] + P[6] * b[2] + P[9];
+    double x1 = P[1] * b[0] + P[4] * b[1] + P[7] * b[2] + P[10];
+    double x2 = P[2] * b[0] + P[5] * b[1] + P[8] * b[2] + P[11];
+    x[0] = x0 / x2;
+    x[1] = x1 / x2;
+}
+
 /* Finite-difference step of the reference (mex_bundle_1_XABeUVWeAeB.c:23,52). */
 #define VLG_FD_H 1e-10
+
+/* (x1 - x0) / h of the forward differences (mex_bundle_1 :39-40, 68-69),
+ * correctly rounded without a division.  Markstein's theorem (IBM J. R&D 34,
+ * 1990; Cornea-Hasegan, Golliver, Markstein, ARITH-14 1999): if y is within
+ * half an ulp of 1/h and q is within one ulp of d/h, the remainder
+ * r = d - q h is exact (one FMA) and RN(q + r y) = RN(d/h).  Here
+ * y = RN(1/h) and y h = 1 + e1 with |e1| <= 2^-54 (checked exactly in
+ * tests/test_oracle.py::test_fd_quotient), so q = RN(d y) is within one ulp
+ * of d/h.  Both theorems need d and q h away from the subnormal range; tiny
+ * |d| (including 0, whose sign the remainder step would lose) and non-finite
+ * d take the plain division.  The device uses this (3 fp64 ops instead of
+ * ~10 + a quarter-rate reciprocal); the oracle keeps '/' as the reference
+ * writes it, and the stage-1 parity tests compare the two bit for bit. */
+#define VLG_FD_RH (1.0 / VLG_FD_H)
+VLG_HD double vlg_fd_quot(double d)
+{
+    const double ad = fabs(d);
+    if (!(ad >= 0x1p-900 && ad <= 0x1p900)) return d / VLG_FD_H;
+    const double q = d * VLG_FD_RH;
+    const double r = fma(-q, VLG_FD_H, d);
+    return fma(r, VLG_FD_RH, q);
+}
 
 /* ---- 3x3 symmetric pseudo-inverse ------------------------------------------
  * The reference inverts every damped point block with MATLAB pinv

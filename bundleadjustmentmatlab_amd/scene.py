@@ -214,6 +214,23 @@ def banded_scene(m=50, n=10_000, track=6, depth=(80.0, 120.0), noise=0.5, seed=2
     return Scene(K, T, w, X, pt, cam, x, T0, w0, X0)
 
 
+def projective_from(sc):
+    """Projective BA input (bundle_projective.m:1-8) from a Euclidean scene:
+    Pp(:,:,j) = K_j [R(w0_j) | T0_j] / f_j at the perturbed start (a 3 x 4 x m
+    projective reconstruction of arbitrary per-camera scale, as
+    mview_reconstruction.m:148 hands over), Xp = X0 with Xp(4,:) = 1, and the
+    scene's observations.  Returns (Pp, Xp)."""
+    R = rodrigues(sc.w0)
+    m = sc.m
+    Pp = np.zeros((3, 4, m), order="F")
+    for j in range(m):
+        fx, fy, cx, cy = sc.K[:, j]
+        Kj = np.array([[fx, 0, cx], [0, fy, cy], [0, 0, 1.0]])
+        Pp[:, :, j] = Kj @ np.hstack([R[j], sc.T0[:, j:j + 1]]) / fx
+    Xp = np.asfortranarray(sc.X0.copy())
+    return Pp, Xp
+
+
 CONFIGS = {
     # name: (factory, kwargs)   -- BASELINE.json "configs"
     "cfg1": (mview_scene, dict(m=10, min_n=100, max_n=200, depth=100.0, seed=1)),

@@ -1,9 +1,10 @@
 /*
- * vlgba.h -- C ABI of libvlgba, the MI355X (gfx950) Euclidean bundle adjuster.
+ * vlgba.h -- C ABI of libvlgba, the MI355X (gfx950) bundle adjuster.
  *
- * Drop-in for the Levenberg-Marquardt path of caomw/BundleAdjustmentMatlab
- * (VLG toolbox/bundle).  Plain C: pointers and sizes only, no C++ / torch /
- * HIP types.  All arrays are fp64 column major in the reference's MATLAB
+ * Drop-in for the Levenberg-Marquardt paths of caomw/BundleAdjustmentMatlab
+ * (VLG toolbox/bundle): Euclidean (bundle_euclid.m + mex_bundle_{1,2,3}) and
+ * projective (bundle_projective.m + mex_bundle_proj_{1,2,3}).  Plain C:
+ * pointers and sizes only, no C++ / torch / HIP types.  All arrays are fp64 column major in the reference's MATLAB
  * layouts unless stated otherwise; indices are 0-based int32.
  *
  * Return codes: 0 on success; VLGBA_E_* (< 0) for argument errors; a
@@ -20,29 +21,41 @@ extern "C" {
 #endif
 
 #define VLGBA_E_ARG (-1001)      /* bad size / option                        */
-#define VLGBA_E_NUMA (-1002)     /* num_a not in {6, 7, 10}                  */
+#define VLGBA_E_NUMA (-1002)     /* num_a not in {6, 7, 10} (Euclidean) / 12 (projective) */
 #define VLGBA_E_ORDER (-1003)    /* observation list not point-major / dups  */
 #define VLGBA_E_NOMEM (-1004)    /* host allocation failed                    */
 #define VLGBA_E_COMM (-1005)     /* RCCL failure                              */
 
+/* camera models (vlgba_problem.model) */
+#define VLGBA_MODEL_EUCLIDEAN 0   /* bundle_euclid.m: a = [w; T; (K)], num_a 6/7/10     */
+#define VLGBA_MODEL_PROJECTIVE 1  /* bundle_projective.m: a = P(:) (3x4), num_a = 12   */
+
 /* ------------------------------------------------------------------------
  * Problem: the reference's packed parameters and a COO observation list.
- *   a      num_a x m   [w; T; (K)] per camera  (bundle_euclid.m:88-96)
- *   b      3 x n       Xe(1:3,:)               (bundle_euclid.m:99)
+ *   a      num_a x m   [w; T; (K)] per camera  (bundle_euclid.m:88-96), or
+ *                      P(:) per camera          (bundle_projective.m:70-73)
+ *   b      3 x n       Xe(1:3,:)               (bundle_euclid.m:99;
+ *                      Xp(1:3,:), bundle_projective.m:76)
  *   obs    visible (point, camera) pairs of x(1:2,:,:) / 'visibility'
  *          (bundle_euclid.m:50,71,102); any order, duplicates rejected.
  * ------------------------------------------------------------------------ */
 typedef struct {
     int m;                 /* cameras                                            */
     int n;                 /* points                                             */
-    int num_a;             /* 6 fix_calibration, 7 fix_principal, 10 variable K  */
+    int num_a;             /* 6 fix_calibration, 7 fix_principal, 10 variable K;
+                              12 projective                                      */
     long long num_obs;     /* visible observations                               */
     const int *obs_pt;     /* [num_obs] point index                              */
     const int *obs_cam;    /* [num_obs] camera index                             */
     const double *obs_x;   /* [2*num_obs] measured (u, v)                        */
-    const double *K;       /* [4*m] fx fy cx cy (mex_bundle_1_XABeUVWeAeB.c:186) */
+    const double *K;       /* [4*m] fx fy cx cy (mex_bundle_1_XABeUVWeAeB.c:186);
+                              unused (may be NULL) for the projective model      */
     double num_vis;        /* sum of the visibility values (bundle_euclid.m:82);
                               <= 0 means num_obs                                 */
+    int model;             /* VLGBA_MODEL_*; 0 (zero-initialised) = Euclidean.
+                              Projective: LM rule of bundle_projective.m:182-207
+                              (errors / num_vis compared, lambda / 10 on accept,
+                              * 10 on reject); fix_pivot is not an option there */
 } vlgba_problem;
 
 typedef struct {
@@ -189,6 +202,27 @@ int vlgba_mex_bundle_3(int m, int n, int num_a, const double *W, const double *d
                        const double *eB, const double *Vinv, const double *K, const double *a,
                        const double *b, const double *X, const double *vis, double *db,
                        double *a_new, double *b_new, double *X_hat);
+
+/* Projective stages (mex_bundle_proj_*.c: the same layouts with num_a = 12
+ * and no K):
+ * [X_hat A B e U V W eA eB] = mex_bundle_proj_1_XABeUVWeAeB(a, b, X, visible)
+ * replaces toolbox/bundle/mex_bundle_proj_1_XABeUVWeAeB.c:88-332. */
+int vlgba_mex_bundle_proj_1(int m, int n, const double *a, const double *b, const double *X,
+                            const double *vis, double *X_hat, double *A, double *B, double *e,
+                            double *U, double *V, double *W, double *eA, double *eB);
+
+/* [S e_] = mex_bundle_proj_2_Se_(Y, W, U, eA, eB)
+ * replaces toolbox/bundle/mex_bundle_proj_2_Se_.c:15-158 (num_a = 12). */
+int vlgba_mex_bundle_proj_2(int m, int n, const double *Y, const double *W, const double *U,
+                            const double *eA, const double *eB, double *S, double *e_);
+
+/* [db a_new b_new X_hat] = mex_bundle_proj_3_db_new(W, da, eB, V_inv, a, b, X, visible)
+ * replaces toolbox/bundle/mex_bundle_proj_3_db_new.c:34-178 (db uses
+ * da(1:6,j) only, :107-121, as the Euclidean stage does). */
+int vlgba_mex_bundle_proj_3(int m, int n, const double *W, const double *da, const double *eB,
+                            const double *Vinv, const double *a, const double *b,
+                            const double *X, const double *vis, double *db, double *a_new,
+                            double *b_new, double *X_hat);
 
 /* Multi-GPU: rank 0 creates the 128-byte RCCL unique id, the caller
  * broadcasts it (e.g. torch.distributed) and passes it as opt->comm_id. */

@@ -1,5 +1,10 @@
 /*
- * ba_oracle.c -- CPU restatement of the reference's Euclidean LM stages.
+ * ba_oracle.c -- CPU restatement of the reference's LM stages: Euclidean
+ * (toolbox/bundle/mex_bundle_{1,2,3}*.c, num_a = 6 / 7 / 10) and projective
+ * (mex_bundle_proj_{1,2,3}*.c, num_a = 12: same loops, camera P(:) instead of
+ * [w; T; (K)]; mex_bundle_proj_2_Se_.c differs from mex_bundle_2_Se_.c only
+ * in fixing num_a = 12, and mex_bundle_proj_3_db_new.c keeps the 6-term
+ * back substitution of App. A Q3).
  *
  * TEST INFRASTRUCTURE ONLY.  Nothing in bundleadjustmentmatlab_amd/ links,
  * loads or calls this library; only tests/, __graft_entry__.smoke() and
@@ -31,7 +36,8 @@
 #include <math.h>
 #include "../bundleadjustmentmatlab_amd/csrc/vlg_math.h"
 
-#define ORC_MAX_NUM_A 10
+#define ORC_MAX_NUM_A 12
+#define ORC_PROJ_NUM_A 12  /* num_a of the projective model (bundle_projective.m:70) */
 
 /* reproject_point.h:16-57 (calibration override + Rodrigues + projection). */
 void oracle_reproject(const double K4[4], const double *a, const double b[3],
@@ -43,14 +49,45 @@ void oracle_reproject(const double K4[4], const double *a, const double b[3],
     vlg_project(Kc, R, a + 3, b, x);
 }
 
+/* reproject_projective_point, mex_bundle_proj_1_XABeUVWeAeB.c:13-32 */
+void oracle_reproject_proj(const double *a, const double b[3], double x[2])
+{
+    vlg_project_proj(a, b, x);
+}
+
+/* The camera model follows num_a: 12 is the projective camera P(:) of
+ * bundle_projective.m:70-73 (K4 unused, may be NULL); 6 / 7 / 10 the
+ * Euclidean [w; T; (K)] of bundle_euclid.m:88-96. */
+static void orc_project(const double *K4, const double *a, const double b[3], int num_a,
+                        double x[2])
+{
+    if (num_a == ORC_PROJ_NUM_A)
+        vlg_project_proj(a, b, x);
+    else
+        oracle_reproject(K4, a, b, num_a - 6, x);
+}
+
+static const double *orc_k4(const double *K4, int j)
+{
+    return K4 ? K4 + 4 * (size_t)j : NULL;
+}
+
 void oracle_rodrigues(const double om[3], double R[9]) { vlg_rodrigues(R, om); }
+/* the device's division-free FD quotient (vlg_math.h), exported only so the
+ * tests can check it against d / h; the oracle itself divides */
+void oracle_fd_quot_device(const double *d, double *out, long long n)
+{
+    long long k;
+    for (k = 0; k < n; k++)
+        out[k] = vlg_fd_quot(d[k]);
+}
 double oracle_sin(double x) { return VLG_SIN(x); }
 double oracle_cos(double x) { return VLG_COS(x); }
 void oracle_pinv3(const double M[9], double P[9]) { vlg_pinv3(M, P); }
 
 /* Camera-parameter derivative, forward difference:
  * mex_bundle_1_XABeUVWeAeB.c:14-41 (a1 = a0 + h*e_k for every component,
- * divide by h). */
+ * divide by h); projective: mex_bundle_proj_1_XABeUVWeAeB.c:34-59. */
 static void orc_dcam(const double K4[4], const double *a0, const double b[3], int num_a,
                      int k, const double x0[2], double out[2])
 {
@@ -59,12 +96,13 @@ static void orc_dcam(const double K4[4], const double *a0, const double b[3], in
     int c;
     for (c = 0; c < num_a; c++)
         a1[c] = a0[c] + h * (c == k ? 1.0 : 0.0);
-    oracle_reproject(K4, a1, b, num_a - 6, x1);
+    orc_project(K4, a1, b, num_a, x1);
     out[0] = (x1[0] - x0[0]) / h;
     out[1] = (x1[1] - x0[1]) / h;
 }
 
-/* Point derivative: mex_bundle_1_XABeUVWeAeB.c:43-70. */
+/* Point derivative: mex_bundle_1_XABeUVWeAeB.c:43-70
+ * (mex_bundle_proj_1_XABeUVWeAeB.c:61-86). */
 static void orc_dpt(const double K4[4], const double *a, const double b0[3], int num_a,
                     int k, const double x0[2], double out[2])
 {
@@ -73,7 +111,7 @@ static void orc_dpt(const double K4[4], const double *a, const double b0[3], int
     int c;
     for (c = 0; c < 3; c++)
         b1[c] = b0[c] + h * (c == k ? 1.0 : 0.0);
-    oracle_reproject(K4, a, b1, num_a - 6, x1);
+    orc_project(K4, a, b1, num_a, x1);
     out[0] = (x1[0] - x0[0]) / h;
     out[1] = (x1[1] - x0[1]) / h;
 }
@@ -85,7 +123,7 @@ static void orc_linearize_obs(const double K4[4], const double *a, const double 
                               double *A, double *B, double e[2])
 {
     int k;
-    oracle_reproject(K4, a, b, num_a - 6, xh);
+    orc_project(K4, a, b, num_a, xh);
     for (k = 0; k < num_a; k++)
         orc_dcam(K4, a, b, num_a, k, xh, A + 2 * k);
     for (k = 0; k < 3; k++)
@@ -140,7 +178,7 @@ void oracle_mex1(int m, int n, int num_a, const double *K4, const double *a,
         for (i = 0; i < n; i++) {
             p = (size_t)i + (size_t)n * j;
             if (vis[p] != 0.0) {
-                orc_linearize_obs(K4 + 4 * j, a + (size_t)num_a * j, b + 3 * (size_t)i,
+                orc_linearize_obs(orc_k4(K4, j), a + (size_t)num_a * j, b + 3 * (size_t)i,
                                   X + 2 * p, num_a, X_hat + 2 * p, A + 2 * num_a * p,
                                   B + 6 * p, e + 2 * p);
             } else {
@@ -240,8 +278,8 @@ void oracle_mex3(int m, int n, int num_a, const double *W, const double *da,
         for (i = 0; i < n; i++) {
             p = (size_t)i + (size_t)n * j;
             if (vis[p] != 0.0) {
-                oracle_reproject(K4 + 4 * j, a_new + (size_t)num_a * j, b_new + 3 * (size_t)i,
-                                 num_a - 6, X_hat + 2 * p);
+                orc_project(orc_k4(K4, j), a_new + (size_t)num_a * j, b_new + 3 * (size_t)i,
+                            num_a, X_hat + 2 * p);
             } else {
                 X_hat[2 * p] = X[2 * p];
                 X_hat[2 * p + 1] = X[2 * p + 1];
@@ -277,7 +315,7 @@ void oracle_sp_linearize(int m, int n, int num_a, const int *pt_ptr, const int *
             int j = obs_cam[o];
             double *w = W + (size_t)num_a * 3 * o;
             memset(w, 0, sizeof(double) * num_a * 3);
-            orc_linearize_obs(K4 + 4 * j, a + (size_t)num_a * j, b + 3 * (size_t)i,
+            orc_linearize_obs(orc_k4(K4, j), a + (size_t)num_a * j, b + 3 * (size_t)i,
                               obs_x + 2 * (size_t)o, num_a, obs_xhat + 2 * (size_t)o,
                               A + 2 * (size_t)num_a * o, B + 6 * (size_t)o, e + 2 * (size_t)o);
             orc_accum_obs(A + 2 * (size_t)num_a * o, B + 6 * (size_t)o, e + 2 * (size_t)o,
@@ -397,8 +435,8 @@ double oracle_sp_update_nd(int m, int n, int num_a, int ndb, const int *pt_ptr,
         for (o = pt_ptr[i]; o < pt_ptr[i + 1]; o++) {
             int j = obs_cam[o];
             double *xh = obs_xhat + 2 * (size_t)o, d0, d1;
-            oracle_reproject(K4 + 4 * j, a_new + (size_t)num_a * j, b_new + 3 * (size_t)i,
-                             num_a - 6, xh);
+            orc_project(orc_k4(K4, j), a_new + (size_t)num_a * j, b_new + 3 * (size_t)i,
+                        num_a, xh);
             d0 = obs_x[2 * (size_t)o] - xh[0];
             d1 = obs_x[2 * (size_t)o + 1] - xh[1];
             sse += d0 * d0 + d1 * d1;

@@ -50,7 +50,9 @@ def _lib(variant: str = ""):
 
 
 def P(a):
-    """ctypes pointer to a contiguous float64 / int32 numpy buffer."""
+    """ctypes pointer to a contiguous float64 / int32 numpy buffer (None -> NULL)."""
+    if a is None:
+        return None
     if a.dtype == np.float64:
         assert a.flags.c_contiguous or a.flags.f_contiguous
         return a.ctypes.data_as(_dp)
@@ -231,7 +233,8 @@ def sp_update(pb, W, da, eB, Vinv, a, b, num_a, lib=None, ndb=6):
     b_new = np.zeros((3, pb.n), order="F")
     xh = np.zeros((pb.N, 2))
     sse = lib.oracle_sp_update_nd(pb.m, pb.n, num_a, ndb, P(pb.pt_ptr), P(pb.obs_cam),
-                                  P(pb.obs_x), P(W), P(F(da)), P(F(eB)), P(F(Vinv)), P(pb.K),
+                                  P(pb.obs_x), P(W), P(F(da)), P(F(eB)), P(F(Vinv)),
+                                  None if pb.K is None else P(pb.K),
                                   P(F(a)), P(F(b)), P(db), P(a_new), P(b_new), P(xh))
     return db, a_new, b_new, xh, sse
 

@@ -57,3 +57,30 @@ def random_problem(seed, m=6, n=40, num_a=6, density=0.6, zero_w_cam=True):
     b = np.asfortranarray(sc.X0[0:3])
     X = np.asfortranarray(x[0:2])
     return K, a, b, X, np.asfortranarray(vis), sc
+
+
+@pytest.fixture(scope="session")
+def poracle():
+    """Projective oracle (oracle/bundle_projective_ref.py)."""
+    import bundle_projective_ref as pref
+    import bundle_euclid_ref as ref
+    ref._lib()
+    return pref
+
+
+def random_projective_problem(seed, m=6, n=40, density=0.6):
+    """Small random mex_bundle_proj_* problem: a = P(:) (12 x m) of a perturbed
+    Euclidean scene (scene.projective_from), b 3 x n, X 2 x n x m, vis n x m."""
+    from bundleadjustmentmatlab_amd.scene import make_config, projective_from
+    rng = np.random.default_rng(seed)
+    sc = make_config("cfg1", m=m, min_n=n // 2, max_n=n, seed=seed)
+    x, vis = sc.dense()
+    n = sc.n
+    keep = rng.random(vis.shape) < density
+    keep[np.arange(n), rng.integers(0, m, n)] = True
+    vis = vis * keep
+    Pp, Xp = projective_from(sc)
+    a = np.asfortranarray(Pp.reshape(12, m, order="F"))
+    b = np.asfortranarray(Xp[0:3])
+    X = np.asfortranarray(x[0:2])
+    return a, b, X, np.asfortranarray(vis), sc, Pp, Xp

@@ -48,6 +48,12 @@ def test_bad_arguments_rejected_before_device_work():
     K = np.ones(8)
     prob.K = K.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
     assert L.vlgba_create(ctypes.byref(prob), None, ctypes.byref(h)) == -1002
+    prob.num_a, prob.model = 6, 1          # projective needs num_a = 12
+    assert L.vlgba_create(ctypes.byref(prob), None, ctypes.byref(h)) == -1002
+    prob.num_a, prob.model = 12, 0         # 12 is not a Euclidean num_a
+    assert L.vlgba_create(ctypes.byref(prob), None, ctypes.byref(h)) == -1002
+    prob.model = 7                         # unknown model
+    assert L.vlgba_create(ctypes.byref(prob), None, ctypes.byref(h)) == -1001
 
 
 C_LAYOUT = r"""
@@ -60,6 +66,7 @@ int main(void) {
          sizeof(vlgba_problem), sizeof(vlgba_options), sizeof(vlgba_stats),
          sizeof(vlgba_step_info));
   P(vlgba_problem, num_obs) P(vlgba_problem, obs_x) P(vlgba_problem, num_vis)
+  P(vlgba_problem, model) P(vlgba_options, semantics)
   P(vlgba_options, pivot) P(vlgba_options, lambda0) P(vlgba_options, comm_id)
   P(vlgba_stats, lambda) P(vlgba_stats, seconds)
   P(vlgba_step_info, accepted) P(vlgba_step_info, chol_failed)
@@ -84,6 +91,8 @@ def test_struct_layouts_match_ctypes(tmp_path):
     chk = {"vlgba_problem.num_obs": B.VlgbaProblem.num_obs.offset,
            "vlgba_problem.obs_x": B.VlgbaProblem.obs_x.offset,
            "vlgba_problem.num_vis": B.VlgbaProblem.num_vis.offset,
+           "vlgba_problem.model": B.VlgbaProblem.model.offset,
+           "vlgba_options.semantics": B.VlgbaOptions.semantics.offset,
            "vlgba_options.pivot": B.VlgbaOptions.pivot.offset,
            "vlgba_options.lambda0": B.VlgbaOptions.lambda0.offset,
            "vlgba_options.comm_id": B.VlgbaOptions.comm_id.offset,
