@@ -124,7 +124,7 @@ struct ba_dev {
     double *spart;     // [ngs][NA*NA] per group slot
     double *epart;     // [nge][NA] per group e-slot
     double *upart;     // [nes][NA(NA+1)/2 + NA] per-chunk U_j (lower) | eA_j partials
-    double *chsse;     // [nch] per-chunk SSE partials of the linearisation
+    double *chsse;     // [3][nch] per-chunk partials: linearisation SSE, new SSE, point dpg
     int ns, nes;
     int ch_max_terms, ch_max_slots;   // per-chunk maxima: LDS staging of the term lists
     long long nterm_fast;             // (obs, obs) Schur terms of the chunk plan
@@ -135,6 +135,7 @@ struct ba_dev {
     int grp_max_s, grp_max_e;         // LDS accumulator sizes (largest non-direct group)
     unsigned *blob;                   // per-chunk metadata records (see build_plan)
     int *ch_blob, *ch_obase;          // [nch+1] record offsets (words), first local obs
+    unsigned char *obs_lpt;           // [N] chunk-local point of each observation
     int max_blob;
     int *grp_ch, *grp_gs, *grp_ge;    // [ngrp+1] chunk / group-slot / group-eslot ranges
     unsigned short *cs_g, *ce_g;      // chunk slot / chunk e-slot -> group-local id

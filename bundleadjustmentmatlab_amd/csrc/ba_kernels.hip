@@ -179,6 +179,58 @@ struct cam_view<NA, true> {
 };
 
 // -------------------------------------------------------------------------
+// The 9 FD columns of [A | B] for fix_calibration (NA = 6), shared by the two
+// lanes of an observation with one instruction stream and the work each
+// column really needs (mex_bundle_1_XABeUVWeAeB.c:14-70, the same
+// expressions as project_col):
+//   3 "full" rounds   lane 0: rotation column t  -- R(w + h e_t), t + 0, b
+//                     lane 1: point column t     -- R(w), t, b + h e_t
+//   2 "shift" rounds  translation columns 3, 4 | 5, -: R(w + 0) b is shared
+//                     (vlg_rot_b), only S + (t + h e_k) is formed per column
+// Every operand is formed exactly as the reference forms it (a0 + h * 0.0 for
+// the unperturbed camera components of a camera column, a0 itself for a
+// point column), so the columns are bit-identical to project_col's.
+// -------------------------------------------------------------------------
+__device__ __forceinline__ void fd_columns_6(const cam_view<6> &cv, const double b[3],
+                                             const double xh[2], int half, double *row)
+{
+    const double *t0 = cv.a0 + 3;
+#pragma unroll 1
+    for (int t = 0; t < 3; t++) {
+        const double *Rs = cv.R + 9 * (half ? 0 : 1 + t);
+        double Rk[9], tt[3], bb[3], x1[2];
+#pragma unroll
+        for (int q = 0; q < 9; q++) Rk[q] = Rs[q];
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            tt[c] = half ? t0[c] : t0[c] + H_FD * 0.0;
+            bb[c] = half ? b[c] + H_FD * ((c == t) ? 1.0 : 0.0) : b[c];
+        }
+        vlg_project(cv.Kc, Rk, tt, bb, x1);
+        const int col = half ? 6 + t : t;
+        row[2 * col] = vlg_fd_quot(x1[0] - xh[0]);
+        row[2 * col + 1] = vlg_fd_quot(x1[1] - xh[1]);
+    }
+    double S[3], R4[9];
+    const double *Rs4 = cv.R + 36;
+#pragma unroll
+    for (int q = 0; q < 9; q++) R4[q] = Rs4[q];
+    vlg_rot_b(R4, b, S);
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+        const int k = 3 + 2 * u + half;      // 3, 4 | 5, (6: idle)
+        if (k < 6) {
+            double tt[3], x1[2];
+#pragma unroll
+            for (int c = 0; c < 3; c++) tt[c] = t0[c] + H_FD * ((3 + c == k) ? 1.0 : 0.0);
+            vlg_project_s(cv.Kc, S, tt, x1);
+            row[2 * k] = vlg_fd_quot(x1[0] - xh[0]);
+            row[2 * k + 1] = vlg_fd_quot(x1[1] - xh[1]);
+        }
+    }
+}
+
+// -------------------------------------------------------------------------
 // rotations: R(a), R(a + h e_k) k = 0..2, R(a + 0) per camera (5 x 9)
 // -------------------------------------------------------------------------
 template <int NA>
@@ -314,11 +366,14 @@ __global__ __launch_bounds__(256) void k_linearize(
 // U_j / eA_j (sequential over the chunk's points), reduced per camera in chunk
 // order by k_camera_reduce_chunks.  jrec is never written.
 // -------------------------------------------------------------------------
+// 7 waves per SIMD for NA = 6: the LDS rows (21.7 KB) allow 7 workgroups per
+// CU; the bound keeps the register allocation from costing one of them
 template <int NA>
-__global__ __launch_bounds__(256) void k_linearize_chunk(
-    const int *__restrict__ ch_pt, const int *__restrict__ ch_eslot,
-    const int *__restrict__ eslot_optr, const unsigned short *__restrict__ eslot_obs,
-    const int *__restrict__ pt_ptr, const int *__restrict__ obs_cam,
+__global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
+    const int *__restrict__ ch_pt, const int *__restrict__ ch_obase,
+    const int *__restrict__ ch_eslot, const int *__restrict__ eslot_optr,
+    const unsigned short *__restrict__ eslot_obs, const int *__restrict__ pt_ptr,
+    const int *__restrict__ obs_cam, const unsigned char *__restrict__ obs_lpt,
     const double *__restrict__ obs_x, const double *__restrict__ K4,
     const double *__restrict__ a, const double *__restrict__ rot,
     const double *__restrict__ b, ba_flags f, const unsigned char *__restrict__ pivot,
@@ -328,44 +383,51 @@ __global__ __launch_bounds__(256) void k_linearize_chunk(
     constexpr int NC0 = (NA + 4) / 2;       // lane 0: base + FD columns [0, NC0)
     constexpr int RS = 2 * NA + 8;          // LDS row: A (2 NA), B (6), e (2)
     constexpr int NU = NA * (NA + 1) / 2;
-    __shared__ double rows[BA_CH_OBS * RS];
-    __shared__ int lpt[BA_CH_OBS];
+    static_assert(BA_CH_OBS + 1 <= 256 && BA_CH_PTS + 1 <= 256, "one metadata word per lane");
+    __shared__ __attribute__((aligned(16))) double rows[BA_CH_OBS * RS];
+    __shared__ int lptr[BA_CH_PTS + 1];     // chunk-local observation offsets per point
     __shared__ int eoff[BA_CH_OBS + 1];
     __shared__ unsigned short eobl[BA_CH_OBS];
+    __shared__ unsigned char wz[BA_CH_OBS]; // W_ij forced to zero (fix masks, :140-154)
     const int ch = blockIdx.x, tid = threadIdx.x;
-    const int p0 = ch_pt[ch], p1 = ch_pt[ch + 1], np = p1 - p0;
-    const int obase = pt_ptr[p0], nobs = pt_ptr[p1] - obase;
+    const int p0 = ch_pt[ch], np = ch_pt[ch + 1] - p0;
+    const int obase = ch_obase[ch], nobs = ch_obase[ch + 1] - obase;
     const int e0 = ch_eslot[ch], nes = ch_eslot[ch + 1] - e0;
-    if (tid < np)
-        for (int o = pt_ptr[p0 + tid]; o < pt_ptr[p0 + tid + 1]; o++) lpt[o - obase] = tid;
-    {
-        const int u0 = eslot_optr[e0], nu = eslot_optr[e0 + nes] - u0;
-        for (int q = tid; q < nu; q += 256) eobl[q] = eslot_obs[u0 + q];
-        for (int q = tid; q <= nes; q += 256) eoff[q] = eslot_optr[e0 + q] - u0;
-    }
-    __syncthreads();
+    STAMP_DECL;
+    // Metadata of the reduction phases: loaded now, stored to LDS after the
+    // projections, so its dependent loads ride along with the observation and
+    // camera loads instead of adding round trips (and a barrier) up front.
+    const int u0 = eslot_optr[e0], nu = eslot_optr[e0 + nes] - u0;
+    const int m_eoff = tid <= nes ? eslot_optr[e0 + tid] - u0 : 0;
+    const int m_lptr = tid <= np ? pt_ptr[p0 + tid] - obase : 0;
+    const int m_eobl = tid < nu ? eslot_obs[u0 + tid] : 0;
+    STAMP(16);
     double sse = 0.0;
     {
         const int lo = tid >> 1, half = tid & 1;
         if (lo < nobs) {
-            const int o = obase + lo, j = obs_cam[o], i = p0 + lpt[lo];
+            const int o = obase + lo, j = obs_cam[o], i = p0 + obs_lpt[o];
             const double bi[3] = {b[3 * (size_t)i], b[3 * (size_t)i + 1],
                                   b[3 * (size_t)i + 2]};
             cam_view<NA> cv(a, K4, rot, j);
             double xh[2];
             cv.project(bi, xh);
             double *row = rows + RS * lo;
-            // the NA + 3 FD columns of [A | B] (mex_bundle_1 :201-219) split
-            // evenly: lane 0 columns [0, NC0), lane 1 [NC0, NA + 3), one
-            // instruction stream for both (project_col has no branch)
+            if constexpr (NA == 6) {
+                fd_columns_6(cv, bi, xh, half, row);
+            } else {
+                // the NA + 3 FD columns of [A | B] (mex_bundle_1 :201-219) split
+                // evenly: lane 0 columns [0, NC0), lane 1 [NC0, NA + 3), one
+                // instruction stream for both (project_col has no branch)
 #pragma unroll 1
-            for (int t = 0; t < NC0; t++) {
-                const int col = half ? NC0 + t : t;
-                if (col < NA + 3) {
-                    double x1[2];
-                    cv.project_col(col, bi, x1);
-                    row[2 * col] = vlg_fd_quot(x1[0] - xh[0]);
-                    row[2 * col + 1] = vlg_fd_quot(x1[1] - xh[1]);
+                for (int t = 0; t < NC0; t++) {
+                    const int col = half ? NC0 + t : t;
+                    if (col < NA + 3) {
+                        double x1[2];
+                        cv.project_col(col, bi, x1);
+                        row[2 * col] = vlg_fd_quot(x1[0] - xh[0]);
+                        row[2 * col + 1] = vlg_fd_quot(x1[1] - xh[1]);
+                    }
                 }
             }
             if (!half) {
@@ -374,26 +436,32 @@ __global__ __launch_bounds__(256) void k_linearize_chunk(
                 row[2 * NA + 6] = e0;
                 row[2 * NA + 7] = e1;
                 sse = e0 * e0 + e1 * e1;
+                wz[lo] = f.fix_structure || f.fix_motion || (f.has_pivot && pivot[j]);
             }
         }
     }
+    if (tid <= nes) eoff[tid] = m_eoff;
+    if (tid <= np) lptr[tid] = m_lptr;
+    if (tid < nu) eobl[tid] = (unsigned short)m_eobl;
     __syncthreads();
-    // W_ij = A^T B onto a zeroed output (:305-314): the chunk's rows are contiguous
+    STAMP(17);
+    // W_ij = A^T B onto a zeroed output (:305-314): the chunk's W rows are one
+    // contiguous HBM range, written lane by lane (coalesced)
     {
         double *wdst = W + (size_t)3 * NA * obase;
         for (int q = tid; q < nobs * 3 * NA; q += 256) {
-            const int lo = q / (3 * NA), e = q % (3 * NA), r = e % NA, c = e / NA;
-            const int j = obs_cam[obase + lo];
-            const bool wzero = f.fix_structure || f.fix_motion || (f.has_pivot && pivot[j]);
+            const int lo = q / (3 * NA), e = q - 3 * NA * lo, c = e / NA, r = e - NA * c;
             const double *row = rows + RS * lo;
-            const double *B = row + 2 * NA;
-            wdst[q] = wzero ? 0.0 : 0.0 + (row[2 * r] * B[2 * c] + row[2 * r + 1] * B[2 * c + 1]);
+            const double2 ar = *reinterpret_cast<const double2 *>(row + 2 * r);
+            const double2 bc = *reinterpret_cast<const double2 *>(row + 2 * NA + 2 * c);
+            wdst[q] = wz[lo] ? 0.0 : 0.0 + (ar.x * bc.x + ar.y * bc.y);
         }
     }
+    STAMP(18);
     // V_i += B^T B, eB_i += B^T e over the point's cameras (:293-302, :326-332)
     for (int q = tid; q < np * 12; q += 256) {
         const int pl = q / 12, e = q % 12, i = p0 + pl;
-        const int lo0 = pt_ptr[i] - obase, lo1 = pt_ptr[i + 1] - obase;
+        const int lo0 = lptr[pl], lo1 = lptr[pl + 1];
         double acc = 0.0;
         if (e < 9) {
             const int r = e % 3, c = e / 3;
@@ -412,6 +480,7 @@ __global__ __launch_bounds__(256) void k_linearize_chunk(
         if (e < 9) V[9 * (size_t)i + e] = acc;
         else eB[3 * (size_t)i + e - 9] = acc;
     }
+    STAMP(19);
     // U_j (lower triangle) / eA_j partials per camera of the chunk
     for (int q = tid; q < nes * (NU + NA); q += 256) {
         const int s = q / (NU + NA), l = q % (NU + NA);
@@ -433,32 +502,54 @@ __global__ __launch_bounds__(256) void k_linearize_chunk(
         }
         upart[(size_t)(NU + NA) * (e0 + s) + l] = acc;
     }
+    STAMP(20);
     block_sum_to<256>(sse, part_sse + blockIdx.x);
+    STAMP(21);
+#ifdef BA_STAMPS
+    if (tid == 0) atomicAdd(&g_stamp[22], 1ull);
+#endif
 }
 
-// U_j, eA_j from the per-chunk partials, in chunk order (fast path)
+// U_j, eA_j from the per-chunk partials (fast path).  One 256-lane workgroup
+// per camera: lane (entry l, stream p) sums the camera's partials p, p + P,
+// p + 2P, ... (P = 256 / (NU + NA) streams, so ~P loads are in flight per
+// entry instead of one dependent chain); the streams are then added in
+// stream order.  Fixed order -> deterministic run to run.
 template <int NA>
-__global__ void k_camera_reduce_chunks(const int *__restrict__ cam_eptr,
-                                       const int *__restrict__ cam_eslots,
-                                       const double *__restrict__ upart, int m, ba_flags f,
-                                       const unsigned char *__restrict__ pivot,
-                                       double *__restrict__ U, double *__restrict__ eA)
+__global__ __launch_bounds__(256) void k_camera_reduce_chunks(const int *__restrict__ cam_eptr,
+                                                              const int *__restrict__ cam_eslots,
+                                                              const double *__restrict__ upart,
+                                                              int m, ba_flags f,
+                                                              const unsigned char *__restrict__ pivot,
+                                                              double *__restrict__ U,
+                                                              double *__restrict__ eA)
 {
     constexpr int NU = NA * (NA + 1) / 2;
-    const int j = blockIdx.x, l = threadIdx.x;
-    if (j >= m || l >= NU + NA) return;
+    constexpr int NT = NU + NA;
+    constexpr int P = 256 / NT;
+    __shared__ double part[P][NT];
+    const int j = blockIdx.x, tid = threadIdx.x;
+    const int l = tid % NT, p = tid / NT;
+    if (p < P) {
+        const int q0 = cam_eptr[j], q1 = cam_eptr[j + 1];
+        double acc = 0.0;
+        for (int q = q0 + p; q < q1; q += P) acc += upart[(size_t)NT * cam_eslots[q] + l];
+        part[p][l] = acc;
+    }
+    __syncthreads();
+    if (tid >= NT) return;
     double acc = 0.0;
-    for (int q = cam_eptr[j]; q < cam_eptr[j + 1]; q++)
-        acc += upart[(size_t)(NU + NA) * cam_eslots[q] + l];
+#pragma unroll
+    for (int k = 0; k < P; k++) acc += part[k][tid];
     if (f.fix_motion || (f.has_pivot && pivot[j])) acc = 0.0;
-    if (l < NU) {
-        int t = l, c = 0;
+    if (tid < NU) {
+        int t = tid, c = 0;
         while (t >= NA - c) { t -= NA - c; c++; }
         const int r = c + t;
         U[(size_t)NA * NA * j + r + NA * c] = acc;
         U[(size_t)NA * NA * j + c + NA * r] = acc;
     } else {
-        eA[(size_t)NA * j + l - NU] = acc;
+        eA[(size_t)NA * j + tid - NU] = acc;
     }
 }
 
@@ -1229,6 +1320,99 @@ __global__ __launch_bounds__(256) void k_point_update(
     block_sum_to<256>(dpg, part_dpg + blockIdx.x);
 }
 
+// -------------------------------------------------------------------------
+// Fast-path update, one workgroup per Schur chunk (<= BA_CH_OBS observations
+// of consecutive points; the same arithmetic as k_point_update, with
+// coalesced, LDS-staged accesses instead of one lane walking a point's W):
+//   lane (obs, r): t_o[r] = W_o(:, r)' da_j over da(1 .. ndb)   (:113-120)
+//   lane per point: rhs = eB_i - t_o1 - t_o2 - ... (cameras ascending),
+//                   db_i = V_inv_i rhs, b_new = b + db, dp'(lambda dp + g)
+//   lane per obs:   new projection with a_new, b_new, new SSE     (:149-166)
+// SSE / dpg partials per chunk, summed in chunk order by k_sum_parts.
+// -------------------------------------------------------------------------
+template <int NA>
+__global__ __launch_bounds__(256) void k_point_update_chunk(
+    const int *__restrict__ ch_pt, const int *__restrict__ ch_obase,
+    const int *__restrict__ pt_ptr, const int *__restrict__ obs_cam,
+    const unsigned char *__restrict__ obs_lpt, const double *__restrict__ obs_x,
+    const double *__restrict__ K4, const double *__restrict__ W,
+    const double *__restrict__ da, const double *__restrict__ eB,
+    const double *__restrict__ Vinv, const double *__restrict__ b,
+    const double *__restrict__ a_new, const double *__restrict__ rot_new, int ndb,
+    double lambda, double *__restrict__ db, double *__restrict__ b_new,
+    double *__restrict__ part_sse, double *__restrict__ part_dpg)
+{
+    __shared__ double ts[BA_CH_OBS * 3];
+    __shared__ double bn[BA_CH_PTS * 3];
+    __shared__ int lptr[BA_CH_PTS + 1];
+    const int ch = blockIdx.x, tid = threadIdx.x;
+    const int p0 = ch_pt[ch], np = ch_pt[ch + 1] - p0;
+    const int obase = ch_obase[ch], nobs = ch_obase[ch + 1] - obase;
+    if (tid <= np) lptr[tid] = pt_ptr[p0 + tid] - obase;
+    for (int q = tid; q < nobs * 3; q += 256) {
+        const int lo = q / 3, r = q - 3 * lo, o = obase + lo;
+        const double *wr = W + (size_t)3 * NA * o + NA * r;
+        const double *d = da + (size_t)NA * obs_cam[o];
+        double dl[NA], w[NA];
+#pragma unroll
+        for (int k = 0; k < NA; k++) {
+            w[k] = wr[k];
+            dl[k] = k < ndb ? d[k] : 0.0;
+        }
+        double t = w[0] * dl[0] + w[1] * dl[1] + w[2] * dl[2] + w[3] * dl[3] + w[4] * dl[4] +
+                   w[5] * dl[5];
+#pragma unroll
+        for (int k = 6; k < NA; k++)   // nomex semantics only (ndb = NA)
+            if (k < ndb) t = t + w[k] * dl[k];
+        ts[q] = t;
+    }
+    __syncthreads();
+    double dpg = 0.0, sse = 0.0;
+    if (tid < np) {
+        const int i = p0 + tid;
+        double rhs[3] = {eB[3 * (size_t)i], eB[3 * (size_t)i + 1], eB[3 * (size_t)i + 2]};
+        for (int lo = lptr[tid]; lo < lptr[tid + 1]; lo++) {
+#pragma unroll
+            for (int r = 0; r < 3; r++) rhs[r] -= ts[3 * lo + r];
+        }
+        const double *vi = Vinv + 9 * (size_t)i;
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            const double dbr = vi[r] * rhs[0] + vi[r + 3] * rhs[1] + vi[r + 6] * rhs[2];
+            const double bnr = b[3 * (size_t)i + r] + dbr;
+            db[3 * (size_t)i + r] = dbr;
+            b_new[3 * (size_t)i + r] = bnr;
+            bn[3 * tid + r] = bnr;
+            dpg += dbr * (lambda * dbr + eB[3 * (size_t)i + r]);
+        }
+    }
+    __syncthreads();
+    if (tid < nobs) {
+        const int o = obase + tid, j = obs_cam[o], pl = obs_lpt[o];
+        const double bl[3] = {bn[3 * pl], bn[3 * pl + 1], bn[3 * pl + 2]};
+        double an[NA], xh[2];
+#pragma unroll
+        for (int c = 0; c < NA; c++) an[c] = a_new[(size_t)NA * j + c];
+        if constexpr (NA == BA_PROJ_NA) {   // mex_bundle_proj_3_db_new.c:160-165
+            vlg_project_proj(an, bl, xh);
+        } else {
+            double k4[4], Kc[9], R[9];
+#pragma unroll
+            for (int c = 0; c < 4; c++) k4[c] = K4[4 * (size_t)j + c];
+#pragma unroll
+            for (int q = 0; q < 9; q++) R[q] = rot_new[9 * (size_t)j + q];
+            vlg_calib(Kc, k4, an, NA - 6);
+            vlg_project(Kc, R, an + 3, bl, xh);
+        }
+        const double d0 = obs_x[2 * (size_t)o] - xh[0];
+        const double d1 = obs_x[2 * (size_t)o + 1] - xh[1];
+        sse = d0 * d0 + d1 * d1;
+    }
+    block_sum_to<256>(sse, part_sse + ch);
+    __syncthreads();
+    block_sum_to<256>(dpg, part_dpg + ch);
+}
+
 // fixed-order sum of nparts partials -> out (one 1024-thread block; four
 // independent loads in flight per lane, so the latency of ~25 dependent
 // rounds of HBM loads does not set the time)
@@ -1287,9 +1471,10 @@ int ba_launch_linearize(ba_dev *d, ba_flags f)
         KT_B(d);
         if (d->nch > 0)
             BA_DISPATCH(d->na, (k_linearize_chunk<NA><<<d->nch, 256, 0, d->stream>>>(
-                                   d->ch_pt, d->ch_eslot, d->eslot_optr, d->eslot_obs,
-                                   d->pt_ptr, d->obs_cam, d->obs_x, d->K4, d->a, d->rot, d->b,
-                                   f, d->pivot, d->W, d->V, d->eB, d->upart, d->chsse)));
+                                   d->ch_pt, d->ch_obase, d->ch_eslot, d->eslot_optr,
+                                   d->eslot_obs, d->pt_ptr, d->obs_cam, d->obs_lpt, d->obs_x,
+                                   d->K4, d->a, d->rot, d->b, f, d->pivot, d->W, d->V, d->eB,
+                                   d->upart, d->chsse)));
         KT_E(d, KT_LIN);
         k_sum_parts<<<1, BA_SUM_BS, 0, d->stream>>>(d->chsse, d->nch, d->scal + 0);
         return -(int)hipGetLastError();
@@ -1310,7 +1495,7 @@ int ba_launch_camera_reduce(ba_dev *d, ba_flags f)
     const int bs = ((d->na * (d->na + 1) / 2 + d->na) + 63) / 64 * 64;
     if (!d->ordered) {
         KT_B(d);
-        BA_DISPATCH(d->na, (k_camera_reduce_chunks<NA><<<d->m, bs, 0, d->stream>>>(
+        BA_DISPATCH(d->na, (k_camera_reduce_chunks<NA><<<d->m, 256, 0, d->stream>>>(
                                d->cam_eptr, d->cam_eslots, d->upart, d->m, f, d->pivot, d->U,
                                d->eA)));
         KT_E(d, KT_CAMRED);
@@ -1434,6 +1619,19 @@ int ba_launch_update(ba_dev *d, double lambda)
                            d->a, d->da, d->eA, d->m, lambda, d->a_new, d->rot_new, d->part)));
     KT_E(d, KT_CAMUPD);
     k_sum_parts<<<1, BA_SUM_BS, 0, d->stream>>>(d->part, gc, d->scal + 2);
+    if (!d->ordered && d->nch > 0 && !d->obs_vis && !d->xh_out) {
+        KT_B(d);
+        BA_DISPATCH(d->na, (k_point_update_chunk<NA><<<d->nch, 256, 0, d->stream>>>(
+                               d->ch_pt, d->ch_obase, d->pt_ptr, d->obs_cam, d->obs_lpt,
+                               d->obs_x, d->K4, d->W, d->da, d->eB, d->Vinv, d->b, d->a_new,
+                               d->rot_new, d->ndb, lambda, d->db, d->b_new, d->chsse + d->nch,
+                               d->chsse + 2 * (size_t)d->nch)));
+        KT_E(d, KT_PTUPD);
+        k_sum_parts<<<1, BA_SUM_BS, 0, d->stream>>>(d->chsse + d->nch, d->nch, d->scal + 1);
+        k_sum_parts<<<1, BA_SUM_BS, 0, d->stream>>>(d->chsse + 2 * (size_t)d->nch, d->nch,
+                                                     d->scal + 3);
+        return -(int)hipGetLastError();
+    }
     const int g = grid_for(d->n, 256, PT_GRID_CAP);
     KT_B(d);
     BA_DISPATCH(d->na, (k_point_update<NA><<<g, 256, 0, d->stream>>>(

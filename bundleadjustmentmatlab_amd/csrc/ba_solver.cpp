@@ -704,6 +704,16 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         TRY(upload(d.blob, plan.blob.data(), plan.blob.size(), s));
         TRY(upload(d.ch_blob, plan.ch_blob.data(), plan.ch_blob.size(), s));
         TRY(upload(d.ch_obase, plan.ch_obase.data(), plan.ch_obase.size(), s));
+        {   // chunk-local point of every observation (k_linearize_chunk)
+            std::vector<unsigned char> lpt(d.N > 0 ? d.N : 1, 0);
+            for (size_t ch = 0; ch + 1 < plan.ch_pt.size(); ch++)
+                for (int i = plan.ch_pt[ch]; i < plan.ch_pt[ch + 1]; i++)
+                    for (int o = lptr[i]; o < lptr[i + 1]; o++)
+                        lpt[o] = (unsigned char)(i - plan.ch_pt[ch]);
+            TRY(ctx_alloc(c, &d.obs_lpt, lpt.size()));
+            TRY(upload(d.obs_lpt, lpt.data(), lpt.size(), s));
+            VLGBA_CHECK(hipStreamSynchronize(s));
+        }
         d.grp_max_s = plan.grp_max_s;
         d.grp_max_e = plan.grp_max_e;
         d.ngs = (int)plan.gslot_blk.size();
@@ -729,7 +739,7 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         TRY(upload(d.cam_gptr, plan.cam_gptr.data(), plan.cam_gptr.size(), s));
         TRY(upload(d.cam_gslots, plan.cam_gslots.data(), plan.cam_gslots.size(), s));
         TRY(ctx_alloc(c, &d.upart, (size_t)(na * (na + 1) / 2 + na) * d.nes));
-        TRY(ctx_alloc(c, &d.chsse, (size_t)d.nch));
+        TRY(ctx_alloc(c, &d.chsse, 3 * (size_t)d.nch));   // lin SSE | new SSE | dpg
         TRY(upload(d.ch_pt, plan.ch_pt.data(), plan.ch_pt.size(), s));
         TRY(upload(d.ch_slot, plan.ch_slot.data(), plan.ch_slot.size(), s));
         TRY(upload(d.ch_eslot, plan.ch_eslot.data(), plan.ch_eslot.size(), s));

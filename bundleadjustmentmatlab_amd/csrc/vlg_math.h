@@ -214,17 +214,36 @@ VLG_HD void vlg_calib(double Kc[9], const double K4[4], const double *a, int nvk
 
 /* ---- projection: reproject_point.h:46-56, rotation given -----------------
  * x = dehom(Kc * (R*b + t)), every sum left-to-right as written there.      */
-VLG_HD void vlg_project(const double Kc[9], const double R[9], const double t[3],
-                        const double b[3], double x[2])
+/* The same expression in two steps, so a kernel can share the rotated point
+ * between projections that differ only in t: S = R*b without t (the first
+ * three terms of each left-to-right row sum), then x = dehom(Kc * (S + t)).
+ * vlg_project(Kc, R, t, b) == vlg_project_s(Kc, S, t) for S = vlg_rot_b(R, b)
+ * bit for bit: C evaluates ((R0 b0 + R3 b1) + R6 b2) + t0 in that order. */
+VLG_HD void vlg_rot_b(const double R[9], const double b[3], double S[3])
 {
-    double Rb0 = R[0] * b[0] + R[3] * b[1] + R[6] * b[2] + t[0];
-    double Rb1 = R[1] * b[0] + R[4] * b[1] + R[7] * b[2] + t[1];
-    double Rb2 = R[2] * b[0] + R[5] * b[1] + R[8] * b[2] + t[2];
+    S[0] = R[0] * b[0] + R[3] * b[1] + R[6] * b[2];
+    S[1] = R[1] * b[0] + R[4] * b[1] + R[7] * b[2];
+    S[2] = R[2] * b[0] + R[5] * b[1] + R[8] * b[2];
+}
+
+VLG_HD void vlg_project_s(const double Kc[9], const double S[3], const double t[3], double x[2])
+{
+    double Rb0 = S[0] + t[0];
+    double Rb1 = S[1] + t[1];
+    double Rb2 = S[2] + t[2];
     double x0 = Kc[0] * Rb0 + Kc[3] * Rb1 + Kc[6] * Rb2;
     double x1 = Kc[1] * Rb0 + Kc[4] * Rb1 + Kc[7] * Rb2;
     double x2 = Kc[2] * Rb0 + Kc[5] * Rb1 + Kc[8] * Rb2;
     x[0] = x0 / x2;
     x[1] = x1 / x2;
+}
+
+VLG_HD void vlg_project(const double Kc[9], const double R[9], const double t[3],
+                        const double b[3], double x[2])
+{
+    double S[3];
+    vlg_rot_b(R, b, S);
+    vlg_project_s(Kc, S, t, x);
 }
 
 /* Projective camera (a = P(:), 3 x 4 column major, num_a = 12):

@@ -53,7 +53,7 @@ def main():
     print(f"{kern}: {wgs:.0f} workgroups, {chunks:.0f} chunks per pass")
     tot = sum(v[:len(names)])
     for i, name in enumerate(names):
-        print(f"  {name:12s} {v[i] / 1e6:9.2f} Mcycles  {100 * v[i] / tot:5.1f}%  "
+        print(f"  {name:12s} {v[i] / 1e6:9.2f} Mcycles  {100 * v[i] / max(tot, 1):5.1f}%  "
               f"{v[i] / max(chunks, 1):9.0f} cycles/chunk")
     if kern == "k_schur_mfma" and v[11] > 0:
         # s_memrealtime runs at 100 MHz: calibrates s_memtime and the WG lifetime
@@ -61,6 +61,12 @@ def main():
         life_us = v[11] / wgs / 100.0
         print(f"  s_memtime clock {ghz:.2f} GHz; mean workgroup lifetime {life_us:.1f} us; "
               f"sum of lifetimes {v[11] / 100.0:.0f} us")
+    lin = ["prologue", "projections", "W", "V/eB", "U/eA partials", "sse reduce"]
+    tot = sum(v[16:22])
+    print(f"k_linearize_chunk: {v[22]:.0f} workgroups per pass")
+    for i, name in enumerate(lin):
+        print(f"  {name:14s} {v[16 + i] / 1e6:9.2f} Mcycles  {100 * v[16 + i] / max(tot, 1):5.1f}%  "
+              f"{v[16 + i] / max(v[22], 1):9.0f} cycles/workgroup")
     ba.close()
 
 
