@@ -606,6 +606,59 @@ __global__ __launch_bounds__(256) void k_cr_back(const int *__restrict__ elim, i
     gemv64_t(Ls, t, part, x + (long long)NB * e, 1.0);
 }
 
+// ---------------------------------------------------------------------------
+// One launch builds every envelope tile of S for the factorisation: zeros
+// (clearing the previous factorisation's in-place results and fill), the
+// lower entries of the co-visible blocks that overlap the tile (S_jk, row >=
+// col; bundle_euclid.m:192-193), and for diagonal tiles the pinv rule for
+// exactly-zero rows (App. A Q2, Q8: unit diagonal, rhs 0; padding rows past
+// NA*m included).  Workgroup 0 also clears the factorisation status.
+// Replaces k_zero_env + k_assemble + k_fix_diag + two memsets (5 launches).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_assemble_tiles(
+    double *__restrict__ S, long long lds, const int *__restrict__ env,
+    const int *__restrict__ tb_ptr, const int *__restrict__ tb_blk,
+    const int *__restrict__ blk_jk, const double *__restrict__ sblk, int na, long long ld,
+    double *__restrict__ rhs, double *__restrict__ status)
+{
+    __shared__ double T[NB * (NB + 1)];
+    const int ti = env[2 * blockIdx.x], tk = env[2 * blockIdx.x + 1], tid = threadIdx.x;
+    for (int q = tid; q < NB * (NB + 1); q += 256) T[q] = 0.0;
+    if (blockIdx.x == 0 && tid == 0) status[0] = 0.0;
+    __syncthreads();
+    const long long r0 = (long long)NB * ti, c0 = (long long)NB * tk;
+    const int na2 = na * na;
+    const int u0 = tb_ptr[blockIdx.x], nq = (tb_ptr[blockIdx.x + 1] - u0) * na2;
+    for (int q = tid; q < nq; q += 256) {   // (block, entry) pairs, all lanes busy
+        const int u = q / na2, l = q - na2 * u;
+        const int bk = tb_blk[u0 + u];
+        const int r = l % na, c = l / na;
+        const long long row = (long long)na * blk_jk[2 * bk] + r;
+        const long long col = (long long)na * blk_jk[2 * bk + 1] + c;
+        if (row < col || row < r0 || row >= r0 + NB || col < c0 || col >= c0 + NB) continue;
+        T[(row - r0) * (NB + 1) + (col - c0)] = sblk[(size_t)na2 * bk + l];
+    }
+    __syncthreads();
+    if (ti == tk && tid < NB) {   // pinv semantics for exactly-zero rows, padding rows
+        double *d = T + tid * (NB + 1) + tid;
+        const long long r = r0 + tid;
+        if (*d == 0.0) {
+            *d = 1.0;
+            rhs[r] = 0.0;
+        } else if (r >= ld) {
+            rhs[r] = 0.0;
+        }
+    }
+    __syncthreads();
+    double *base = S + r0 + lds * c0;
+    const int r = tid & 63, cq = tid >> 6;
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+        const int c = cq + 4 * u;
+        base[r + lds * c] = T[r * (NB + 1) + c];
+    }
+}
+
 // zero every envelope tile of S (fill from the previous factorisation)
 __global__ void k_zero_env(double *__restrict__ S, long long lds, const int *__restrict__ env)
 {
@@ -661,6 +714,34 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
                 env.push_back(k);
             }
     d->n_env = (int)env.size() / 2;
+    {   // per envelope tile: the co-visible blocks (j >= k) overlapping it
+        std::vector<int> tid_of((size_t)nt * nt, -1);
+        for (int e = 0; e < d->n_env; e++) tid_of[(size_t)env[2 * e] * nt + env[2 * e + 1]] = e;
+        std::vector<std::vector<int>> lists(d->n_env);
+        for (int b = 0; b < nb; b++) {
+            const long long r0 = (long long)d->na * blk_jk[2 * b], c0 = (long long)d->na * blk_jk[2 * b + 1];
+            const int t0 = (int)(r0 / NB), t1 = (int)((r0 + d->na - 1) / NB);
+            const int u0 = (int)(c0 / NB), u1 = (int)((c0 + d->na - 1) / NB);
+            for (int t = t0; t <= t1; t++)
+                for (int u = u0; u <= u1 && u <= t; u++) {
+                    const int e = tid_of[(size_t)t * nt + u];
+                    if (e >= 0) lists[e].push_back(b);
+                }
+        }
+        std::vector<int> tptr(d->n_env + 1, 0), tblk;
+        for (int e = 0; e < d->n_env; e++) {
+            tblk.insert(tblk.end(), lists[e].begin(), lists[e].end());
+            tptr[e + 1] = (int)tblk.size();
+        }
+        VLGBA_CHECK(hipMalloc(&d->tb_ptr, sizeof(int) * tptr.size()));
+        VLGBA_CHECK(hipMalloc(&d->tb_blk, sizeof(int) * (tblk.size() + 1)));
+        VLGBA_CHECK(hipMemcpyAsync(d->tb_ptr, tptr.data(), sizeof(int) * tptr.size(),
+                                   hipMemcpyHostToDevice, d->stream));
+        if (!tblk.empty())
+            VLGBA_CHECK(hipMemcpyAsync(d->tb_blk, tblk.data(), sizeof(int) * tblk.size(),
+                                       hipMemcpyHostToDevice, d->stream));
+        VLGBA_CHECK(hipStreamSynchronize(d->stream));
+    }
     // cyclic reduction when S is tile-tridiagonal (dense_solve 0 = auto)
     bool tridiag = d->dense_solve == 0 && nt > 1;
     for (int i = 1; tridiag && i < nt; i++)
@@ -730,10 +811,21 @@ void ba_chol_free(ba_dev *d)
     d->cr_elim = d->cr_keep = nullptr;
     d->crL = nullptr;
     d->cr_nlev = 0;
+    if (d->tb_ptr) (void)hipFree(d->tb_ptr);
+    if (d->tb_blk) (void)hipFree(d->tb_blk);
+    d->tb_ptr = d->tb_blk = nullptr;
     if (d->pan_list) (void)hipFree(d->pan_list);
     if (d->env_tiles) (void)hipFree(d->env_tiles);
     d->h_tfirst = d->pan_ptr_h = nullptr;
     d->pan_list = d->env_tiles = nullptr;
+}
+
+int ba_assemble_tiles(ba_dev *d)
+{
+    k_assemble_tiles<<<d->n_env, 256, 0, d->stream>>>(d->S, d->lds, d->env_tiles, d->tb_ptr,
+                                                      d->tb_blk, d->blk_jk, d->sblk, d->na, d->ld,
+                                                      d->rhs, d->scal + 4);
+    return -(int)hipGetLastError();
 }
 
 int ba_chol_prepare(ba_dev *d)
@@ -765,8 +857,7 @@ int ba_chol_solve(ba_dev *d)
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
         attr_done = true;
     }
-    VLGBA_CHECK(hipMemsetAsync(d->scal + 4, 0, sizeof(double), d->stream));
-    if (d->cr_nlev > 0) {
+    if (d->cr_nlev > 0) {   // (status cleared by k_assemble_tiles)
         for (int l = 0; l < d->cr_nlev; l++) {
             const int e0 = d->cr_eptr_h[l], ne = d->cr_eptr_h[l + 1] - e0;
             const int k0 = d->cr_kptr_h[l], nk = d->cr_kptr_h[l + 1] - k0;

@@ -12,7 +12,7 @@
 //   per observation:    jrec[N][JS]   A (2 x NA, column major) then e (2)
 //                       W[N][3*NA], Y[N][3*NA]  (NA x 3 column major, as W_ij)
 //                       t[N][NA]      Y_o * eB_i (the e_ contribution)
-//   per camera:         a[NA*m], a_new, K4[4*m], rot[m][5][9], rot_new[m][9],
+//   per camera:         a[NA*m], a_new, K4[4*m], rot[m][5][9], rot_new[m][5][9],
 //                       U[NA*NA*m], eA[NA*m]
 //   per point:          b[3n], b_new, V[9n], eB[3n], Vinv[9n], db[3n]
 //   reduced system:     blocks (j >= k) with co-visibility: blk_jk[nb][2],
@@ -90,6 +90,7 @@ struct ba_dev {
     int *pan_ptr_h;    // host [nt+1]  offsets into pan_list (panel tiles of step k)
     int *pan_list;     // device: tile rows i > k with tfirst[i] <= k, per k
     int *env_tiles;    // device [n_env][2] (i, k) tiles inside the envelope
+    int *tb_ptr, *tb_blk;  // device: per envelope tile, the co-visible blocks overlapping it
     int n_env;
     int dense_solve;   // 0 auto, 1: every lower tile (measurement), 2: envelope, no CR
     // block cyclic reduction (tile-tridiagonal S): per level, eliminated tiles
@@ -187,6 +188,7 @@ int ba_launch_assemble_plain(ba_dev *d, double *S, long long ld);
 int ba_chol_setup(ba_dev *d, const int *blk_jk_host, int nb);
 void ba_chol_free(ba_dev *d);
 int ba_chol_prepare(ba_dev *d);
+int ba_assemble_tiles(ba_dev *d);   // envelope tiles of S + pinv rule + status, one launch
 int ba_chol_fix_diag(ba_dev *d);
 int ba_chol_solve(ba_dev *d);
 

@@ -233,15 +233,9 @@ __device__ __forceinline__ void fd_columns_6(const cam_view<6> &cv, const double
 // -------------------------------------------------------------------------
 // rotations: R(a), R(a + h e_k) k = 0..2, R(a + 0) per camera (5 x 9)
 // -------------------------------------------------------------------------
-template <int NA>
-__global__ void k_rotations(const double *__restrict__ a, double *__restrict__ rot, int m)
+__device__ __forceinline__ void rotations5(const double w[3], double *__restrict__ out)
 {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= m) return;
-    const double *aj = a + (size_t)NA * j;
-    double w[3] = {aj[0], aj[1], aj[2]};
     double R[9];
-    double *out = rot + 45 * (size_t)j;
     vlg_rodrigues(R, w);
 #pragma unroll
     for (int q = 0; q < 9; q++) out[q] = R[q];
@@ -256,6 +250,16 @@ __global__ void k_rotations(const double *__restrict__ a, double *__restrict__ r
 #pragma unroll
         for (int q = 0; q < 9; q++) out[9 * (1 + k) + q] = R[q];
     }
+}
+
+template <int NA>
+__global__ void k_rotations(const double *__restrict__ a, double *__restrict__ rot, int m)
+{
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const double *aj = a + (size_t)NA * j;
+    const double w[3] = {aj[0], aj[1], aj[2]};
+    rotations5(w, rot + 45 * (size_t)j);
 }
 
 // -------------------------------------------------------------------------
@@ -522,13 +526,29 @@ __global__ __launch_bounds__(256) void k_camera_reduce_chunks(const int *__restr
                                                               int m, ba_flags f,
                                                               const unsigned char *__restrict__ pivot,
                                                               double *__restrict__ U,
-                                                              double *__restrict__ eA)
+                                                              double *__restrict__ eA,
+                                                              const double *__restrict__ chsse,
+                                                              int nch, double *__restrict__ sse_out,
+                                                              double *__restrict__ sse_out2)
 {
     constexpr int NU = NA * (NA + 1) / 2;
     constexpr int NT = NU + NA;
     constexpr int P = 256 / NT;
     __shared__ double part[P][NT];
     const int j = blockIdx.x, tid = threadIdx.x;
+    if (j == m) {   // extra workgroup: the linearisation SSE (old_error), fixed order
+        double v[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        int q = tid;
+        for (; q + 7 * 256 < nch; q += 8 * 256) {
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] += chsse[q + 256 * u];
+        }
+        for (; q < nch; q += 256) v[0] += chsse[q];
+        block_sum_to<256>(((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7])),
+                          sse_out);
+        if (tid == 0) sse_out2[0] = sse_out[0];
+        return;
+    }
     const int l = tid % NT, p = tid / NT;
     if (p < P) {
         const int q0 = cam_eptr[j], q1 = cam_eptr[j + 1];
@@ -1211,17 +1231,20 @@ __global__ void k_assemble(const int *__restrict__ blk_jk, const double *__restr
 }
 
 // -------------------------------------------------------------------------
-// camera update: a_new = a + da (mex_bundle_3_db_new.c:294-298), R(a_new),
-// and the camera part of dp'(lambda dp + g) (bundle_euclid.m:215-217)
+// camera update: a_new = a + da (mex_bundle_3_db_new.c:294-298), the rotation
+// table of a_new (R(a_new), R(a_new + h e_k), R(a_new + 0): k_rotations' five,
+// so an accepted step swaps it in and the next linearisation needs no
+// rotation launch), and the camera part of dp'(lambda dp + g)
+// (bundle_euclid.m:215-217), one partial per 64-lane workgroup.
 // -------------------------------------------------------------------------
 template <int NA>
-__global__ __launch_bounds__(256) void k_camera_update(
+__global__ __launch_bounds__(64) void k_camera_update(
     const double *__restrict__ a, const double *__restrict__ da,
     const double *__restrict__ eA, int m, double lambda, double *__restrict__ a_new,
     double *__restrict__ rot_new, double *__restrict__ part)
 {
     double acc = 0.0;
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int j = blockIdx.x * 64 + threadIdx.x;
     if (j < m) {
         double an[NA];
 #pragma unroll
@@ -1231,14 +1254,9 @@ __global__ __launch_bounds__(256) void k_camera_update(
             a_new[(size_t)NA * j + c] = an[c];
             acc += d * (lambda * d + eA[(size_t)NA * j + c]);
         }
-        if constexpr (NA != BA_PROJ_NA) {
-            double R[9];
-            vlg_rodrigues(R, an);
-#pragma unroll
-            for (int q = 0; q < 9; q++) rot_new[9 * (size_t)j + q] = R[q];
-        }
+        if constexpr (NA != BA_PROJ_NA) rotations5(an, rot_new + 45 * (size_t)j);
     }
-    block_sum_to<256>(acc, part + blockIdx.x);
+    block_sum_to<64>(acc, part + blockIdx.x);
 }
 
 // -------------------------------------------------------------------------
@@ -1302,7 +1320,7 @@ __global__ __launch_bounds__(256) void k_point_update(
 #pragma unroll
                 for (int c = 0; c < 4; c++) k4[c] = K4[4 * (size_t)j + c];
 #pragma unroll
-                for (int q = 0; q < 9; q++) R[q] = rot_new[9 * (size_t)j + q];
+                for (int q = 0; q < 9; q++) R[q] = rot_new[45 * (size_t)j + q];
                 vlg_calib(Kc, k4, an, NA - 6);
                 vlg_project(Kc, R, an + 3, bn, xh);
             }
@@ -1400,7 +1418,7 @@ __global__ __launch_bounds__(256) void k_point_update_chunk(
 #pragma unroll
             for (int c = 0; c < 4; c++) k4[c] = K4[4 * (size_t)j + c];
 #pragma unroll
-            for (int q = 0; q < 9; q++) R[q] = rot_new[9 * (size_t)j + q];
+            for (int q = 0; q < 9; q++) R[q] = rot_new[45 * (size_t)j + q];
             vlg_calib(Kc, k4, an, NA - 6);
             vlg_project(Kc, R, an + 3, bl, xh);
         }
@@ -1411,6 +1429,29 @@ __global__ __launch_bounds__(256) void k_point_update_chunk(
     block_sum_to<256>(sse, part_sse + ch);
     __syncthreads();
     block_sum_to<256>(dpg, part_dpg + ch);
+}
+
+// three fixed-order sums in one launch (block b: part[b] over n[b] -> out[b])
+struct ba_sum3 {
+    const double *part[3];
+    int n[3];
+    double *out[3];
+};
+
+__global__ __launch_bounds__(1024) void k_sum_parts3(ba_sum3 a)
+{
+    const double *part = a.part[blockIdx.x];
+    const int nparts = a.n[blockIdx.x];
+    double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+    int q = threadIdx.x;
+    for (; q + 3 * 1024 < nparts; q += 4 * 1024) {
+        v0 += part[q];
+        v1 += part[q + 1024];
+        v2 += part[q + 2 * 1024];
+        v3 += part[q + 3 * 1024];
+    }
+    for (; q < nparts; q += 1024) v0 += part[q];
+    block_sum_to<1024>((v0 + v1) + (v2 + v3), a.out[blockIdx.x]);
 }
 
 // fixed-order sum of nparts partials -> out (one 1024-thread block; four
@@ -1475,8 +1516,7 @@ int ba_launch_linearize(ba_dev *d, ba_flags f)
                                    d->eslot_obs, d->pt_ptr, d->obs_cam, d->obs_lpt, d->obs_x,
                                    d->K4, d->a, d->rot, d->b, f, d->pivot, d->W, d->V, d->eB,
                                    d->upart, d->chsse)));
-        KT_E(d, KT_LIN);
-        k_sum_parts<<<1, BA_SUM_BS, 0, d->stream>>>(d->chsse, d->nch, d->scal + 0);
+        KT_E(d, KT_LIN);   // the SSE partials are summed by ba_launch_camera_reduce
         return -(int)hipGetLastError();
     }
     const int g = grid_for(d->n, 256, PT_GRID_CAP);
@@ -1495,9 +1535,11 @@ int ba_launch_camera_reduce(ba_dev *d, ba_flags f)
     const int bs = ((d->na * (d->na + 1) / 2 + d->na) + 63) / 64 * 64;
     if (!d->ordered) {
         KT_B(d);
-        BA_DISPATCH(d->na, (k_camera_reduce_chunks<NA><<<d->m, 256, 0, d->stream>>>(
+        // m camera workgroups + one for the SSE: scal[0] and the old_sse slot
+        // after U | eA (all-reduced together with them)
+        BA_DISPATCH(d->na, (k_camera_reduce_chunks<NA><<<d->m + 1, 256, 0, d->stream>>>(
                                d->cam_eptr, d->cam_eslots, d->upart, d->m, f, d->pivot, d->U,
-                               d->eA)));
+                               d->eA, d->chsse, d->nch, d->scal + 0, d->eA + d->ld)));
         KT_E(d, KT_CAMRED);
         return -(int)hipGetLastError();
     }
@@ -1600,25 +1642,19 @@ int ba_launch_yeb(ba_dev *d)
 
 int ba_launch_assemble(ba_dev *d)
 {
-    TRY_RC(ba_chol_prepare(d));   // zero the envelope tiles (last factor's fill)
-    if (d->lds > d->ld)
-        VLGBA_CHECK(
-            hipMemsetAsync(d->rhs + d->ld, 0, sizeof(double) * (d->lds - d->ld), d->stream));
-    const long long work = (long long)d->nb * d->na * d->na;
-    const int g = (int)((work + 255) / 256);
-    BA_DISPATCH(d->na, (k_assemble<NA><<<g, 256, 0, d->stream>>>(d->blk_jk, d->sblk, d->nb,
-                                                                   d->lds, 1, d->S)));
-    return ba_chol_fix_diag(d);
+    KT_B(d);
+    TRY_RC(ba_assemble_tiles(d));
+    KT_E(d, KT_ASSEMBLE);
+    return 0;
 }
 
 int ba_launch_update(ba_dev *d, double lambda)
 {
-    const int gc = grid_for(d->m, 256, 1 << 30);
+    const int gc = (d->m + 63) / 64;
     KT_B(d);
-    BA_DISPATCH(d->na, (k_camera_update<NA><<<gc, 256, 0, d->stream>>>(
+    BA_DISPATCH(d->na, (k_camera_update<NA><<<gc, 64, 0, d->stream>>>(
                            d->a, d->da, d->eA, d->m, lambda, d->a_new, d->rot_new, d->part)));
     KT_E(d, KT_CAMUPD);
-    k_sum_parts<<<1, BA_SUM_BS, 0, d->stream>>>(d->part, gc, d->scal + 2);
     if (!d->ordered && d->nch > 0 && !d->obs_vis && !d->xh_out) {
         KT_B(d);
         BA_DISPATCH(d->na, (k_point_update_chunk<NA><<<d->nch, 256, 0, d->stream>>>(
@@ -1627,11 +1663,14 @@ int ba_launch_update(ba_dev *d, double lambda)
                                d->rot_new, d->ndb, lambda, d->db, d->b_new, d->chsse + d->nch,
                                d->chsse + 2 * (size_t)d->nch)));
         KT_E(d, KT_PTUPD);
-        k_sum_parts<<<1, BA_SUM_BS, 0, d->stream>>>(d->chsse + d->nch, d->nch, d->scal + 1);
-        k_sum_parts<<<1, BA_SUM_BS, 0, d->stream>>>(d->chsse + 2 * (size_t)d->nch, d->nch,
-                                                     d->scal + 3);
+        // new SSE, point dpg, camera dpg: one launch
+        ba_sum3 s3 = {{d->chsse + d->nch, d->chsse + 2 * (size_t)d->nch, d->part},
+                      {d->nch, d->nch, gc},
+                      {d->scal + 1, d->scal + 3, d->scal + 2}};
+        k_sum_parts3<<<3, 1024, 0, d->stream>>>(s3);
         return -(int)hipGetLastError();
     }
+    k_sum_parts<<<1, BA_SUM_BS, 0, d->stream>>>(d->part, gc, d->scal + 2);
     const int g = grid_for(d->n, 256, PT_GRID_CAP);
     KT_B(d);
     BA_DISPATCH(d->na, (k_point_update<NA><<<g, 256, 0, d->stream>>>(

@@ -667,7 +667,7 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
     TRY(ctx_alloc(c, &d.b, 3 * (size_t)d.n));
     TRY(ctx_alloc(c, &d.b_new, 3 * (size_t)d.n));
     TRY(ctx_alloc(c, &d.rot, 45 * (size_t)p->m));
-    TRY(ctx_alloc(c, &d.rot_new, 9 * (size_t)p->m));
+    TRY(ctx_alloc(c, &d.rot_new, 45 * (size_t)p->m));
     // W, eB, V*^-1 carry one zero row past the end: the MFMA Schur kernel points
     // the fragment loads of absent (point, camera) pairs at it
     TRY(ctx_alloc(c, &d.W, (size_t)3 * na * (d.N + 1)));
@@ -911,13 +911,16 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
     const double lam = c->lambda;
     mark(c, 0);
     if (relinearize || !c->lin_valid) {
-        TRY(ba_launch_rotations(&d, d.a, d.rot, 1));
+        // the rotation table of d.a is current: set_params builds it and an
+        // accepted step swaps in the one k_camera_update built for a_new
         TRY(ba_launch_linearize(&d, c->flags));
         mark(c, 1);
         TRY(ba_launch_camera_reduce(&d, c->flags));
-        // U | eA | old_sse travel in one all-reduce
-        VLGBA_CHECK(hipMemcpyAsync(d.eA + d.ld, d.scal + 0, sizeof(double),
-                                   hipMemcpyDeviceToDevice, d.stream));
+        // U | eA | old_sse travel in one all-reduce (the fast path's reduce
+        // kernel writes the old_sse slot itself)
+        if (d.ordered)
+            VLGBA_CHECK(hipMemcpyAsync(d.eA + d.ld, d.scal + 0, sizeof(double),
+                                       hipMemcpyDeviceToDevice, d.stream));
         TRY(allreduce(c, d.U, (size_t)d.na * d.na * d.m + d.ld + 1));
         c->lin_valid = 1;
     } else {
@@ -942,9 +945,9 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
     mark(c, 7);
     // scalars: [0] old_sse(local) [1] new_sse [2] dpg cameras [3] dpg points [4] chol status
     double hs[5];
-    VLGBA_CHECK(hipMemcpyAsync(d.scal + 0, d.eA + d.ld, sizeof(double), hipMemcpyDeviceToDevice,
-                               d.stream));
     if (c->world > 1) {
+        VLGBA_CHECK(hipMemcpyAsync(d.scal + 0, d.eA + d.ld, sizeof(double),
+                                   hipMemcpyDeviceToDevice, d.stream));
         // global old_sse is already in d.eA[ld]; new_sse and the point part of dpg
         // are local; the camera part of dpg is identical on every rank.
         TRY(allreduce(c, d.scal + 1, 1));
@@ -988,6 +991,7 @@ static void lm_apply(vlgba_ctx *c, const vlgba_step_info *info)
     if (info->accepted) {
         std::swap(d.a, d.a_new);
         std::swap(d.b, d.b_new);
+        std::swap(d.rot, d.rot_new);   // rotation table of the new a
         if (proj)
             c->lambda = c->lambda / 10;
         else
@@ -1047,6 +1051,7 @@ int vlgba_set_params(vlgba_ctx *c, const double *a, const double *b)
     if (!c || !a || !b) return VLGBA_E_ARG;
     TRY(upload(c->d.a, a, (size_t)c->d.ld, c->d.stream));
     TRY(upload(c->d.b, b + 3 * (size_t)c->p0, 3 * (size_t)c->d.n, c->d.stream));
+    TRY(ba_launch_rotations(&c->d, c->d.a, c->d.rot, 1));
     c->lin_valid = 0;
     VLGBA_CHECK(hipStreamSynchronize(c->d.stream));
     return 0;
@@ -1086,8 +1091,9 @@ int vlgba_get_linearization(vlgba_ctx *c, double *U, double *eA, double *V, doub
     TRY(ba_launch_rotations(&d, d.a, d.rot, 1));
     TRY(ba_launch_linearize(&d, c->flags));
     TRY(ba_launch_camera_reduce(&d, c->flags));
-    VLGBA_CHECK(hipMemcpyAsync(d.eA + d.ld, d.scal + 0, sizeof(double), hipMemcpyDeviceToDevice,
-                               d.stream));
+    if (d.ordered)
+        VLGBA_CHECK(hipMemcpyAsync(d.eA + d.ld, d.scal + 0, sizeof(double),
+                                   hipMemcpyDeviceToDevice, d.stream));
     TRY(allreduce(c, d.U, (size_t)d.na * d.na * d.m + d.ld + 1));
     c->lin_valid = 1;
     if (U) TRY(download(U, d.U, (size_t)d.na * d.na * d.m, d.stream));
