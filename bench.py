@@ -45,7 +45,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-points", type=int, default=0,
                     help="points of the CPU-baseline sample (0 = full scene)")
+    ap.add_argument("--mode", choices=["pass", "solve"], default="pass",
+                    help="pass: one LM pass per step (headline); solve: one full LM "
+                         "solve to convergence per step (bundle_euclid.m:111-249)")
     args = ap.parse_args()
+    if args.config == "cfg5":
+        return bench_incremental(args)
 
     import torch
     import torch.distributed as dist
@@ -100,6 +105,8 @@ def main():
     ba.set_timing(False)
     ph = {k: float(np.median([p[k] for p in phases])) for k in phases[0]}
 
+    if args.mode == "solve":
+        return bench_solve(args, ba, sc, a0, b0, world, rank, barrier, torch, dist)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -168,6 +175,92 @@ def main():
     ba.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_solve(args, ba, sc, a0, b0, world, rank, barrier, torch, dist):
+    """--mode solve: K full LM solves to convergence from the same start
+    (set_params + vlgba_run each; the parameter upload is inside the timed
+    region).  value = LM passes/s over the whole solves."""
+    for _ in range(args.warmup):
+        ba.set_params(a0, b0)
+        ba.run()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    passes = 0
+    err = st = None
+    for _ in range(args.steps):
+        ba.set_params(a0, b0)
+        err, st = ba.run()
+        passes += st.iterations
+    barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    out = {
+        "metric": "LM iterations/sec (full solves to convergence)",
+        "value": passes / dt, "unit": "LM iterations/s",
+        "observations_per_s": passes / dt * sc.num_obs,
+        "solves_per_s": args.steps / dt, "ms_per_solve": 1e3 * dt / args.steps,
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic (seeded, SURVEY.md 8.d)",
+        "config": {"workload": f"{args.config}: {sc.m} cams x {sc.n} pts x {sc.num_obs} obs, "
+                               "fix_calibration, bundle_euclid.m LM to convergence per step",
+                   "cameras": sc.m, "points": sc.n, "observations": sc.num_obs,
+                   "parallelism": f"point-shard x{world}"},
+        "lm": {"passes_per_solve": st.iterations, "accepted": st.accepted,
+               "error_first": float(err[0]), "error_final": float(err[-1])},
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ba.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_incremental(args):
+    """--config cfg5 (BASELINE.json configs[4]): replay the growing-BA call
+    sequence of incr_reconstruction.m:223-341 (two bundle_euclid solves per
+    added camera) on the seeded 50-camera test_incremental scene.  A step is
+    one whole replay; value = BA solves/s."""
+    import torch
+    from bundleadjustmentmatlab_amd.incremental import incremental_bundle
+    from bundleadjustmentmatlab_amd.scene import make_config
+    torch.cuda.set_device(0)
+    sc = make_config("cfg5")
+    for _ in range(args.warmup):
+        incremental_bundle(sc)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = None
+    for _ in range(args.steps):
+        res = incremental_bundle(sc)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    sol = res["solves"]
+    passes = sum(q["passes"] for q in sol)
+    obs_passes = sum(q["passes"] * q["observations"] for q in sol)
+    out = {
+        "metric": "incremental BA solves/sec (test_incremental-style growing BA)",
+        "value": args.steps * len(sol) / dt, "unit": "BA solves/s",
+        "lm_iterations_per_s": args.steps * passes / dt,
+        "observations_per_s": args.steps * obs_passes / dt,
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (seeded generate_scene_and_motion restatement, SURVEY.md 8.d)",
+        "config": {"workload": f"cfg5: {sc.m} cams x {sc.n} pts x {sc.num_obs} obs, "
+                               f"{len(sol)} growing solves per replay",
+                   "cameras": sc.m, "points": sc.n, "observations": sc.num_obs,
+                   "parallelism": "x1"},
+        "final": {"cameras": sol[-1]["cameras"], "points": sol[-1]["points"],
+                  "error_final": float(sol[-1]["error"][-1])},
+    }
+    print(json.dumps(out), flush=True)
 
 
 # timer name (vlgba_kernel_name) -> device kernel base name in rocprofv3 output

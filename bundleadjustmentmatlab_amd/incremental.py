@@ -1,0 +1,123 @@
+"""Growing (incremental) bundle adjustment -- the BA call sequence of
+toolbox/geometry/incr_reconstruction.m:223-341 (SURVEY.md sec. 8.f rank 2,
+BASELINE.json config 5).
+
+The reference adds cameras one at a time.  Per added camera j it estimates
+the pose (estimate_camera.m), removes outliers, runs ``bundle_euclid`` over
+the cameras added so far and the points reconstructed so far, aligns the
+scene (align_scene.m), triangulates the points that now have >= 2 views,
+removes outliers again and runs ``bundle_euclid`` a second time.  The BA
+solves are the hot path and run on the GPU here (``bundle_euclid_obs``);
+pose estimation, outlier removal and triangulation are out of scope (SURVEY.md
+sec. 2) and are replaced by the synthetic scene's perturbed initial values
+(the new camera's (w0, T0), the point's X0) -- the BA sequence, its growing
+problem sizes and its visibility subsets are the reference's.
+
+``incremental_bundle(scene)`` returns the per-solve log and the final
+reconstruction.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+
+from .bundle import bundle_euclid_obs
+from .evaluation import align_scene, vl_irodr, vl_rodr
+
+__all__ = ["incremental_bundle"]
+
+
+def _subset_obs(sc, cams, pts):
+    """Observations of points ``pts`` in cameras ``cams`` re-indexed to the
+    subset (point-major), as x(:, X3d_index, status) / vis(X3d_index, status)
+    select them (incr_reconstruction.m:254-258)."""
+    cmap = np.full(sc.m, -1)
+    cmap[cams] = np.arange(len(cams))
+    pmap = np.full(sc.n, -1)
+    pmap[pts] = np.arange(len(pts))
+    keep = (cmap[sc.obs_cam] >= 0) & (pmap[sc.obs_pt] >= 0)
+    return pmap[sc.obs_pt[keep]], cmap[sc.obs_cam[keep]], sc.obs_x[keep]
+
+
+def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, device=0,
+                       verbose=False):
+    """Replay the incremental reconstruction's BA sequence on scene ``sc``
+    (scene.Scene).  Cameras ``init_cams`` form the initial two-view
+    reconstruction (VLmvg.m's two_view step); every other camera is added in
+    index order (incr_reconstruction.m:223-227).
+
+    Returns dict(solves=[...], K, T, w, X, status) where each solve records the
+    cameras / points / observations it adjusted, its error_ trace, LM passes
+    and wall seconds."""
+    m, n = sc.m, sc.n
+    K = np.array(sc.K, dtype=np.float64)
+    T = np.array(sc.T0, dtype=np.float64)
+    w = np.array(sc.w0, dtype=np.float64)
+    X = np.zeros((4, n))
+    status = np.zeros(m, dtype=bool)
+    status[list(init_cams)] = True
+    nvis = np.zeros(n, dtype=int)
+    np.add.at(nvis, sc.obs_pt, status[sc.obs_cam])
+    tri = nvis >= 2                                      # two-view triangulation
+    X[:3, tri] = sc.X0[:3, tri]
+    X[3, tri] = 1.0
+    opts = ("fix_calibration",) if fix_calibration else ()
+    solves = []
+
+    def ba(tag, j):
+        cams = np.nonzero(status)[0]
+        pts = np.nonzero(X[3] == 1)[0]                   # X3d_index (:252)
+        if len(pts) == 0 or len(cams) < 2:
+            return
+        pt, cam, ox = _subset_obs(sc, cams, pts)
+        t0 = time.perf_counter()
+        K_, T_, w_, X_, err, st = bundle_euclid_obs(
+            K[:, cams], T[:, cams], w[:, cams], X[:, pts], pt, cam, ox, *opts,
+            num_vis=float(len(pt)), device=device, return_stats=True)
+        secs = time.perf_counter() - t0
+        if align:                                        # :273 align_scene(T_, Omega_, X_ba_)
+            T_, w_, X_ = align_scene(T_, w_, X_)
+        K[:, cams], T[:, cams], w[:, cams] = K_, T_, w_
+        X[:, pts] = X_
+        solves.append(dict(tag=tag, camera=int(j), cameras=len(cams), points=len(pts),
+                           observations=len(pt), error=np.asarray(err), passes=st.iterations,
+                           accepted=st.accepted, seconds=secs))
+        if verbose:
+            print(f"[incremental] camera {j} {tag}: {len(cams)} cams {len(pts)} pts "
+                  f"{len(pt)} obs  error_ {err[0]:.4g} -> {err[-1]:.4g}  {st.iterations} passes")
+
+    for j in range(m):                                   # :223
+        if status[j]:
+            continue
+        status[j] = True
+        s_, R_, t_ = _similarity(sc, X)                  # ground truth -> current frame
+        Rc = vl_rodr(sc.w0[:, j]) @ R_.T                 # estimate_camera stand-in: the
+        w[:, j] = vl_irodr(Rc)                           # perturbed pose in the current frame
+        T[:, j] = s_ * sc.T0[:, j] - Rc @ t_
+        ba("before-triangulation", j)                    # :250-267
+        nvis[:] = 0
+        np.add.at(nvis, sc.obs_pt, status[sc.obs_cam])
+        new = (X[3] == 0) & (nvis >= 2)                  # :281-296 triangulation stand-in
+        s_, R_, t_ = _similarity(sc, X)
+        X[:3, new] = s_ * R_ @ sc.X0[:3, new] + t_[:, None]
+        X[3, new] = 1.0
+        ba("after-triangulation", j)                     # :300-318
+    return dict(solves=solves, K=K, T=T, w=w, X=X, status=status)
+
+
+def _similarity(sc, X):
+    """(s, R, t) with X_current ~ s R X_truth + t, fitted (Umeyama) on the
+    points reconstructed so far; identity when the frame is not aligned yet."""
+    old = X[3] == 1
+    if not np.any(old):
+        return 1.0, np.eye(3), np.zeros(3)
+    A = sc.X[:3, old]
+    B = X[:3, old]
+    ca, cb = A.mean(1, keepdims=True), B.mean(1, keepdims=True)
+    U, sv, Vt = np.linalg.svd((B - cb) @ (A - ca).T)
+    D = np.diag([1.0, 1.0, np.sign(np.linalg.det(U @ Vt))])
+    R = U @ D @ Vt
+    s = (sv * np.diag(D)).sum() / ((A - ca) ** 2).sum()
+    t = (cb - s * R @ ca).reshape(3)
+    return s, R, t

@@ -1,0 +1,75 @@
+"""Host-side evaluation helpers (error_reproj.m, align_scene.m, Rodrigues maps)
+and the incremental driver's bookkeeping.  Tolerances: closed-form identities
+to 1e-12 relative; invariances to 1e-9."""
+import numpy as np
+import pytest
+
+from bundleadjustmentmatlab_amd import evaluation as ev
+from bundleadjustmentmatlab_amd.scene import make_config
+
+
+def test_irodr_inverts_rodr():
+    rng = np.random.default_rng(0)
+    for w in [rng.normal(0, 0.3, 3), rng.normal(0, 1.0, 3), np.array([1e-9, 0, 0]),
+              np.array([0.0, 3.0, 0.1])]:
+        R = ev.vl_rodr(w)
+        assert np.allclose(R @ R.T, np.eye(3), atol=1e-14)
+        assert np.allclose(ev.vl_rodr(ev.vl_irodr(R)), R, atol=1e-12)
+
+
+def test_error_reproj_zero_on_truth_and_q16():
+    sc = make_config("cfg1", m=5, min_n=20, max_n=40, seed=3)
+    x, vis = sc.dense()
+    from bundleadjustmentmatlab_amd.scene import project
+    xt, _ = project(sc.K, sc.w, sc.T, sc.X, sc.obs_cam, sc.obs_pt)
+    x[0, sc.obs_pt, sc.obs_cam] = xt[:, 0]
+    x[1, sc.obs_pt, sc.obs_cam] = xt[:, 1]
+    err, e = ev.error_reproj(x, sc.K, sc.T, sc.w, sc.X, "visibility", vis,
+                             per_pair_visibility=True)
+    assert err < 1e-9 and e.shape == vis.shape
+    # Q16: the reference tests vis(n,m) for every pair -> with vis(n,m) = 0
+    # nothing contributes; with per-pair visibility the noisy pairs do
+    x2, _ = sc.dense()
+    vis2 = vis.copy()
+    vis2[-1, -1] = 0.0
+    err_q16, _ = ev.error_reproj(x2, sc.K, sc.T, sc.w, sc.X, "visibility", vis2)
+    err_fix, _ = ev.error_reproj(x2, sc.K, sc.T, sc.w, sc.X, "visibility", vis2,
+                                 per_pair_visibility=True)
+    assert err_q16 == 0.0 and err_fix > 0.1
+
+
+def test_align_scene_frame_and_invariance():
+    sc = make_config("cfg1", m=6, min_n=20, max_n=40, seed=4)
+    x, vis = sc.dense()
+    T_, w_, X_ = ev.align_scene(sc.T, sc.w, sc.X)
+    assert np.allclose(T_[:, 0], 0, atol=1e-12) and np.allclose(w_[:, 0], 0, atol=1e-12)
+    # the default reference XRef = ones(4,n) (align_scene.m:58-62) has centroid
+    # (1,1,1): the aligned centroid's norm is sqrt(3), not the 1 its help says
+    c = X_[:3, X_[3] == 1].mean(1)
+    assert abs(np.linalg.norm(c) - np.sqrt(3.0)) < 1e-9
+    # the similarity leaves every reprojection unchanged
+    e0 = ev.error_reproj(x, sc.K, sc.T, sc.w, sc.X, "visibility", vis,
+                         per_pair_visibility=True)[1]
+    e1 = ev.error_reproj(x, sc.K, T_, w_, X_, "visibility", vis, per_pair_visibility=True)[1]
+    assert np.allclose(e0, e1, rtol=1e-9, atol=1e-9)
+    # aligning twice is idempotent
+    T2, w2, X2 = ev.align_scene(T_, w_, X_)
+    assert np.allclose(T2, T_, atol=1e-10) and np.allclose(X2, X_, atol=1e-10)
+
+
+def test_incremental_subset_and_similarity():
+    from bundleadjustmentmatlab_amd.incremental import _similarity, _subset_obs
+    sc = make_config("cfg1", m=6, min_n=20, max_n=40, seed=5)
+    cams = np.array([0, 2, 3])
+    pts = np.array([1, 4, 7, 9])
+    pt, cam, ox = _subset_obs(sc, cams, pts)
+    for p, c, o in zip(pt, cam, ox):
+        k = np.nonzero((sc.obs_pt == pts[p]) & (sc.obs_cam == cams[c]))[0]
+        assert len(k) == 1 and np.array_equal(sc.obs_x[k[0]], o)
+    assert np.all(np.diff(pt) >= 0)
+    X = np.zeros((4, sc.n))
+    R = ev.vl_rodr(np.array([0.1, -0.2, 0.3]))
+    X[:3] = 2.5 * R @ sc.X[:3] + np.array([[1.0], [2.0], [3.0]])
+    X[3] = 1.0
+    s, R2, t = _similarity(sc, X)
+    assert abs(s - 2.5) < 1e-9 and np.allclose(R2, R, atol=1e-9) and np.allclose(t, [1, 2, 3])
