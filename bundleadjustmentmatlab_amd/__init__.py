@@ -1,7 +1,8 @@
-"""bundleadjustmentmatlab_amd -- MI355X-native Euclidean bundle adjustment.
+"""bundleadjustmentmatlab_amd -- MI355X-native bundle adjustment.
 
-Drop-in for the Levenberg-Marquardt path of caomw/BundleAdjustmentMatlab
-(VLG toolbox/bundle: bundle_euclid.m + mex_bundle_{1,2,3}*.c), built on
+Drop-in for the Levenberg-Marquardt paths of caomw/BundleAdjustmentMatlab
+(VLG toolbox/bundle: bundle_euclid.m + mex_bundle_{1,2,3}*.c, bundle_projective.m
++ mex_bundle_proj_{1,2,3}*.c, the *_nomex.m twins), built on
 hand-written gfx950 HIP kernels behind the C ABI in include/vlgba.h
 (libvlgba.so, built in-tree).
 """
