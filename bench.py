@@ -350,39 +350,62 @@ def kernel_roofline(name, tot_ms, calls, plan, n_passes):
 
 
 def cpu_baseline(sc, a0, b0, num_a, sample_points):
-    """One LM pass of the oracle restatement (C stages, single thread, + MATLAB
-    pinv of S via numpy/OpenBLAS) on the host cores."""
+    """One LM pass of the multi-threaded CPU port (oracle/ba_cpu_mt.c, OpenMP
+    over the host cores with the reference's per-element arithmetic and
+    reduction orders; SURVEY.md 8.d "ref_sparse_mt") on the GPU box's host,
+    with the reduced solve as a dense LAPACK Cholesky (scipy / OpenBLAS)."""
+    import ctypes
+    import scipy.linalg as sl
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import bundle_euclid_ref as ref
+    import bundle_euclid_ref as ref   # builds oracle/build (incl. libba_cpu_mt.so) if needed
+    ref._lib()
+    L = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libba_cpu_mt.so"))
+    L.mt_linearize.restype = ctypes.c_double
+    L.mt_update.restype = ctypes.c_double
     if sample_points and sample_points < sc.n:
         keep = sc.obs_pt < sample_points
         pt, cam, x = sc.obs_pt[keep], sc.obs_cam[keep], sc.obs_x[keep]
         n = sample_points
-        b = np.asfortranarray(b0[:, :n])
         desc = f"1 LM pass, first {n} points ({keep.sum()} obs) of the scene"
     else:
-        pt, cam, x, n, b = sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, b0
+        pt, cam, x, n = sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n
         desc = f"1 full LM pass of the scene ({len(pt)} obs)"
-    t0 = time.perf_counter()
-    pb = ref.SparseProblem(sc.m, n, pt, cam, x, sc.K)
-    L = ref.sp_linearize(pb, a0, b, num_a)
+    m, N = sc.m, len(pt)
+    P = lambda arr: arr.ctypes.data_as(ctypes.c_void_p)
+    i32 = lambda arr: np.ascontiguousarray(arr, dtype=np.int32)
+    f64 = lambda arr: np.ascontiguousarray(arr, dtype=np.float64)
+    pt, cam, x = i32(pt), i32(cam), f64(x)
+    pt_ptr = i32(np.concatenate([[0], np.cumsum(np.bincount(pt, minlength=n))]))
+    order = np.argsort(cam, kind="stable")                  # camera-major, points ascending
+    cam_obs = i32(order)
+    cam_ptr = i32(np.concatenate([[0], np.cumsum(np.bincount(cam, minlength=m))]))
+    K = f64(sc.K.T.reshape(-1))
+    a = f64(np.asarray(a0).T.reshape(-1))
+    b = f64(np.asarray(b0)[:, :n].T.reshape(-1))
+    jrec, W, Y = np.empty(20 * N), np.empty(18 * N), np.empty(18 * N)
+    V, eB, Vinv = np.empty(9 * n), np.empty(3 * n), np.empty(9 * n)
+    U, eA = np.empty(36 * m), np.empty(6 * m)
+    ld = 6 * m
+    S, e_ = np.empty((ld, ld), order="F"), np.empty(ld)
+    db, b_new, a_new = np.empty(3 * n), np.empty(3 * n), np.empty(6 * m)
     lam = 1e-3
-    Us = L["U"].copy(order="F")
-    for k in range(num_a):
-        Us[k, k] = (1 + lam) * L["U"][k, k]
-    Vs = L["V"].copy(order="F")
-    for k in range(3):
-        Vs[k, k] = (1 + lam) * L["V"][k, k]
-    Vinv = ref.matlab_pinv(Vs)
-    Y = ref.sp_y(pb, L["W"], np.asfortranarray(Vinv), num_a)
-    S, e_ = ref.sp_schur(pb, Y, L["W"], Us, L["eA"], L["eB"], num_a)
-    da = ref.matlab_pinv(S) @ e_
-    ref.sp_update(pb, L["W"], da, L["eB"], Vinv, a0, b, num_a)
+    ref.chol_solve_fixed(np.eye(8) * 2.0, np.ones(8))     # LAPACK / thread-pool start-up
+    t0 = time.perf_counter()
+    old = L.mt_linearize(n, P(pt_ptr), P(cam), P(x), P(K), P(a), P(b), P(jrec), P(W), P(V),
+                         P(eB))
+    L.mt_camera_reduce(m, P(cam_ptr), P(cam_obs), P(jrec), P(U), P(eA))
+    L.mt_damp_y(n, P(pt_ptr), ctypes.c_double(lam), P(V), P(W), P(Vinv), P(Y))
+    L.mt_schur(m, P(cam_ptr), P(cam_obs), P(pt), P(pt_ptr), P(cam), P(Y), P(W), P(U),
+               ctypes.c_double(lam), P(eA), P(eB), P(S), P(e_))
+    da = f64(ref.chol_solve_fixed(S, e_).reshape(-1))     # bundle_euclid.m:193 (dpotrf)
+    new = L.mt_update(m, n, P(pt_ptr), P(cam), P(x), P(K), P(W), P(da), P(eB), P(Vinv), P(a),
+                      P(b), P(db), P(a_new), P(b_new))
     dt = time.perf_counter() - t0
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = int(L.mt_threads())
+    log(f"[bench] cpu port: old_sse={old:.9g} new_sse={new:.9g} {dt:.2f} s")
     return {"value": 1.0 / dt, "unit": "LM iterations/s", "cores": threads, "kind": "port",
-            "sample": desc + f"; stages single-threaded C, pinv(S) OpenBLAS "
-                             f"({threads} threads); {dt:.2f} s"}
+            "sample": desc + f"; OpenMP C port of the MEX stages ({threads} threads) + "
+                             f"LAPACK Cholesky of S; {dt:.2f} s"}
 
 
 if __name__ == "__main__":

@@ -1,0 +1,207 @@
+/*
+ * ba_cpu_mt.c -- multi-threaded CPU port of one Euclidean LM pass, the
+ * "ref_sparse_mt" baseline of SURVEY.md sec. 8.d.
+ *
+ * TEST / BASELINE INFRASTRUCTURE ONLY: bench.py's cpu_baseline leg times it on
+ * the GPU box's host cores; nothing in bundleadjustmentmatlab_amd/ loads it.
+ *
+ * The per-element arithmetic is ba_oracle.c's (the MEX stages'
+ * mex_bundle_1_XABeUVWeAeB.c:192-334, mex_bundle_2_Se_.c:72-155,
+ * mex_bundle_3_db_new.c:99-166, shared vlg_math.h), on the point-major COO
+ * observation list, parallelised with OpenMP so that every reduction keeps the
+ * reference's ascending order: points in parallel for the per-observation
+ * work and V_i / eB_i / db_i; cameras in parallel for U_j / eA_j (camera-major
+ * lists, points ascending); block rows j of S in parallel for the Schur
+ * complement (each S_jk sums its points ascending).  The reduced solve (a
+ * dense Cholesky, LAPACK dpotrf via scipy) runs in bench.py.
+ */
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+#include "../bundleadjustmentmatlab_amd/csrc/vlg_math.h"
+
+#include <omp.h>
+
+#define MT_NA 6   /* fix_calibration (num_a = 6), the config-3 workload */
+
+int mt_threads(void) { return omp_get_max_threads(); }
+
+static void proj6(const double *K4, const double *a, const double *b, double x[2])
+{
+    double Kc[9], R[9];
+    vlg_calib(Kc, K4, a, 0);
+    vlg_rodrigues(R, a);
+    vlg_project(Kc, R, a + 3, b, x);
+}
+
+/* stage 1: A | B | e per observation (jrec[N][20]), W[N][18], V[9n], eB[3n];
+ * returns e'e */
+double mt_linearize(int n, const int *pt_ptr, const int *obs_cam, const double *obs_x,
+                    const double *K4, const double *a, const double *b, double *jrec,
+                    double *W, double *V, double *eB)
+{
+    double sse = 0.0;
+    int i;
+#pragma omp parallel for schedule(static) reduction(+ : sse)
+    for (i = 0; i < n; i++) {
+        double v[9] = {0}, eb[3] = {0};
+        int o, k, r, c;
+        for (o = pt_ptr[i]; o < pt_ptr[i + 1]; o++) {
+            const int j = obs_cam[o];
+            const double *aj = a + MT_NA * (size_t)j, *bi = b + 3 * (size_t)i;
+            const double *k4 = K4 + 4 * (size_t)j;
+            double xh[2], x1[2], a1[MT_NA], b1[3];
+            double *A = jrec + 20 * (size_t)o, *B = A + 12, *e = A + 18;
+            proj6(k4, aj, bi, xh);
+            for (k = 0; k < MT_NA; k++) {
+                for (c = 0; c < MT_NA; c++) a1[c] = aj[c] + VLG_FD_H * (c == k ? 1.0 : 0.0);
+                proj6(k4, a1, bi, x1);
+                A[2 * k] = (x1[0] - xh[0]) / VLG_FD_H;
+                A[2 * k + 1] = (x1[1] - xh[1]) / VLG_FD_H;
+            }
+            for (k = 0; k < 3; k++) {
+                for (c = 0; c < 3; c++) b1[c] = bi[c] + VLG_FD_H * (c == k ? 1.0 : 0.0);
+                proj6(k4, aj, b1, x1);
+                B[2 * k] = (x1[0] - xh[0]) / VLG_FD_H;
+                B[2 * k + 1] = (x1[1] - xh[1]) / VLG_FD_H;
+            }
+            e[0] = obs_x[2 * (size_t)o] - xh[0];
+            e[1] = obs_x[2 * (size_t)o + 1] - xh[1];
+            sse += e[0] * e[0] + e[1] * e[1];
+            for (c = 0; c < 3; c++)
+                for (r = 0; r < MT_NA; r++)
+                    W[18 * (size_t)o + r + MT_NA * c] =
+                        0.0 + (A[2 * r] * B[2 * c] + A[2 * r + 1] * B[2 * c + 1]);
+            for (c = 0; c < 3; c++)
+                for (r = 0; r < 3; r++)
+                    v[r + 3 * c] += B[2 * r] * B[2 * c] + B[2 * r + 1] * B[2 * c + 1];
+            for (r = 0; r < 3; r++) eb[r] += B[2 * r] * e[0] + B[2 * r + 1] * e[1];
+        }
+        memcpy(V + 9 * (size_t)i, v, sizeof v);
+        memcpy(eB + 3 * (size_t)i, eb, sizeof eb);
+    }
+    return sse;
+}
+
+/* U_j, eA_j from the camera-major lists (observations with points ascending) */
+void mt_camera_reduce(int m, const int *cam_ptr, const int *cam_obs, const double *jrec,
+                      double *U, double *eA)
+{
+    int j;
+#pragma omp parallel for schedule(dynamic, 8)
+    for (j = 0; j < m; j++) {
+        double u[MT_NA * MT_NA] = {0}, ea[MT_NA] = {0};
+        int s, r, c;
+        for (s = cam_ptr[j]; s < cam_ptr[j + 1]; s++) {
+            const double *A = jrec + 20 * (size_t)cam_obs[s], *e = A + 18;
+            for (c = 0; c < MT_NA; c++)
+                for (r = 0; r < MT_NA; r++)
+                    u[r + MT_NA * c] += A[2 * r] * A[2 * c] + A[2 * r + 1] * A[2 * c + 1];
+            for (r = 0; r < MT_NA; r++) ea[r] += A[2 * r] * e[0] + A[2 * r + 1] * e[1];
+        }
+        memcpy(U + MT_NA * MT_NA * (size_t)j, u, sizeof u);
+        memcpy(eA + MT_NA * (size_t)j, ea, sizeof ea);
+    }
+}
+
+/* damping, V*^-1 (vlg_pinv3), Y = W V*^-1 */
+void mt_damp_y(int n, const int *pt_ptr, double lambda, const double *V, const double *W,
+               double *Vinv, double *Y)
+{
+    int i;
+#pragma omp parallel for schedule(static)
+    for (i = 0; i < n; i++) {
+        double vs[9], *vi = Vinv + 9 * (size_t)i;
+        int o, r, c, k;
+        memcpy(vs, V + 9 * (size_t)i, sizeof vs);
+        for (k = 0; k < 3; k++) vs[4 * k] = (1 + lambda) * V[9 * (size_t)i + 4 * k];
+        vlg_pinv3(vs, vi);
+        for (o = pt_ptr[i]; o < pt_ptr[i + 1]; o++) {
+            const double *w = W + 18 * (size_t)o;
+            double *y = Y + 18 * (size_t)o;
+            for (c = 0; c < 3; c++)
+                for (r = 0; r < MT_NA; r++)
+                    y[r + MT_NA * c] = w[r] * vi[3 * c] + w[r + MT_NA] * vi[1 + 3 * c] +
+                                       w[r + 2 * MT_NA] * vi[2 + 3 * c];
+        }
+    }
+}
+
+/* S (dense, ld = 6m, column major, both triangles) and e_: block row j per
+ * thread; S_jk and e_j sum their points ascending (mex_bundle_2_Se_.c) */
+void mt_schur(int m, const int *cam_ptr, const int *cam_obs, const int *obs_pt,
+              const int *pt_ptr, const int *obs_cam, const double *Y, const double *W,
+              const double *U, double lambda, const double *eA, const double *eB, double *S,
+              double *e_)
+{
+    const size_t ld = (size_t)MT_NA * m;
+    int j;
+#pragma omp parallel for schedule(dynamic, 4)
+    for (j = 0; j < m; j++) {
+        const size_t rj = (size_t)MT_NA * j;
+        double acc[MT_NA] = {0};
+        int s, ob, r, c;
+        size_t q;
+        for (q = 0; q < ld; q++)
+            for (r = 0; r < MT_NA; r++) S[rj + r + ld * q] = 0.0;
+        for (c = 0; c < MT_NA; c++)
+            for (r = 0; r < MT_NA; r++) {
+                const double u = U[r + MT_NA * c + MT_NA * MT_NA * (size_t)j];
+                S[rj + r + ld * (rj + c)] = r == c ? (1 + lambda) * u : u;
+            }
+        for (s = cam_ptr[j]; s < cam_ptr[j + 1]; s++) {
+            const int oa = cam_obs[s], i = obs_pt[oa];
+            const double *y = Y + 18 * (size_t)oa, *eb = eB + 3 * (size_t)i;
+            for (ob = pt_ptr[i]; ob < pt_ptr[i + 1]; ob++) {
+                const double *w = W + 18 * (size_t)ob;
+                const size_t ck = (size_t)MT_NA * obs_cam[ob];
+                for (c = 0; c < MT_NA; c++)
+                    for (r = 0; r < MT_NA; r++)
+                        S[rj + r + ld * (ck + c)] -=
+                            y[r] * w[c] + y[r + MT_NA] * w[c + MT_NA] +
+                            y[r + 2 * MT_NA] * w[c + 2 * MT_NA];
+            }
+            for (r = 0; r < MT_NA; r++)
+                acc[r] += y[r] * eb[0] + y[r + MT_NA] * eb[1] + y[r + 2 * MT_NA] * eb[2];
+        }
+        for (r = 0; r < MT_NA; r++) e_[rj + r] = eA[rj + r] - acc[r];
+    }
+}
+
+/* back substitution (6-term db, App. A Q3), update, new projections; returns
+ * e_new'e_new */
+double mt_update(int m, int n, const int *pt_ptr, const int *obs_cam, const double *obs_x,
+                 const double *K4, const double *W, const double *da, const double *eB,
+                 const double *Vinv, const double *a, const double *b, double *db,
+                 double *a_new, double *b_new)
+{
+    double sse = 0.0;
+    int i, k;
+    for (k = 0; k < MT_NA * m; k++) a_new[k] = a[k] + da[k];
+#pragma omp parallel for schedule(static) reduction(+ : sse)
+    for (i = 0; i < n; i++) {
+        double rhs[3] = {eB[3 * (size_t)i], eB[3 * (size_t)i + 1], eB[3 * (size_t)i + 2]};
+        const double *vi = Vinv + 9 * (size_t)i;
+        int o, r;
+        for (o = pt_ptr[i]; o < pt_ptr[i + 1]; o++) {
+            const double *w = W + 18 * (size_t)o, *d = da + MT_NA * (size_t)obs_cam[o];
+            for (r = 0; r < 3; r++) {
+                const double *wr = w + MT_NA * r;
+                rhs[r] -= wr[0] * d[0] + wr[1] * d[1] + wr[2] * d[2] + wr[3] * d[3] +
+                          wr[4] * d[4] + wr[5] * d[5];
+            }
+        }
+        for (r = 0; r < 3; r++) {
+            db[3 * (size_t)i + r] = vi[r] * rhs[0] + vi[r + 3] * rhs[1] + vi[r + 6] * rhs[2];
+            b_new[3 * (size_t)i + r] = b[3 * (size_t)i + r] + db[3 * (size_t)i + r];
+        }
+        for (o = pt_ptr[i]; o < pt_ptr[i + 1]; o++) {
+            const int j = obs_cam[o];
+            double xh[2];
+            proj6(K4 + 4 * (size_t)j, a_new + MT_NA * (size_t)j, b_new + 3 * (size_t)i, xh);
+            const double d0 = obs_x[2 * (size_t)o] - xh[0], d1 = obs_x[2 * (size_t)o + 1] - xh[1];
+            sse += d0 * d0 + d1 * d1;
+        }
+    }
+    return sse;
+}
