@@ -57,6 +57,29 @@ __device__ __forceinline__ void load_tile_t(const double *__restrict__ S, long l
     for (int u = 0; u < 16; u++) T[(c0 + 4 * u) * LP + r] = v[u];
 }
 
+// split forms of load_tile / load_tile_t: fetch to registers, then put, so
+// that several tiles' loads can be in flight together
+__device__ __forceinline__ void fetch_tile(const double *__restrict__ S, long long lds, int ti,
+                                           int tj, double v[16])
+{
+    const double *base = S + (long long)NB * ti + lds * (long long)NB * tj;
+    const int r = threadIdx.x & 63, c0 = threadIdx.x >> 6;
+#pragma unroll
+    for (int u = 0; u < 16; u++) v[u] = base[r + lds * (c0 + 4 * u)];
+}
+
+__device__ __forceinline__ void put_tile(double *T, const double v[16], bool transposed)
+{
+    const int r = threadIdx.x & 63, c0 = threadIdx.x >> 6;
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+        if (transposed)
+            T[(c0 + 4 * u) * LP + r] = v[u];
+        else
+            T[r * LP + c0 + 4 * u] = v[u];
+    }
+}
+
 // LDS T[r][c] -> row-major 64x64 dst[r*64 + c]
 __device__ __forceinline__ void store_rowmajor(double *__restrict__ dst, const double *T)
 {
@@ -221,9 +244,40 @@ static __device__ __forceinline__ double rdlane(double v, int l)
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// lane q's value to every lane of its 16-lane row (DPP row_newbcast, one
+// v_mov_b64_dpp; no SGPR round trip).  q must fold to a constant.
+template <int Q> __device__ __forceinline__ double rowbcast_c(double v)
+{
+    const long long u = __builtin_bit_cast(long long, v);
+    const long long r = __builtin_amdgcn_mov_dpp(u, 0x150 + Q, 0xf, 0xf, true);
+    return __builtin_bit_cast(double, r);
+}
+
+static __device__ __forceinline__ double rowbcast(double v, int q)
+{
+    switch (q) {
+    case 0: return rowbcast_c<0>(v);
+    case 1: return rowbcast_c<1>(v);
+    case 2: return rowbcast_c<2>(v);
+    case 3: return rowbcast_c<3>(v);
+    case 4: return rowbcast_c<4>(v);
+    case 5: return rowbcast_c<5>(v);
+    case 6: return rowbcast_c<6>(v);
+    case 7: return rowbcast_c<7>(v);
+    case 8: return rowbcast_c<8>(v);
+    case 9: return rowbcast_c<9>(v);
+    case 10: return rowbcast_c<10>(v);
+    case 11: return rowbcast_c<11>(v);
+    case 12: return rowbcast_c<12>(v);
+    case 13: return rowbcast_c<13>(v);
+    case 14: return rowbcast_c<14>(v);
+    default: return rowbcast_c<15>(v);
+    }
+}
+
 // One wave: Cholesky of the 16x16 diagonal block at (o, o) of As and its
 // inverse (lane r keeps row r of L, then column r of L^-1, in registers;
-// broadcasts by readlane).  L (zero upper) -> As, L^-1 (zero upper) -> Bs.
+// column broadcasts by DPP, pivots by readlane).  L (zero upper) -> As, L^-1 (zero upper) -> Bs.
 __device__ __forceinline__ bool wave_factor16(double *As, double *Bs, int o)
 {
     const int r = threadIdx.x & 63;
@@ -254,12 +308,12 @@ __device__ __forceinline__ bool wave_factor16(double *As, double *Bs, int o)
         // lanes r < q only touch their upper part (zeroed below), lanes r < c
         // hold d[c] = 0 and are unchanged.
         if (c + 1 < 16) {
-            d[c + 1] = fma(-d[c], rdlane(d[c], c + 1), d[c + 1]);
+            d[c + 1] = fma(-d[c], rowbcast(d[c], c + 1), d[c + 1]);
             pv = rdlane(d[c + 1], c + 1);
             y = rsq(pv);
         }
 #pragma unroll
-        for (int q = c + 2; q < 16; q++) d[q] = fma(-d[c], rdlane(d[c], q), d[q]);
+        for (int q = c + 2; q < 16; q++) d[q] = fma(-d[c], rowbcast(d[c], q), d[q]);
     }
     if (r < 16) {
 #pragma unroll
@@ -289,17 +343,24 @@ __device__ __forceinline__ bool wave_factor16(double *As, double *Bs, int o)
 // factors the diagonal block, three waves form the panel blocks with MFMA
 // against its inverse, and the four waves apply the trailing MFMA updates; the
 // off-diagonal blocks of L^-1 follow as Li_ij = -Li_ii sum_t L_it Li_tj.
-// Writes L (zero upper) to As and L^-1 (zero upper) to Li.  Returns false on a
-// non-positive pivot.
-__device__ __forceinline__ bool block_potrf_inv(double *As, double *Li)
+// Writes L to the lower triangle of As (the upper triangle is zeroed only if
+// zero_upper: the 16x16 blocks above the diagonal keep A otherwise) and L^-1
+// (zero upper) to Li.  Returns false on a non-positive pivot.  The caller
+// synchronises after filling As; the result is visible after return.
+__device__ __forceinline__ bool block_potrf_inv(double *As, double *Li, bool zero_upper = true)
 {
     __shared__ double Xs[4][16 * LP];
     __shared__ __attribute__((aligned(16))) int bad;   // keeps the static LDS a
                                                        // multiple of 16 B (G17)
     const int tid = threadIdx.x, w = tid >> 6;
-    for (int q = tid; q < NB * LP; q += blockDim.x) Li[q] = 0.0;
-    if (tid == 0) bad = 0;
-    __syncthreads();
+    // the six 16x16 blocks above the diagonal of L^-1 (everything else is
+    // written below); ordered before their readers by the step barriers
+    for (int q = tid; q < 6 * 256; q += blockDim.x) {
+        const int b = q >> 8, e = q & 255;
+        const int bi = b < 3 ? 0 : (b < 5 ? 1 : 2), bj = b < 3 ? b + 1 : (b < 5 ? b - 1 : 3);
+        Li[(16 * bi + (e >> 4)) * LP + 16 * bj + (e & 15)] = 0.0;
+    }
+    if (tid == 0) bad = 0;   // same wave as the writer below: program order
     for (int kb = 0; kb < 4; kb++) {
         const int o = 16 * kb;
         if (w == 0 && !wave_factor16(As, Li, o) && (tid & 63) == 0) bad = 1;
@@ -334,11 +395,13 @@ __device__ __forceinline__ bool block_potrf_inv(double *As, double *Li)
         }
         __syncthreads();
     }
-    for (int q = tid; q < NB * NB; q += blockDim.x) {   // zero the upper triangle of L
-        const int r = q >> 6, c = q & 63;
-        if (c > r) As[r * LP + c] = 0.0;
+    if (zero_upper) {
+        for (int q = tid; q < NB * NB; q += blockDim.x) {   // zero the upper triangle of L
+            const int r = q >> 6, c = q & 63;
+            if (c > r) As[r * LP + c] = 0.0;
+        }
+        __syncthreads();
     }
-    __syncthreads();
     return bad == 0;
 }
 
@@ -482,27 +545,132 @@ __global__ __launch_bounds__(256) void k_backward(const double *__restrict__ S, 
 // reverse level order: x_e = L_e^-T (y_e - Lp_e^T x_p - Lq_e^T x_q).
 // C(i, j), i > j, lives in S tile (i, j); Lp / Lq in crL[2][nt][64*64].
 // ---------------------------------------------------------------------------
+// Rows 32h .. 32h+31 of the 64x64 product acc = As[r][:] . Bs[c][:] (K = 64):
+// wave w owns rows 32h + 16(w>>1) .. +15, cols 32(w&1) .. +31 (two 16x16
+// MFMA tiles), half the MFMA chain of mfma_64x64.
+__device__ __forceinline__ void mfma_half(const double *As, const double *Bs, int h, d4 acc[2],
+                                          bool zero)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r0 = 32 * h + 16 * (w >> 1), c0 = 32 * (w & 1);
+    const int li = lane & 15, lk = lane >> 4;
+    if (zero) acc[0] = acc[1] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+    for (int s = 0; s < NB / 4; s++) {
+        const int kk = 4 * s + lk;
+        const double a0 = As[(r0 + li) * LP + kk];
+        const double b0 = Bs[(c0 + li) * LP + kk];
+        const double b1 = Bs[(c0 + 16 + li) * LP + kk];
+        acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[1], 0, 0, 0);
+    }
+}
+
+// mfma_half's result: T[r][c] = scale * acc (+ T[r][c] if add)
+__device__ __forceinline__ void half_to_lds(const d4 acc[2], double *T, int h, double scale,
+                                            bool add)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r0 = 32 * h + 16 * (w >> 1), c0 = 32 * (w & 1);
+#pragma unroll
+    for (int y = 0; y < 2; y++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int r = r0 + (lane >> 4) + 4 * q, c = c0 + 16 * y + (lane & 15);
+            const double v = scale * acc[y][q];
+            T[r * LP + c] = add ? T[r * LP + c] + v : v;
+        }
+}
+
+// rows 32h .. +31 of LDS T[r][c] -> row-major dst[r*64 + c]
+__device__ __forceinline__ void store_rowmajor_half(double *__restrict__ dst, const double *T,
+                                                    int h)
+{
+    const int c = threadIdx.x & 63, r0 = 32 * h + (threadIdx.x >> 6);
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) v[u] = T[(r0 + 4 * u) * LP + c];
+#pragma unroll
+    for (int u = 0; u < 8; u++) dst[(r0 + 4 * u) * NB + c] = v[u];
+}
+
+// rows 32h .. +31 of S tile (ti, tj) <-> LDS T[r][c]; thread (row, 8 columns)
+__device__ __forceinline__ void load_tile_half(const double *__restrict__ S, long long lds, int ti,
+                                               int tj, double *T, int h)
+{
+    const double *base = S + (long long)NB * ti + lds * (long long)NB * tj;
+    const int r = 32 * h + (threadIdx.x & 31), c0 = threadIdx.x >> 5;
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) v[u] = base[r + lds * (c0 + 8 * u)];
+#pragma unroll
+    for (int u = 0; u < 8; u++) T[r * LP + c0 + 8 * u] = v[u];
+}
+
+__device__ __forceinline__ void store_tile_half(double *__restrict__ S, long long lds, int ti,
+                                                int tj, const double *T, int h)
+{
+    double *base = S + (long long)NB * ti + lds * (long long)NB * tj;
+    const int r = 32 * h + (threadIdx.x & 31), c0 = threadIdx.x >> 5;
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) v[u] = T[r * LP + c0 + 8 * u];
+#pragma unroll
+    for (int u = 0; u < 8; u++) base[r + lds * (c0 + 8 * u)] = v[u];
+}
+
+// Factor step of a level.  split = 0: one workgroup per eliminated tile does
+// everything.  split = 1 (levels narrow enough that 5 workgroups per tile fit
+// the chip): workgroup role 0 factors D_e and writes L_e^-1 and y_e; roles
+// 1-2 (rows halves of Lp_e) and 3-4 (of Lq_e) redo the same factorisation --
+// deterministic, bit-identical -- with their C tile loaded alongside, and form
+// their 32 rows of the panel.  The critical path loses both 64x64 panel GEMMs.
 __global__ __launch_bounds__(256) void k_cr_factor(double *__restrict__ S, long long lds,
                                                    const int *__restrict__ elim, int nt,
                                                    double *__restrict__ linv,
                                                    double *__restrict__ crL,
                                                    const double *__restrict__ rhs,
                                                    double *__restrict__ y,
-                                                   double *__restrict__ status)
+                                                   double *__restrict__ status, int split)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double *As = sm, *Bs = sm + NB * LP, *Cs = sm + 2 * NB * LP;
     __shared__ double rk[NB];
     __shared__ double part[4][NB];
     const int tid = threadIdx.x;
-    const int e = elim[3 * blockIdx.x], p = elim[3 * blockIdx.x + 1], q = elim[3 * blockIdx.x + 2];
-    load_tile(S, lds, e, e, As);
-    if (tid < NB) rk[tid] = rhs[(long long)NB * e + tid];
+    const int x = split ? blockIdx.x / 5 : blockIdx.x, role = split ? blockIdx.x % 5 : -1;
+    const int e = elim[3 * x], p = elim[3 * x + 1], q = elim[3 * x + 2];
+    if ((role == 1 || role == 2) && p < 0) return;
+    if ((role == 3 || role == 4) && q < 0) return;
+    {
+        double va[16], vc[16];
+        fetch_tile(S, lds, e, e, va);
+        if (role > 0) {   // C(p, e) = tile(e, p)^T  |  C(q, e) = tile(q, e)
+            if (role <= 2)
+                fetch_tile(S, lds, e, p, vc);
+            else
+                fetch_tile(S, lds, q, e, vc);
+        }
+        if (role <= 0 && tid < NB) rk[tid] = rhs[(long long)NB * e + tid];
+        put_tile(As, va, false);
+        if (role > 0) put_tile(Cs, vc, role <= 2);
+    }
     __syncthreads();
-    const bool ok = block_potrf_inv(As, Bs);
+    const bool ok = block_potrf_inv(As, Bs, false);
+    if (role > 0) {
+        const int h = (role - 1) & 1;
+        d4 acc[2];
+        mfma_half(Cs, Bs, h, acc, true);
+        __syncthreads();
+        half_to_lds(acc, Cs, h, 1.0, false);
+        __syncthreads();
+        store_rowmajor_half(crL + (long long)NB * NB * (role <= 2 ? e : nt + e), Cs, h);
+        return;
+    }
     gemv64(Bs, rk, part, y + (long long)NB * e, 1.0);
     store_rowmajor(linv + (long long)NB * NB * e, Bs);
     if (tid == 0 && !ok) status[0] = 1.0;
+    if (split) return;
     d4 acc[2][2];
     if (p >= 0) {   // C(p, e) = tile(e, p)^T
         load_tile_t(S, lds, e, p, Cs);
@@ -525,20 +693,64 @@ __global__ __launch_bounds__(256) void k_cr_factor(double *__restrict__ S, long 
     }
 }
 
+// Update step of a level.  split = 0: one workgroup per kept tile.  split = 1:
+// four workgroups per kept tile -- roles 0/1 update rows halves of D_k (role 0
+// also r_k), roles 2/3 form rows halves of the fill C(k2, k).
 __global__ __launch_bounds__(256) void k_cr_update(double *__restrict__ S, long long lds,
                                                    const int *__restrict__ keep, int nt,
                                                    const double *__restrict__ crL,
                                                    double *__restrict__ rhs,
-                                                   const double *__restrict__ y)
+                                                   const double *__restrict__ y, int split)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double *As = sm, *Bs = sm + NB * LP, *Cs = sm + 2 * NB * LP;
     __shared__ double ym[NB], yp[NB], um[NB], up[NB];
     __shared__ double part[4][NB];
     const int tid = threadIdx.x;
-    const int *kp = keep + 4 * blockIdx.x;
+    const int x = split ? blockIdx.x >> 2 : blockIdx.x, role = split ? blockIdx.x & 3 : -1;
+    const int *kp = keep + 4 * x;
     const int k = kp[0], em = kp[1], ep = kp[2], k2 = kp[3];
     const long long T2 = (long long)NB * NB;
+    if (role >= 2) {   // C(k2, k) = -Lq_{e+} Lp_{e+}^T, rows half role - 2
+        if (k2 < 0) return;
+        const int h = role - 2;
+        load_rowmajor(crL + T2 * (nt + ep), Bs);
+        load_rowmajor(crL + T2 * ep, Cs);
+        __syncthreads();
+        d4 acc[2];
+        mfma_half(Bs, Cs, h, acc, true);
+        half_to_lds(acc, As, h, -1.0, false);
+        __syncthreads();
+        store_tile_half(S, lds, k2, k, As, h);
+        return;
+    }
+    if (role >= 0) {   // rows half `role` of D_k
+        const int h = role;
+        load_tile_half(S, lds, k, k, As, h);
+        load_rowmajor(crL + T2 * (nt + em), Bs);   // Lq_{e-} = L(k, e-)
+        if (ep >= 0) load_rowmajor(crL + T2 * ep, Cs);   // Lp_{e+} = L(k, e+)
+        if (h == 0 && tid < NB) {
+            ym[tid] = y[(long long)NB * em + tid];
+            yp[tid] = (ep >= 0) ? y[(long long)NB * ep + tid] : 0.0;
+        }
+        __syncthreads();
+        d4 acc[2];
+        mfma_half(Bs, Bs, h, acc, true);
+        if (ep >= 0) mfma_half(Cs, Cs, h, acc, false);
+        half_to_lds(acc, As, h, -1.0, true);   // each thread updates the elements it owns
+        if (h == 0) {
+            gemv64(Bs, ym, part, um, 1.0);
+            if (ep >= 0) gemv64(Cs, yp, part, up, 1.0);
+            if (tid < NB) {
+                double r = rhs[(long long)NB * k + tid] - um[tid];
+                if (ep >= 0) r -= up[tid];
+                rhs[(long long)NB * k + tid] = r;
+            }
+        }
+        __syncthreads();
+        store_tile_half(S, lds, k, k, As, h);
+        return;
+    }
     load_tile(S, lds, k, k, As);
     load_rowmajor(crL + T2 * (nt + em), Bs);   // Lq_{e-} = L(k, e-)
     if (ep >= 0) load_rowmajor(crL + T2 * ep, Cs);   // Lp_{e+} = L(k, e+)
@@ -858,18 +1070,28 @@ int ba_chol_solve(ba_dev *d)
         attr_done = true;
     }
     if (d->cr_nlev > 0) {   // (status cleared by k_assemble_tiles)
+        // one workgroup per CU (LDS): fan a level out over 5 (factor) / 4
+        // (update) workgroups per tile while that still fits in one wave of
+        // workgroups -- the levels are latency bound, the chip mostly idle
+        static int ncu = 0;
+        if (!ncu) {
+            int dev = 0;
+            VLGBA_CHECK(hipGetDevice(&dev));
+            VLGBA_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        }
         for (int l = 0; l < d->cr_nlev; l++) {
             const int e0 = d->cr_eptr_h[l], ne = d->cr_eptr_h[l + 1] - e0;
             const int k0 = d->cr_kptr_h[l], nk = d->cr_kptr_h[l + 1] - k0;
+            const int fs = 5 * ne <= ncu, us = 4 * nk <= ncu;
             KT_B(d);
-            k_cr_factor<<<ne, 256, smem3, d->stream>>>(d->S, d->lds, d->cr_elim + 3 * e0, nt,
-                                                       d->linv, d->crL, d->rhs, d->ywork,
-                                                       d->scal + 4);
+            k_cr_factor<<<fs ? 5 * ne : ne, 256, smem3, d->stream>>>(
+                d->S, d->lds, d->cr_elim + 3 * e0, nt, d->linv, d->crL, d->rhs, d->ywork,
+                d->scal + 4, fs);
             KT_E(d, KT_CR_FACTOR);
             if (nk > 0) {
                 KT_B(d);
-                k_cr_update<<<nk, 256, smem3, d->stream>>>(d->S, d->lds, d->cr_keep + 4 * k0, nt,
-                                                           d->crL, d->rhs, d->ywork);
+                k_cr_update<<<us ? 4 * nk : nk, 256, smem3, d->stream>>>(
+                    d->S, d->lds, d->cr_keep + 4 * k0, nt, d->crL, d->rhs, d->ywork, us);
                 KT_E(d, KT_CR_UPDATE);
             }
         }

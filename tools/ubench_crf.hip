@@ -1,0 +1,154 @@
+// Diagnostic micro-benchmark (not part of the library): in-kernel cycle
+// stamps of the phases of block_potrf_inv and k_cr_factor on one SPD tile.
+// Build: hipcc -O3 --offload-arch=gfx950 -ffp-contract=off -I include
+//   tools/ubench_crf.hip -o tools/ubench_crf
+#include "../bundleadjustmentmatlab_amd/csrc/ba_chol.hip"
+
+void kt_begin(ba_ktimer *, hipStream_t) {}
+void kt_end(ba_ktimer *, hipStream_t, int) {}
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+__device__ __forceinline__ unsigned long long stamp()
+{
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+
+#define MARK(i) do { __syncthreads(); if (threadIdx.x == 0) ts[i] = stamp(); } while (0)
+
+__device__ void bpi_dbg(double *As, double *Li, unsigned long long *ts)
+{
+    __shared__ double Xs[4][16 * LP];
+    __shared__ __attribute__((aligned(16))) int bad;
+    const int tid = threadIdx.x, w = tid >> 6;
+    for (int q = tid; q < NB * LP; q += blockDim.x) Li[q] = 0.0;
+    if (tid == 0) bad = 0;
+    MARK(1);
+    for (int kb = 0; kb < 4; kb++) {
+        const int o = 16 * kb;
+        if (w == 0 && !wave_factor16(As, Li, o) && (tid & 63) == 0) bad = 1;
+        MARK(2 + 3 * kb);
+        if (w >= 1 && kb + w <= 3) {
+            const int i = kb + w;
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
+            acc = mfma16_nt(As, 16 * i, o, Li, o, o, acc);
+            put16(As, 16 * i, o, acc, 1.0, false);
+        }
+        MARK(3 + 3 * kb);
+        int pidx = 0;
+        for (int j = kb + 1; j < 4; j++)
+            for (int i = j; i < 4; i++, pidx++)
+                if ((pidx & 3) == w) {
+                    d4 acc = {0.0, 0.0, 0.0, 0.0};
+                    acc = mfma16_nt(As, 16 * i, o, As, 16 * j, o, acc);
+                    put16(As, 16 * i, 16 * j, acc, -1.0, true);
+                }
+        MARK(4 + 3 * kb);
+    }
+    for (int i = 1; i < 4; i++) {
+        if (w < i) {
+            const int j = w;
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
+            for (int t = j; t < i; t++) acc = mfma16_nn(As, 16 * i, 16 * t, Li, 16 * t, 16 * j, acc);
+            put16(Xs[w], 0, 0, acc, 1.0, false);
+            d4 acc2 = {0.0, 0.0, 0.0, 0.0};
+            acc2 = mfma16_nn(Li, 16 * i, 16 * i, Xs[w], 0, 0, acc2);
+            put16(Li, 16 * i, 16 * j, acc2, -1.0, false);
+        }
+        MARK(13 + i);
+    }
+    for (int q = tid; q < NB * NB; q += blockDim.x) {
+        const int r = q >> 6, c = q & 63;
+        if (c > r) As[r * LP + c] = 0.0;
+    }
+    MARK(17);
+}
+
+__global__ __launch_bounds__(256) void k_crf_dbg(double *S, long long lds, double *linv,
+                                                 double *crL, const double *rhs, double *y,
+                                                 unsigned long long *out)
+{
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double *As = sm, *Bs = sm + NB * LP, *Cs = sm + 2 * NB * LP;
+    __shared__ double rk[NB];
+    __shared__ double part[4][NB];
+    __shared__ unsigned long long ts[32];
+    const int tid = threadIdx.x;
+    const int e = 1, p = 0, q = 2, nt = 3;
+    MARK(0);
+    load_tile(S, lds, e, e, As);
+    if (tid < NB) rk[tid] = rhs[(long long)NB * e + tid];
+    MARK(18);
+    bpi_dbg(As, Bs, ts);
+    gemv64(Bs, rk, part, y + (long long)NB * e, 1.0);
+    MARK(19);
+    store_rowmajor(linv + (long long)NB * NB * e, Bs);
+    MARK(20);
+    d4 acc[2][2];
+    load_tile_t(S, lds, e, p, Cs);
+    MARK(21);
+    mfma_64x64(Cs, Bs, acc);
+    MARK(22);
+    acc_to_lds(acc, Cs, 1.0, false);
+    MARK(23);
+    store_rowmajor(crL + (long long)NB * NB * e, Cs);
+    MARK(24);
+    load_tile(S, lds, q, e, Cs);
+    __syncthreads();
+    mfma_64x64(Cs, Bs, acc);
+    __syncthreads();
+    acc_to_lds(acc, Cs, 1.0, false);
+    __syncthreads();
+    store_rowmajor(crL + (long long)NB * NB * (nt + e), Cs);
+    MARK(25);
+    if (tid == 0)
+        for (int i = 0; i < 26; i++) out[i] = ts[i];
+}
+
+int main()
+{
+    const int n = 192;
+    std::vector<double> M((size_t)n * n), h((size_t)n * n);
+    srand(1);
+    for (auto &v : M) v = (rand() / (double)RAND_MAX) - 0.5;
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            double s = (i == j) ? n : 0.0;
+            for (int k = 0; k < n; k++) s += M[i * n + k] * M[j * n + k];
+            h[i + (size_t)n * j] = s;
+        }
+    double *S, *linv, *crL, *rhs, *y;
+    unsigned long long *out;
+    hipMalloc(&S, sizeof(double) * n * n);
+    hipMalloc(&linv, sizeof(double) * 3 * 64 * 64);
+    hipMalloc(&crL, sizeof(double) * 6 * 64 * 64);
+    hipMalloc(&rhs, sizeof(double) * n);
+    hipMalloc(&y, sizeof(double) * n);
+    hipMalloc(&out, sizeof(unsigned long long) * 32);
+    hipMemcpy(S, h.data(), sizeof(double) * n * n, hipMemcpyHostToDevice);
+    hipMemset(rhs, 0, sizeof(double) * n);
+    const size_t smem3 = sizeof(double) * 3 * NB * LP;
+    hipFuncSetAttribute((const void *)k_crf_dbg, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)smem3);
+    unsigned long long ho[32];
+    for (int it = 0; it < 3; it++) {
+        k_crf_dbg<<<1, 256, smem3>>>(S, n, linv, crL, rhs, y, out);
+        hipMemcpy(ho, out, sizeof(unsigned long long) * 26, hipMemcpyDeviceToHost);
+    }
+    const char *nm[26] = {"start", "zeroLi", "f16_0", "pan_0", "trail_0", "f16_1", "pan_1",
+                          "trail_1", "f16_2", "pan_2", "trail_2", "f16_3", "pan_3", "trail_3",
+                          "inv_1", "inv_2", "inv_3", "zeroU", "load", "gemv", "store_linv",
+                          "load_t", "mfma", "acc_lds", "store_crL", "panel_q"};
+    const int order[26] = {0, 18, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17,
+                           19, 20, 21, 22, 23, 24, 25};
+    for (int k = 1; k < 26; k++)
+        printf("%-11s %8llu\n", nm[order[k]], ho[order[k]] - ho[order[k - 1]]);
+    printf("total      %8llu cycles\n", ho[25] - ho[0]);
+    return 0;
+}
