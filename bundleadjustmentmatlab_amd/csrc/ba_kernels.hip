@@ -967,22 +967,26 @@ __global__ __launch_bounds__(256) void k_point_vinv(const double *__restrict__ V
 // Schur complement on fp64 MFMA, operands register-resident (default fast
 // path when every track fits).  A chunk holds <= BA_MF_PTS = 4 x 5 consecutive
 // points seeing <= BA_MF_CMAX cameras; wave w owns the chunk's points
-// 5w .. 5w + 4, i.e. rows k = 3 p' + q (p' < 5, q < 3; row 15 zero) of the
-// 16-row K-block w of the dense chunk slabs
-//     Wk[k][NA cs + r] = W_o[r][q],   Yk = D Wk,   D[3p'+q][3p'+t] = V*^-1_p[t][q]
-// (o = observation of point p in camera slot cs, cameras ascending; zero where
-// p does not see cs).  Yk holds Y_o = W_o V*^-1_p (bundle_euclid.m:182).
-// Per 4-row K step s the lane (li = l & 15, lk = l >> 4) holds the B fragment
-// Wk[4s + lk][16 t + li] of every column tile t (gathered straight from the
-// point-major W in HBM) and the A fragment D[li][4s + lk]; then
-//     Y tile t   = sum_s mfma(D frag s, W frag s t)         (K = 16)
-//     S(ti, tj) += sum_s mfma(Y tile ti reg s, W frag s tj)  (lower tiles)
-// The Y accumulator's register s IS the A fragment of K step s
-// (v_mfma_f64_16x16x4f64: C row = lk + 4 reg, col = li; A lane = [li][lk]),
-// so Y never leaves the registers and no LDS or barrier is needed per chunk.
+// 5w .. 5w + 4.  With the dense chunk slabs
+//     Wk[k][NA cs + r] = W_o[r][q],   Yk[k][NA cs + r] = Y_o[r][q],
+// Y_o = W_o V*^-1_p (bundle_euclid.m:182; o = observation of point p in camera
+// slot cs, cameras ascending; zero where p does not see cs), the wave's 16 K
+// rows k = (point, component) are laid out per 4-row MFMA K step s and lane
+// quarter lk (li = l & 15, lk = l >> 4) as
+//     s = 0, 1, 2 : point 5w + lk, component q = s
+//     s = 3       : point 5w + 4,  component q = lk  (lk = 3: zero row)
+// so that for s < 3 a lane holds all three components of ITS point: it forms
+//     Yk[(lk, s)][16 t + li] = sum_u Wk[(lk, u)][16 t + li] V*^-1[u][s]
+// on the VALU from its own W fragments, and for s = 3 one MFMA per column tile
+// (A = V*^-1 of point 5w + 4 in rows 0..2, B = its W fragment) leaves Y in
+// register 0 in exactly the A-fragment layout.  Then
+//     S(ti, tj) += sum_s mfma(Yk frag s ti, Wk frag s tj)   (lower tiles)
+// (v_mfma_f64_16x16x4f64: A lane = [li][lk], B lane = [lk][li], C row =
+// lk + 4 reg, col = li), i.e.
 //     S_chunk[NA cs_j + r][NA cs_k + c] = sum_i Y_ij[r] . W_ik[c]
 // over the chunk's points (mex_bundle_2_Se_.c:80-118; the pairs a point does
 // not see add exact zeros); e_ partials sum_k Yk[k][.] eB[k] (:132-155).
+// Y costs 3 MFMAs per chunk and wave (12 when it was D Wk on the matrix pipe).
 // Consecutive chunks with one camera list (a run of video-like tracks) keep
 // accumulating in the registers; at a change of cameras ("flush") the four
 // waves add their sums of each lower entry of each co-visible block to the
@@ -1025,22 +1029,25 @@ __global__ __launch_bounds__(256, (NA == 6) ? 2 : 1) void k_schur_mfma(
     // lane constants: K rows of its fragments, slab columns of its tiles
     int kp[4], kq[4], ccs[RT], crr[RT];
 #pragma unroll
-    for (int s = 0; s < 4; s++) {
-        const int k = 4 * s + lk;
-        kp[s] = k < 3 * BA_MF_KB ? k / 3 : -1;
-        kq[s] = k % 3;
+    for (int s = 0; s < 3; s++) {
+        kp[s] = lk;
+        kq[s] = s;
     }
+    kp[3] = lk < 3 ? 4 : -1;
+    kq[3] = lk < 3 ? lk : 0;
 #pragma unroll
     for (int t = 0; t < RT; t++) {
         ccs[t] = (16 * t + li) / NA;
         crr[t] = (16 * t + li) % NA;
     }
-    const int dp = li < 3 * BA_MF_KB ? li / 3 : -2, dq = li % 3;
     // fragments of one chunk, unconditional loads from clamped addresses
     // Absent entries read the exact zeros of the row past the end of W / V*^-1 /
     // eB (no select after a load: its wait lands at the MFMA that consumes it);
     // addresses are a uniform chunk base plus a 32-bit lane offset.
-    auto load = [&](int k, double (&wf)[4][RT], double (&df)[4], double (&ef)[4]) {
+    // vf: V*^-1 of point 5w + lk, entries (0,0) (1,0) (2,0) (1,1) (2,1) (2,2)
+    // (symmetric); vf[6]: the s = 3 Y MFMA's A fragment V*^-1[lk][li] of point
+    // 5w + 4 (zero outside rows li < 3, K lk < 3)
+    auto load = [&](int k, double (&wf)[4][RT], double (&vf)[7], double (&ef)[4]) {
         const unsigned *r = rec + gbo[k];
         const int np = gp0[k + 1] - gp0[k], i0 = gp0[k], ob = gob[k];
         const int C = (int)(r[1] & 0xffu);
@@ -1059,9 +1066,19 @@ __global__ __launch_bounds__(256, (NA == 6) ? 2 : 1) void k_schur_mfma(
                 const int idx = cv ? (int)tab[p * C + ccs[t]] : 0xff;
                 wf[s][t] = wbase[idx != 0xff ? WS * idx + crr[t] + NA * kq[s] : wz];
             }
-            const bool dv = pv && kp[s] == dp;
-            df[s] = vbase[dv ? 9 * p + kq[s] + 3 * dq : vz];
             ef[s] = ebase[pv ? 3 * p + kq[s] : ez];
+        }
+        {
+            const int p = BA_MF_KB * wv + lk;
+            const bool pv = p < np;
+#pragma unroll
+            for (int u = 0; u < 6; u++) {
+                constexpr int off[6] = {0, 1, 2, 4, 5, 8};
+                vf[u] = vbase[pv ? 9 * p + off[u] : vz];
+            }
+            const int p4 = BA_MF_KB * wv + 4;
+            const bool dv = p4 < np && li < 3 && lk < 3;
+            vf[6] = vbase[dv ? 9 * p4 + lk + 3 * li : vz];
         }
     };
     d4 accS[NTL];
@@ -1071,7 +1088,7 @@ __global__ __launch_bounds__(256, (NA == 6) ? 2 : 1) void k_schur_mfma(
 #pragma unroll
     for (int t = 0; t < RT; t++) eacc[t] = 0.0;
     // one chunk: Y tiles, e_ sums, lower S tiles; flush at a change of cameras
-    auto process = [&](int k, const double (&wc)[4][RT], const double (&dc)[4],
+    auto process = [&](int k, const double (&wc)[4][RT], const double (&vc)[7],
                        const double (&ec)[4]) {
         const unsigned *r = rec + gbo[k];
         const unsigned h1 = r[1];
@@ -1081,19 +1098,28 @@ __global__ __launch_bounds__(256, (NA == 6) ? 2 : 1) void k_schur_mfma(
         // past the chunk's columns multiply exact zeros): no branch between the
         // next chunk's loads and the MFMAs, so their waits stay precise
         (void)nt;
+        // s = 3 first, all column tiles: point 5w + 4 on the matrix pipe
+        // (register 0 = A fragment), in flight while the VALU forms the rest
+        double y4[RT];
+#pragma unroll
+        for (int ti = 0; ti < RT; ti++)
+            y4[ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(vc[6], wc[3][ti],
+                                                          d4{0.0, 0.0, 0.0, 0.0}, 0, 0, 0)[0];
 #pragma unroll
         for (int ti = 0; ti < RT; ti++) {
             {
-                d4 y = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                for (int s = 0; s < 4; s++)
-                    y = __builtin_amdgcn_mfma_f64_16x16x4f64(dc[s], wc[s][ti], y, 0, 0, 0);
+                double y[4];
+                y[3] = y4[ti];
+                // s < 3: Y_o[r][s] = sum_u W_o[r][u] V*^-1[u][s], the lane's own point
+                y[0] = fma(wc[2][ti], vc[2], fma(wc[1][ti], vc[1], wc[0][ti] * vc[0]));
+                y[1] = fma(wc[2][ti], vc[4], fma(wc[1][ti], vc[3], wc[0][ti] * vc[1]));
+                y[2] = fma(wc[2][ti], vc[5], fma(wc[1][ti], vc[4], wc[0][ti] * vc[2]));
                 eacc[ti] = fma(y[3], ec[3], fma(y[2], ec[2], fma(y[1], ec[1],
                                                                  fma(y[0], ec[0], eacc[ti]))));
 #pragma unroll
-                for (int tj = 0; tj <= ti; tj++) {
+                for (int s = 0; s < 4; s++) {   // K step outer: neighbours independent
 #pragma unroll
-                    for (int s = 0; s < 4; s++)
+                    for (int tj = 0; tj <= ti; tj++)
                         accS[ti * (ti + 1) / 2 + tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(
                             y[s], wc[s][tj], accS[ti * (ti + 1) / 2 + tj], 0, 0, 0);
                 }
@@ -1149,7 +1175,7 @@ __global__ __launch_bounds__(256, (NA == 6) ? 2 : 1) void k_schur_mfma(
     };
     // two register sets, software pipelined: the next chunk's fragments are in
     // flight while this chunk's MFMAs run (no register copies between sets)
-    double wa[4][RT], da[4], ea[4], wb[4][RT], db[4], eb[4];
+    double wa[4][RT], da[7], ea[4], wb[4][RT], db[7], eb[4];
     load(0, wa, da, ea);
     for (int k = 0; k < nc; k += 2) {
         load(min(k + 1, nc - 1), wb, db, eb);   // unconditional: a clamped reload at the end

@@ -111,6 +111,81 @@ __global__ __launch_bounds__(256) void k_crf_dbg(double *S, long long lds, doubl
         for (int i = 0; i < 26; i++) out[i] = ts[i];
 }
 
+
+// current wave_factor16 with stamps: [0] LDS read, [1] pivot loop, [2] L write, [3] inverse, [4] Li write
+__device__ void wf16_dbg(double *As, double *Bs, int o, unsigned long long *tw)
+{
+    const int r = threadIdx.x & 63;
+    double d[16], rd[16];
+    unsigned long long t0 = stamp();
+#pragma unroll
+    for (int c = 0; c < 16; c++) d[c] = (r < 16) ? As[(o + r) * LP + o + c] : 0.0;
+    asm volatile("" ::"v"(d[0]), "v"(d[15]));
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    unsigned long long t1 = stamp();
+    auto rsq = [&](double piv) {
+        if (!(piv > 0.0)) piv = 1.0;
+        double y = __builtin_amdgcn_rsq(piv);
+        const double hp = 0.5 * piv;
+        y = y * fma(-hp * y, y, 1.5);
+        y = y * fma(-hp * y, y, 1.5);
+        return y;
+    };
+    double pv = rdlane(d[0], 0);
+    double y = rsq(pv);
+#pragma unroll
+    for (int c = 0; c < 16; c++) {
+        rd[c] = y;
+        d[c] = (r == c) ? pv * y : ((r > c) ? d[c] * y : 0.0);
+        if (c + 1 < 16) {
+            d[c + 1] = fma(-d[c], rowbcast(d[c], c + 1), d[c + 1]);
+            pv = rdlane(d[c + 1], c + 1);
+            y = rsq(pv);
+        }
+#pragma unroll
+        for (int q = c + 2; q < 16; q++) d[q] = fma(-d[c], rowbcast(d[c], q), d[q]);
+    }
+    asm volatile("" ::"v"(d[15]), "v"(d[0]), "v"(d[7]));
+    unsigned long long t2 = stamp();
+    if (r < 16) {
+#pragma unroll
+        for (int c = 0; c < 16; c++) As[(o + r) * LP + o + c] = (c <= r) ? d[c] : 0.0;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    unsigned long long t3 = stamp();
+    double x[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) x[q] = (q == r) ? 1.0 : 0.0;
+#pragma unroll
+    for (int t = 0; t < 16; t++) {
+        x[t] = x[t] * rd[t];
+#pragma unroll
+        for (int q = t + 1; q < 16; q++) x[q] = fma(-As[(o + q) * LP + o + t], x[t], x[q]);
+    }
+    asm volatile("" ::"v"(x[15]), "v"(x[0]));
+    unsigned long long t4 = stamp();
+    if (r < 16) {
+#pragma unroll
+        for (int c = 0; c < 16; c++) Bs[(o + c) * LP + o + r] = x[c];
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    unsigned long long t5 = stamp();
+    tw[0] = t1 - t0; tw[1] = t2 - t1; tw[2] = t3 - t2; tw[3] = t4 - t3; tw[4] = t5 - t4;
+}
+
+__global__ __launch_bounds__(256) void k_wf_dbg(const double *S, long long lds, unsigned long long *out)
+{
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double *As = sm, *Bs = sm + NB * LP;
+    load_tile(S, lds, 0, 0, As);
+    __syncthreads();
+    unsigned long long tw[5];
+    if (threadIdx.x < 64) wf16_dbg(As, Bs, 0, tw);
+    if (threadIdx.x == 0)
+        for (int q = 0; q < 5; q++) out[q] = tw[q];
+}
+
 int main()
 {
     const int n = 192;
@@ -150,5 +225,13 @@ int main()
     for (int k = 1; k < 26; k++)
         printf("%-11s %8llu\n", nm[order[k]], ho[order[k]] - ho[order[k - 1]]);
     printf("total      %8llu cycles\n", ho[25] - ho[0]);
+    hipFuncSetAttribute((const void *)k_wf_dbg, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)smem3);
+    for (int it = 0; it < 3; it++) {
+        k_wf_dbg<<<1, 256, smem3>>>(S, n, out);
+        hipMemcpy(ho, out, sizeof(unsigned long long) * 5, hipMemcpyDeviceToHost);
+    }
+    printf("wave_factor16: lds read %llu  pivot loop %llu  L write %llu  inverse %llu  Li write %llu\n",
+           ho[0], ho[1], ho[2], ho[3], ho[4]);
     return 0;
 }
