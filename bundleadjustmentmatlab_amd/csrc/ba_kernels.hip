@@ -1027,14 +1027,7 @@ __global__ __launch_bounds__(256, (NA == 6) ? 2 : 1) void k_schur_mfma(
     }
     __syncthreads();
     // lane constants: K rows of its fragments, slab columns of its tiles
-    int kp[4], kq[4], ccs[RT], crr[RT];
-#pragma unroll
-    for (int s = 0; s < 3; s++) {
-        kp[s] = lk;
-        kq[s] = s;
-    }
-    kp[3] = lk < 3 ? 4 : -1;
-    kq[3] = lk < 3 ? lk : 0;
+    int ccs[RT], crr[RT];
 #pragma unroll
     for (int t = 0; t < RT; t++) {
         ccs[t] = (16 * t + li) / NA;
@@ -1056,27 +1049,32 @@ __global__ __launch_bounds__(256, (NA == 6) ? 2 : 1) void k_schur_mfma(
         const double *vbase = Vinv + 9 * (size_t)i0;
         const double *ebase = eB + 3 * (size_t)i0;
         const int wz = WS * (nobs_all - ob), vz = 9 * (n_all - i0), ez = 3 * (n_all - i0);
+        // one lane offset per (point, column tile) -- the zero row's when absent;
+        // the components are immediate offsets from it (zero row: 3 NA doubles)
+        const int pA = BA_MF_KB * wv + lk, p4 = BA_MF_KB * wv + 4;
+        const bool pvA = pA < np, pv4 = lk < 3 && p4 < np;
 #pragma unroll
-        for (int s = 0; s < 4; s++) {
-            const int p = BA_MF_KB * wv + kp[s];
-            const bool pv = kp[s] >= 0 && p < np;
+        for (int t = 0; t < RT; t++) {
+            const bool cvA = pvA && ccs[t] < C, cv4 = pv4 && ccs[t] < C;
+            const int iA = tab[cvA ? pA * C + ccs[t] : 0];   // clamped read, no branch
+            const int i4 = tab[cv4 ? p4 * C + ccs[t] : 0];
+            const int oA = (cvA && iA != 0xff ? WS * iA : wz) + crr[t];
+            const int o4 = (cv4 && i4 != 0xff ? WS * i4 + NA * lk : wz) + crr[t];
 #pragma unroll
-            for (int t = 0; t < RT; t++) {
-                const bool cv = pv && ccs[t] < C;
-                const int idx = cv ? (int)tab[p * C + ccs[t]] : 0xff;
-                wf[s][t] = wbase[idx != 0xff ? WS * idx + crr[t] + NA * kq[s] : wz];
-            }
-            ef[s] = ebase[pv ? 3 * p + kq[s] : ez];
+            for (int s = 0; s < 3; s++) wf[s][t] = wbase[oA + NA * s];
+            wf[3][t] = wbase[o4];
         }
         {
-            const int p = BA_MF_KB * wv + lk;
-            const bool pv = p < np;
+            const int oe = pvA ? 3 * pA : ez;
+#pragma unroll
+            for (int s = 0; s < 3; s++) ef[s] = ebase[oe + s];
+            ef[3] = ebase[pv4 ? 3 * p4 + lk : ez];
+            const int ov = pvA ? 9 * pA : vz;
 #pragma unroll
             for (int u = 0; u < 6; u++) {
                 constexpr int off[6] = {0, 1, 2, 4, 5, 8};
-                vf[u] = vbase[pv ? 9 * p + off[u] : vz];
+                vf[u] = vbase[ov + off[u]];
             }
-            const int p4 = BA_MF_KB * wv + 4;
             const bool dv = p4 < np && li < 3 && lk < 3;
             vf[6] = vbase[dv ? 9 * p4 + lk + 3 * li : vz];
         }
