@@ -319,9 +319,8 @@ __device__ __forceinline__ bool wave_factor16(double *As, double *Bs, int o)
 #pragma unroll
         for (int c = 0; c < 16; c++) As[(o + r) * LP + o + c] = (c <= r) ? d[c] : 0.0;
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed
-    __builtin_amdgcn_wave_barrier();
-    // column r of the inverse, right-looking: x_t /= L_tt, x_q -= L_qt x_t
+    // column r of the inverse, right-looking: x_t /= L_tt, x_q -= L_qt x_t, with
+    // L_qt = lane q's d[t] broadcast by DPP (no LDS round trip)
     double x[16];
 #pragma unroll
     for (int q = 0; q < 16; q++) x[q] = (q == r) ? 1.0 : 0.0;
@@ -329,7 +328,7 @@ __device__ __forceinline__ bool wave_factor16(double *As, double *Bs, int o)
     for (int t = 0; t < 16; t++) {
         x[t] = x[t] * rd[t];
 #pragma unroll
-        for (int q = t + 1; q < 16; q++) x[q] = fma(-As[(o + q) * LP + o + t], x[t], x[q]);
+        for (int q = t + 1; q < 16; q++) x[q] = fma(-rowbcast(d[t], q), x[t], x[q]);
     }
     if (r < 16) {
 #pragma unroll

@@ -161,7 +161,7 @@ __device__ void wf16_dbg(double *As, double *Bs, int o, unsigned long long *tw)
     for (int t = 0; t < 16; t++) {
         x[t] = x[t] * rd[t];
 #pragma unroll
-        for (int q = t + 1; q < 16; q++) x[q] = fma(-As[(o + q) * LP + o + t], x[t], x[q]);
+        for (int q = t + 1; q < 16; q++) x[q] = fma(-rowbcast(d[t], q), x[t], x[q]);
     }
     asm volatile("" ::"v"(x[15]), "v"(x[0]));
     unsigned long long t4 = stamp();
