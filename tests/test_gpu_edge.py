@@ -1,0 +1,118 @@
+"""GPU edge cases of one LM pass vs the oracle restatement: ragged and
+degenerate observation structures the reference handles through its general
+code path (bundle_euclid.m + mex_bundle_1/2/3):
+
+* a camera that sees no point (its U / W / eA are exact zeros, so S has exactly
+  zero rows and the pinv rule of App. A Q2/Q8 applies);
+* a point that no camera sees (V = 0 -> pinv3(0) = 0, db = 0) and points seen
+  by a single camera;
+* a track longer than the chunk caps (falls back to the ordered kernels) and
+  tracks longer than the MFMA Schur camera cap (the per-term Schur kernel);
+* the smallest problem (two cameras, one point).
+
+Tolerances as tests/test_gpu_parity.py::test_single_pass_config2: the
+linearisation SSE to summation order (1e-12), the post-step SSE within 1e-7
+relative of the oracle's LAPACK-Cholesky step (+ 1e-10 of the linearisation
+SSE, for the near-exact fit of the two-camera case).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _scene(m, n, seed):
+    from bundleadjustmentmatlab_amd.scene import make_config
+    return make_config("cfg2", m=m, n=n, seed=seed)
+
+
+def _pass_vs_oracle(gpu, oracle, m, n, pt, cam, ox, K, a, b, num_a=6, lam=1e-3):
+    pb = oracle.SparseProblem(m, n, pt, cam, ox, K)
+    L = oracle.sp_linearize(pb, a, b, num_a)
+    Us = L["U"].copy(order="F")
+    for k in range(num_a):
+        Us[k, k] = (1 + lam) * L["U"][k, k]
+    Vs = L["V"].copy(order="F")
+    for k in range(3):
+        Vs[k, k] = (1 + lam) * L["V"][k, k]
+    Vinv = oracle.pinv3_formula(Vs)
+    Y = oracle.sp_y(pb, L["W"], Vinv, num_a)
+    S, e_ = oracle.sp_schur(pb, Y, L["W"], Us, L["eA"], L["eB"], num_a)
+    da = oracle.chol_solve_fixed(S, e_)
+    db, a_new, b_new, xh, sse = oracle.sp_update(pb, L["W"], da, L["eB"], Vinv, a, b, num_a)
+    old = float(L["e"].reshape(-1) @ L["e"].reshape(-1))
+    ba = gpu.BundleAdjuster(K, pt, cam, ox, n, num_a)
+    ba.set_params(a, b)
+    info = ba.step(relinearize=True, update_lm=False)
+    plan = ba.plan_info()
+    ba.close()
+    assert info.chol_failed == 0
+    assert abs(info.old_sse - old) <= 1e-12 * old, (info.old_sse, old)
+    # near-exact fits (the two-camera case) leave a tiny post-step SSE: the
+    # step's rounding is then judged against the linearisation SSE
+    assert abs(info.new_sse - sse) <= 1e-7 * sse + 1e-10 * old, (info.new_sse, sse)
+    return plan, da
+
+
+def _params(sc):
+    a = np.zeros((6, sc.m), order="F")
+    a[0:3], a[3:6] = sc.w0, sc.T0
+    return a, np.asfortranarray(sc.X0[:3])
+
+
+def test_camera_without_observations(gpu, oracle):
+    sc = _scene(12, 400, seed=3)
+    keep = sc.obs_cam != 5
+    pt, cam, ox = sc.obs_pt[keep], sc.obs_cam[keep], sc.obs_x[keep]
+    a, b = _params(sc)
+    _, da = _pass_vs_oracle(gpu, oracle, sc.m, sc.n, pt, cam, ox, sc.K, a, b)
+    assert np.all(da[6 * 5:6 * 6] == 0.0)       # the unseen camera does not move
+
+
+def test_unseen_and_single_view_points(gpu, oracle):
+    sc = _scene(10, 300, seed=4)
+    # drop every observation of points 0..9 and all but the first of points 10..59
+    first = np.r_[True, sc.obs_pt[1:] != sc.obs_pt[:-1]]
+    keep = ~(sc.obs_pt < 10) & ~((sc.obs_pt >= 10) & (sc.obs_pt < 60) & ~first)
+    pt, cam, ox = sc.obs_pt[keep], sc.obs_cam[keep], sc.obs_x[keep]
+    assert np.bincount(pt, minlength=sc.n)[:10].sum() == 0
+    assert np.all(np.bincount(pt, minlength=sc.n)[10:60] == 1)
+    a, b = _params(sc)
+    _pass_vs_oracle(gpu, oracle, sc.m, sc.n, pt, cam, ox, sc.K, a, b)
+
+
+def test_track_longer_than_chunk_cap(gpu, oracle):
+    """One point seen by all 140 cameras (> 128 observations in one chunk): the
+    plan falls back to the ordered kernels; result unchanged."""
+    sc = _scene(140, 2000, seed=5)
+    a, b = _params(sc)
+    # point 0 observed in every camera: project it with the true cameras
+    from bundleadjustmentmatlab_amd.scene import project
+    allc = np.arange(sc.m)
+    extra, z = project(sc.K, sc.w, sc.T, sc.X, allc, np.zeros(sc.m, dtype=int))
+    assert np.all(z > 0)
+    keep = sc.obs_pt != 0
+    pt = np.r_[np.zeros(sc.m, int), sc.obs_pt[keep]].astype(np.int32)
+    cam = np.r_[allc, sc.obs_cam[keep]].astype(np.int32)
+    ox = np.r_[np.asarray(extra).reshape(sc.m, 2), sc.obs_x[keep]]
+    order = np.lexsort((cam, pt))
+    pt, cam, ox = pt[order], cam[order], ox[order]
+    plan, _ = _pass_vs_oracle(gpu, oracle, sc.m, sc.n, pt, cam, ox, sc.K, a, b)
+    assert plan["ordered"] == 1
+
+
+def test_tracks_longer_than_mfma_cap(gpu, oracle):
+    """Points seen by 10 cameras (> 8 = the MFMA Schur chunk's camera cap for
+    num_a = 6): the per-term Schur kernel runs; result unchanged."""
+    from bundleadjustmentmatlab_amd.scene import make_config
+    sc = make_config("cfg3", m=40, n=2000, seed=6, track=10)
+    a, b = _params(sc)
+    plan, _ = _pass_vs_oracle(gpu, oracle, sc.m, sc.n, sc.obs_pt, sc.obs_cam, sc.obs_x,
+                              sc.K, a, b)
+    assert plan["mfma"] == 0 and plan["ordered"] == 0
+
+
+def test_two_cameras_one_point(gpu, oracle):
+    sc = _scene(2, 1, seed=7)
+    a, b = _params(sc)
+    _pass_vs_oracle(gpu, oracle, sc.m, sc.n, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.K, a, b)
