@@ -150,6 +150,12 @@ struct ba_dev {
     double scal_host[8];
     struct ba_ktimer *kt;   // NULL unless kernel timing is enabled
     hipStream_t stream;
+    // second stream: the camera reduction runs there, concurrently with V*^-1
+    // and the Schur chunks, when the pass is single-rank and untimed;
+    // k_schur_reduce (the first consumer of U / eA) waits for ev_join
+    hipStream_t side;
+    hipEvent_t ev_fork, ev_join;
+    int join_pending;
 };
 
 #define KT_B(d) \

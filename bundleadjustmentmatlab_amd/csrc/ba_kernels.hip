@@ -1637,6 +1637,10 @@ static int launch_schur_fast(ba_dev *d, double lambda)
     KT_E(d, KT_SCHUR_CHUNK);
     }
     const int bs = ((NA * NA + NA) + 63) / 64 * 64;
+    if (d->join_pending) {   // U / eA from the side stream's camera reduction
+        VLGBA_CHECK(hipStreamWaitEvent(d->stream, d->ev_join, 0));
+        d->join_pending = 0;
+    }
     KT_B(d);
     k_schur_reduce<NA><<<d->nb, bs, 0, d->stream>>>(
         d->blk_jk, d->blk_gptr, d->blk_gslots, d->cam_gptr, d->cam_gslots, d->spart, d->epart,

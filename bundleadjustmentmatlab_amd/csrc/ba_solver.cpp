@@ -572,6 +572,9 @@ static void ctx_free(vlgba_ctx *c)
     ba_chol_free(&c->d);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->d.stream) (void)hipStreamDestroy(c->d.stream);
+    if (c->d.side) (void)hipStreamDestroy(c->d.side);
+    if (c->d.ev_fork) (void)hipEventDestroy(c->d.ev_fork);
+    if (c->d.ev_join) (void)hipEventDestroy(c->d.ev_join);
     delete c;
 }
 
@@ -819,7 +822,10 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
     int rc = 0;
     do {
         if (hipSetDevice(o->device) != hipSuccess) { rc = VLGBA_E_ARG; break; }
-        if (hipStreamCreateWithFlags(&c->d.stream, hipStreamNonBlocking) != hipSuccess) {
+        if (hipStreamCreateWithFlags(&c->d.stream, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&c->d.side, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&c->d.ev_fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->d.ev_join, hipEventDisableTiming) != hipSuccess) {
             rc = -1;
             break;
         }
@@ -915,7 +921,22 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
         // accepted step swaps in the one k_camera_update built for a_new
         TRY(ba_launch_linearize(&d, c->flags));
         mark(c, 1);
-        TRY(ba_launch_camera_reduce(&d, c->flags));
+        if (!d.ordered && c->world == 1 && !c->timing) {
+            // U / eA / old SSE on the side stream, overlapping V*^-1 and the
+            // Schur chunks (no collective in between at world size 1);
+            // launch_schur_fast joins before k_schur_reduce
+            VLGBA_CHECK(hipEventRecord(d.ev_fork, d.stream));
+            VLGBA_CHECK(hipStreamWaitEvent(d.side, d.ev_fork, 0));
+            hipStream_t s0 = d.stream;
+            d.stream = d.side;
+            const int rc = ba_launch_camera_reduce(&d, c->flags);
+            d.stream = s0;
+            TRY(rc);
+            VLGBA_CHECK(hipEventRecord(d.ev_join, d.side));
+            d.join_pending = 1;
+        } else {
+            TRY(ba_launch_camera_reduce(&d, c->flags));
+        }
         // U | eA | old_sse travel in one all-reduce (the fast path's reduce
         // kernel writes the old_sse slot itself)
         if (d.ordered)
