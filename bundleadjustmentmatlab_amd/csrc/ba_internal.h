@@ -156,6 +156,12 @@ struct ba_dev {
     hipStream_t side;
     hipEvent_t ev_fork, ev_join;
     int join_pending;
+    // host-mapped pass results: [0..4] the scal slots, [7] the pass sequence
+    // number written last (k_publish); the host spins on it instead of a
+    // device-to-host copy + stream synchronisation
+    volatile double *hres;     // host view
+    double *hres_dev;          // device view
+    unsigned long long seq;
 };
 
 #define KT_B(d) \
@@ -188,6 +194,7 @@ int ba_launch_schur(ba_dev *d, double lambda);
 int ba_launch_assemble(ba_dev *d);
 int ba_launch_update(ba_dev *d, double lambda);
 int ba_launch_yeb(ba_dev *d);
+int ba_launch_publish(ba_dev *d);   // scal[0..4] + ++seq -> hres (host-mapped)
 int ba_launch_schur_fast(ba_dev *d, double lambda);   // fused damp + Vinv + Y + S + e_
 int ba_launch_assemble_plain(ba_dev *d, double *S, long long ld);
 // ---- ba_chol.hip ----

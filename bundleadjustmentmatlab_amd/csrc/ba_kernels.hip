@@ -1660,6 +1660,26 @@ int ba_launch_schur_fast(ba_dev *d, double lambda)
     }
 }
 
+// the pass's scalars to host-mapped memory, the sequence number after them
+// (system-scope release): the host reads them without a copy or a stream sync
+__global__ void k_publish(const double *__restrict__ scal, double *hres, double seq)
+{
+    if (threadIdx.x < 5) hres[threadIdx.x] = scal[threadIdx.x];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __atomic_store_n((unsigned long long *)(hres + 7), __double_as_longlong(seq),
+                         __ATOMIC_RELEASE);
+    }
+}
+
+int ba_launch_publish(ba_dev *d)
+{
+    d->seq++;
+    k_publish<<<1, 64, 0, d->stream>>>(d->scal, d->hres_dev, (double)d->seq);
+    return -(int)hipGetLastError();
+}
+
 int ba_launch_yeb(ba_dev *d)
 {
     const int g = grid_for(d->n, 256, 1 << 30);

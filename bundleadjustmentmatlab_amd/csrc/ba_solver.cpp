@@ -19,10 +19,12 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <numeric>
 #include <vector>
@@ -536,6 +538,13 @@ void kt_end(ba_ktimer *t, hipStream_t s, int kid)
 }
 
 // =========================================================================
+struct ba_aux {
+    int device;
+    hipStream_t stream, side;
+    hipEvent_t ev_fork, ev_join;
+    double *hres_host, *hres_dev;
+};
+
 struct vlgba_ctx {
     ba_dev d;
     ba_flags flags;
@@ -556,12 +565,64 @@ struct vlgba_ctx {
     double phase_ms[7] = {};
     std::vector<void *> allocs;
     std::vector<double> hb_tmp;   // host staging for b gather
+    ba_aux aux;                   // streams / events / host result block (pooled)
+    bool has_aux = false;
 };
+
+// Per-device pool of the context's streams, fork/join events and host-mapped
+// result block: creating them (pinned host memory above all) costs ~0.4 ms,
+// which the growing-BA replay would pay per solve.  A context takes one set
+// for its lifetime and returns it idle (both streams synchronised).
+static std::mutex g_aux_mu;
+static std::vector<ba_aux> g_aux_pool;
+
+static int aux_acquire(int device, ba_aux &a)
+{
+    {
+        std::lock_guard<std::mutex> lk(g_aux_mu);
+        for (size_t q = 0; q < g_aux_pool.size(); q++)
+            if (g_aux_pool[q].device == device) {
+                a = g_aux_pool[q];
+                g_aux_pool.erase(g_aux_pool.begin() + (long)q);
+                a.hres_host[7] = 0.0;   // sequence numbers restart at 1
+                return 0;
+            }
+    }
+    std::memset(&a, 0, sizeof a);
+    a.device = device;
+    void *h = nullptr;
+    if (hipStreamCreateWithFlags(&a.stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&a.side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&a.ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&a.ev_join, hipEventDisableTiming) != hipSuccess ||
+        hipHostMalloc(&h, 8 * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess ||
+        hipHostGetDevicePointer((void **)&a.hres_dev, h, 0) != hipSuccess) {
+        if (a.stream) (void)hipStreamDestroy(a.stream);
+        if (a.side) (void)hipStreamDestroy(a.side);
+        if (a.ev_fork) (void)hipEventDestroy(a.ev_fork);
+        if (a.ev_join) (void)hipEventDestroy(a.ev_join);
+        if (h) (void)hipHostFree(h);
+        return -1;
+    }
+    std::memset(h, 0, 8 * sizeof(double));
+    a.hres_host = (double *)h;
+    return 0;
+}
+
+static void aux_release(const ba_aux &a)
+{
+    (void)hipStreamSynchronize(a.stream);
+    (void)hipStreamSynchronize(a.side);
+    std::lock_guard<std::mutex> lk(g_aux_mu);
+    g_aux_pool.push_back(a);
+}
 
 static void ctx_free(vlgba_ctx *c)
 {
     if (!c) return;
     if (c->d.stream) (void)hipStreamSynchronize(c->d.stream);
+    if (c->d.side) (void)hipStreamSynchronize(c->d.side);
     for (void *p : c->allocs) (void)hipFree(p);
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -571,10 +632,7 @@ static void ctx_free(vlgba_ctx *c)
     }
     ba_chol_free(&c->d);
     if (c->comm) ncclCommDestroy(c->comm);
-    if (c->d.stream) (void)hipStreamDestroy(c->d.stream);
-    if (c->d.side) (void)hipStreamDestroy(c->d.side);
-    if (c->d.ev_fork) (void)hipEventDestroy(c->d.ev_fork);
-    if (c->d.ev_join) (void)hipEventDestroy(c->d.ev_join);
+    if (c->has_aux) aux_release(c->aux);
     delete c;
 }
 
@@ -822,13 +880,17 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
     int rc = 0;
     do {
         if (hipSetDevice(o->device) != hipSuccess) { rc = VLGBA_E_ARG; break; }
-        if (hipStreamCreateWithFlags(&c->d.stream, hipStreamNonBlocking) != hipSuccess ||
-            hipStreamCreateWithFlags(&c->d.side, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&c->d.ev_fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c->d.ev_join, hipEventDisableTiming) != hipSuccess) {
+        if (aux_acquire(o->device, c->aux)) {
             rc = -1;
             break;
         }
+        c->has_aux = true;
+        c->d.stream = c->aux.stream;
+        c->d.side = c->aux.side;
+        c->d.ev_fork = c->aux.ev_fork;
+        c->d.ev_join = c->aux.ev_join;
+        c->d.hres = c->aux.hres_host;
+        c->d.hres_dev = c->aux.hres_dev;
         host_obs h;
         rc = sort_obs(p, h);
         if (rc) break;
@@ -974,8 +1036,35 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
         TRY(allreduce(c, d.scal + 1, 1));
         TRY(allreduce(c, d.scal + 3, 1));
     }
-    TRY(download(hs, d.scal, 5, d.stream));
-    VLGBA_CHECK(hipStreamSynchronize(d.stream));
+    if (c->world == 1 && !c->timing) {
+        // spin on the host-mapped sequence number k_publish writes last (lower
+        // latency than a copy + hipStreamSynchronize); a stalled stream falls
+        // back to the synchronisation, which reports the error
+        TRY(ba_launch_publish(&d));
+        const double want = (double)d.seq;
+        const auto t0 = std::chrono::steady_clock::now();
+        bool got = false;
+        for (long it = 0;; it++) {
+            if (d.hres[7] == want) {
+                got = true;
+                break;
+            }
+            if ((it & 1023) == 1023 &&
+                std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5))
+                break;
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        if (got) {
+            for (int q = 0; q < 5; q++) hs[q] = d.hres[q];
+        } else {
+            VLGBA_CHECK(hipStreamSynchronize(d.stream));
+            TRY(download(hs, d.scal, 5, d.stream));
+            VLGBA_CHECK(hipStreamSynchronize(d.stream));
+        }
+    } else {
+        TRY(download(hs, d.scal, 5, d.stream));
+        VLGBA_CHECK(hipStreamSynchronize(d.stream));
+    }
     if (c->timing) {
         float ms;
         const int map[7][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {6, 7}};
