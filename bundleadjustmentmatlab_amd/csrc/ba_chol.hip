@@ -896,6 +896,13 @@ __global__ void k_fix_diag(double *__restrict__ S, double *__restrict__ rhs, lon
 }
 
 // ===========================================================================
+template <typename T>
+static int dev_alloc(T **p, size_t bytes)
+{
+    *p = (T *)ba_dmalloc(bytes);
+    return *p ? 0 : -(int)hipErrorOutOfMemory;
+}
+
 int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
 {
     const int nt = (int)(d->lds / NB);
@@ -944,8 +951,8 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
             tblk.insert(tblk.end(), lists[e].begin(), lists[e].end());
             tptr[e + 1] = (int)tblk.size();
         }
-        VLGBA_CHECK(hipMalloc(&d->tb_ptr, sizeof(int) * tptr.size()));
-        VLGBA_CHECK(hipMalloc(&d->tb_blk, sizeof(int) * (tblk.size() + 1)));
+        TRY_RC(dev_alloc(&d->tb_ptr, sizeof(int) * tptr.size()));
+        TRY_RC(dev_alloc(&d->tb_blk, sizeof(int) * (tblk.size() + 1)));
         VLGBA_CHECK(hipMemcpyAsync(d->tb_ptr, tptr.data(), sizeof(int) * tptr.size(),
                                    hipMemcpyHostToDevice, d->stream));
         if (!tblk.empty())
@@ -986,9 +993,9 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
         d->cr_kptr_h = new int[kptr.size()];
         for (size_t q = 0; q < eptr.size(); q++) d->cr_eptr_h[q] = eptr[q];
         for (size_t q = 0; q < kptr.size(); q++) d->cr_kptr_h[q] = kptr[q];
-        VLGBA_CHECK(hipMalloc(&d->cr_elim, sizeof(int) * elim.size()));
-        VLGBA_CHECK(hipMalloc(&d->cr_keep, sizeof(int) * (keep.size() + 1)));
-        VLGBA_CHECK(hipMalloc(&d->crL, sizeof(double) * 2 * (size_t)nt * NB * NB));
+        TRY_RC(dev_alloc(&d->cr_elim, sizeof(int) * elim.size()));
+        TRY_RC(dev_alloc(&d->cr_keep, sizeof(int) * (keep.size() + 1)));
+        TRY_RC(dev_alloc(&d->crL, sizeof(double) * 2 * (size_t)nt * NB * NB));
         VLGBA_CHECK(hipMemcpyAsync(d->cr_elim, elim.data(), sizeof(int) * elim.size(),
                                    hipMemcpyHostToDevice, d->stream));
         if (!keep.empty())
@@ -997,8 +1004,8 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
     }
     d->pan_ptr_h = new int[nt + 1];
     for (int k = 0; k <= nt; k++) d->pan_ptr_h[k] = ptr[k];
-    VLGBA_CHECK(hipMalloc(&d->pan_list, sizeof(int) * (list.size() + 1)));
-    VLGBA_CHECK(hipMalloc(&d->env_tiles, sizeof(int) * (env.size() + 1)));
+    TRY_RC(dev_alloc(&d->pan_list, sizeof(int) * (list.size() + 1)));
+    TRY_RC(dev_alloc(&d->env_tiles, sizeof(int) * (env.size() + 1)));
     if (!list.empty())
         VLGBA_CHECK(hipMemcpyAsync(d->pan_list, list.data(), sizeof(int) * list.size(),
                                    hipMemcpyHostToDevice, d->stream));
@@ -1016,17 +1023,17 @@ void ba_chol_free(ba_dev *d)
     delete[] d->cr_eptr_h;
     delete[] d->cr_kptr_h;
     d->cr_eptr_h = d->cr_kptr_h = nullptr;
-    if (d->cr_elim) (void)hipFree(d->cr_elim);
-    if (d->cr_keep) (void)hipFree(d->cr_keep);
-    if (d->crL) (void)hipFree(d->crL);
+    if (d->cr_elim) ba_dfree(d->cr_elim);
+    if (d->cr_keep) ba_dfree(d->cr_keep);
+    if (d->crL) ba_dfree(d->crL);
     d->cr_elim = d->cr_keep = nullptr;
     d->crL = nullptr;
     d->cr_nlev = 0;
-    if (d->tb_ptr) (void)hipFree(d->tb_ptr);
-    if (d->tb_blk) (void)hipFree(d->tb_blk);
+    if (d->tb_ptr) ba_dfree(d->tb_ptr);
+    if (d->tb_blk) ba_dfree(d->tb_blk);
     d->tb_ptr = d->tb_blk = nullptr;
-    if (d->pan_list) (void)hipFree(d->pan_list);
-    if (d->env_tiles) (void)hipFree(d->env_tiles);
+    if (d->pan_list) ba_dfree(d->pan_list);
+    if (d->env_tiles) ba_dfree(d->env_tiles);
     d->h_tfirst = d->pan_ptr_h = nullptr;
     d->pan_list = d->env_tiles = nullptr;
 }

@@ -194,7 +194,9 @@ int ba_launch_schur(ba_dev *d, double lambda);
 int ba_launch_assemble(ba_dev *d);
 int ba_launch_update(ba_dev *d, double lambda);
 int ba_launch_yeb(ba_dev *d);
-int ba_launch_publish(ba_dev *d);   // scal[0..4] + ++seq -> hres (host-mapped)
+int ba_launch_publish(ba_dev *d);
+void *ba_dmalloc(size_t bytes);   // per-device caching allocator (ba_solver.cpp)
+void ba_dfree(void *p);   // scal[0..4] + ++seq -> hres (host-mapped)
 int ba_launch_schur_fast(ba_dev *d, double lambda);   // fused damp + Vinv + Y + S + e_
 int ba_launch_assemble_plain(ba_dev *d, double *S, long long ld);
 // ---- ba_chol.hip ----

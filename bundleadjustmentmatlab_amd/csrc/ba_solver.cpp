@@ -25,21 +25,95 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <unordered_map>
+#include <map>
 #include <new>
 #include <numeric>
 #include <vector>
 
 #define VLGBA_VERSION_STR "vlgba 0.1 (gfx950, fp64, MFMA-f64 Cholesky)"
 
+// ---------------------------------------------------------------------------
+// Device memory: a per-device caching allocator.  A solve's context makes a few
+// dozen allocations; hipMalloc / hipFree of each costs tens of microseconds,
+// which the growing-BA replay (hundreds of small solves) would pay every time.
+// Blocks are rounded up to a power of two (256 B .. 1 GiB) and kept on a free
+// list when released; larger blocks go straight back to HIP.
+// ---------------------------------------------------------------------------
+namespace {
+std::mutex g_mem_mu;
+std::multimap<std::pair<int, size_t>, void *> g_mem_free;     // (device, bucket) -> block
+std::unordered_map<void *, std::pair<int, size_t>> g_mem_live;  // block -> (device, bucket)
+constexpr size_t BA_MEM_CACHE_MAX = size_t(1) << 30;
+
+size_t mem_bucket(size_t bytes)
+{
+    if (bytes > BA_MEM_CACHE_MAX) return bytes;
+    size_t b = 256;
+    while (b < bytes) b <<= 1;
+    return b;
+}
+}   // namespace
+
+void *ba_dmalloc(size_t bytes)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    const size_t b = mem_bucket(bytes ? bytes : 1);
+    {
+        std::lock_guard<std::mutex> lk(g_mem_mu);
+        auto it = g_mem_free.find({dev, b});
+        if (it != g_mem_free.end()) {
+            void *p = it->second;
+            g_mem_free.erase(it);
+            g_mem_live[p] = {dev, b};
+            return p;
+        }
+    }
+    void *p = nullptr;
+    if (hipMalloc(&p, b) != hipSuccess) {
+        // out of memory with blocks cached: give them back and retry once
+        std::vector<void *> drop;
+        {
+            std::lock_guard<std::mutex> lk(g_mem_mu);
+            for (auto &kv : g_mem_free) drop.push_back(kv.second);
+            g_mem_free.clear();
+        }
+        for (void *q : drop) (void)hipFree(q);
+        if (hipMalloc(&p, b) != hipSuccess) return nullptr;
+    }
+    std::lock_guard<std::mutex> lk(g_mem_mu);
+    g_mem_live[p] = {dev, b};
+    return p;
+}
+
+void ba_dfree(void *p)
+{
+    if (!p) return;
+    std::unique_lock<std::mutex> lk(g_mem_mu);
+    auto it = g_mem_live.find(p);
+    if (it == g_mem_live.end()) {   // not ours
+        lk.unlock();
+        (void)hipFree(p);
+        return;
+    }
+    const auto key = it->second;
+    g_mem_live.erase(it);
+    if (key.second > BA_MEM_CACHE_MAX) {
+        lk.unlock();
+        (void)hipFree(p);
+        return;
+    }
+    g_mem_free.emplace(key, p);
+}
+
 namespace {
 
 template <typename T>
 int dalloc(T **p, size_t count)
 {
-    *p = nullptr;
-    if (count == 0) count = 1;
-    hipError_t e = hipMalloc((void **)p, sizeof(T) * count);
-    return e == hipSuccess ? 0 : -(int)e;
+    *p = (T *)ba_dmalloc(sizeof(T) * (count ? count : 1));
+    return *p ? 0 : -(int)hipErrorOutOfMemory;
 }
 
 template <typename T>
@@ -623,7 +697,7 @@ static void ctx_free(vlgba_ctx *c)
     if (!c) return;
     if (c->d.stream) (void)hipStreamSynchronize(c->d.stream);
     if (c->d.side) (void)hipStreamSynchronize(c->d.side);
-    for (void *p : c->allocs) (void)hipFree(p);
+    for (void *p : c->allocs) ba_dfree(p);
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->d.kt) {
@@ -1183,7 +1257,7 @@ int vlgba_get_params(vlgba_ctx *c, double *a, double *b)
             int rc = allreduce(c, full, 3 * (size_t)c->n_global);
             if (!rc) rc = download(b, full, 3 * (size_t)c->n_global, c->d.stream);
             (void)hipStreamSynchronize(c->d.stream);
-            (void)hipFree(full);
+            ba_dfree(full);
             if (rc) return rc;
         } else {
             TRY(download(b, c->d.b, 3 * (size_t)c->d.n, c->d.stream));
