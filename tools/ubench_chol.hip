@@ -8,6 +8,13 @@
 // the library's kernel-timer hooks (ba_solver.cpp) are not linked here
 void kt_begin(ba_ktimer *, hipStream_t) {}
 void kt_end(ba_ktimer *, hipStream_t, int) {}
+// the library's caching allocator (ba_solver.cpp) is not linked here either
+void *ba_dmalloc(size_t bytes)
+{
+    void *p = nullptr;
+    return hipMalloc(&p, bytes) == hipSuccess ? p : nullptr;
+}
+void ba_dfree(void *p) { (void)hipFree(p); }
 
 #include <cstdio>
 #include <cstdlib>

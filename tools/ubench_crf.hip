@@ -6,6 +6,13 @@
 
 void kt_begin(ba_ktimer *, hipStream_t) {}
 void kt_end(ba_ktimer *, hipStream_t, int) {}
+// the library's caching allocator (ba_solver.cpp) is not linked here either
+void *ba_dmalloc(size_t bytes)
+{
+    void *p = nullptr;
+    return hipMalloc(&p, bytes) == hipSuccess ? p : nullptr;
+}
+void ba_dfree(void *p) { (void)hipFree(p); }
 
 #include <cstdio>
 #include <cstdlib>
@@ -186,6 +193,20 @@ __global__ __launch_bounds__(256) void k_wf_dbg(const double *S, long long lds, 
         for (int q = 0; q < 5; q++) out[q] = tw[q];
 }
 
+// the library's block_potrf_inv, timed whole
+__global__ __launch_bounds__(256) void k_bpi_lib(const double *S, long long lds,
+                                                 unsigned long long *out)
+{
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double *As = sm, *Bs = sm + NB * LP;
+    __shared__ unsigned long long ts[2];
+    load_tile(S, lds, 1, 1, As);
+    __syncthreads();
+    if (threadIdx.x == 0) ts[0] = stamp();
+    block_potrf_inv(As, Bs, false);
+    if (threadIdx.x == 0) out[0] = stamp() - ts[0];
+}
+
 int main()
 {
     const int n = 192;
@@ -231,6 +252,13 @@ int main()
         k_wf_dbg<<<1, 256, smem3>>>(S, n, out);
         hipMemcpy(ho, out, sizeof(unsigned long long) * 5, hipMemcpyDeviceToHost);
     }
+    hipFuncSetAttribute((const void *)k_bpi_lib, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)smem3);
+    for (int it = 0; it < 3; it++) {
+        k_bpi_lib<<<1, 256, smem3>>>(S, n, out);
+        hipMemcpy(ho + 8, out, sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    }
+    printf("library block_potrf_inv: %llu cycles\n", ho[8]);
     printf("wave_factor16: lds read %llu  pivot loop %llu  L write %llu  inverse %llu  Li write %llu\n",
            ho[0], ho[1], ho[2], ho[3], ho[4]);
     return 0;
