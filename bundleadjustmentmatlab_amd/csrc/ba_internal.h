@@ -162,6 +162,8 @@ struct ba_dev {
     volatile double *hres;     // host view
     double *hres_dev;          // device view
     unsigned long long seq;
+    int publish_req, published;   // fold the publish into the update's final sums
+    unsigned *pub_cnt;            // device counter of k_sum_parts3's blocks (zeroed)
 };
 
 #define KT_B(d) \

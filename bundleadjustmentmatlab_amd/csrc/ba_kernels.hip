@@ -1460,6 +1460,12 @@ struct ba_sum3 {
     const double *part[3];
     int n[3];
     double *out[3];
+    // optional publish (k_publish folded in): the last block to finish copies
+    // scal[0..4] to the host-mapped hres, then the sequence number
+    const double *scal;
+    double *hres;
+    double seq;
+    unsigned *cnt;   // zero between launches (the last block resets it)
 };
 
 __global__ __launch_bounds__(1024) void k_sum_parts3(ba_sum3 a)
@@ -1476,6 +1482,18 @@ __global__ __launch_bounds__(1024) void k_sum_parts3(ba_sum3 a)
     }
     for (; q < nparts; q += 1024) v0 += part[q];
     block_sum_to<1024>((v0 + v1) + (v2 + v3), a.out[blockIdx.x]);
+    if (a.hres && threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(a.cnt, 1u) == 2u) {   // the three sums are in scal
+            __threadfence();
+            const volatile double *sc = a.scal;
+            for (int k = 0; k < 5; k++) a.hres[k] = sc[k];
+            __threadfence_system();
+            *a.cnt = 0u;
+            __atomic_store_n((unsigned long long *)(a.hres + 7), __double_as_longlong(a.seq),
+                             __ATOMIC_RELEASE);
+        }
+    }
 }
 
 // fixed-order sum of nparts partials -> out (one 1024-thread block; four
@@ -1714,7 +1732,15 @@ int ba_launch_update(ba_dev *d, double lambda)
         // new SSE, point dpg, camera dpg: one launch
         ba_sum3 s3 = {{d->chsse + d->nch, d->chsse + 2 * (size_t)d->nch, d->part},
                       {d->nch, d->nch, gc},
-                      {d->scal + 1, d->scal + 3, d->scal + 2}};
+                      {d->scal + 1, d->scal + 3, d->scal + 2},
+                      d->scal, nullptr, 0.0, d->pub_cnt};
+        if (d->publish_req) {
+            d->seq++;
+            s3.hres = d->hres_dev;
+            s3.seq = (double)d->seq;
+            d->publish_req = 0;
+            d->published = 1;
+        }
         k_sum_parts3<<<3, 1024, 0, d->stream>>>(s3);
         return -(int)hipGetLastError();
     }

@@ -926,6 +926,8 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         TRY(upload(d.term, hb.term.data(), hb.term.size(), s));
     }
     VLGBA_CHECK(hipMemsetAsync(d.scal, 0, 8 * sizeof(double), s));
+    TRY(ctx_alloc(c, &d.pub_cnt, 1));
+    VLGBA_CHECK(hipMemsetAsync(d.pub_cnt, 0, sizeof(unsigned), s));
     VLGBA_CHECK(hipStreamSynchronize(s));   // host vectors go out of scope
     return 0;
 }
@@ -1098,7 +1100,11 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
     mark(c, 5);
     TRY(ba_chol_solve(&d));
     mark(c, 6);
+    const bool spin = c->world == 1 && !c->timing;
+    d.publish_req = spin;   // the fast update's final-sums launch publishes
+    d.published = 0;
     TRY(ba_launch_update(&d, lam));
+    d.publish_req = 0;
     mark(c, 7);
     // scalars: [0] old_sse(local) [1] new_sse [2] dpg cameras [3] dpg points [4] chol status
     double hs[5];
@@ -1110,11 +1116,12 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
         TRY(allreduce(c, d.scal + 1, 1));
         TRY(allreduce(c, d.scal + 3, 1));
     }
-    if (c->world == 1 && !c->timing) {
-        // spin on the host-mapped sequence number k_publish writes last (lower
-        // latency than a copy + hipStreamSynchronize); a stalled stream falls
-        // back to the synchronisation, which reports the error
-        TRY(ba_launch_publish(&d));
+    if (spin) {
+        // spin on the host-mapped sequence number written last (by the update's
+        // final sums, or k_publish); lower latency than a copy +
+        // hipStreamSynchronize.  A stalled stream falls back to the
+        // synchronisation, which reports the error
+        if (!d.published) TRY(ba_launch_publish(&d));
         const double want = (double)d.seq;
         const auto t0 = std::chrono::steady_clock::now();
         bool got = false;
