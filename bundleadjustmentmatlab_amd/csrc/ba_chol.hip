@@ -808,6 +808,291 @@ __global__ __launch_bounds__(256) void k_cr_update(double *__restrict__ S, long 
     }
 }
 
+// ---------------------------------------------------------------------------
+// Camera-aligned cyclic reduction on tiles of TB = NA * floor(32 / NA) rows
+// (whole cameras; S rows g = TB * tile + r, r < TB, g < ld).  A tile lives in
+// LDS as 32 x 32 (pitch LP, so the 16 x 16 MFMA helpers above apply): rows or
+// columns r >= TB, or g >= ld, are padding -- zero, with a unit diagonal in a
+// diagonal tile -- so the padded factorisation is that of the TB x TB tile
+// bordered by an identity, and padding never leaks into real entries (the
+// factors' padding rows / columns are zero off the diagonal).  Same algebra
+// and launch structure as the 64-row kernels; the pivot chain per level is
+// 32 columns instead of 64.
+// ---------------------------------------------------------------------------
+#define T32 32
+
+__device__ __forceinline__ void load32(const double *__restrict__ S, long long lds, int TB,
+                                       long long ld, int ti, int tj, double *T, bool transposed,
+                                       bool diag)
+{
+    const int r = threadIdx.x & 31, c0 = threadIdx.x >> 5;
+    const long long gr = (long long)TB * ti + r;
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const int c = c0 + 8 * u;
+        const long long gc = (long long)TB * tj + c;
+        const bool ok = r < TB && c < TB && gr < ld && gc < ld;
+        v[u] = ok ? S[gr + lds * gc] : ((diag && r == c) ? 1.0 : 0.0);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const int c = c0 + 8 * u;
+        if (transposed)
+            T[c * LP + r] = v[u];
+        else
+            T[r * LP + c] = v[u];
+    }
+}
+
+__device__ __forceinline__ void store32(double *__restrict__ S, long long lds, int TB,
+                                        long long ld, int ti, int tj, const double *T)
+{
+    const int r = threadIdx.x & 31, c0 = threadIdx.x >> 5;
+    const long long gr = (long long)TB * ti + r;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const int c = c0 + 8 * u;
+        const long long gc = (long long)TB * tj + c;
+        if (r < TB && c < TB && gr < ld && gc < ld) S[gr + lds * gc] = T[r * LP + c];
+    }
+}
+
+// 32 x 32 LDS tile <-> row-major dst[r * 32 + c]
+__device__ __forceinline__ void store_rm32(double *__restrict__ dst, const double *T)
+{
+    const int c = threadIdx.x & 31, r0 = threadIdx.x >> 5;
+#pragma unroll
+    for (int u = 0; u < 4; u++) dst[(r0 + 8 * u) * T32 + c] = T[(r0 + 8 * u) * LP + c];
+}
+
+__device__ __forceinline__ void load_rm32(const double *__restrict__ src, double *T)
+{
+    const int c = threadIdx.x & 31, r0 = threadIdx.x >> 5;
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[u] = src[(r0 + 8 * u) * T32 + c];
+#pragma unroll
+    for (int u = 0; u < 4; u++) T[(r0 + 8 * u) * LP + c] = v[u];
+}
+
+// acc (one 16 x 16 block per wave: rows 16 (w >> 1), cols 16 (w & 1)) of
+// A B^T over K = 32 (nt form, as mfma_64x64)
+__device__ __forceinline__ d4 mfma32_nt(const double *A, const double *Bt, d4 acc)
+{
+    const int w = threadIdx.x >> 6, ra = 16 * (w >> 1), cb = 16 * (w & 1);
+    acc = mfma16_nt(A, ra, 0, Bt, cb, 0, acc);
+    return mfma16_nt(A, ra, 16, Bt, cb, 16, acc);
+}
+
+__device__ __forceinline__ void put32(double *T, d4 acc, double scale, bool add)
+{
+    const int w = threadIdx.x >> 6;
+    put16(T, 16 * (w >> 1), 16 * (w & 1), acc, scale, add);
+}
+
+// out[r] = scale * sum_c M[r][c] v[c] (t = 0) or sum_c M[c][r] v[c] (t = 1),
+// r < 32: thread (r, part of 4 columns), the 8 parts added in fixed order
+__device__ __forceinline__ void gemv32(const double *M, const double *v, double (*part)[T32],
+                                       double *out, bool t)
+{
+    const int tid = threadIdx.x, r = tid & 31, pq = tid >> 5;
+    double acc = 0.0;
+#pragma unroll
+    for (int c = 4 * pq; c < 4 * pq + 4; c++)
+        acc = fma(t ? M[c * LP + r] : M[r * LP + c], v[c], acc);
+    part[pq][r] = acc;
+    __syncthreads();
+    if (tid < T32)
+        out[tid] = ((((((part[0][tid] + part[1][tid]) + part[2][tid]) + part[3][tid]) +
+                     part[4][tid]) + part[5][tid]) + part[6][tid]) + part[7][tid];
+    __syncthreads();
+}
+
+// the 32 x 32 factor and inverse: two 16-column blocks (schedule of
+// block_potrf_inv).  L -> lower triangle of As (block (0,1) keeps A), L^-1
+// (zero upper) -> Li.
+__device__ __forceinline__ bool potrf32_inv(double *As, double *Li, double *Xs)
+{
+    __shared__ int bad32;
+    const int tid = threadIdx.x, w = tid >> 6;
+    Li[(tid >> 4) * LP + 16 + (tid & 15)] = 0.0;   // block (0, 1) of L^-1
+    if (tid == 0) bad32 = 0;
+    if (w == 0 && !wave_factor16(As, Li, 0) && tid == 0) bad32 = 1;
+    __syncthreads();
+    if (w == 1) {   // L10 = A10 Dinv00^T
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        acc = mfma16_nt(As, 16, 0, Li, 0, 0, acc);
+        put16(As, 16, 0, acc, 1.0, false);
+    }
+    __syncthreads();
+    if (w == 0) {   // A11 -= L10 L10^T, then factor it
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        acc = mfma16_nt(As, 16, 0, As, 16, 0, acc);
+        put16(As, 16, 16, acc, -1.0, true);
+        if (!wave_factor16(As, Li, 16) && tid == 0) bad32 = 1;
+    }
+    __syncthreads();
+    if (w == 1) {   // Li10 = -Li11 (L10 Li00)
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        acc = mfma16_nn(As, 16, 0, Li, 0, 0, acc);
+        put16(Xs, 0, 0, acc, 1.0, false);
+        d4 acc2 = {0.0, 0.0, 0.0, 0.0};
+        acc2 = mfma16_nn(Li, 16, 16, Xs, 0, 0, acc2);
+        put16(Li, 16, 0, acc2, -1.0, false);
+    }
+    __syncthreads();
+    return bad32 == 0;
+}
+
+// factor step: role 0 factors D_e, writes L_e^-1 (row-major 32 x 32) and
+// y_e = L_e^-1 r_e; role 1 / 2 (split, one workgroup each, redoing the same
+// factorisation) or the same workgroup (no split) form Lp_e = C(p, e) L_e^-T
+// and Lq_e = C(q, e) L_e^-T into crL.
+__global__ __launch_bounds__(256) void k_cr32_factor(double *__restrict__ S, long long lds,
+                                                     int TB, long long ld,
+                                                     const int *__restrict__ elim, int nt,
+                                                     double *__restrict__ linv,
+                                                     double *__restrict__ crL,
+                                                     const double *__restrict__ rhs,
+                                                     double *__restrict__ y,
+                                                     double *__restrict__ status, int split)
+{
+    __shared__ __attribute__((aligned(16))) double As[T32 * LP], Bs[T32 * LP], Cs[T32 * LP];
+    __shared__ __attribute__((aligned(16))) double Xs[16 * LP];
+    __shared__ double rk[T32], yk[T32];
+    __shared__ double part[8][T32];
+    const int tid = threadIdx.x;
+    const int x = split ? blockIdx.x / 3 : blockIdx.x, role = split ? blockIdx.x % 3 : -1;
+    const int e = elim[3 * x], p = elim[3 * x + 1], q = elim[3 * x + 2];
+    if ((role == 1 && p < 0) || (role == 2 && q < 0)) return;
+    const long long T2 = (long long)T32 * T32;
+    load32(S, lds, TB, ld, e, e, As, false, true);
+    if (role == 1) load32(S, lds, TB, ld, e, p, Cs, true, false);   // C(p, e) = tile(e, p)^T
+    if (role == 2) load32(S, lds, TB, ld, q, e, Cs, false, false);  // C(q, e) = tile(q, e)
+    if (role <= 0 && tid < T32) {
+        const long long g = (long long)TB * e + tid;
+        rk[tid] = (tid < TB && g < ld) ? rhs[g] : 0.0;
+    }
+    __syncthreads();
+    const bool ok = potrf32_inv(As, Bs, Xs);
+    if (role <= 0) {
+        gemv32(Bs, rk, part, yk, false);
+        if (tid < TB) y[(long long)TB * e + tid] = yk[tid];
+        store_rm32(linv + T2 * e, Bs);
+        if (tid == 0 && !ok) status[0] = 1.0;
+        if (role == 0) return;   // split: roles 1 and 2 form the panels
+    }
+    for (int side = 1; side <= 2; side++) {
+        if (role > 0 && role != side) continue;
+        const int nb = side == 1 ? p : q;
+        if (nb < 0) continue;
+        if (role < 0) {
+            __syncthreads();
+            if (side == 1)
+                load32(S, lds, TB, ld, e, p, Cs, true, false);
+            else
+                load32(S, lds, TB, ld, q, e, Cs, false, false);
+            __syncthreads();
+        }
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        acc = mfma32_nt(Cs, Bs, acc);   // C L^-T: [r][c] = sum_t C[r][t] Li[c][t]
+        __syncthreads();
+        put32(Cs, acc, 1.0, false);
+        __syncthreads();
+        store_rm32(crL + T2 * (side == 1 ? e : nt + e), Cs);
+    }
+}
+
+// update step: D_k -= Lq_{e-} Lq_{e-}^T + Lp_{e+} Lp_{e+}^T, r_k -= Lq y + Lp y,
+// C(k2, k) = -Lq_{e+} Lp_{e+}^T
+__global__ __launch_bounds__(256) void k_cr32_update(double *__restrict__ S, long long lds,
+                                                     int TB, long long ld,
+                                                     const int *__restrict__ keep, int nt,
+                                                     const double *__restrict__ crL,
+                                                     double *__restrict__ rhs,
+                                                     const double *__restrict__ y)
+{
+    __shared__ __attribute__((aligned(16))) double As[T32 * LP], Bs[T32 * LP], Cs[T32 * LP];
+    __shared__ double ym[T32], yp[T32], um[T32], up[T32];
+    __shared__ double part[8][T32];
+    const int tid = threadIdx.x;
+    const int *kp = keep + 4 * blockIdx.x;
+    const int k = kp[0], em = kp[1], ep = kp[2], k2 = kp[3];
+    const long long T2 = (long long)T32 * T32;
+    load32(S, lds, TB, ld, k, k, As, false, true);
+    load_rm32(crL + T2 * (nt + em), Bs);          // Lq_{e-} = L(k, e-)
+    if (ep >= 0) load_rm32(crL + T2 * ep, Cs);    // Lp_{e+} = L(k, e+)
+    if (tid < T32) {
+        ym[tid] = tid < TB ? y[(long long)TB * em + tid] : 0.0;
+        yp[tid] = (ep >= 0 && tid < TB) ? y[(long long)TB * ep + tid] : 0.0;
+    }
+    __syncthreads();
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    acc = mfma32_nt(Bs, Bs, acc);
+    if (ep >= 0) acc = mfma32_nt(Cs, Cs, acc);
+    put32(As, acc, -1.0, true);
+    gemv32(Bs, ym, part, um, false);
+    if (ep >= 0) gemv32(Cs, yp, part, up, false);
+    if (tid < TB) {
+        const long long g = (long long)TB * k + tid;
+        if (g < ld) {
+            double r = rhs[g] - um[tid];
+            if (ep >= 0) r -= up[tid];
+            rhs[g] = r;
+        }
+    }
+    __syncthreads();
+    store32(S, lds, TB, ld, k, k, As);
+    if (k2 >= 0) {   // C(k2, k) = -Lq_{e+} Lp_{e+}^T
+        __syncthreads();
+        load_rm32(crL + T2 * (nt + ep), Bs);
+        __syncthreads();
+        d4 acc2 = {0.0, 0.0, 0.0, 0.0};
+        acc2 = mfma32_nt(Bs, Cs, acc2);
+        put32(As, acc2, -1.0, false);
+        __syncthreads();
+        store32(S, lds, TB, ld, k2, k, As);
+    }
+}
+
+// back substitution: x_e = L_e^-T (y_e - Lp_e^T x_p - Lq_e^T x_q)
+__global__ __launch_bounds__(256) void k_cr32_back(const int *__restrict__ elim, int nt, int TB,
+                                                   long long ld,
+                                                   const double *__restrict__ linv,
+                                                   const double *__restrict__ crL,
+                                                   const double *__restrict__ y,
+                                                   double *__restrict__ x)
+{
+    __shared__ __attribute__((aligned(16))) double Ls[T32 * LP];
+    __shared__ double t[T32], u[T32];
+    __shared__ double part[8][T32];
+    const int tid = threadIdx.x;
+    const int e = elim[3 * blockIdx.x], p = elim[3 * blockIdx.x + 1], q = elim[3 * blockIdx.x + 2];
+    const long long T2 = (long long)T32 * T32;
+    if (tid < T32) t[tid] = tid < TB ? y[(long long)TB * e + tid] : 0.0;
+    for (int side = 0; side < 2; side++) {
+        const int nb = side == 0 ? p : q;
+        if (nb < 0) continue;
+        load_rm32(crL + T2 * (side == 0 ? e : nt + e), Ls);
+        if (tid < T32) {
+            const long long g = (long long)TB * nb + tid;
+            u[tid] = (tid < TB && g < ld) ? x[g] : 0.0;
+        }
+        __syncthreads();
+        gemv32(Ls, u, part, u, true);
+        if (tid < T32) t[tid] -= u[tid];
+        __syncthreads();
+    }
+    load_rm32(linv + T2 * e, Ls);
+    __syncthreads();
+    gemv32(Ls, t, part, u, true);
+    if (tid < TB) {
+        const long long g = (long long)TB * e + tid;
+        if (g < ld) x[g] = u[tid];
+    }
+}
+
 __global__ __launch_bounds__(256) void k_cr_back(const int *__restrict__ elim, int nt,
                                                  const double *__restrict__ linv,
                                                  const double *__restrict__ crL,
@@ -985,12 +1270,34 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
                                        hipMemcpyHostToDevice, d->stream));
         VLGBA_CHECK(hipStreamSynchronize(d->stream));
     }
-    // cyclic reduction when S is tile-tridiagonal (dense_solve 0 = auto)
+    // cyclic reduction when S is tile-tridiagonal (dense_solve 0 = auto):
+    // camera-aligned 32-row tiles when the co-visibility band allows them
+    // (every block (j, k) within neighbouring groups of floor(32 / NA)
+    // cameras), else the 64-row tiles
+    d->cr_nlev = 0;
+    d->cr32 = 0;
+    int ntc = nt;
+    if (d->dense_solve == 0 && d->na <= 32) {
+        const int G = 32 / d->na, TB = d->na * G;
+        const int nt32 = (int)((d->ld + TB - 1) / TB);
+        bool ok = nt32 > 1;
+        for (int b = 0; ok && b < nb; b++) {
+            const int dj = blk_jk[2 * b] / G - blk_jk[2 * b + 1] / G;
+            if (dj > 1 || dj < -1) ok = false;
+        }
+        if (ok) {
+            d->cr32 = 1;
+            d->tb32 = TB;
+            d->nt32 = nt32;
+            ntc = nt32;
+        }
+    }
     bool tridiag = d->dense_solve == 0 && nt > 1;
     for (int i = 1; tridiag && i < nt; i++)
         if (d->h_tfirst[i] < i - 1) tridiag = false;
-    d->cr_nlev = 0;
+    if (d->cr32) tridiag = true;
     if (tridiag) {
+        const int nt = ntc;   // the CR tile count (64- or camera-aligned 32-row tiles)
         std::vector<int> act(nt), elim, keep, eptr{0}, kptr{0};
         for (int i = 0; i < nt; i++) act[i] = i;
         while (!act.empty()) {
@@ -1020,7 +1327,8 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
         for (size_t q = 0; q < kptr.size(); q++) d->cr_kptr_h[q] = kptr[q];
         TRY_RC(dev_alloc(&d->cr_elim, sizeof(int) * elim.size()));
         TRY_RC(dev_alloc(&d->cr_keep, sizeof(int) * (keep.size() + 1)));
-        TRY_RC(dev_alloc(&d->crL, sizeof(double) * 2 * (size_t)nt * NB * NB));
+        TRY_RC(dev_alloc(&d->crL, sizeof(double) * 2 * (size_t)nt *
+                                      (d->cr32 ? T32 * T32 : NB * NB)));
         VLGBA_CHECK(hipMemcpyAsync(d->cr_elim, elim.data(), sizeof(int) * elim.size(),
                                    hipMemcpyHostToDevice, d->stream));
         if (!keep.empty())
@@ -1099,6 +1407,40 @@ int ba_chol_solve(ba_dev *d)
         VLGBA_CHECK(hipFuncSetAttribute((const void *)k_syrk,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
         attr_done = true;
+    }
+    if (d->cr_nlev > 0 && d->cr32) {   // camera-aligned 32-row tiles
+        static int ncu32 = 0;
+        if (!ncu32) {
+            int dev = 0;
+            VLGBA_CHECK(hipGetDevice(&dev));
+            VLGBA_CHECK(hipDeviceGetAttribute(&ncu32, hipDeviceAttributeMultiprocessorCount, dev));
+        }
+        const int n32 = d->nt32, TB = d->tb32;
+        for (int l = 0; l < d->cr_nlev; l++) {
+            const int e0 = d->cr_eptr_h[l], ne = d->cr_eptr_h[l + 1] - e0;
+            const int k0 = d->cr_kptr_h[l], nk = d->cr_kptr_h[l + 1] - k0;
+            const int fs = 3 * ne <= 2 * ncu32;   // ~60 KB LDS: two workgroups per CU
+            KT_B(d);
+            k_cr32_factor<<<fs ? 3 * ne : ne, 256, 0, d->stream>>>(
+                d->S, d->lds, TB, d->ld, d->cr_elim + 3 * e0, n32, d->linv, d->crL, d->rhs,
+                d->ywork, d->scal + 4, fs);
+            KT_E(d, KT_CR_FACTOR);
+            if (nk > 0) {
+                KT_B(d);
+                k_cr32_update<<<nk, 256, 0, d->stream>>>(d->S, d->lds, TB, d->ld,
+                                                         d->cr_keep + 4 * k0, n32, d->crL,
+                                                         d->rhs, d->ywork);
+                KT_E(d, KT_CR_UPDATE);
+            }
+        }
+        for (int l = d->cr_nlev - 1; l >= 0; l--) {
+            const int e0 = d->cr_eptr_h[l], ne = d->cr_eptr_h[l + 1] - e0;
+            KT_B(d);
+            k_cr32_back<<<ne, 256, 0, d->stream>>>(d->cr_elim + 3 * e0, n32, TB, d->ld,
+                                                   d->linv, d->crL, d->ywork, d->da);
+            KT_E(d, KT_CR_BACK);
+        }
+        return -(int)hipGetLastError();
     }
     if (d->cr_nlev > 0) {   // (status cleared by k_assemble_tiles)
         // one workgroup per CU (LDS): fan a level out over 5 (factor) / 4

@@ -99,6 +99,12 @@ struct ba_dev {
     int *cr_eptr_h, *cr_kptr_h;   // host [nlev+1]
     int *cr_elim, *cr_keep;       // device [3 * ne], [4 * nk]
     double *crL;                  // [2][nt][64*64] L(p, e) | L(q, e)
+    // camera-aligned cyclic reduction: tiles of tb32 = NA * floor(32 / NA)
+    // rows (whole cameras, <= 32), padded to 32 in LDS with an identity block;
+    // chosen when S is tridiagonal at that granularity (half the pivot chain
+    // per level of the 64-row tiles).  crL then holds [2][nt32][32*32] and
+    // linv [nt32][32*32].
+    int cr32, tb32, nt32;
     // reductions: partial sums per block of the reducing kernels, in fixed order
     double *part;      // [3][PART_MAX]
     double *scal;      // [8] : 0 old_sse, 1 new_sse, 2 dpg cams, 3 dpg pts, 4 chol status

@@ -905,7 +905,7 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
     if (!stage_mode) {
         TRY(ctx_alloc(c, &d.S, (size_t)(d.lds * d.lds)));
         TRY(ctx_alloc(c, &d.linv, (size_t)(d.lds / 64) * 64 * 64));
-        TRY(ctx_alloc(c, &d.ywork, (size_t)d.lds));
+        TRY(ctx_alloc(c, &d.ywork, (size_t)d.lds + 64));   // + the 32-row CR's last tile
         TRY(ctx_alloc(c, &d.da, (size_t)d.lds));
         TRY(ba_chol_setup(&d, hb.jk.data(), d.nb));
     } else {
@@ -1344,7 +1344,8 @@ int vlgba_plan_info(vlgba_ctx *c, long long *info, int len)
     const long long v[VLGBA_NPLAN] = {d.N,   d.n,    d.m,   d.na,         d.nch,  d.ns,
                                       d.nes, d.ngrp, d.ngs, d.nge,        d.nb,   d.nt,
                                       d.cr_nlev, ne, nk,    d.ordered,    d.ordered ? d.T : d.nterm_fast,
-                                      d.blob_words, d.mfma};
+                                      d.blob_words, d.mfma,
+                                      d.cr_nlev ? (d.cr32 ? d.tb32 : 64) : 0};
     for (int k = 0; k < len && k < VLGBA_NPLAN; k++) info[k] = v[k];
     return VLGBA_NPLAN;
 }

@@ -170,9 +170,10 @@ const char *vlgba_kernel_name(int k);
  * [11] 64-row tiles of S [12] cyclic-reduction levels (0: tile Cholesky)
  * [13] eliminated tiles [14] kept-tile updates [15] ordered mode
  * [16] Schur (obs, obs) terms [17] chunk metadata words [18] MFMA Schur
- * chunks in use.
+ * chunks in use [19] rows per cyclic-reduction tile (64, or NA * floor(32 /
+ * NA) for the camera-aligned tiles; 0 without cyclic reduction).
  * Writes min(len, VLGBA_NPLAN) entries, returns VLGBA_NPLAN. */
-#define VLGBA_NPLAN 19
+#define VLGBA_NPLAN 20
 int vlgba_plan_info(vlgba_ctx *ctx, long long *info, int len);
 
 /* ---- stage entries with the reference MEX argument layouts ---------------
