@@ -1014,6 +1014,7 @@ __global__ __launch_bounds__(256) void k_cr32_update(double *__restrict__ S, lon
                                                      const double *__restrict__ y)
 {
     __shared__ __attribute__((aligned(16))) double As[T32 * LP], Bs[T32 * LP], Cs[T32 * LP];
+    __shared__ __attribute__((aligned(16))) double Ds[T32 * LP];
     __shared__ double ym[T32], yp[T32], um[T32], up[T32];
     __shared__ double part[8][T32];
     const int tid = threadIdx.x;
@@ -1023,6 +1024,7 @@ __global__ __launch_bounds__(256) void k_cr32_update(double *__restrict__ S, lon
     load32(S, lds, TB, ld, k, k, As, false, true);
     load_rm32(crL + T2 * (nt + em), Bs);          // Lq_{e-} = L(k, e-)
     if (ep >= 0) load_rm32(crL + T2 * ep, Cs);    // Lp_{e+} = L(k, e+)
+    if (k2 >= 0) load_rm32(crL + T2 * (nt + ep), Ds);   // Lq_{e+}, for the fill
     if (tid < T32) {
         ym[tid] = tid < TB ? y[(long long)TB * em + tid] : 0.0;
         yp[tid] = (ep >= 0 && tid < TB) ? y[(long long)TB * ep + tid] : 0.0;
@@ -1045,11 +1047,9 @@ __global__ __launch_bounds__(256) void k_cr32_update(double *__restrict__ S, lon
     __syncthreads();
     store32(S, lds, TB, ld, k, k, As);
     if (k2 >= 0) {   // C(k2, k) = -Lq_{e+} Lp_{e+}^T
-        __syncthreads();
-        load_rm32(crL + T2 * (nt + ep), Bs);
-        __syncthreads();
         d4 acc2 = {0.0, 0.0, 0.0, 0.0};
-        acc2 = mfma32_nt(Bs, Cs, acc2);
+        acc2 = mfma32_nt(Ds, Cs, acc2);
+        __syncthreads();   // As has been stored
         put32(As, acc2, -1.0, false);
         __syncthreads();
         store32(S, lds, TB, ld, k2, k, As);
