@@ -1004,56 +1004,102 @@ __global__ __launch_bounds__(256) void k_cr32_factor(double *__restrict__ S, lon
     }
 }
 
-// update step: D_k -= Lq_{e-} Lq_{e-}^T + Lp_{e+} Lp_{e+}^T, r_k -= Lq y + Lp y,
-// C(k2, k) = -Lq_{e+} Lp_{e+}^T
-__global__ __launch_bounds__(256) void k_cr32_update(double *__restrict__ S, long long lds,
-                                                     int TB, long long ld,
-                                                     const int *__restrict__ keep, int nt,
-                                                     const double *__restrict__ crL,
-                                                     double *__restrict__ rhs,
-                                                     const double *__restrict__ y)
+// Level L >= 1 of the camera-aligned CR with the previous level's update folded
+// in (one launch per level instead of two).  Tile k of level L carries the
+// update of level L-1,
+//     D_k -= L(k, em) L(k, em)^T + L(k, ep) L(k, ep)^T,  r_k -= L(k, em) y_em + L(k, ep) y_ep
+// (em / ep: the tiles eliminated at L-1 next to k), and the coupling of two
+// neighbours k < k2 at level L is the fill C(k2, k) = -L(k2, e) L(k, e)^T of
+// the tile e eliminated between them.  Workgroups 3x + role for the tiles
+// eliminated here (role 0: apply the update in LDS, factor, y, L^-1; roles 1 /
+// 2: the same factorisation plus their fill tile C(p, e) / C(q, e), then the
+// panel), then one workgroup per surviving tile (apply the update, write D_k
+// and r_k back).  Records: fused (e, p, q, em, ep), survivor (k, em, ep).
+__global__ __launch_bounds__(256) void k_cr32_level(double *__restrict__ S, long long lds, int TB,
+                                                    long long ld, const int *__restrict__ frec,
+                                                    int ne, const int *__restrict__ srec, int nt,
+                                                    double *__restrict__ linv,
+                                                    double *__restrict__ crL,
+                                                    double *__restrict__ rhs,
+                                                    double *__restrict__ y,
+                                                    double *__restrict__ status)
 {
     __shared__ __attribute__((aligned(16))) double As[T32 * LP], Bs[T32 * LP], Cs[T32 * LP];
-    __shared__ __attribute__((aligned(16))) double Ds[T32 * LP];
-    __shared__ double ym[T32], yp[T32], um[T32], up[T32];
+    __shared__ __attribute__((aligned(16))) double Ds[T32 * LP], Es[T32 * LP];
+    __shared__ __attribute__((aligned(16))) double Xs[16 * LP];
+    __shared__ double rk[T32], ym[T32], yp[T32], um[T32], up[T32];
     __shared__ double part[8][T32];
     const int tid = threadIdx.x;
-    const int *kp = keep + 4 * blockIdx.x;
-    const int k = kp[0], em = kp[1], ep = kp[2], k2 = kp[3];
     const long long T2 = (long long)T32 * T32;
+    const bool surv = (int)blockIdx.x >= 3 * ne;
+    int k, p = -1, q = -1, em, ep, role = 0;
+    if (surv) {
+        const int *r = srec + 3 * (blockIdx.x - 3 * ne);
+        k = r[0];
+        em = r[1];
+        ep = r[2];
+    } else {
+        const int *r = frec + 5 * (blockIdx.x / 3);
+        role = blockIdx.x % 3;
+        k = r[0];
+        p = r[1];
+        q = r[2];
+        em = r[3];
+        ep = r[4];
+        if ((role == 1 && p < 0) || (role == 2 && q < 0)) return;
+    }
     load32(S, lds, TB, ld, k, k, As, false, true);
-    load_rm32(crL + T2 * (nt + em), Bs);          // Lq_{e-} = L(k, e-)
-    if (ep >= 0) load_rm32(crL + T2 * ep, Cs);    // Lp_{e+} = L(k, e+)
-    if (k2 >= 0) load_rm32(crL + T2 * (nt + ep), Ds);   // Lq_{e+}, for the fill
-    if (tid < T32) {
+    load_rm32(crL + T2 * (nt + em), Bs);            // L(k, em)
+    if (ep >= 0) load_rm32(crL + T2 * ep, Cs);      // L(k, ep)
+    if (role == 1) load_rm32(crL + T2 * em, Ds);    // L(p, em)
+    if (role == 2) load_rm32(crL + T2 * (nt + ep), Ds);   // L(q, ep)
+    const bool rows = surv || role == 0;
+    if (rows && tid < T32) {
+        const long long g = (long long)TB * k + tid;
+        rk[tid] = (tid < TB && g < ld) ? rhs[g] : 0.0;
         ym[tid] = tid < TB ? y[(long long)TB * em + tid] : 0.0;
         yp[tid] = (ep >= 0 && tid < TB) ? y[(long long)TB * ep + tid] : 0.0;
     }
     __syncthreads();
-    d4 acc = {0.0, 0.0, 0.0, 0.0};
-    acc = mfma32_nt(Bs, Bs, acc);
-    if (ep >= 0) acc = mfma32_nt(Cs, Cs, acc);
-    put32(As, acc, -1.0, true);
-    gemv32(Bs, ym, part, um, false);
-    if (ep >= 0) gemv32(Cs, yp, part, up, false);
-    if (tid < TB) {
-        const long long g = (long long)TB * k + tid;
-        if (g < ld) {
-            double r = rhs[g] - um[tid];
-            if (ep >= 0) r -= up[tid];
-            rhs[g] = r;
-        }
+    if (role > 0) {   // the fill: C(p, e) = -L(p, em) L(e, em)^T | C(q, e) = -L(q, ep) L(e, ep)^T
+        d4 f = {0.0, 0.0, 0.0, 0.0};
+        f = mfma32_nt(Ds, role == 1 ? Bs : Cs, f);
+        put32(Es, f, -1.0, false);
+    }
+    {
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        acc = mfma32_nt(Bs, Bs, acc);
+        if (ep >= 0) acc = mfma32_nt(Cs, Cs, acc);
+        put32(As, acc, -1.0, true);   // each thread updates the elements it owns
+    }
+    if (rows) {
+        gemv32(Bs, ym, part, um, false);
+        if (ep >= 0) gemv32(Cs, yp, part, up, false);
+        if (tid < T32) rk[tid] = (rk[tid] - um[tid]) - (ep >= 0 ? up[tid] : 0.0);
     }
     __syncthreads();
-    store32(S, lds, TB, ld, k, k, As);
-    if (k2 >= 0) {   // C(k2, k) = -Lq_{e+} Lp_{e+}^T
-        d4 acc2 = {0.0, 0.0, 0.0, 0.0};
-        acc2 = mfma32_nt(Ds, Cs, acc2);
-        __syncthreads();   // As has been stored
-        put32(As, acc2, -1.0, false);
-        __syncthreads();
-        store32(S, lds, TB, ld, k2, k, As);
+    if (surv) {
+        store32(S, lds, TB, ld, k, k, As);
+        if (tid < TB) {
+            const long long g = (long long)TB * k + tid;
+            if (g < ld) rhs[g] = rk[tid];
+        }
+        return;
     }
+    const bool ok = potrf32_inv(As, Bs, Xs);   // L^-1 over L(k, em), no longer needed
+    if (role == 0) {
+        gemv32(Bs, rk, part, um, false);
+        if (tid < TB) y[(long long)TB * k + tid] = um[tid];
+        store_rm32(linv + T2 * k, Bs);
+        if (tid == 0 && !ok) status[0] = 1.0;
+        return;
+    }
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    acc = mfma32_nt(Es, Bs, acc);   // C L^-T
+    __syncthreads();
+    put32(Es, acc, 1.0, false);
+    __syncthreads();
+    store_rm32(crL + T2 * (role == 1 ? k : nt + k), Es);
 }
 
 // back substitution: x_e = L_e^-T (y_e - Lp_e^T x_p - Lq_e^T x_q)
@@ -1321,6 +1367,45 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
             act.swap(next);
         }
         d->cr_nlev = (int)eptr.size() - 1;
+        if (d->cr32) {   // the fused levels' records (see k_cr32_level)
+            const int nl = d->cr_nlev;
+            std::vector<int> frec, srec, fptr(nl + 1, 0), sptr(nl + 1, 0);
+            std::vector<int> em_of(nt, -1), ep_of(nt, -1);
+            for (int L = 1; L < nl; L++) {
+                for (int i = kptr[L - 1]; i < kptr[L]; i++) {
+                    em_of[keep[4 * i]] = keep[4 * i + 1];
+                    ep_of[keep[4 * i]] = keep[4 * i + 2];
+                }
+                for (int i = eptr[L]; i < eptr[L + 1]; i++) {
+                    const int e = elim[3 * i];
+                    frec.insert(frec.end(), {e, elim[3 * i + 1], elim[3 * i + 2], em_of[e],
+                                             ep_of[e]});
+                }
+                for (int i = kptr[L]; i < kptr[L + 1]; i++) {
+                    const int k = keep[4 * i];
+                    srec.insert(srec.end(), {k, em_of[k], ep_of[k]});
+                }
+                fptr[L + 1] = (int)frec.size() / 5;
+                sptr[L + 1] = (int)srec.size() / 3;
+            }
+            fptr[1] = 0;
+            sptr[1] = 0;
+            d->crf_ptr_h = new int[nl + 1];
+            d->crs_ptr_h = new int[nl + 1];
+            for (int L = 0; L <= nl; L++) {
+                d->crf_ptr_h[L] = L >= 1 ? fptr[L] : 0;
+                d->crs_ptr_h[L] = L >= 1 ? sptr[L] : 0;
+            }
+            TRY_RC(dev_alloc(&d->crf, sizeof(int) * (frec.size() + 1)));
+            TRY_RC(dev_alloc(&d->crs, sizeof(int) * (srec.size() + 1)));
+            if (!frec.empty())
+                VLGBA_CHECK(hipMemcpyAsync(d->crf, frec.data(), sizeof(int) * frec.size(),
+                                           hipMemcpyHostToDevice, d->stream));
+            if (!srec.empty())
+                VLGBA_CHECK(hipMemcpyAsync(d->crs, srec.data(), sizeof(int) * srec.size(),
+                                           hipMemcpyHostToDevice, d->stream));
+            VLGBA_CHECK(hipStreamSynchronize(d->stream));
+        }
         d->cr_eptr_h = new int[eptr.size()];
         d->cr_kptr_h = new int[kptr.size()];
         for (size_t q = 0; q < eptr.size(); q++) d->cr_eptr_h[q] = eptr[q];
@@ -1356,6 +1441,12 @@ void ba_chol_free(ba_dev *d)
     delete[] d->cr_eptr_h;
     delete[] d->cr_kptr_h;
     d->cr_eptr_h = d->cr_kptr_h = nullptr;
+    if (d->crf) ba_dfree(d->crf);
+    if (d->crs) ba_dfree(d->crs);
+    delete[] d->crf_ptr_h;
+    delete[] d->crs_ptr_h;
+    d->crf = d->crs = nullptr;
+    d->crf_ptr_h = d->crs_ptr_h = nullptr;
     if (d->cr_elim) ba_dfree(d->cr_elim);
     if (d->cr_keep) ba_dfree(d->cr_keep);
     if (d->crL) ba_dfree(d->crL);
@@ -1416,22 +1507,24 @@ int ba_chol_solve(ba_dev *d)
             VLGBA_CHECK(hipDeviceGetAttribute(&ncu32, hipDeviceAttributeMultiprocessorCount, dev));
         }
         const int n32 = d->nt32, TB = d->tb32;
-        for (int l = 0; l < d->cr_nlev; l++) {
-            const int e0 = d->cr_eptr_h[l], ne = d->cr_eptr_h[l + 1] - e0;
-            const int k0 = d->cr_kptr_h[l], nk = d->cr_kptr_h[l + 1] - k0;
+        {   // level 0 on the assembled S
+            const int ne = d->cr_eptr_h[1];
             const int fs = 3 * ne <= 2 * ncu32;   // ~60 KB LDS: two workgroups per CU
             KT_B(d);
             k_cr32_factor<<<fs ? 3 * ne : ne, 256, 0, d->stream>>>(
-                d->S, d->lds, TB, d->ld, d->cr_elim + 3 * e0, n32, d->linv, d->crL, d->rhs,
-                d->ywork, d->scal + 4, fs);
+                d->S, d->lds, TB, d->ld, d->cr_elim, n32, d->linv, d->crL, d->rhs, d->ywork,
+                d->scal + 4, fs);
             KT_E(d, KT_CR_FACTOR);
-            if (nk > 0) {
-                KT_B(d);
-                k_cr32_update<<<nk, 256, 0, d->stream>>>(d->S, d->lds, TB, d->ld,
-                                                         d->cr_keep + 4 * k0, n32, d->crL,
-                                                         d->rhs, d->ywork);
-                KT_E(d, KT_CR_UPDATE);
-            }
+        }
+        // levels >= 1: the previous level's update folded into the factor launch
+        for (int l = 1; l < d->cr_nlev; l++) {
+            const int f0 = d->crf_ptr_h[l], ne = d->crf_ptr_h[l + 1] - f0;
+            const int s0 = d->crs_ptr_h[l], ns = d->crs_ptr_h[l + 1] - s0;
+            KT_B(d);
+            k_cr32_level<<<3 * ne + ns, 256, 0, d->stream>>>(
+                d->S, d->lds, TB, d->ld, d->crf + 5 * f0, ne, d->crs + 3 * s0, n32, d->linv,
+                d->crL, d->rhs, d->ywork, d->scal + 4);
+            KT_E(d, KT_CR_FACTOR);
         }
         for (int l = d->cr_nlev - 1; l >= 0; l--) {
             const int e0 = d->cr_eptr_h[l], ne = d->cr_eptr_h[l + 1] - e0;

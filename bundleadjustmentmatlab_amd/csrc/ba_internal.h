@@ -105,6 +105,9 @@ struct ba_dev {
     // per level of the 64-row tiles).  crL then holds [2][nt32][32*32] and
     // linv [nt32][32*32].
     int cr32, tb32, nt32;
+    // fused levels (L >= 1): records (e, p, q, em, ep) and survivors (k, em, ep)
+    int *crf, *crs;               // device
+    int *crf_ptr_h, *crs_ptr_h;   // host [nlev + 1], entries per level (level 0 empty)
     // reductions: partial sums per block of the reducing kernels, in fixed order
     double *part;      // [3][PART_MAX]
     double *scal;      // [8] : 0 old_sse, 1 new_sse, 2 dpg cams, 3 dpg pts, 4 chol status
