@@ -1208,14 +1208,31 @@ __global__ void k_schur_reduce(const int *__restrict__ blk_jk, const int *__rest
             const double u = U[(size_t)NA * NA * j + r + NA * c];
             acc = (r == c) ? (1 + lambda) * u : u;
         }
-        for (int q = blk_sptr[bk]; q < blk_sptr[bk + 1]; q++)
-            acc -= spart[(size_t)NA * NA * blk_slots[q] + l];
+        // 8 independent loads in flight, subtracted in slot order (same result)
+        int q = blk_sptr[bk];
+        const int qe = blk_sptr[bk + 1];
+        for (; q + 8 <= qe; q += 8) {
+            double v[8];
+#pragma unroll
+            for (int t = 0; t < 8; t++) v[t] = spart[(size_t)NA * NA * blk_slots[q + t] + l];
+#pragma unroll
+            for (int t = 0; t < 8; t++) acc -= v[t];
+        }
+        for (; q < qe; q++) acc -= spart[(size_t)NA * NA * blk_slots[q] + l];
         sblk[(size_t)NA * NA * bk + l] = acc;
     } else if (j == k && l < NA * NA + NA) {
         const int r = l - NA * NA;
         double acc = owner ? eA[(size_t)NA * j + r] : 0.0;
-        for (int q = cam_eptr[j]; q < cam_eptr[j + 1]; q++)
-            acc -= epart[(size_t)NA * cam_eslots[q] + r];
+        int q = cam_eptr[j];
+        const int qe = cam_eptr[j + 1];
+        for (; q + 8 <= qe; q += 8) {
+            double v[8];
+#pragma unroll
+            for (int t = 0; t < 8; t++) v[t] = epart[(size_t)NA * cam_eslots[q + t] + r];
+#pragma unroll
+            for (int t = 0; t < 8; t++) acc -= v[t];
+        }
+        for (; q < qe; q++) acc -= epart[(size_t)NA * cam_eslots[q] + r];
         rhs[(size_t)NA * j + r] = acc;
     }
 }
