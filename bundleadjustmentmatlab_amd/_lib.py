@@ -81,6 +81,7 @@ SIGNATURES = {
     "vlgba_version": (c_int, [ctypes.c_char_p, c_int]),
     "vlgba_get_unique_id": (c_int, [ctypes.c_void_p]),
     "vlgba_device_count": (c_int, []),
+    "vlgba_debug_sincos": (c_int, [c_dp, c_dp, c_dp, c_ll]),
 }
 
 ERRORS = {-1001: "bad argument",

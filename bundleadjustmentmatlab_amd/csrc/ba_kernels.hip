@@ -12,8 +12,8 @@
 //   k_linearize_chunk  fast path: linearisation per chunk of points + U/eA partials
 //   k_schur_group      fast path: damp + V*^-1 + Y + S / e_ partials per group of chunks
 //   k_assemble         dense S for the reduced solve (bundle_euclid.m:193)
-//   k_camera_update    mex_bundle_3_db_new.c:294-298 (a_new) + rotations of a_new
-//   k_point_update     mex_bundle_3_db_new.c:257-324 (db, b_new, new projections)
+//   k_camera_update    mex_bundle_3_db_new.c:137-140 (a_new) + rotations of a_new
+//   k_point_update     mex_bundle_3_db_new.c:99-166 (db, b_new, new projections)
 //                      and the cost / rho terms of bundle_euclid.m:205-217
 //
 // Parity: every per-element expression keeps the reference's operation order,
@@ -25,6 +25,7 @@
 // use tree reductions (MATLAB's BLAS dot order is unknowable anyway).
 #include "ba_internal.h"
 #include "vlg_math.h"
+#include "../../include/vlgba.h"
 
 #define H_FD VLG_FD_H
 
@@ -260,6 +261,38 @@ __global__ void k_rotations(const double *__restrict__ a, double *__restrict__ r
     const double *aj = a + (size_t)NA * j;
     const double w[3] = {aj[0], aj[1], aj[2]};
     rotations5(w, rot + 45 * (size_t)j);
+}
+
+// device sin / cos of the rotations (vlg_libm.h), exported for the parity
+// test that compares them with the host libm (vlgba_debug_sincos)
+__global__ void k_sincos(const double *__restrict__ x, double *__restrict__ s,
+                         double *__restrict__ c, long long n)
+{
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double v = x[i];
+    s[i] = vlg_lm_sin(v);
+    c[i] = vlg_lm_cos(v);
+}
+
+extern "C" int vlgba_debug_sincos(const double *x, double *s, double *c, long long n)
+{
+    if (n < 0 || (n > 0 && (!x || !s || !c))) return VLGBA_E_ARG;
+    if (n == 0) return 0;
+    double *d = nullptr;
+    VLGBA_CHECK(hipMalloc(&d, sizeof(double) * 3 * (size_t)n));
+    int rc = 0;
+    do {
+        if (hipMemcpy(d, x, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess) { rc = -1; break; }
+        const long long nb = (n + 255) / 256;
+        hipLaunchKernelGGL(k_sincos, dim3((unsigned)nb), dim3(256), 0, 0, d, d + n, d + 2 * n, n);
+        if (hipGetLastError() != hipSuccess) { rc = -1; break; }
+        if (hipMemcpy(s, d + n, sizeof(double) * n, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(c, d + 2 * n, sizeof(double) * n, hipMemcpyDeviceToHost) != hipSuccess)
+            rc = -1;
+    } while (0);
+    (void)hipFree(d);
+    return rc;
 }
 
 // -------------------------------------------------------------------------
@@ -1272,7 +1305,7 @@ __global__ void k_assemble(const int *__restrict__ blk_jk, const double *__restr
 }
 
 // -------------------------------------------------------------------------
-// camera update: a_new = a + da (mex_bundle_3_db_new.c:294-298), the rotation
+// camera update: a_new = a + da (mex_bundle_3_db_new.c:137-140), the rotation
 // table of a_new (R(a_new), R(a_new + h e_k), R(a_new + 0): k_rotations' five,
 // so an accepted step swaps it in and the next linearisation needs no
 // rotation launch), and the camera part of dp'(lambda dp + g)

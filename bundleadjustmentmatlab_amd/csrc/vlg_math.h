@@ -1,31 +1,33 @@
 /*
- * vlg_math.h -- deterministic fp64 math shared by the gfx950 kernels and the CPU oracle.
+ * vlg_math.h -- deterministic fp64 math of the gfx950 kernels (product code;
+ * the CPU oracle restates the same reference formulas independently with the
+ * host libm and never includes this file).
  *
  * Why this file exists
  * --------------------
  * The reference builds every Jacobian by forward differences with h = 1e-10
  * (toolbox/bundle/mex_bundle_1_XABeUVWeAeB.c:23,39-40,52,68-69).  A one-ulp
  * difference in a projection is amplified by 1/h, so the device projection has
- * to be bit-identical to the CPU oracle.  Device OCML sin/cos and host glibc
- * sin/cos may disagree by an ulp, so both sides use the SAME sin/cos defined
- * here (fdlibm-style: Cody-Waite reduction by pi/2 plus the published minimax
- * kernels), compiled with -ffp-contract=off on both sides and IEEE division
- * and sqrt (HIP f64 '/' and sqrt are correctly rounded).
+ * to be bit-identical to the reference arithmetic: the rotations use glibc's
+ * own sin / cos algorithm (vlg_libm.h, equal to the host libm bit for bit),
+ * every expression keeps the reference's evaluation order, the kernels are
+ * compiled with -ffp-contract=off, and '/' and sqrt are IEEE (HIP f64 '/' and
+ * sqrt are correctly rounded).
  *
  * Contents
- *   vlg_sin / vlg_cos       deterministic sin / cos (< 1 ulp, see tests)
  *   vlg_rodrigues           VLFeat vl_rodrigues (R only), SURVEY.md App. B,
  *                           called from toolbox/bundle/reproject_point.h:44
- *   vlg_project             toolbox/bundle/reproject_point.h:16-57 with the
+ *   vlg_calib, vlg_project  toolbox/bundle/reproject_point.h:16-57 with the
  *                           rotation supplied by the caller (so a kernel can
  *                           hoist the per-camera Rodrigues out of the
  *                           per-observation loop without changing a bit)
  *   vlg_project_proj        reproject_projective_point of
  *                           toolbox/bundle/mex_bundle_proj_1_XABeUVWeAeB.c:13-32
+ *   vlg_fd_quot             (x1 - x0) / h without a division, bit-identical
+ *   vlg_pinv3               3x3 pseudo-inverse of the damped point blocks
  *
  * Every expression keeps the reference's evaluation order.
- * Include from C99, C++ or HIP.  Define VLG_ORACLE_LIBM to make the oracle use
- * the host libm sin/cos instead (used only to quantify the libm gap in tests).
+ * Include from C99, C++ or HIP.
  */
 #ifndef VLG_MATH_H
 #define VLG_MATH_H
@@ -40,123 +42,12 @@
 #include <string.h>
 #include <math.h>
 
-/* ---- bit helpers ------------------------------------------------------- */
-VLG_HD uint32_t vlg_high_word(double x)
-{
-    uint64_t u;
-    memcpy(&u, &x, sizeof u);
-    return (uint32_t)(u >> 32);
-}
+#include "vlg_libm.h"
 
-/* ---- minimax kernels on [-pi/4, pi/4] (fdlibm k_sin.c / k_cos.c constants) */
-VLG_HD double vlg_ksin(double x, double y, int iy)
-{
-    const double S1 = -1.66666666666666324348e-01;
-    const double S2 = 8.33333333332248946124e-03;
-    const double S3 = -1.98412698298579493134e-04;
-    const double S4 = 2.75573137070700676789e-06;
-    const double S5 = -2.50507602534068634195e-08;
-    const double S6 = 1.58969099521155010221e-10;
-    double z = x * x;
-    double w = z * z;
-    double r = S2 + z * (S3 + z * S4) + z * w * (S5 + z * S6);
-    double v = z * x;
-    if (iy == 0)
-        return x + v * (S1 + z * r);
-    return x - ((z * (0.5 * y - v * r) - y) - v * S1);
-}
-
-VLG_HD double vlg_kcos(double x, double y)
-{
-    const double C1 = 4.16666666666666019037e-02;
-    const double C2 = -1.38888888888741095749e-03;
-    const double C3 = 2.48015872894767294178e-05;
-    const double C4 = -2.75573143513906633035e-07;
-    const double C5 = 2.08757232129817482790e-09;
-    const double C6 = -1.13596475577881948265e-11;
-    double z = x * x;
-    double w = z * z;
-    double r = z * (C1 + z * (C2 + z * C3)) + w * w * (C4 + z * (C5 + z * C6));
-    double hz = 0.5 * z;
-    double t = 1.0 - hz;
-    return t + (((1.0 - t) - hz) + (z * r - x * y));
-}
-
-/* Cody-Waite reduction x = n*pi/2 + (y0 + y1), three rounds (fdlibm e_rem_pio2.c
- * "medium" path).  Exact enough for |x| < 2^20*pi/2; rotation angles are tiny
- * compared with that.  Returns n. */
-VLG_HD int vlg_rem_pio2(double x, double *y0, double *y1)
-{
-    const double invpio2 = 6.36619772367581382433e-01;
-    const double pio2_1 = 1.57079632673412561417e+00;
-    const double pio2_1t = 6.07710050650619224932e-11;
-    const double pio2_2 = 6.07710050630396597660e-11;
-    const double pio2_2t = 2.02226624879595063154e-21;
-    const double pio2_3 = 2.02226624871116645580e-21;
-    const double pio2_3t = 8.47842766036889956997e-32;
-    const double toint = 6755399441055744.0; /* 1.5 * 2^52 : round to nearest */
-    double fn = (x * invpio2 + toint) - toint;
-    int n = (int)fn;
-    double r = x - fn * pio2_1;
-    double w = fn * pio2_1t;
-    int j = (int)((vlg_high_word(x) >> 20) & 0x7ff);
-    double t;
-    *y0 = r - w;
-    if (j - (int)((vlg_high_word(*y0) >> 20) & 0x7ff) > 16) {
-        t = r;
-        w = fn * pio2_2;
-        r = t - w;
-        w = fn * pio2_2t - ((t - r) - w);
-        *y0 = r - w;
-        if (j - (int)((vlg_high_word(*y0) >> 20) & 0x7ff) > 49) {
-            t = r;
-            w = fn * pio2_3;
-            r = t - w;
-            w = fn * pio2_3t - ((t - r) - w);
-            *y0 = r - w;
-        }
-    }
-    *y1 = (r - *y0) - w;
-    return n;
-}
-
-VLG_HD double vlg_sin(double x)
-{
-    double y0, y1;
-    int n;
-    if ((vlg_high_word(x) & 0x7fffffffu) <= 0x3fe921fbu)
-        return vlg_ksin(x, 0.0, 0);
-    n = vlg_rem_pio2(x, &y0, &y1);
-    switch (n & 3) {
-    case 0: return vlg_ksin(y0, y1, 1);
-    case 1: return vlg_kcos(y0, y1);
-    case 2: return -vlg_ksin(y0, y1, 1);
-    default: return -vlg_kcos(y0, y1);
-    }
-}
-
-VLG_HD double vlg_cos(double x)
-{
-    double y0, y1;
-    int n;
-    if ((vlg_high_word(x) & 0x7fffffffu) <= 0x3fe921fbu)
-        return vlg_kcos(x, 0.0);
-    n = vlg_rem_pio2(x, &y0, &y1);
-    switch (n & 3) {
-    case 0: return vlg_kcos(y0, y1);
-    case 1: return -vlg_ksin(y0, y1, 1);
-    case 2: return -vlg_kcos(y0, y1);
-    default: return vlg_ksin(y0, y1, 1);
-    }
-}
-
-#if defined(VLG_ORACLE_LIBM) && !defined(__HIPCC__)
-#define VLG_SIN sin
-#define VLG_COS cos
-#else
-#define VLG_SIN vlg_sin
-#define VLG_COS vlg_cos
-#endif
+/* sin / cos of the rotations: glibc's algorithm (vlg_libm.h), bit-identical to
+ * the host libm that VLFeat's vl_rodrigues -- and the oracle -- call */
+#define VLG_SIN vlg_lm_sin
+#define VLG_COS vlg_lm_cos
 
 /* ---- Rodrigues: rotation vector -> R (3x3, column major R[i + 3*j]) --------
  * VLFeat vl_rodrigues (not vendored; spec recovered in SURVEY.md App. B):

@@ -197,7 +197,7 @@ int vlgba_mex_bundle_2(int m, int n, int num_a, const double *Y, const double *W
                        double *e_);
 
 /* [db a_new b_new X_hat] = mex_bundle_3_db_new(W, da, eB, V_inv, K, a, b, X, visible)
- * replaces toolbox/bundle/mex_bundle_3_db_new.c:170-328 (db uses da(1:6,j)
+ * replaces toolbox/bundle/mex_bundle_3_db_new.c:12-170 (db :99-134 uses da(1:6,j)
  * only, as the reference does). */
 int vlgba_mex_bundle_3(int m, int n, int num_a, const double *W, const double *da,
                        const double *eB, const double *Vinv, const double *K, const double *a,
@@ -228,6 +228,11 @@ int vlgba_mex_bundle_proj_3(int m, int n, const double *W, const double *da, con
 /* Multi-GPU: rank 0 creates the 128-byte RCCL unique id, the caller
  * broadcasts it (e.g. torch.distributed) and passes it as opt->comm_id. */
 int vlgba_get_unique_id(void *id128);
+
+/* Diagnostics: the device sin / cos the rotation tables use (glibc's
+ * algorithm, vlg_libm.h) for n host arguments -- the parity tests compare them
+ * with the host libm bit for bit.  |x| < 105414350. */
+int vlgba_debug_sincos(const double *x, double *s, double *c, long long n);
 
 /* Library / device info: writes a NUL-terminated string, returns its length. */
 int vlgba_version(char *buf, int len);

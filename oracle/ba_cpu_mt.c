@@ -7,7 +7,7 @@
  *
  * The per-element arithmetic is ba_oracle.c's (the MEX stages'
  * mex_bundle_1_XABeUVWeAeB.c:192-334, mex_bundle_2_Se_.c:72-155,
- * mex_bundle_3_db_new.c:99-166, shared vlg_math.h), on the point-major COO
+ * mex_bundle_3_db_new.c:99-166, orc_math.h), on the point-major COO
  * observation list, parallelised with OpenMP so that every reduction keeps the
  * reference's ascending order: points in parallel for the per-observation
  * work and V_i / eB_i / db_i; cameras in parallel for U_j / eA_j (camera-major
@@ -18,7 +18,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <math.h>
-#include "../bundleadjustmentmatlab_amd/csrc/vlg_math.h"
+#include "orc_math.h"
 
 #include <omp.h>
 
@@ -26,12 +26,10 @@
 
 int mt_threads(void) { return omp_get_max_threads(); }
 
+/* reproject_point (num_variableK = 0): Rodrigues per call, as the reference */
 static void proj6(const double *K4, const double *a, const double *b, double x[2])
 {
-    double Kc[9], R[9];
-    vlg_calib(Kc, K4, a, 0);
-    vlg_rodrigues(R, a);
-    vlg_project(Kc, R, a + 3, b, x);
+    orc_reproject(K4, a, b, 0, x);
 }
 
 /* stage 1: A | B | e per observation (jrec[N][20]), W[N][18], V[9n], eB[3n];
@@ -54,16 +52,16 @@ double mt_linearize(int n, const int *pt_ptr, const int *obs_cam, const double *
             double *A = jrec + 20 * (size_t)o, *B = A + 12, *e = A + 18;
             proj6(k4, aj, bi, xh);
             for (k = 0; k < MT_NA; k++) {
-                for (c = 0; c < MT_NA; c++) a1[c] = aj[c] + VLG_FD_H * (c == k ? 1.0 : 0.0);
+                for (c = 0; c < MT_NA; c++) a1[c] = aj[c] + ORC_FD_H * (c == k ? 1.0 : 0.0);
                 proj6(k4, a1, bi, x1);
-                A[2 * k] = (x1[0] - xh[0]) / VLG_FD_H;
-                A[2 * k + 1] = (x1[1] - xh[1]) / VLG_FD_H;
+                A[2 * k] = (x1[0] - xh[0]) / ORC_FD_H;
+                A[2 * k + 1] = (x1[1] - xh[1]) / ORC_FD_H;
             }
             for (k = 0; k < 3; k++) {
-                for (c = 0; c < 3; c++) b1[c] = bi[c] + VLG_FD_H * (c == k ? 1.0 : 0.0);
+                for (c = 0; c < 3; c++) b1[c] = bi[c] + ORC_FD_H * (c == k ? 1.0 : 0.0);
                 proj6(k4, aj, b1, x1);
-                B[2 * k] = (x1[0] - xh[0]) / VLG_FD_H;
-                B[2 * k + 1] = (x1[1] - xh[1]) / VLG_FD_H;
+                B[2 * k] = (x1[0] - xh[0]) / ORC_FD_H;
+                B[2 * k + 1] = (x1[1] - xh[1]) / ORC_FD_H;
             }
             e[0] = obs_x[2 * (size_t)o] - xh[0];
             e[1] = obs_x[2 * (size_t)o + 1] - xh[1];
@@ -104,7 +102,7 @@ void mt_camera_reduce(int m, const int *cam_ptr, const int *cam_obs, const doubl
     }
 }
 
-/* damping, V*^-1 (vlg_pinv3), Y = W V*^-1 */
+/* damping, V*^-1 (formula pinv, orc_math.h), Y = W V*^-1 */
 void mt_damp_y(int n, const int *pt_ptr, double lambda, const double *V, const double *W,
                double *Vinv, double *Y)
 {
@@ -115,7 +113,7 @@ void mt_damp_y(int n, const int *pt_ptr, double lambda, const double *V, const d
         int o, r, c, k;
         memcpy(vs, V + 9 * (size_t)i, sizeof vs);
         for (k = 0; k < 3; k++) vs[4 * k] = (1 + lambda) * V[9 * (size_t)i + 4 * k];
-        vlg_pinv3(vs, vi);
+        orc_pinv3_formula(vs, vi);
         for (o = pt_ptr[i]; o < pt_ptr[i + 1]; o++) {
             const double *w = W + 18 * (size_t)o;
             double *y = Y + 18 * (size_t)o;

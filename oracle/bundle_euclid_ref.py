@@ -14,7 +14,8 @@ Knobs (all default to the reference's semantics):
           'sparse' -> oracle_sp_* on the point-major observation list
   vinv  = 'pinv'   -> MATLAB pinv of each damped 3x3 block (SVD, tol =
                       max(size)*eps(sigma_max)), bundle_euclid.m:180
-          'formula'-> the device's closed-form vlg_pinv3 (bit-exact chain)
+          'formula'-> the closed-form 3x3 pinv the GPU uses, restated in
+                      oracle/orc_math.h (bit-exact chain; bounded vs 'pinv')
   solve = 'pinv'   -> da = pinv(S) * e_ (bundle_euclid.m:193)
           'chol'   -> Cholesky with exact-zero rows fixed (the device's rule)
 """
@@ -41,10 +42,6 @@ def _lib(variant: str = ""):
         lib = ctypes.CDLL(path)
         lib.oracle_sp_update.restype = ctypes.c_double
         lib.oracle_sp_update_nd.restype = ctypes.c_double
-        lib.oracle_sin.restype = ctypes.c_double
-        lib.oracle_cos.restype = ctypes.c_double
-        lib.oracle_sin.argtypes = [ctypes.c_double]
-        lib.oracle_cos.argtypes = [ctypes.c_double]
         _LIBS[variant] = lib
     return _LIBS[variant]
 
@@ -147,7 +144,7 @@ def chol_solve_fixed(S, e_):
 
 
 def pinv3_formula(Vs, lib=None):
-    """The device's vlg_pinv3 applied to each (3,3,i) block."""
+    """orc_pinv3_formula (oracle/orc_math.h) applied to each (3,3,i) block."""
     lib = lib or _lib()
     Vs = F(Vs)
     out = np.zeros_like(Vs, order="F")

@@ -2,7 +2,7 @@
 
 TEST INFRASTRUCTURE ONLY (cross-check of the C oracle; never imported by the
 product).  Follows the reference's pure-MATLAB twin, vectorised over the
-visible observations, with host-libm rotations (numpy sin/cos) and numpy's
+visible observations, with host-libm rotations (math.sin/cos) and numpy's
 own reductions, so it shares no arithmetic code path with ba_oracle.c:
 
   reprojection_point.m:11-22, derivative_camera.m:9-13 / derivative_point.m:9-13
@@ -13,6 +13,8 @@ own reductions, so it shares no arithmetic code path with ba_oracle.c:
   Xe_(4,:) = 1, App. A Q5).
 """
 from __future__ import annotations
+
+import math
 
 import numpy as np
 
@@ -25,7 +27,9 @@ def _rodrigues(w):
     small = th < 1e-6
     ths = np.where(small, 1.0, th)
     x, y, z = (w / ths[:, None]).T
-    s, c = np.sin(th), np.cos(th)
+    # glibc sin / cos one argument at a time (numpy's vectorised sin is not libm)
+    s = np.array([math.sin(t) for t in th])
+    c = np.array([math.cos(t) for t in th])
     mc = 1.0 - c
     R = np.empty((w.shape[0], 3, 3))
     R[:, 0, 0] = 1 - mc * (y * y + z * z)

@@ -124,3 +124,15 @@ def test_product_does_not_touch_oracle():
                 for bad in ("bundle_euclid_ref", "ba_oracle", "nomex_numpy", "libba_oracle",
                             "oracle/"):
                     assert bad not in txt, (f, bad)
+
+
+def test_oracle_does_not_include_product_headers():
+    """The CPU oracle restates the reference on its own (it used to
+    compile the product's vlg_math.h, so its bit-exact claims compared the code
+    with itself)."""
+    odir = os.path.join(ROOT, "oracle")
+    for f in os.listdir(odir):
+        if f.endswith((".c", ".h", "Makefile")):
+            for line in open(os.path.join(odir, f)):
+                if "#include" in line or ".h" in line and ":" in line and "$(" in line:
+                    assert "bundleadjustmentmatlab_amd" not in line and "vlg_" not in line, (f, line)
