@@ -57,13 +57,13 @@ class VlgbaStepInfo(ctypes.Structure):
 # name -> (restype, argtypes); must match include/vlgba.h exactly
 SIGNATURES = {
     "vlgba_solve": (c_int, [ctypes.POINTER(VlgbaProblem), ctypes.POINTER(VlgbaOptions), c_dp,
-                            c_dp, c_dp, ctypes.POINTER(VlgbaStats)]),
+                            c_dp, c_dp, c_int, ctypes.POINTER(VlgbaStats)]),
     "vlgba_create": (c_int, [ctypes.POINTER(VlgbaProblem), ctypes.POINTER(VlgbaOptions),
                              ctypes.POINTER(ctypes.c_void_p)]),
     "vlgba_set_params": (c_int, [ctypes.c_void_p, c_dp, c_dp]),
     "vlgba_get_params": (c_int, [ctypes.c_void_p, c_dp, c_dp]),
     "vlgba_step": (c_int, [ctypes.c_void_p, c_int, c_int, ctypes.POINTER(VlgbaStepInfo)]),
-    "vlgba_run": (c_int, [ctypes.c_void_p, c_dp, ctypes.POINTER(VlgbaStats)]),
+    "vlgba_run": (c_int, [ctypes.c_void_p, c_dp, c_int, ctypes.POINTER(VlgbaStats)]),
     "vlgba_get_linearization": (c_int, [ctypes.c_void_p, c_dp, c_dp, c_dp, c_dp, c_dp]),
     "vlgba_sync": (c_int, [ctypes.c_void_p]),
     "vlgba_destroy": (None, [ctypes.c_void_p]),

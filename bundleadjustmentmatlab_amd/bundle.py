@@ -141,6 +141,7 @@ class BundleAdjuster:
         self.m = int(m) if m is not None else self.K.shape[1]
         self.n = int(n)
         self.num_a = int(num_a)
+        self.max_iter = int(max_iter) if max_iter > 0 else 20   # bundle_euclid.m:117
         self._pt = np.ascontiguousarray(obs_pt, dtype=np.int32)
         self._cam = np.ascontiguousarray(obs_cam, dtype=np.int32)
         self._x = np.ascontiguousarray(obs_x, dtype=np.float64).reshape(-1, 2)
@@ -215,10 +216,13 @@ class BundleAdjuster:
               "vlgba_step")
         return info
 
-    def run(self, max_err=64):
-        err = np.zeros(max_err)
+    def run(self):
+        """The LM loop (vlgba_run): (error_, stats).  error_ has at most
+        max_iter entries (bundle_euclid.m:117-123)."""
+        err = np.zeros(self.max_iter + 1)
         st = VlgbaStats()
-        check(self._L.vlgba_run(self._h, _dp(err), ctypes.byref(st)), "vlgba_run")
+        check(self._L.vlgba_run(self._h, _dp(err), err.size, ctypes.byref(st)), "vlgba_run")
+        assert st.num_error <= err.size
         return err[: st.num_error].copy(), st
 
     def sync(self):

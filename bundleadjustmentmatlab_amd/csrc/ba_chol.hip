@@ -1487,25 +1487,12 @@ int ba_chol_solve(ba_dev *d)
     const int nt = d->nt;
     const size_t smem = sizeof(double) * 2 * NB * LP;
     const size_t smem3 = sizeof(double) * 3 * NB * LP;
-    static bool attr_done = false;
-    if (!attr_done) {
-        VLGBA_CHECK(hipFuncSetAttribute((const void *)k_factor_panel,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem3));
-        VLGBA_CHECK(hipFuncSetAttribute((const void *)k_cr_factor,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem3));
-        VLGBA_CHECK(hipFuncSetAttribute((const void *)k_cr_update,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem3));
-        VLGBA_CHECK(hipFuncSetAttribute((const void *)k_syrk,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-        attr_done = true;
-    }
+    TRY_RC(ba_ensure_dyn_lds((const void *)k_factor_panel, smem3));
+    TRY_RC(ba_ensure_dyn_lds((const void *)k_cr_factor, smem3));
+    TRY_RC(ba_ensure_dyn_lds((const void *)k_cr_update, smem3));
+    TRY_RC(ba_ensure_dyn_lds((const void *)k_syrk, smem));
     if (d->cr_nlev > 0 && d->cr32) {   // camera-aligned 32-row tiles
-        static int ncu32 = 0;
-        if (!ncu32) {
-            int dev = 0;
-            VLGBA_CHECK(hipGetDevice(&dev));
-            VLGBA_CHECK(hipDeviceGetAttribute(&ncu32, hipDeviceAttributeMultiprocessorCount, dev));
-        }
+        const int ncu32 = d->ncu;
         const int n32 = d->nt32, TB = d->tb32;
         {   // level 0 on the assembled S
             const int ne = d->cr_eptr_h[1];
@@ -1539,12 +1526,7 @@ int ba_chol_solve(ba_dev *d)
         // one workgroup per CU (LDS): fan a level out over 5 (factor) / 4
         // (update) workgroups per tile while that still fits in one wave of
         // workgroups -- the levels are latency bound, the chip mostly idle
-        static int ncu = 0;
-        if (!ncu) {
-            int dev = 0;
-            VLGBA_CHECK(hipGetDevice(&dev));
-            VLGBA_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-        }
+        const int ncu = d->ncu;
         for (int l = 0; l < d->cr_nlev; l++) {
             const int e0 = d->cr_eptr_h[l], ne = d->cr_eptr_h[l + 1] - e0;
             const int k0 = d->cr_kptr_h[l], nk = d->cr_kptr_h[l + 1] - k0;

@@ -62,6 +62,7 @@ struct ba_flags {
 
 struct ba_dev {
     int m, n, na, N, js;
+    int device, ncu;   // HIP device ordinal and its CU count
     // problem (read-only)
     int *obs_cam, *pt_ptr, *cam_ptr, *cam_obs;
     double *obs_x, *K4;
@@ -207,6 +208,9 @@ int ba_launch_update(ba_dev *d, double lambda);
 int ba_launch_yeb(ba_dev *d);
 int ba_launch_publish(ba_dev *d);
 void *ba_dmalloc(size_t bytes);   // per-device caching allocator (ba_solver.cpp)
+// raise kernel fn's dynamic-LDS limit to >= bytes on the current device (cached
+// per (kernel, device), thread-safe; ba_solver.cpp)
+int ba_ensure_dyn_lds(const void *fn, size_t bytes);
 void ba_dfree(void *p);   // scal[0..4] + ++seq -> hres (host-mapped)
 int ba_launch_schur_fast(ba_dev *d, double lambda);   // fused damp + Vinv + Y + S + e_
 int ba_launch_assemble_plain(ba_dev *d, double *S, long long ld);

@@ -1673,13 +1673,7 @@ static int launch_schur_fast(ba_dev *d, double lambda)
         KT_E(d, KT_DAMP);
         const size_t sm2 = sizeof(double) * (gcap * NA * NA + ecap * NA) +
                            sizeof(unsigned) * (size_t)bcap;
-        static size_t attr2 = 0;
-        if (sm2 > attr2) {
-            VLGBA_CHECK(hipFuncSetAttribute((const void *)k_schur_mfma<NA>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            (int)sm2));
-            attr2 = sm2;
-        }
+        TRY_RC(ba_ensure_dyn_lds((const void *)k_schur_mfma<NA>, sm2));
         KT_B(d);
         if (d->ngrp > 0)
             k_schur_mfma<NA><<<d->ngrp, 256, sm2, d->stream>>>(
@@ -1691,12 +1685,7 @@ static int launch_schur_fast(ba_dev *d, double lambda)
                                     ecap * NA) +
                   sizeof(unsigned) * bcap;
     smem = (smem + 15) & ~(size_t)15;
-    static size_t attr = 0;
-    if (smem > attr) {
-        VLGBA_CHECK(hipFuncSetAttribute((const void *)k_schur_group<NA>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-        attr = smem;
-    }
+    TRY_RC(ba_ensure_dyn_lds((const void *)k_schur_group<NA>, smem));
     KT_B(d);
     if (d->ngrp > 0)
         k_schur_group<NA><<<d->ngrp, 256, smem, d->stream>>>(

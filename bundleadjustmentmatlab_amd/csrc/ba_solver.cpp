@@ -107,6 +107,22 @@ void ba_dfree(void *p)
     g_mem_free.emplace(key, p);
 }
 
+int ba_ensure_dyn_lds(const void *fn, size_t bytes)
+{
+    static std::mutex mu;
+    static std::map<std::pair<const void *, int>, size_t> done;
+    int dev = 0;
+    VLGBA_CHECK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(mu);
+    size_t &have = done[{fn, dev}];
+    if (bytes > have) {
+        VLGBA_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)bytes));
+        have = bytes;
+    }
+    return 0;
+}
+
 namespace {
 
 template <typename T>
@@ -744,6 +760,8 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
 {
     ba_dev &d = c->d;
     const int na = p->num_a;
+    d.device = c->aux.device;
+    VLGBA_CHECK(hipDeviceGetAttribute(&d.ncu, hipDeviceAttributeMultiprocessorCount, d.device));
     d.m = p->m;
     d.na = na;
     d.js = 2 * na + 2;
@@ -1197,6 +1215,13 @@ static void lm_apply(vlgba_ctx *c, const vlgba_step_info *info)
     }
 }
 
+// every handle entry point runs on the context's device, whatever the calling
+// thread's current device is (allocations and launches follow hipGetDevice)
+static int ctx_enter(vlgba_ctx *c)
+{
+    return hipSetDevice(c->aux.device) == hipSuccess ? 0 : VLGBA_E_ARG;
+}
+
 // =========================================================================
 // C ABI
 // =========================================================================
@@ -1235,11 +1260,16 @@ int vlgba_create(const vlgba_problem *prob, const vlgba_options *opt, vlgba_ctx 
     return ctx_create(prob, opt, out, true, true, false);
 }
 
-void vlgba_destroy(vlgba_ctx *ctx) { ctx_free(ctx); }
+void vlgba_destroy(vlgba_ctx *ctx)
+{
+    if (ctx) (void)ctx_enter(ctx);
+    ctx_free(ctx);
+}
 
 int vlgba_set_params(vlgba_ctx *c, const double *a, const double *b)
 {
     if (!c || !a || !b) return VLGBA_E_ARG;
+    TRY(ctx_enter(c));
     TRY(upload(c->d.a, a, (size_t)c->d.ld, c->d.stream));
     TRY(upload(c->d.b, b + 3 * (size_t)c->p0, 3 * (size_t)c->d.n, c->d.stream));
     TRY(ba_launch_rotations(&c->d, c->d.a, c->d.rot, 1));
@@ -1251,6 +1281,7 @@ int vlgba_set_params(vlgba_ctx *c, const double *a, const double *b)
 int vlgba_get_params(vlgba_ctx *c, double *a, double *b)
 {
     if (!c) return VLGBA_E_ARG;
+    TRY(ctx_enter(c));
     if (a) TRY(download(a, c->d.a, (size_t)c->d.ld, c->d.stream));
     if (b) {
         if (c->world > 1) {
@@ -1278,6 +1309,7 @@ int vlgba_get_linearization(vlgba_ctx *c, double *U, double *eA, double *V, doub
                             double *W)
 {
     if (!c) return VLGBA_E_ARG;
+    TRY(ctx_enter(c));
     ba_dev &d = c->d;
     TRY(ba_launch_rotations(&d, d.a, d.rot, 1));
     TRY(ba_launch_linearize(&d, c->flags));
@@ -1299,6 +1331,7 @@ int vlgba_get_linearization(vlgba_ctx *c, double *U, double *eA, double *V, doub
 int vlgba_set_timing(vlgba_ctx *c, int on)
 {
     if (!c) return VLGBA_E_ARG;
+    TRY(ctx_enter(c));
     if (on && !c->ev[0])
         for (auto &e : c->ev) VLGBA_CHECK(hipEventCreate(&e));
     if (on && !c->d.kt) {
@@ -1360,6 +1393,7 @@ int vlgba_phase_ms(vlgba_ctx *c, double *ms7)
 int vlgba_sync(vlgba_ctx *c)
 {
     if (!c) return VLGBA_E_ARG;
+    TRY(ctx_enter(c));
     VLGBA_CHECK(hipStreamSynchronize(c->d.stream));
     return 0;
 }
@@ -1367,6 +1401,7 @@ int vlgba_sync(vlgba_ctx *c)
 int vlgba_step(vlgba_ctx *c, int relinearize, int update_lm, vlgba_step_info *info)
 {
     if (!c) return VLGBA_E_ARG;
+    TRY(ctx_enter(c));
     vlgba_step_info tmp;
     if (!info) info = &tmp;
     TRY(lm_pass(c, relinearize, info));
@@ -1375,9 +1410,10 @@ int vlgba_step(vlgba_ctx *c, int relinearize, int update_lm, vlgba_step_info *in
 }
 
 // bundle_euclid.m:111-249
-int vlgba_run(vlgba_ctx *c, double *error_out, vlgba_stats *stats)
+int vlgba_run(vlgba_ctx *c, double *error_out, int error_cap, vlgba_stats *stats)
 {
-    if (!c) return VLGBA_E_ARG;
+    if (!c || (error_out && error_cap < 0)) return VLGBA_E_ARG;
+    TRY(ctx_enter(c));
     auto t0 = std::chrono::steady_clock::now();
     c->lambda = c->lambda0;
     c->nu = 2.0;
@@ -1412,8 +1448,8 @@ int vlgba_run(vlgba_ctx *c, double *error_out, vlgba_stats *stats)
         lm_apply(c, &info);
     }
     VLGBA_CHECK(hipStreamSynchronize(c->d.stream));
-    if (error_out)
-        for (size_t q = 0; q < err.size(); q++) error_out[q] = err[q];
+    if (error_out)   // at most error_cap entries; stats->num_error is the full count
+        for (size_t q = 0; q < err.size() && q < (size_t)error_cap; q++) error_out[q] = err[q];
     if (stats) {
         stats->iterations = passes;
         stats->accepted = acc;
@@ -1426,13 +1462,13 @@ int vlgba_run(vlgba_ctx *c, double *error_out, vlgba_stats *stats)
 }
 
 int vlgba_solve(const vlgba_problem *prob, const vlgba_options *opt, double *a, double *b,
-                double *error_out, vlgba_stats *stats)
+                double *error_out, int error_cap, vlgba_stats *stats)
 {
     if (!a || !b) return VLGBA_E_ARG;
     vlgba_ctx *c = nullptr;
     TRY(vlgba_create(prob, opt, &c));
     int rc = vlgba_set_params(c, a, b);
-    if (!rc) rc = vlgba_run(c, error_out, stats);
+    if (!rc) rc = vlgba_run(c, error_out, error_cap, stats);
     if (!rc) rc = vlgba_get_params(c, a, b);
     vlgba_destroy(c);
     return rc;

@@ -128,10 +128,11 @@ typedef struct vlgba_ctx vlgba_ctx;
 /* ---- fused solver: the whole bundle_euclid.m LM loop on the GPU -----------
  * Replaces bundle_euclid.m:111-249 (and its three MEX calls :139,192,204).
  * a (num_a*m) and b (3*n) are read as the start point and overwritten with
- * the result.  error_out (>= max_iter+1 doubles, may be NULL) receives
- * error_ (SSE / num_vis per accepted step, :219-231). */
+ * the result.  error_out (may be NULL) receives error_ (SSE / num_vis per
+ * accepted step, :219-231): at most error_cap entries are written (error_ has
+ * at most max_iter entries; stats->num_error is its full length). */
 int vlgba_solve(const vlgba_problem *prob, const vlgba_options *opt, double *a, double *b,
-                double *error_out, vlgba_stats *stats);
+                double *error_out, int error_cap, vlgba_stats *stats);
 
 /* ---- handle API -------------------------------------------------------- */
 int vlgba_create(const vlgba_problem *prob, const vlgba_options *opt, vlgba_ctx **out);
@@ -149,7 +150,9 @@ int vlgba_step(vlgba_ctx *ctx, int relinearize, int update_lm, vlgba_step_info *
  * be NULL.  Also marks the linearisation valid for the next vlgba_step. */
 int vlgba_get_linearization(vlgba_ctx *ctx, double *U, double *eA, double *V, double *eB,
                             double *W);
-int vlgba_run(vlgba_ctx *ctx, double *error_out, vlgba_stats *stats);
+/* the LM loop from the context's parameters; error_out / error_cap as
+ * vlgba_solve.  Every handle entry point makes the context's device current. */
+int vlgba_run(vlgba_ctx *ctx, double *error_out, int error_cap, vlgba_stats *stats);
 int vlgba_sync(vlgba_ctx *ctx);
 void vlgba_destroy(vlgba_ctx *ctx);
 /* device-kernel timing of the last vlgba_step, milliseconds per phase:

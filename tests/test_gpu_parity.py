@@ -388,3 +388,71 @@ def test_single_pass_config2(gpu, oracle):
     assert abs(info.old_sse - old) <= 1e-12 * old
     assert abs(info.new_sse - sse) <= 1e-7 * sse, (info.new_sse, sse)
     ba.close()
+
+
+@pytest.mark.parametrize("num_a,track,rows", [(7, 5, 28), (10, 4, 30), (12, 3, 24)])
+def test_cyclic_reduction_tile_heights(gpu, num_a, track, rows):
+    """Camera-aligned cyclic-reduction tiles of NA * floor(32 / NA) rows for
+    num_a = 7 / 10 and the projective camera (12): tracks of G + 1 consecutive
+    cameras keep S tridiagonal in G-camera tiles.  The fused level kernel's
+    fill / survivor records for these heights agree with the envelope
+    Cholesky to rounding."""
+    from bundleadjustmentmatlab_amd.scene import make_config, projective_from
+    m = 90
+    sc = make_config("cfg2", m=m, n=40 * m, track=track, seed=41)
+    if num_a == 12:
+        Pp, Xp = projective_from(sc)
+        a = np.asfortranarray(Pp.reshape(12, m, order="F"))
+        b = np.asfortranarray(Xp[0:3])
+        kw = dict(model="projective", m=m)
+        K = None
+    else:
+        a = np.zeros((num_a, m), order="F")
+        a[0:3], a[3:6] = sc.w0, sc.T0
+        if num_a == 7:
+            a[6] = sc.K[0]
+        else:
+            a[6:10] = sc.K
+        b = np.asfortranarray(sc.X0[:3])
+        kw = {}
+        K = sc.K
+    out = {}
+    for solver in ("auto", "envelope"):
+        ba = gpu.BundleAdjuster(K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, num_a, solver=solver,
+                                **kw)
+        ba.set_params(a, b)
+        info = ba.step(relinearize=True, update_lm=False)
+        out[solver] = (info, ba.plan_info())
+        ba.close()
+    assert out["auto"][1]["cr_rows"] == rows
+    assert out["envelope"][1]["cr_levels"] == 0
+    cr, env = out["auto"][0], out["envelope"][0]
+    assert cr.chol_failed == 0 and env.chol_failed == 0
+    assert cr.old_sse == env.old_sse
+    assert abs(cr.new_sse - env.new_sse) <= 1e-9 * env.new_sse, (cr.new_sse, env.new_sse)
+    assert abs(cr.dpg - env.dpg) <= 1e-9 * abs(env.dpg), (cr.dpg, env.dpg)
+
+
+def test_run_error_capacity(gpu):
+    """error_ is sized from max_iter (a 64-entry buffer used to be
+    passed whatever max_iter was); the library clamps to the capacity given."""
+    from bundleadjustmentmatlab_amd.scene import make_config
+    sc = make_config("cfg2", m=20, n=1500, seed=4)
+    a = np.zeros((6, sc.m), order="F")
+    a[0:3], a[3:6] = sc.w0, sc.T0
+    b = np.asfortranarray(sc.X0[:3])
+    ba = gpu.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, 6, max_iter=100,
+                            max_iter2=30)
+    ba.set_params(a, b)
+    err, st = ba.run()
+    assert len(err) == st.num_error <= 100 and np.all(np.isfinite(err))
+    # an explicit small capacity: only the first entries are written
+    import ctypes
+    ba.set_params(a, b)
+    buf = np.full(4, -1.0)
+    st2 = gpu._lib.VlgbaStats()
+    rc = gpu.lib().vlgba_run(ba._h, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), 2,
+                             ctypes.byref(st2))
+    ba.close()
+    assert rc == 0 and st2.num_error == st.num_error
+    assert np.array_equal(buf[:2], err[:2]) and np.all(buf[2:] == -1.0)
