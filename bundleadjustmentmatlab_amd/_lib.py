@@ -34,7 +34,7 @@ class VlgbaOptions(ctypes.Structure):
                 ("world_size", c_int), ("comm_id", ctypes.c_void_p), ("dense_solve", c_int),
                 ("ordered", c_int), ("allreduce", ctypes.c_void_p),
                 ("allreduce_user", ctypes.c_void_p), ("schur_kernel", c_int),
-                ("semantics", c_int)]
+                ("semantics", c_int), ("stop_rel", c_double)]
 
 
 NKERNELS = 16   # VLGBA_NKERNELS
@@ -51,7 +51,7 @@ class VlgbaStats(ctypes.Structure):
 class VlgbaStepInfo(ctypes.Structure):
     _fields_ = [("old_sse", c_double), ("new_sse", c_double), ("dpg", c_double),
                 ("rho", c_double), ("lambda_", c_double), ("accepted", c_int),
-                ("chol_failed", c_int)]
+                ("chol_failed", c_int), ("pinv", c_int)]
 
 
 # name -> (restype, argtypes); must match include/vlgba.h exactly
@@ -64,6 +64,8 @@ SIGNATURES = {
     "vlgba_get_params": (c_int, [ctypes.c_void_p, c_dp, c_dp]),
     "vlgba_step": (c_int, [ctypes.c_void_p, c_int, c_int, ctypes.POINTER(VlgbaStepInfo)]),
     "vlgba_run": (c_int, [ctypes.c_void_p, c_dp, c_int, ctypes.POINTER(VlgbaStats)]),
+    "vlgba_get_step": (c_int, [ctypes.c_void_p, c_dp, c_dp]),
+    "vlgba_get_reduced_system": (c_int, [ctypes.c_void_p, c_ip, c_dp, c_dp]),
     "vlgba_get_linearization": (c_int, [ctypes.c_void_p, c_dp, c_dp, c_dp, c_dp, c_dp]),
     "vlgba_sync": (c_int, [ctypes.c_void_p]),
     "vlgba_destroy": (None, [ctypes.c_void_p]),
@@ -82,6 +84,7 @@ SIGNATURES = {
     "vlgba_get_unique_id": (c_int, [ctypes.c_void_p]),
     "vlgba_device_count": (c_int, []),
     "vlgba_debug_sincos": (c_int, [c_dp, c_dp, c_dp, c_ll]),
+    "vlgba_debug_pinv_solve": (c_int, [c_int, c_dp, c_dp, c_dp]),
 }
 
 ERRORS = {-1001: "bad argument",

@@ -122,10 +122,14 @@ class BundleAdjuster:
     picks the fast-path Schur complement kernel: "auto" (dense per-chunk
     products on fp64 MFMA when the tracks fit) or "terms" (per-term sums).
     ``semantics`` is "mex" (bundle_euclid.m) or "nomex" (bundle_euclid_nomex.m).
+    ``parity=True`` runs the parity mode (vlgba_options.ordered = 2: ordered
+    sums, sequential Cholesky, LM scalars in the reference's flat order --
+    the LM trajectory is bit-identical to the CPU oracle's).  ``stop_rel``
+    replaces the 1e-3 of the stop rule (bundle_euclid.m:123).
     ``model="projective"`` solves bundle_projective.m instead: num_a = 12
     (a = P(:) per camera), K is None and ``m`` gives the camera count.
     """
-    SOLVERS = {"auto": 0, "dense": 1, "envelope": 2}
+    SOLVERS = {"auto": 0, "dense": 1, "envelope": 2, "sequential": 3}
     SCHUR_KERNELS = {"auto": 0, "terms": 1}
     SEMANTICS = {"mex": 0, "nomex": 1}
     MODELS = {"euclidean": MODEL_EUCLIDEAN, "projective": MODEL_PROJECTIVE}
@@ -134,7 +138,8 @@ class BundleAdjuster:
                  fix_motion=False, pivot=None, verbose=False, num_vis=0.0, device=0,
                  rank=0, world_size=1, comm_id=None, max_iter=0, max_iter2=0, lambda0=0.0,
                  dense_solve=False, ordered=False, allreduce=None, solver=None,
-                 schur_kernel="auto", semantics="mex", model="euclidean", m=None):
+                 schur_kernel="auto", semantics="mex", model="euclidean", m=None,
+                 parity=False, stop_rel=0.0):
         L = lib()
         solve_mode = self.SOLVERS[solver] if solver is not None else int(bool(dense_solve))
         self.K = _F(K) if K is not None else None
@@ -172,9 +177,10 @@ class BundleAdjuster:
                            int(verbose), int(max_iter), int(max_iter2), float(lambda0),
                            int(device), int(rank), int(world_size),
                            ctypes.cast(self._comm, ctypes.c_void_p) if self._comm else None,
-                           solve_mode, int(ordered),
+                           solve_mode, 2 if parity else int(ordered),
                            ctypes.cast(self._ar, ctypes.c_void_p) if self._ar else None, None,
-                           self.SCHUR_KERNELS[schur_kernel], self.SEMANTICS[semantics])
+                           self.SCHUR_KERNELS[schur_kernel], self.SEMANTICS[semantics],
+                           float(stop_rel))
         h = ctypes.c_void_p()
         check(L.vlgba_create(ctypes.byref(prob), ctypes.byref(opt), ctypes.byref(h)),
               "vlgba_create")
@@ -224,6 +230,36 @@ class BundleAdjuster:
         check(self._L.vlgba_run(self._h, _dp(err), err.size, ctypes.byref(st)), "vlgba_run")
         assert st.num_error <= err.size
         return err[: st.num_error].copy(), st
+
+    def last_step(self):
+        """(da (num_a, m), db (3, n)) of the last pass (vlgba_get_step)."""
+        da = np.zeros(self.num_a * self.m)
+        db = np.zeros(3 * self.n)
+        check(self._L.vlgba_get_step(self._h, _dp(da), _dp(db)), "vlgba_get_step")
+        return da.reshape(self.num_a, self.m, order="F"), db.reshape(3, self.n, order="F")
+
+    def reduced_system(self, dense=True):
+        """S (lower triangle: blocks j >= k; dense (na m) x (na m) if dense,
+        else (blk_jk (nb, 2), blocks (nb, na, na))) and e_ at the current
+        lambda (vlgba_get_reduced_system)."""
+        nb = self.plan_info()["blocks"]
+        na = self.num_a
+        jk = np.zeros(2 * nb, dtype=np.int32)
+        blocks = np.zeros(na * na * nb)
+        e_ = np.zeros(na * self.m)
+        check(self._L.vlgba_get_reduced_system(self._h, jk.ctypes.data_as(c_ip), _dp(blocks),
+                                               _dp(e_)), "vlgba_get_reduced_system")
+        jk = jk.reshape(nb, 2)
+        blocks = blocks.reshape(nb, na, na).transpose(0, 2, 1)   # [b, r, c]
+        if not dense:
+            return jk, blocks, e_
+        S = np.zeros((na * self.m, na * self.m))
+        for (j, k), B in zip(jk, blocks):
+            if j == k:
+                S[na * j:na * j + na, na * k:na * k + na] = np.tril(B)
+            else:
+                S[na * j:na * j + na, na * k:na * k + na] = B
+        return S, e_
 
     def sync(self):
         check(self._L.vlgba_sync(self._h), "vlgba_sync")
@@ -280,8 +316,10 @@ class BundleAdjuster:
 # ---------------------------------------------------------------------------
 def bundle_euclid_obs(K, Te, w, Xe, obs_pt, obs_cam, obs_x, *varargin, num_vis=0.0, device=0,
                       rank=0, world_size=1, comm_id=None, return_stats=False,
-                      semantics="mex"):
-    """bundle_euclid on a COO observation list (0-based point / camera ids)."""
+                      semantics="mex", **solver):
+    """bundle_euclid on a COO observation list (0-based point / camera ids).
+    ``solver`` keywords go to BundleAdjuster (parity, stop_rel, max_iter,
+    max_iter2, lambda0, solver, ordered, schur_kernel)."""
     K, Te, w, Xe = _F(K), _F(Te), _F(w), _F(Xe)
     m, n = w.shape[1], Xe.shape[1]
     nomex = semantics == "nomex"
@@ -294,7 +332,7 @@ def bundle_euclid_obs(K, Te, w, Xe, obs_pt, obs_cam, obs_x, *varargin, num_vis=0
                         fix_structure=o["fix_structure"], fix_motion=o["fix_motion"],
                         pivot=o["pivot"] if o["fix_pivot"] else None, verbose=o["verbose"],
                         num_vis=num_vis, device=device, rank=rank, world_size=world_size,
-                        comm_id=comm_id, semantics=semantics) as ba:
+                        comm_id=comm_id, semantics=semantics, **solver) as ba:
         ba.set_params(a, b)
         err, st = ba.run()
         a, b = ba.get_params()
@@ -303,7 +341,8 @@ def bundle_euclid_obs(K, Te, w, Xe, obs_pt, obs_cam, obs_x, *varargin, num_vis=0
     return out + (st,) if return_stats else out
 
 
-def bundle_euclid(K, Te, w, Xe, x, *varargin, device=0, return_stats=False, semantics="mex"):
+def bundle_euclid(K, Te, w, Xe, x, *varargin, device=0, return_stats=False, semantics="mex",
+                  **solver):
     """[K_ Te_ w_ Xe_ error_] = bundle_euclid(K, Te, w, Xe, x, ...)  (bundle_euclid.m:1)."""
     x = _F(x)
     m, n = np.shape(w)[1], x.shape[1]
@@ -326,15 +365,16 @@ def bundle_euclid(K, Te, w, Xe, x, *varargin, device=0, return_stats=False, sema
         rest.append(varargin[k])
         k += 1
     return bundle_euclid_obs(K, Te, w, Xe, pt, cam, obs_x, *rest, num_vis=num_vis,
-                             device=device, return_stats=return_stats, semantics=semantics)
+                             device=device, return_stats=return_stats, semantics=semantics,
+                             **solver)
 
 
-def bundle_euclid_nomex(K, Te, w, Xe, x, *varargin, device=0, return_stats=False):
+def bundle_euclid_nomex(K, Te, w, Xe, x, *varargin, device=0, return_stats=False, **solver):
     """[K_ Te_ w_ Xe_ error_] = bundle_euclid_nomex(K, Te, w, Xe, x, ...)
     (bundle_euclid_nomex.m:1): the same LM loop with the twin's semantics --
     db from every camera parameter (:268-277), no 'fix_pivot', Xe_(4,:) = 1."""
     return bundle_euclid(K, Te, w, Xe, x, *varargin, device=device,
-                         return_stats=return_stats, semantics="nomex")
+                         return_stats=return_stats, semantics="nomex", **solver)
 
 
 # ---------------------------------------------------------------------------

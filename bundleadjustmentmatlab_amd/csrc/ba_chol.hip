@@ -1251,6 +1251,130 @@ __global__ void k_fix_diag(double *__restrict__ S, double *__restrict__ rhs, lon
     }
 }
 
+// ---------------------------------------------------------------------------
+// Sequential reduced solve (dense_solve = 3, the parity mode): left-looking
+// Cholesky of the lower triangle, every sum in ascending index order, then the
+// two triangular solves -- exactly the loops of the CPU oracle's
+// sequential Cholesky, so da is bit-identical to it.  One
+// workgroup: the diagonal entry of column j by lane 0, the column's rows by
+// the other lanes (each row's sum stays sequential).  The exactly-zero rows
+// have their unit diagonal / zero rhs from k_assemble_tiles (App. A Q8).
+// For the small problems of the parity tests (ld of a few hundred).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_chol_seq(double *__restrict__ S, long long lds,
+                                                  int n, double *__restrict__ rhs,
+                                                  double *__restrict__ x,
+                                                  double *__restrict__ status)
+{
+    __shared__ double piv;
+    __shared__ int bad;
+    const int tid = threadIdx.x;
+    if (tid == 0) bad = 0;
+    __syncthreads();
+    for (int j = 0; j < n; j++) {
+        if (tid == 0) {
+            double s = S[j + lds * j];
+            for (int k = 0; k < j; k++) {
+                const double l = S[j + lds * k];
+                s = s - l * l;
+            }
+            if (!(s > 0.0)) bad = 1;
+            piv = sqrt(s);
+            S[j + lds * j] = piv;
+        }
+        __syncthreads();
+        if (bad) break;
+        const double p = piv;
+        for (int i = j + 1 + tid; i < n; i += 256) {
+            double t = S[i + lds * j];
+            for (int k = 0; k < j; k++) t = t - S[i + lds * k] * S[j + lds * k];
+            S[i + lds * j] = t / p;
+        }
+        __syncthreads();
+    }
+    if (bad) {
+        if (tid == 0) status[0] = 1.0;
+        return;
+    }
+    if (tid == 0) {   // L y = rhs, then L^T x = y (x over y in place)
+        for (int i = 0; i < n; i++) {
+            double t = rhs[i];
+            for (int k = 0; k < i; k++) t = t - S[i + lds * k] * x[k];
+            x[i] = t / S[i + lds * i];
+        }
+        for (int i = n - 1; i >= 0; i--) {
+            double t = x[i];
+            for (int k = i + 1; k < n; k++) t = t - S[k + lds * i] * x[k];
+            x[i] = t / S[i + lds * i];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// pinv(S) e_ from the symmetric eigen-decomposition (the fallback when the
+// Cholesky meets a non-positive pivot: bundle_euclid.m:193 always takes
+// pinv(S)*e_).  MATLAB's pinv keeps the singular values
+// (= |eigenvalues| here) above max(size) * eps(max singular value).
+//   k_pinv_w: w_k = (v_k . rhs) / ev_k  for |ev_k| > tol, else 0
+//   k_pinv_x: da_i = sum_k V[i][k] w_k
+// one workgroup per output entry, fixed-order reductions (deterministic).
+// ---------------------------------------------------------------------------
+static __device__ double dev_eps_of(double x)
+{
+    if (!(x > 0.0)) return 4.9406564584124654e-324;
+    int e;
+    (void)frexp(x, &e);
+    return ldexp(1.0, e - 53);
+}
+
+__global__ __launch_bounds__(256) void k_pinv_w(const double *__restrict__ V,
+                                                const double *__restrict__ ev, long long ld,
+                                                const double *__restrict__ rhs,
+                                                double *__restrict__ w)
+{
+    __shared__ double red[256];
+    const long long k = blockIdx.x;
+    double acc = 0.0;
+    for (long long i = threadIdx.x; i < ld; i += 256) acc += V[i + ld * k] * rhs[i];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const double emax = fmax(fabs(ev[0]), fabs(ev[ld - 1]));
+        const double tol = (double)ld * dev_eps_of(emax);
+        w[k] = fabs(ev[k]) > tol ? red[0] / ev[k] : 0.0;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pinv_x(const double *__restrict__ V, long long ld,
+                                                const double *__restrict__ w,
+                                                double *__restrict__ da)
+{
+    __shared__ double red[256];
+    const long long i = blockIdx.x;
+    double acc = 0.0;
+    for (long long k = threadIdx.x; k < ld; k += 256) acc += V[i + ld * k] * w[k];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) da[i] = red[0];
+}
+
+int ba_pinv_apply(ba_dev *d, const double *V, const double *ev, long long ld, const double *rhs,
+                  double *work, double *da)
+{
+    if (ld <= 0) return 0;
+    k_pinv_w<<<(unsigned)ld, 256, 0, d->stream>>>(V, ev, ld, rhs, work);
+    k_pinv_x<<<(unsigned)ld, 256, 0, d->stream>>>(V, ld, work, da);
+    return -(int)hipGetLastError();
+}
+
 // ===========================================================================
 template <typename T>
 static int dev_alloc(T **p, size_t bytes)
@@ -1264,8 +1388,11 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
     const int nt = (int)(d->lds / NB);
     d->nt = nt;
     d->h_tfirst = new int[nt];
-    for (int i = 0; i < nt; i++) d->h_tfirst[i] = d->dense_solve ? 0 : i;
-    if (!d->dense_solve)
+    // every lower tile for the measurement mode (1) and the sequential parity
+    // solve (3); the envelope otherwise (0 auto, 2 envelope without CR)
+    const bool all_tiles = d->dense_solve == 1 || d->dense_solve == 3;
+    for (int i = 0; i < nt; i++) d->h_tfirst[i] = all_tiles ? 0 : i;
+    if (!all_tiles)
         for (int b = 0; b < nb; b++) {
             const int j = blk_jk[2 * b], k = blk_jk[2 * b + 1];   // j >= k
             const long long r0 = (long long)d->na * j, c0 = (long long)d->na * k;
@@ -1491,6 +1618,13 @@ int ba_chol_solve(ba_dev *d)
     TRY_RC(ba_ensure_dyn_lds((const void *)k_cr_factor, smem3));
     TRY_RC(ba_ensure_dyn_lds((const void *)k_cr_update, smem3));
     TRY_RC(ba_ensure_dyn_lds((const void *)k_syrk, smem));
+    if (d->dense_solve == 3) {   // sequential parity solve
+        KT_B(d);
+        k_chol_seq<<<1, 256, 0, d->stream>>>(d->S, d->lds, (int)d->ld, d->rhs, d->da,
+                                             d->scal + 4);
+        KT_E(d, KT_FACTOR);
+        return -(int)hipGetLastError();
+    }
     if (d->cr_nlev > 0 && d->cr32) {   // camera-aligned 32-row tiles
         const int ncu32 = d->ncu;
         const int n32 = d->nt32, TB = d->tb32;

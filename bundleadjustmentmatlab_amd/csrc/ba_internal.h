@@ -93,7 +93,8 @@ struct ba_dev {
     int *env_tiles;    // device [n_env][2] (i, k) tiles inside the envelope
     int *tb_ptr, *tb_blk;  // device: per envelope tile, the co-visible blocks overlapping it
     int n_env;
-    int dense_solve;   // 0 auto, 1: every lower tile (measurement), 2: envelope, no CR
+    int dense_solve;   // 0 auto, 1: every lower tile (measurement), 2: envelope, no CR,
+                       // 3: sequential Cholesky (parity mode)
     // block cyclic reduction (tile-tridiagonal S): per level, eliminated tiles
     // (e, p, q) and kept tiles (k, e-, e+, k2); -1 = none
     int cr_nlev;
@@ -117,6 +118,8 @@ struct ba_dev {
     // per chunk the co-visible blocks it touches ("slots") and the cameras it
     // sees ("e-slots") get one partial each, reduced per block in chunk order.
     int ordered;       // 1: sequential bit-exact kernels (k_damp_point + k_schur)
+    int parity;        // ordered = 2: + sequential solve and LM scalars (bit-identical
+                       // LM trajectory with the oracle)
     int mfma;          // fast path: 1 = MFMA Schur chunks (k_schur_mfma), 0 = term lists
     int no_mfma;       // option: force the term-list Schur kernel
     int ndb;           // camera parameters in the back substitution: 6 (MEX, App. A
@@ -213,7 +216,10 @@ void *ba_dmalloc(size_t bytes);   // per-device caching allocator (ba_solver.cpp
 int ba_ensure_dyn_lds(const void *fn, size_t bytes);
 void ba_dfree(void *p);   // scal[0..4] + ++seq -> hres (host-mapped)
 int ba_launch_schur_fast(ba_dev *d, double lambda);   // fused damp + Vinv + Y + S + e_
-int ba_launch_assemble_plain(ba_dev *d, double *S, long long ld);
+int ba_launch_assemble_plain(ba_dev *d, double *S, long long ld, int lower_only);
+// parity mode (ordered = 2): sequential LM scalars in the reference's flat order
+int ba_launch_parity_old_sse(ba_dev *d);
+int ba_launch_parity_new_sums(ba_dev *d, double lambda);
 // ---- ba_chol.hip ----
 int ba_chol_setup(ba_dev *d, const int *blk_jk_host, int nb);
 void ba_chol_free(ba_dev *d);
@@ -221,6 +227,10 @@ int ba_chol_prepare(ba_dev *d);
 int ba_assemble_tiles(ba_dev *d);   // envelope tiles of S + pinv rule + status, one launch
 int ba_chol_fix_diag(ba_dev *d);
 int ba_chol_solve(ba_dev *d);
+// da = pinv(S) rhs from the eigen-decomposition S = V diag(ev) V^T (ev
+// ascending, V column major ld x ld): MATLAB's tolerance ld * eps(max |ev|)
+int ba_pinv_apply(ba_dev *d, const double *V, const double *ev, long long ld, const double *rhs,
+                  double *work, double *da);
 
 #define TRY_RC(x)                                                                   \
     do {                                                                            \

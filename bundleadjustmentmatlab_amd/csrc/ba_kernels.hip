@@ -1797,14 +1797,79 @@ int ba_launch_update(ba_dev *d, double lambda)
     return -(int)hipGetLastError();
 }
 
+// -------------------------------------------------------------------------
+// Parity mode (vlgba_options.ordered = 2): the LM scalars summed sequentially
+// in the reference's flat orders, by one lane, so that they equal the oracle's
+// bit for bit:
+//   e'e  over the dense 2 x n x m residual array in MATLAB's column-major
+//        order (bundle_euclid.m:207-210: camera-major, points ascending, u then
+//        v; the invisible entries are exact zeros and change nothing)
+//   dp'(lambda dp + g) over dp = [da; db], g = [eA; eB] (:213-217)
+// -------------------------------------------------------------------------
+template <int NA>
+__global__ void k_seq_old_sse(const int *__restrict__ cam_ptr, const int *__restrict__ cam_obs,
+                              const double *__restrict__ jrec, int m, double *__restrict__ out)
+{
+    if (threadIdx.x != 0) return;
+    constexpr int JS = 2 * NA + 2;
+    double s = 0.0;
+    for (int j = 0; j < m; j++)
+        for (int q = cam_ptr[j]; q < cam_ptr[j + 1]; q++) {
+            const double *e = jrec + (size_t)JS * cam_obs[q] + 2 * NA;
+            s = s + e[0] * e[0];
+            s = s + e[1] * e[1];
+        }
+    *out = s;
+}
+
+__global__ void k_seq_new_sums(const int *__restrict__ cam_ptr, const int *__restrict__ cam_obs,
+                               const double *__restrict__ obs_x, const double *__restrict__ xh,
+                               int m, const double *__restrict__ da,
+                               const double *__restrict__ eA, long long ld,
+                               const double *__restrict__ db, const double *__restrict__ eB,
+                               int n, double lambda, double *__restrict__ scal)
+{
+    if (threadIdx.x != 0) return;
+    double s = 0.0;
+    for (int j = 0; j < m; j++)
+        for (int q = cam_ptr[j]; q < cam_ptr[j + 1]; q++) {
+            const int o = cam_obs[q];
+            const double d0 = obs_x[2 * (size_t)o] - xh[2 * (size_t)o];
+            const double d1 = obs_x[2 * (size_t)o + 1] - xh[2 * (size_t)o + 1];
+            s = s + d0 * d0;
+            s = s + d1 * d1;
+        }
+    double g = 0.0;
+    for (long long k = 0; k < ld; k++) g = g + da[k] * (lambda * da[k] + eA[k]);
+    for (long long k = 0; k < 3 * (long long)n; k++) g = g + db[k] * (lambda * db[k] + eB[k]);
+    scal[1] = s;
+    scal[2] = g;
+    scal[3] = 0.0;
+}
+
+int ba_launch_parity_old_sse(ba_dev *d)
+{
+    BA_DISPATCH(d->na, (k_seq_old_sse<NA><<<1, 64, 0, d->stream>>>(d->cam_ptr, d->cam_obs,
+                                                                   d->jrec, d->m, d->scal + 0)));
+    return -(int)hipGetLastError();
+}
+
+int ba_launch_parity_new_sums(ba_dev *d, double lambda)
+{
+    k_seq_new_sums<<<1, 64, 0, d->stream>>>(d->cam_ptr, d->cam_obs, d->obs_x, d->xh_out, d->m,
+                                            d->da, d->eA, d->ld, d->db, d->eB, d->n, lambda,
+                                            d->scal);
+    return -(int)hipGetLastError();
+}
+
 // dense (unpadded, both triangles) S for the stage-2 entry
-int ba_launch_assemble_plain(ba_dev *d, double *S, long long ld)
+int ba_launch_assemble_plain(ba_dev *d, double *S, long long ld, int lower_only)
 {
     VLGBA_CHECK(hipMemsetAsync(S, 0, sizeof(double) * ld * ld, d->stream));
     const long long work = (long long)d->nb * d->na * d->na;
     const int g = (int)((work + 255) / 256);
     if (g > 0)
         BA_DISPATCH(d->na, (k_assemble<NA><<<g, 256, 0, d->stream>>>(d->blk_jk, d->sblk, d->nb,
-                                                                       ld, 0, S)));
+                                                                       ld, lower_only, S)));
     return -(int)hipGetLastError();
 }

@@ -17,6 +17,9 @@
 #include "../../include/vlgba.h"
 
 #include <rccl/rccl.h>
+#include <rocsolver/rocsolver.h>   // types only: the library is dlopen'ed on first use
+
+#include <dlfcn.h>
 
 #include <algorithm>
 #include <atomic>
@@ -657,6 +660,11 @@ struct vlgba_ctx {
     std::vector<double> hb_tmp;   // host staging for b gather
     ba_aux aux;                   // streams / events / host result block (pooled)
     bool has_aux = false;
+    double stop_rel = 1e-3;       // bundle_euclid.m:123 relative-decrease stop
+    // pinv fallback of the reduced solve (allocated on first use)
+    double *pinv_S = nullptr, *pinv_ev = nullptr, *pinv_e = nullptr, *pinv_w = nullptr;
+    int *pinv_info = nullptr;
+    int pinv_used = 0;            // passes that took the pinv fallback
 };
 
 // Per-device pool of the context's streams, fork/join events and host-mapped
@@ -714,6 +722,9 @@ static void ctx_free(vlgba_ctx *c)
     if (c->d.stream) (void)hipStreamSynchronize(c->d.stream);
     if (c->d.side) (void)hipStreamSynchronize(c->d.side);
     for (void *p : c->allocs) ba_dfree(p);
+    for (void *p : {(void *)c->pinv_S, (void *)c->pinv_ev, (void *)c->pinv_e, (void *)c->pinv_w,
+                    (void *)c->pinv_info})
+        if (p) ba_dfree(p);
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->d.kt) {
@@ -1037,11 +1048,25 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
         c->lambda0 = c->lambda = o->lambda0 > 0 ? o->lambda0 : 1e-3;
         c->verbose = o->verbose;
         c->d.dense_solve = o->dense_solve;
-        c->d.ordered = o->ordered;
+        c->d.ordered = o->ordered != 0;
+        if (o->ordered == 2) {   // parity mode: + sequential solve and LM scalars
+            if (c->world > 1) { rc = VLGBA_E_ARG; break; }
+            c->d.parity = 1;
+            c->d.dense_solve = 3;
+        } else if (o->ordered < 0 || o->ordered > 2 || o->dense_solve < 0 ||
+                   o->dense_solve > 3) {
+            rc = VLGBA_E_ARG;
+            break;
+        }
+        c->stop_rel = o->stop_rel > 0 ? o->stop_rel : 1e-3;
         c->d.no_mfma = o->schur_kernel == 1;
         c->d.ndb = o->semantics == 1 ? p->num_a : 6;
         rc = ctx_setup(c, p, h, pt_ptr_all, lower_blocks, all_diag, stage_mode);
         if (rc) break;
+        if (c->d.parity) {   // new projections for the sequential new-SSE sum
+            rc = ctx_alloc(c, &c->d.xh_out, 2 * (size_t)c->d.N + 2);
+            if (rc) break;
+        }
         if (c->flags.has_pivot) {
             rc = ctx_alloc(c, &c->d.pivot, (size_t)p->m);
             if (rc) break;
@@ -1067,42 +1092,10 @@ static inline void mark(vlgba_ctx *c, int q)
     if (c->timing) (void)hipEventRecord(c->ev[q], c->d.stream);
 }
 
-static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
+// damping + V*^-1 + Y + Schur complement (S blocks, e_) and their all-reduce
+static int schur_phase(vlgba_ctx *c, double lam)
 {
     ba_dev &d = c->d;
-    const double lam = c->lambda;
-    mark(c, 0);
-    if (relinearize || !c->lin_valid) {
-        // the rotation table of d.a is current: set_params builds it and an
-        // accepted step swaps in the one k_camera_update built for a_new
-        TRY(ba_launch_linearize(&d, c->flags));
-        mark(c, 1);
-        if (!d.ordered && c->world == 1 && !c->timing) {
-            // U / eA / old SSE on the side stream, overlapping V*^-1 and the
-            // Schur chunks (no collective in between at world size 1);
-            // launch_schur_fast joins before k_schur_reduce
-            VLGBA_CHECK(hipEventRecord(d.ev_fork, d.stream));
-            VLGBA_CHECK(hipStreamWaitEvent(d.side, d.ev_fork, 0));
-            hipStream_t s0 = d.stream;
-            d.stream = d.side;
-            const int rc = ba_launch_camera_reduce(&d, c->flags);
-            d.stream = s0;
-            TRY(rc);
-            VLGBA_CHECK(hipEventRecord(d.ev_join, d.side));
-            d.join_pending = 1;
-        } else {
-            TRY(ba_launch_camera_reduce(&d, c->flags));
-        }
-        // U | eA | old_sse travel in one all-reduce (the fast path's reduce
-        // kernel writes the old_sse slot itself)
-        if (d.ordered)
-            VLGBA_CHECK(hipMemcpyAsync(d.eA + d.ld, d.scal + 0, sizeof(double),
-                                       hipMemcpyDeviceToDevice, d.stream));
-        TRY(allreduce(c, d.U, (size_t)d.na * d.na * d.m + d.ld + 1));
-        c->lin_valid = 1;
-    } else {
-        mark(c, 1);
-    }
     mark(c, 2);
     if (d.ordered) {
         TRY(ba_launch_damp_point(&d, lam));
@@ -1113,19 +1106,14 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
         TRY(ba_launch_schur_fast(&d, lam));
     }
     TRY(allreduce(c, d.sblk, (size_t)d.na * d.na * d.nb + d.ld));
-    mark(c, 4);
-    TRY(ba_launch_assemble(&d));
-    mark(c, 5);
-    TRY(ba_chol_solve(&d));
-    mark(c, 6);
-    const bool spin = c->world == 1 && !c->timing;
-    d.publish_req = spin;   // the fast update's final-sums launch publishes
-    d.published = 0;
-    TRY(ba_launch_update(&d, lam));
-    d.publish_req = 0;
-    mark(c, 7);
-    // scalars: [0] old_sse(local) [1] new_sse [2] dpg cameras [3] dpg points [4] chol status
-    double hs[5];
+    return 0;
+}
+
+// the pass scalars after the update: cross-rank sums, then to the host (spin
+// on the host-mapped block when single-rank and untimed, else a copy)
+static int collect_scalars(vlgba_ctx *c, bool spin, double hs[5])
+{
+    ba_dev &d = c->d;
     if (c->world > 1) {
         VLGBA_CHECK(hipMemcpyAsync(d.scal + 0, d.eA + d.ld, sizeof(double),
                                    hipMemcpyDeviceToDevice, d.stream));
@@ -1155,14 +1143,163 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
         std::atomic_thread_fence(std::memory_order_acquire);
         if (got) {
             for (int q = 0; q < 5; q++) hs[q] = d.hres[q];
-        } else {
-            VLGBA_CHECK(hipStreamSynchronize(d.stream));
-            TRY(download(hs, d.scal, 5, d.stream));
-            VLGBA_CHECK(hipStreamSynchronize(d.stream));
+            return 0;
         }
-    } else {
-        TRY(download(hs, d.scal, 5, d.stream));
         VLGBA_CHECK(hipStreamSynchronize(d.stream));
+    }
+    TRY(download(hs, d.scal, 5, d.stream));
+    VLGBA_CHECK(hipStreamSynchronize(d.stream));
+    return 0;
+}
+
+// rocSOLVER's symmetric eigensolver, loaded on first use (the library is
+// ~0.9 GB; a pass that never meets a non-positive pivot never loads it)
+namespace {
+struct rs_api {
+    rocblas_status (*create)(rocblas_handle *);
+    rocblas_status (*set_stream)(rocblas_handle, hipStream_t);
+    rocblas_status (*syevd)(rocblas_handle, const rocblas_evect, const rocblas_fill,
+                            const rocblas_int, double *, const rocblas_int, double *, double *,
+                            rocblas_int *);
+    bool ok = false;
+};
+rs_api *rs_load()
+{
+    static rs_api api;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *h = dlopen("librocsolver.so.0", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librocsolver.so.0", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return;
+        api.create = (decltype(api.create))dlsym(h, "rocblas_create_handle");
+        api.set_stream = (decltype(api.set_stream))dlsym(h, "rocblas_set_stream");
+        api.syevd = (decltype(api.syevd))dlsym(h, "rocsolver_dsyevd");
+        api.ok = api.create && api.set_stream && api.syevd;
+    });
+    return api.ok ? &api : nullptr;
+}
+std::mutex g_rs_mu;
+std::map<int, rocblas_handle> g_rs_handle;   // per device
+}   // namespace
+
+// da = pinv(S) * e_ on the GPU (bundle_euclid.m:193) for a pass whose
+// Cholesky met a non-positive pivot: S and e_ again (the solve overwrote them
+// in place), the lower triangle of S assembled densely, rocSOLVER dsyevd,
+// then V diag(1/ev, |ev| > tol) V^T e_ (ba_pinv_apply), and the update with
+// that da.  Every rank runs it on the identical all-reduced system.
+static int pinv_fallback(vlgba_ctx *c, double lam, double hs[5])
+{
+    ba_dev &d = c->d;
+    rs_api *rs = rs_load();
+    if (!rs) return VLGBA_E_ARG;
+    const long long ld = d.ld;
+    if (ld > 0x7fffffffLL) return VLGBA_E_ARG;
+    if (!c->pinv_S) {
+        TRY(dalloc(&c->pinv_S, (size_t)(ld * ld)));
+        TRY(dalloc(&c->pinv_ev, (size_t)ld));
+        TRY(dalloc(&c->pinv_e, (size_t)ld));
+        TRY(dalloc(&c->pinv_w, (size_t)ld));
+        TRY(dalloc(&c->pinv_info, 1));
+    }
+    rocblas_handle hdl = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_rs_mu);
+        auto it = g_rs_handle.find(d.device);
+        if (it == g_rs_handle.end()) {
+            if (rs->create(&hdl) != rocblas_status_success) return VLGBA_E_ARG;
+            g_rs_handle[d.device] = hdl;
+        } else {
+            hdl = it->second;
+        }
+    }
+    TRY(schur_phase(c, lam));
+    TRY(ba_launch_assemble_plain(&d, c->pinv_S, ld, 1));
+    // the library stream is non-blocking: make S complete before rocSOLVER
+    // (parts of dsyevd are ordered against the legacy stream, not ours)
+    VLGBA_CHECK(hipStreamSynchronize(d.stream));
+    {
+        std::lock_guard<std::mutex> lk(g_rs_mu);
+        if (rs->set_stream(hdl, d.stream) != rocblas_status_success ||
+            rs->syevd(hdl, rocblas_evect_original, rocblas_fill_lower, (rocblas_int)ld,
+                      c->pinv_S, (rocblas_int)ld, c->pinv_ev, c->pinv_e,
+                      c->pinv_info) != rocblas_status_success)
+            return VLGBA_E_ARG;
+        VLGBA_CHECK(hipStreamSynchronize(d.stream));
+    }
+    {
+        int info = 0;
+        VLGBA_CHECK(hipMemcpy(&info, c->pinv_info, sizeof info, hipMemcpyDeviceToHost));
+        if (info != 0) return VLGBA_E_ARG;   // the eigensolver did not converge
+    }
+    TRY(ba_pinv_apply(&d, c->pinv_S, c->pinv_ev, ld, d.rhs, c->pinv_w, d.da));
+    d.publish_req = 0;
+    d.published = 0;
+    TRY(ba_launch_update(&d, lam));
+    if (d.parity) TRY(ba_launch_parity_new_sums(&d, lam));
+    TRY(collect_scalars(c, false, hs));
+    c->pinv_used++;
+    return 0;
+}
+
+static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
+{
+    ba_dev &d = c->d;
+    const double lam = c->lambda;
+    mark(c, 0);
+    if (relinearize || !c->lin_valid) {
+        // the rotation table of d.a is current: set_params builds it and an
+        // accepted step swaps in the one k_camera_update built for a_new
+        TRY(ba_launch_linearize(&d, c->flags));
+        mark(c, 1);
+        if (!d.ordered && c->world == 1 && !c->timing) {
+            // U / eA / old SSE on the side stream, overlapping V*^-1 and the
+            // Schur chunks (no collective in between at world size 1);
+            // launch_schur_fast joins before k_schur_reduce
+            VLGBA_CHECK(hipEventRecord(d.ev_fork, d.stream));
+            VLGBA_CHECK(hipStreamWaitEvent(d.side, d.ev_fork, 0));
+            hipStream_t s0 = d.stream;
+            d.stream = d.side;
+            const int rc = ba_launch_camera_reduce(&d, c->flags);
+            d.stream = s0;
+            TRY(rc);
+            VLGBA_CHECK(hipEventRecord(d.ev_join, d.side));
+            d.join_pending = 1;
+        } else {
+            TRY(ba_launch_camera_reduce(&d, c->flags));
+        }
+        if (d.parity) TRY(ba_launch_parity_old_sse(&d));
+        // U | eA | old_sse travel in one all-reduce (the fast path's reduce
+        // kernel writes the old_sse slot itself)
+        if (d.ordered)
+            VLGBA_CHECK(hipMemcpyAsync(d.eA + d.ld, d.scal + 0, sizeof(double),
+                                       hipMemcpyDeviceToDevice, d.stream));
+        TRY(allreduce(c, d.U, (size_t)d.na * d.na * d.m + d.ld + 1));
+        c->lin_valid = 1;
+    } else {
+        mark(c, 1);
+    }
+    TRY(schur_phase(c, lam));
+    mark(c, 4);
+    TRY(ba_launch_assemble(&d));
+    mark(c, 5);
+    TRY(ba_chol_solve(&d));
+    mark(c, 6);
+    const bool spin = c->world == 1 && !c->timing;
+    d.publish_req = spin;   // the fast update's final-sums launch publishes
+    d.published = 0;
+    TRY(ba_launch_update(&d, lam));
+    d.publish_req = 0;
+    if (d.parity) TRY(ba_launch_parity_new_sums(&d, lam));
+    mark(c, 7);
+    // scalars: [0] old_sse(local) [1] new_sse [2] dpg cameras [3] dpg points [4] chol status
+    double hs[5];
+    TRY(collect_scalars(c, spin, hs));
+    info->pinv = 0;
+    if (hs[4] != 0.0) {
+        // non-positive pivot: bundle_euclid.m:193 takes pinv(S)*e_ whatever S is
+        // (App. A Q8), so does the fallback -- then the same update
+        TRY(pinv_fallback(c, lam, hs));
+        info->pinv = 1;
     }
     if (c->timing) {
         float ms;
@@ -1183,12 +1320,12 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
     info->new_sse = hs[1];
     info->dpg = hs[2] + hs[3];
     info->lambda = lam;
-    info->chol_failed = hs[4] != 0.0;
+    info->chol_failed = info->pinv;   // the Cholesky failed; the step is pinv(S)*e_
     info->rho = (hs[0] - hs[1]) / info->dpg;
     if (c->model == VLGBA_MODEL_PROJECTIVE)   // bundle_projective.m:182-188 (normalised first)
-        info->accepted = 1 / c->num_vis * hs[1] < 1 / c->num_vis * hs[0] && !info->chol_failed;
+        info->accepted = 1 / c->num_vis * hs[1] < 1 / c->num_vis * hs[0];
     else                                      // bundle_euclid.m:218
-        info->accepted = (hs[0] - hs[1]) > 0 && !info->chol_failed;
+        info->accepted = (hs[0] - hs[1]) > 0;
     return 0;
 }
 
@@ -1328,6 +1465,42 @@ int vlgba_get_linearization(vlgba_ctx *c, double *U, double *eA, double *V, doub
     return 0;
 }
 
+int vlgba_get_reduced_system(vlgba_ctx *c, int *blk_jk, double *blocks, double *e_)
+{
+    if (!c) return VLGBA_E_ARG;
+    TRY(ctx_enter(c));
+    ba_dev &d = c->d;
+    if (!c->lin_valid) {   // stage 1 at the current parameters (as a pass would)
+        TRY(ba_launch_linearize(&d, c->flags));
+        TRY(ba_launch_camera_reduce(&d, c->flags));
+        if (d.ordered)
+            VLGBA_CHECK(hipMemcpyAsync(d.eA + d.ld, d.scal + 0, sizeof(double),
+                                       hipMemcpyDeviceToDevice, d.stream));
+        TRY(allreduce(c, d.U, (size_t)d.na * d.na * d.m + d.ld + 1));
+        c->lin_valid = 1;
+    }
+    TRY(schur_phase(c, c->lambda));
+    if (d.join_pending) {
+        VLGBA_CHECK(hipStreamWaitEvent(d.stream, d.ev_join, 0));
+        d.join_pending = 0;
+    }
+    if (blk_jk) TRY(download(blk_jk, d.blk_jk, 2 * (size_t)d.nb, d.stream));
+    if (blocks) TRY(download(blocks, d.sblk, (size_t)d.na * d.na * d.nb, d.stream));
+    if (e_) TRY(download(e_, d.rhs, (size_t)d.ld, d.stream));
+    VLGBA_CHECK(hipStreamSynchronize(d.stream));
+    return 0;
+}
+
+int vlgba_get_step(vlgba_ctx *c, double *da, double *db)
+{
+    if (!c) return VLGBA_E_ARG;
+    TRY(ctx_enter(c));
+    if (da) TRY(download(da, c->d.da, (size_t)c->d.ld, c->d.stream));
+    if (db) TRY(download(db, c->d.db, 3 * (size_t)c->d.n, c->d.stream));
+    VLGBA_CHECK(hipStreamSynchronize(c->d.stream));
+    return 0;
+}
+
 int vlgba_set_timing(vlgba_ctx *c, int on)
 {
     if (!c) return VLGBA_E_ARG;
@@ -1424,7 +1597,7 @@ int vlgba_run(vlgba_ctx *c, double *error_out, int error_cap, vlgba_stats *stats
         if (!(iter < c->max_iter && iter2 < c->max_iter2)) break;
         if (iter >= 3) {
             const double e1 = err[iter - 1], e0 = err[iter - 2];
-            if (!(e1 > 1e-20 && e0 - e1 > 1e-3 * e0)) break;
+            if (!(e1 > 1e-20 && e0 - e1 > c->stop_rel * e0)) break;
         }
         vlgba_step_info info;
         TRY(lm_pass(c, 0, &info));
@@ -1597,7 +1770,7 @@ static int mex2_impl(int model, int m, int n, int num_a, const double *Y, const 
         if ((rc = ba_launch_yeb(&d))) break;
         // U is given already damped (bundle_euclid.m:192 passes U_): lambda = 0
         if ((rc = ba_launch_schur(&d, 0.0))) break;
-        if ((rc = ba_launch_assemble_plain(&d, Sd, ld))) break;
+        if ((rc = ba_launch_assemble_plain(&d, Sd, ld, 0))) break;
         if ((rc = download(S, Sd, (size_t)(ld * ld), d.stream))) break;
         if ((rc = download(e_, d.rhs, (size_t)ld, d.stream))) break;
         if (hipStreamSynchronize(d.stream) != hipSuccess) { rc = -1; break; }
@@ -1674,6 +1847,51 @@ static int mex3_impl(int model, int m, int n, int num_a, const double *W, const 
         X_hat[2 * p + 1] = xh[2 * q + 1];
     }
     return 0;
+}
+
+int vlgba_debug_pinv_solve(int ld, const double *S, const double *e_, double *da)
+{
+    if (ld < 1 || !S || !e_ || !da) return VLGBA_E_ARG;
+    rs_api *rs = rs_load();
+    if (!rs) return VLGBA_E_ARG;
+    int dev = 0;
+    VLGBA_CHECK(hipGetDevice(&dev));
+    ba_dev d;
+    std::memset(&d, 0, sizeof d);
+    d.device = dev;
+    d.stream = nullptr;   // legacy stream: synchronous below
+    double *buf = nullptr;
+    int *info = nullptr;
+    const size_t n = (size_t)ld;
+    TRY(dalloc(&buf, n * n + 4 * n));
+    int rc = dalloc(&info, 1);
+    rocblas_handle hdl = nullptr;
+    do {
+        if (rc) break;
+        double *A = buf, *ev = buf + n * n, *e = ev + n, *w = e + n, *rhs = w + n;
+        if (hipMemcpy(A, S, sizeof(double) * n * n, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(rhs, e_, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess) {
+            rc = -1;
+            break;
+        }
+        if (rs->create(&hdl) != rocblas_status_success ||
+            rs->syevd(hdl, rocblas_evect_original, rocblas_fill_lower, ld, A, ld, ev, e, info) !=
+                rocblas_status_success) {
+            rc = VLGBA_E_ARG;
+            break;
+        }
+        if ((rc = ba_pinv_apply(&d, A, ev, ld, rhs, w, e))) break;
+        if (hipMemcpy(da, e, sizeof(double) * n, hipMemcpyDeviceToHost) != hipSuccess) rc = -1;
+    } while (0);
+    (void)hipDeviceSynchronize();
+    if (hdl) {
+        auto destroy = (rocblas_status(*)(rocblas_handle))dlsym(RTLD_DEFAULT,
+                                                                 "rocblas_destroy_handle");
+        if (destroy) destroy(hdl);
+    }
+    ba_dfree(buf);
+    if (info) ba_dfree(info);
+    return rc;
 }
 
 int vlgba_mex_bundle_1(int m, int n, int num_a, const double *K, const double *a,

@@ -77,13 +77,20 @@ typedef struct {
      *   band narrower than 64 rows), else the envelope tile Cholesky;
      * 1: tile Cholesky over every lower tile (measurement);
      * 2: envelope tile Cholesky (tiles outside the envelope are exactly zero,
-     *   so 1 and 2 give identical results)                                   */
+     *   so 1 and 2 give identical results);
+     * 3: one-workgroup sequential Cholesky (parity mode, small problems).
+     * Any of them meeting a non-positive pivot falls back to pinv(S) e_ from
+     * a symmetric eigen-decomposition on the GPU (vlgba_step_info.pinv)      */
     int dense_solve;
-    /* 1: "ordered" (parity) mode -- every sum over points runs sequentially in
+    /* 1: "ordered" mode -- every sum over points runs sequentially in
      * ascending point order exactly as the reference loops do, making the
-     * reduced system bit-identical to the reference arithmetic; 0 (default):
-     * the fused chunked Schur path (same terms, sums grouped per chunk of
-     * points, deterministic run to run)                                      */
+     * reduced system bit-identical to the reference arithmetic; 2: "parity"
+     * mode -- ordered, plus the sequential Cholesky (dense_solve 3) and the LM
+     * scalars e'e, dp'(lambda dp + g) summed in the reference's flat order,
+     * so the whole LM trajectory (error_, a, b) is bit-identical to the CPU
+     * oracle's (single rank, small problems); 0 (default): the fused chunked
+     * Schur path (same terms, sums grouped per chunk of points, deterministic
+     * run to run)                                                            */
     int ordered;
     /* world_size > 1 without comm_id: a host collective instead of RCCL.  The
      * library copies the buffer to host memory, calls allreduce(buf, count,
@@ -102,6 +109,9 @@ typedef struct {
      * twin: db uses all num_a rows of da, bundle_euclid_nomex.m:268-277; no
      * fix_pivot -- pivot is ignored) */
     int semantics;
+    /* stop rule of bundle_euclid.m:123: stop once the accepted step lowers
+     * error_ by no more than stop_rel * error_(previous); 0 -> 1e-3          */
+    double stop_rel;
 } vlgba_options;
 
 typedef struct {
@@ -120,7 +130,9 @@ typedef struct {
     double rho;
     double lambda;         /* lambda used by this pass                        */
     int accepted;
-    int chol_failed;       /* non-positive pivot in the reduced solve         */
+    int chol_failed;       /* non-positive pivot in the reduced solve: the
+                              step came from the pinv fallback (= pinv)       */
+    int pinv;              /* da = pinv(S) e_ by eigen-decomposition          */
 } vlgba_step_info;
 
 typedef struct vlgba_ctx vlgba_ctx;
@@ -153,6 +165,15 @@ int vlgba_get_linearization(vlgba_ctx *ctx, double *U, double *eA, double *V, do
 /* the LM loop from the context's parameters; error_out / error_cap as
  * vlgba_solve.  Every handle entry point makes the context's device current. */
 int vlgba_run(vlgba_ctx *ctx, double *error_out, int error_cap, vlgba_stats *stats);
+/* the last pass's step: da (num_a * m, the reduced solve) and db (3 x
+ * n_local, this rank's points); either may be NULL */
+int vlgba_get_step(vlgba_ctx *ctx, double *da, double *db);
+/* the reduced camera system at the context's lambda (mex_bundle_2_Se_ output,
+ * bundle_euclid.m:192): the co-visible blocks S_jk, j >= k (num_a x num_a
+ * column major each, lower triangle meaningful for j == k; count =
+ * vlgba_plan_info [10]) with their camera pairs blk_jk [2 * count], and e_
+ * (num_a * m).  Linearises first if the parameters changed.  NULL skips. */
+int vlgba_get_reduced_system(vlgba_ctx *ctx, int *blk_jk, double *blocks, double *e_);
 int vlgba_sync(vlgba_ctx *ctx);
 void vlgba_destroy(vlgba_ctx *ctx);
 /* device-kernel timing of the last vlgba_step, milliseconds per phase:
@@ -236,6 +257,10 @@ int vlgba_get_unique_id(void *id128);
  * algorithm, vlg_libm.h) for n host arguments -- the parity tests compare them
  * with the host libm bit for bit.  |x| < 105414350. */
 int vlgba_debug_sincos(const double *x, double *s, double *c, long long n);
+/* the pinv fallback of the reduced solve (rocSOLVER dsyevd + the pinv kernels)
+ * on a host ld x ld symmetric S (lower triangle read) and e_: da = pinv(S) e_
+ * with MATLAB's tolerance ld * eps(max |eigenvalue|). */
+int vlgba_debug_pinv_solve(int ld, const double *S, const double *e_, double *da);
 
 /* Library / device info: writes a NUL-terminated string, returns its length. */
 int vlgba_version(char *buf, int len);

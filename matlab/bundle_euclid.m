@@ -18,7 +18,9 @@ function [K_, Te_, w_, Xe_, error_] = bundle_euclid(K, Te, w, Xe, x, varargin)
 %   directory serve the reference's own bundle_euclid.m unchanged.
 %
 %   Extra options of this build: 'semantics', 'nomex' (the arithmetic of
-%   bundle_euclid_nomex.m), 'max_iter', N, 'device', D, 'ordered'.
+%   bundle_euclid_nomex.m), 'max_iter', N, 'stop_rel', r (the 1e-3 of the
+%   stop rule), 'device', D, 'ordered' (sequential sums), 'parity' (ordered
+%   sums + sequential solve: the trajectory of the CPU oracle bit for bit).
 
 if nargin < 5
     help bundle_euclid
@@ -28,7 +30,7 @@ m = size(w, 2);
 n = size(x, 2);
 
 opts = struct('fix_structure', 0, 'fix_motion', 0, 'verbose', 0, 'pivot', [], ...
-              'semantics', 0, 'max_iter', 0, 'device', 0, 'ordered', 0);
+              'semantics', 0, 'max_iter', 0, 'stop_rel', 0, 'device', 0, 'ordered', 0);
 nvk = 4;                                    % free fx fy cx cy
 vis = [];
 k = 1;
@@ -44,7 +46,9 @@ while k <= numel(varargin)
     elseif strcmp(name, 'semantics'),      opts.semantics = double(strcmpi(varargin{k+1}, 'nomex')); k = k + 1;
     elseif strcmp(name, 'max_iter'),       opts.max_iter = varargin{k+1}; k = k + 1;
     elseif strcmp(name, 'device'),         opts.device = varargin{k+1}; k = k + 1;
+    elseif strcmp(name, 'stop_rel'),       opts.stop_rel = varargin{k+1}; k = k + 1;
     elseif strcmp(name, 'ordered'),        opts.ordered = 1;
+    elseif strcmp(name, 'parity'),         opts.ordered = 2;
     end                                     % unknown names are ignored, as in VLG
     k = k + 1;
 end

@@ -9,7 +9,9 @@
  *   pivot        1 x m, non-zero = fixed camera  ('fix_pivot', :62-65)
  *   semantics    0 bundle_euclid.m, 1 bundle_euclid_nomex.m
  *   max_iter, max_iter2, lambda0        0 = the reference's 20 / 10 / 1e-3
- *   device, ordered                     HIP device, 1 = ordered (parity) sums
+ *   device                              HIP device
+ *   ordered        1 ordered sums, 2 parity mode (bit-identical LM trajectory)
+ *   stop_rel       relative-decrease stop of bundle_euclid.m:123 (0 = 1e-3)
  */
 #ifndef VLGBA_MEX_LM_H
 #define VLGBA_MEX_LM_H
@@ -65,7 +67,8 @@ static void vm_lm(const char *who, int model, const double *K, const mxArray *pa
     o.max_iter2 = (int)vm_opt(popt, "max_iter2", 0);
     o.lambda0 = vm_opt(popt, "lambda0", 0);
     o.device = (int)vm_opt(popt, "device", 0);
-    o.ordered = vm_opt(popt, "ordered", 0) != 0;
+    o.ordered = (int)vm_opt(popt, "ordered", 0);
+    o.stop_rel = vm_opt(popt, "stop_rel", 0);
     max_iter = o.max_iter > 0 ? o.max_iter : 20;
     {
         const mxArray *pv = popt ? mxGetField(popt, 0, "pivot") : NULL;

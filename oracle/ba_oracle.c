@@ -451,3 +451,76 @@ double oracle_sp_update(int m, int n, int num_a, const int *pt_ptr, const int *o
     return oracle_sp_update_nd(m, n, num_a, 6, pt_ptr, obs_cam, obs_x, W, da, eB, Vinv, K4, a,
                                b, db, a_new, b_new, obs_xhat);
 }
+
+/* ===================================================================== *
+ *  Parity-mode pieces (the GPU's vlgba_options.ordered = 2)             *
+ * ===================================================================== */
+
+/* sum_k x[k] * y[k], sequentially in index order (a naive dot: the order of
+ * MATLAB's e_stack' * e_stack, bundle_euclid.m:207-210, is BLAS's and not
+ * reproducible; this fixes one) */
+double oracle_seq_dot(const double *x, const double *y, long long n)
+{
+    long long k;
+    double s = 0.0;
+    for (k = 0; k < n; k++)
+        s = s + x[k] * y[k];
+    return s;
+}
+
+/* sum_k dp[k] * (lambda * dp[k] + g[k]) sequentially (bundle_euclid.m:217) */
+double oracle_seq_dpg(const double *dp, const double *g, double lambda, long long n)
+{
+    long long k;
+    double s = 0.0;
+    for (k = 0; k < n; k++)
+        s = s + dp[k] * (lambda * dp[k] + g[k]);
+    return s;
+}
+
+/* da = S \ e_ by a left-looking Cholesky of the lower triangle of S (column
+ * major, ld x ld, overwritten by L), every sum in ascending index order, and
+ * the two triangular solves.  Rows whose diagonal is exactly zero (fixed
+ * parameters, App. A Q2/Q8) get a unit diagonal and a zero right-hand side:
+ * pinv(S) e_ is zero there.  Returns 0, or j + 1 for a non-positive pivot at
+ * column j (the caller then uses pinv, as bundle_euclid.m:193 always does). */
+int oracle_chol_seq(int n, double *S, const double *e_, double *da)
+{
+    const size_t ld = (size_t)n;
+    int i, j, k;
+    for (j = 0; j < n; j++)
+        da[j] = e_[j];
+    for (j = 0; j < n; j++)
+        if (S[j + ld * j] == 0.0) {
+            S[j + ld * j] = 1.0;
+            da[j] = 0.0;
+        }
+    for (j = 0; j < n; j++) {
+        double s = S[j + ld * j], p;
+        for (k = 0; k < j; k++)
+            s = s - S[j + ld * k] * S[j + ld * k];
+        if (!(s > 0.0))
+            return j + 1;
+        p = sqrt(s);
+        S[j + ld * j] = p;
+        for (i = j + 1; i < n; i++) {
+            double t = S[i + ld * j];
+            for (k = 0; k < j; k++)
+                t = t - S[i + ld * k] * S[j + ld * k];
+            S[i + ld * j] = t / p;
+        }
+    }
+    for (i = 0; i < n; i++) {
+        double t = da[i];
+        for (k = 0; k < i; k++)
+            t = t - S[i + ld * k] * da[k];
+        da[i] = t / S[i + ld * i];
+    }
+    for (i = n - 1; i >= 0; i--) {
+        double t = da[i];
+        for (k = i + 1; k < n; k++)
+            t = t - S[k + ld * i] * da[k];
+        da[i] = t / S[i + ld * i];
+    }
+    return 0;
+}

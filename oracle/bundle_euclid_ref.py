@@ -18,6 +18,14 @@ Knobs (all default to the reference's semantics):
                       oracle/orc_math.h (bit-exact chain; bounded vs 'pinv')
   solve = 'pinv'   -> da = pinv(S) * e_ (bundle_euclid.m:193)
           'chol'   -> Cholesky with exact-zero rows fixed (the device's rule)
+          'seq'    -> oracle_chol_seq: left-looking Cholesky, sums in index
+                      order (the GPU's parity-mode solve, bit for bit); pinv
+                      on a non-positive pivot
+  sums  = 'blas'   -> e'e and dp'(lambda dp + g) as numpy dots
+          'seq'    -> sequential sums in MATLAB's flat (column-major) order
+                      (the GPU's parity mode)
+  stop_rel / max_iter / max_iter2 / lambda0: the LM constants of
+          bundle_euclid.m:111-123 (defaults 1e-3 / 20 / 10 / 1e-3)
 """
 from __future__ import annotations
 
@@ -42,6 +50,12 @@ def _lib(variant: str = ""):
         lib = ctypes.CDLL(path)
         lib.oracle_sp_update.restype = ctypes.c_double
         lib.oracle_sp_update_nd.restype = ctypes.c_double
+        lib.oracle_seq_dot.restype = ctypes.c_double
+        lib.oracle_seq_dot.argtypes = [_dp, _dp, ctypes.c_longlong]
+        lib.oracle_seq_dpg.restype = ctypes.c_double
+        lib.oracle_seq_dpg.argtypes = [_dp, _dp, ctypes.c_double, ctypes.c_longlong]
+        lib.oracle_chol_seq.restype = ctypes.c_int
+        lib.oracle_chol_seq.argtypes = [ctypes.c_int, _dp, _dp, _dp]
         _LIBS[variant] = lib
     return _LIBS[variant]
 
@@ -141,6 +155,29 @@ def chol_solve_fixed(S, e_):
     rhs[zero] = 0.0
     c = sl.cho_factor(S, lower=True, check_finite=False)
     return sl.cho_solve(c, rhs, check_finite=False).reshape(-1, 1)
+
+
+def chol_seq(S, e_, lib=None):
+    """oracle_chol_seq on a copy of S: (da (ld, 1), rc); rc != 0 = non-positive pivot."""
+    lib = lib or _lib()
+    A = np.array(S, dtype=np.float64, order="F")
+    rhs = np.ascontiguousarray(np.array(e_, dtype=np.float64).reshape(-1))
+    da = np.zeros_like(rhs)
+    rc = lib.oracle_chol_seq(A.shape[0], P(A), P(rhs), P(da))
+    return da.reshape(-1, 1), rc
+
+
+def seq_dot(v, lib=None):
+    lib = lib or _lib()
+    v = np.ascontiguousarray(v, dtype=np.float64).reshape(-1)
+    return float(lib.oracle_seq_dot(P(v), P(v), v.size))
+
+
+def seq_dpg(dp, g, lam, lib=None):
+    lib = lib or _lib()
+    dp = np.ascontiguousarray(dp, dtype=np.float64).reshape(-1)
+    g = np.ascontiguousarray(g, dtype=np.float64).reshape(-1)
+    return float(lib.oracle_seq_dpg(P(dp), P(g), float(lam), dp.size))
 
 
 def pinv3_formula(Vs, lib=None):
@@ -295,7 +332,8 @@ def unpack(K, a, b, Xe, nvk):
 
 
 def bundle_euclid_ref(K, Te, w, Xe, x, *varargin, form="dense", vinv="pinv", solve="pinv",
-                      lib=None, trace=None, semantics="mex"):
+                      lib=None, trace=None, semantics="mex", sums="blas", stop_rel=1e-3,
+                      max_iter=20, max_iter2=10, lambda0=1e-3):
     """[K_ Te_ w_ Xe_ error_] = bundle_euclid(K, Te, w, Xe, x, ...) restated.
 
     trace: optional list; per iteration a dict (lambda, accepted, old, new, rho)
@@ -323,16 +361,18 @@ def bundle_euclid_ref(K, Te, w, Xe, x, *varargin, form="dense", vinv="pinv", sol
         pt, cam, _ = obs_from_visibility(vis)
         obs_x = np.stack([X[0, pt, cam], X[1, pt, cam]], axis=1)
         pb = SparseProblem(m, n, pt, cam, obs_x, K)
-    lam, nu = 0.001, 2.0
-    it, it2, max_iter, max_iter2 = 1, 0, 20, 10
+    lam, nu = lambda0, 2.0
+    it, it2 = 1, 0
     err: list = []
+    if form == "sparse" and sums == "seq":   # camera-major: MATLAB's e(:) order
+        cm = np.lexsort((pb.obs_pt, pb.obs_cam))
 
     def cont():
         if not (it < max_iter and it2 < max_iter2):
             return False
         if it < 3:
             return True
-        return err[it - 1] > 1e-20 and err[it - 2] - err[it - 1] > 1e-3 * err[it - 2]
+        return err[it - 1] > 1e-20 and err[it - 2] - err[it - 1] > stop_rel * err[it - 2]
 
     while cont():
         # (ii)-(iii) linearisation, bundle_euclid.m:139
@@ -370,24 +410,40 @@ def bundle_euclid_ref(K, Te, w, Xe, x, *varargin, form="dense", vinv="pinv", sol
             Y = sp_y(pb, W, Vinv, num_a, lib)
             S, e_ = sp_schur(pb, Y, W, Us, eA, eB, num_a, lib)
         # (vi) reduced solve, :193
-        da = matlab_pinv(S) @ e_ if solve == "pinv" else chol_solve_fixed(S, e_)
+        if solve == "pinv":
+            da = matlab_pinv(S) @ e_
+        elif solve == "seq":
+            da, rc = chol_seq(S, e_, lib)
+            if rc:
+                da = matlab_pinv(S) @ e_
+        else:
+            da = chol_solve_fixed(S, e_)
         da = F(da)
         # (vii)-(viii), :204-210
         if form == "dense":
             db, a_new, b_new, X_hat_new = mex3(W, da, eB, Vinv, K, a, b, X, vis, lib)
             e_new = X - X_hat_new
-            old_error = float(e.reshape(-1, order="F") @ e.reshape(-1, order="F"))
-            new_error = float(e_new.reshape(-1, order="F") @ e_new.reshape(-1, order="F"))
+            if sums == "seq":
+                old_error = seq_dot(e.reshape(-1, order="F"), lib)
+                new_error = seq_dot(e_new.reshape(-1, order="F"), lib)
+            else:
+                old_error = float(e.reshape(-1, order="F") @ e.reshape(-1, order="F"))
+                new_error = float(e_new.reshape(-1, order="F") @ e_new.reshape(-1, order="F"))
         else:
             db, a_new, b_new, xh, _ = sp_update(pb, W, da, eB, Vinv, a, b, num_a, lib,
                                                 ndb=num_a if nomex else 6)
             en = pb.obs_x - xh
-            old_error = float(e.reshape(-1) @ e.reshape(-1))
-            new_error = float(en.reshape(-1) @ en.reshape(-1))
+            if sums == "seq":
+                old_error = seq_dot(e[cm].reshape(-1), lib)
+                new_error = seq_dot(en[cm].reshape(-1), lib)
+            else:
+                old_error = float(e.reshape(-1) @ e.reshape(-1))
+                new_error = float(en.reshape(-1) @ en.reshape(-1))
         # (ix)-(x), :215-241
         g = np.concatenate([eA.reshape(-1, order="F"), eB.reshape(-1, order="F")])
         dp = np.concatenate([da.reshape(-1, order="F"), db.reshape(-1, order="F")])
-        rho = (old_error - new_error) / float(dp @ (lam * dp + g))
+        dpg = seq_dpg(dp, g, lam, lib) if sums == "seq" else float(dp @ (lam * dp + g))
+        rho = (old_error - new_error) / dpg
         accepted = (old_error - new_error) > 0
         if trace is not None:
             trace.append(dict(lam=lam, accepted=bool(accepted), old=old_error, new=new_error,

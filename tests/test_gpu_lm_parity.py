@@ -1,0 +1,207 @@
+"""Whole-LM parity of the GPU path with the CPU oracle.
+
+1. Parity mode (vlgba_options.ordered = 2): ordered sums, the sequential
+   Cholesky (oracle_chol_seq's loops) and the LM scalars e'e and
+   dp'(lambda dp + g) summed in MATLAB's flat column-major order.  The oracle
+   run with the same choices (vinv="formula", solve="seq", sums="seq") is the
+   reference restated with one fixed summation order where MATLAB's BLAS /
+   LAPACK order is unknowable.  Bar: error_ and the returned K_, Te_, w_, Xe_
+   BIT-IDENTICAL (np.array_equal), every pass.
+2. Converged minimum: the default (fast) GPU path and the oracle with the
+   reference's own MATLAB semantics (SVD pinv for V* and S, numpy dots) run
+   with a tightened stop rule (relative decrease < 1e-9, max_iter 100) reach
+   final costs within 1e-6 relative (the north star's bar).
+3. The pinv fallback: a non-positive pivot in the reduced solve takes
+   da = pinv(S) e_ (bundle_euclid.m:193, App. A Q8) instead of a rejection.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _scene(kind):
+    from bundleadjustmentmatlab_amd.scene import make_config
+    if kind == "cfg1":
+        return make_config("cfg1")
+    if kind == "small":
+        return make_config("cfg1", m=6, min_n=30, max_n=60, seed=7)
+    if kind == "banded":
+        return make_config("cfg2", m=24, n=1500, seed=9)
+    raise ValueError(kind)
+
+
+CASES = [
+    ("cfg1", ("fix_calibration",), "mex"),
+    ("small", ("fix_principal",), "mex"),
+    ("small", (), "mex"),
+    ("small", ("fix_calibration", "fix_structure"), "mex"),
+    ("small", ("fix_calibration", "fix_motion"), "mex"),
+    ("small", ("fix_calibration", "fix_pivot", "PIVOT"), "mex"),
+    ("small", (), "nomex"),
+    ("banded", ("fix_calibration",), "mex"),
+]
+
+
+@pytest.mark.parametrize("kind,opts,sem", CASES)
+def test_parity_mode_bit_identical_trajectory(gpu, oracle, kind, opts, sem):
+    sc = _scene(kind)
+    x, vis = sc.dense()
+    opts = tuple(np.arange(sc.m) < 2 if o == "PIVOT" else o for o in opts)
+    got = gpu.bundle_euclid(sc.K, sc.T0, sc.w0, sc.X0, x, "visibility", vis, *opts,
+                            semantics=sem, parity=True)
+    ref = oracle.bundle_euclid_ref(sc.K, sc.T0, sc.w0, sc.X0, x, "visibility", vis, *opts,
+                                   form="sparse", vinv="formula", solve="seq", sums="seq",
+                                   semantics=sem)
+    assert len(got[4]) >= 2
+    assert np.array_equal(got[4], ref[4]), (got[4], ref[4])
+    for g, r, nm in zip(got[:4], ref[:4], ("K_", "Te_", "w_", "Xe_")):
+        assert np.array_equal(g, r), nm
+
+
+def test_parity_mode_visibility_values_and_zero_observation(gpu, oracle):
+    """Non-unit visibility values (num_vis sums the values, bundle_euclid.m:82,
+    App. A Q10) and a visible observation at x = (0, 0) (visible only through
+    'visibility'; the default map x(1)~=0 | x(2)~=0 would drop it)."""
+    sc = _scene("small")
+    x, vis = sc.dense()
+    vis = vis.astype(np.float64)
+    i, j = np.argwhere(vis > 0)[3]
+    x[0:2, i, j] = 0.0                      # measured at the image origin, still visible
+    vis[vis > 0] = np.where(np.arange((vis > 0).sum()) % 3 == 0, 2.5, 1.0)
+    got = gpu.bundle_euclid(sc.K, sc.T0, sc.w0, sc.X0, x, "visibility", vis, "fix_calibration",
+                            parity=True)
+    ref = oracle.bundle_euclid_ref(sc.K, sc.T0, sc.w0, sc.X0, x, "visibility", vis,
+                                   "fix_calibration", form="sparse", vinv="formula",
+                                   solve="seq", sums="seq")
+    assert np.array_equal(got[4], ref[4]), (got[4], ref[4])
+    for g, r in zip(got[:4], ref[:4]):
+        assert np.array_equal(g, r)
+    # num_vis = sum of the values: error_(1) * num_vis = e'e
+    assert vis.sum() != (vis != 0).sum()
+
+
+@pytest.mark.parametrize("kind,opts", [("cfg1", ("fix_calibration",)),
+                                       ("banded", ("fix_calibration",)),
+                                       ("small", ("fix_calibration",))])
+def test_converged_cost_within_1e6(gpu, oracle, kind, opts):
+    """Tightened stop rule: the fast GPU path and the reference's MATLAB
+    semantics (SVD pinv for V* and S) converge to the same minimum: final
+    costs within 1e-6 relative."""
+    sc = _scene(kind)
+    x, vis = sc.dense()
+    kw = dict(stop_rel=1e-9, max_iter=100, max_iter2=30)
+    got = gpu.bundle_euclid(sc.K, sc.T0, sc.w0, sc.X0, x, "visibility", vis, *opts, **kw)
+    ref = oracle.bundle_euclid_ref(sc.K, sc.T0, sc.w0, sc.X0, x, "visibility", vis, *opts,
+                                   form="sparse", vinv="pinv", solve="pinv", **kw)
+    e_g, e_r = got[4][-1], ref[4][-1]
+    assert abs(e_g - e_r) <= 1e-6 * e_r, (got[4], ref[4])
+
+
+def test_pinv_solve_entry_matches_eigh(gpu):
+    """rocSOLVER dsyevd + the pinv kernels on an indefinite symmetric S with a
+    known null space: pinv(S) e_ to 1e-10 of numpy's eigen pinv."""
+    rng = np.random.default_rng(3)
+    n = 90
+    Q, _ = np.linalg.qr(rng.normal(size=(n, n)))
+    ev = rng.uniform(0.5, 5.0, n) * rng.choice([-1.0, 1.0], n)
+    ev[:4] = 0.0                              # exact null space: pinv drops it
+    S = np.asfortranarray((Q * ev) @ Q.T)
+    e_ = rng.normal(size=n)
+    da = np.zeros(n)
+    P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    assert gpu.lib().vlgba_debug_pinv_solve(n, P(S), P(e_), P(da)) == 0
+    w, V = np.linalg.eigh(S)
+    tol = n * np.spacing(np.abs(w).max())
+    keep = np.abs(w) > tol
+    want = V[:, keep] @ ((V[:, keep].T @ e_) / w[keep])
+    assert np.abs(da - want).max() <= 1e-10 * np.abs(want).max()
+
+
+def test_pinv_fallback_takes_the_step(gpu, oracle):
+    """lambda0 = 1e-10 leaves S nearly singular along the gauge (eigenvalues
+    5e-3 .. 5e7): the Cholesky meets a non-positive pivot.  The reference takes
+    pinv(S) e_ anyway (bundle_euclid.m:193); so does the GPU (info.pinv).
+    In ordered mode S and e_ equal the oracle's bit for bit, so the GPU step
+    equals the oracle's eigen-pinv step to the eigensolver's rounding (da 1e-6,
+    new cost 1e-9) and MATLAB's SVD pinv step to S's conditioning (new cost
+    1e-3).  The fast path's S differs from the oracle's by summation order
+    (5e-9 relative here), which at this conditioning moves the near-null
+    directions entirely: it must still take a finite pinv step."""
+    sc = _scene("cfg1")
+    x, vis = sc.dense()
+    pt, cam = np.nonzero(vis)
+    obs_x = np.stack([x[0, pt, cam], x[1, pt, cam]], 1)
+    a = np.vstack([sc.w0, sc.T0])
+    b = np.asfortranarray(sc.X0[:3])
+    pb = oracle.SparseProblem(sc.m, sc.n, pt, cam, obs_x, sc.K)
+    L = oracle.sp_linearize(pb, a, b, 6)
+    lam = 1e-10
+    Us = L["U"].copy(order="F")
+    for k in range(6):
+        Us[k, k] = (1 + lam) * L["U"][k, k]
+    Vs = L["V"].copy(order="F")
+    for k in range(3):
+        Vs[k, k] = (1 + lam) * L["V"][k, k]
+    Vi = oracle.pinv3_formula(Vs)
+    Y = oracle.sp_y(pb, L["W"], Vi, 6)
+    S, e_ = oracle.sp_schur(pb, Y, L["W"], Us, L["eA"], L["eB"], 6)
+    _, rc = oracle.chol_seq(S, e_)
+    assert rc != 0                                   # the Cholesky really fails here
+    e1 = e_.reshape(-1)
+    w, V = np.linalg.eigh(np.tril(S) + np.tril(S, -1).T)
+    keep = np.abs(w) > len(w) * np.spacing(np.abs(w).max())
+    da_eig = V[:, keep] @ ((V[:, keep].T @ e1) / w[keep])
+    _, _, _, _, sse_eig = oracle.sp_update(pb, L["W"], da_eig.reshape(-1, 1), L["eB"], Vi, a, b,
+                                           6)
+    _, _, _, _, sse_svd = oracle.sp_update(pb, L["W"], oracle.matlab_pinv(S) @ e_, L["eB"], Vi,
+                                           a, b, 6)
+    for solver in ("auto", "sequential"):
+        for ordered in (True, False):
+            ba = gpu.BundleAdjuster(sc.K, pt, cam, obs_x, sc.n, 6, lambda0=lam, solver=solver,
+                                    ordered=ordered)
+            ba.set_params(a, b)
+            info = ba.step(relinearize=True, update_lm=False)
+            da, _ = ba.last_step()
+            ba.close()
+            assert info.pinv == 1 and info.chol_failed == 1, (solver, ordered)
+            assert np.isfinite(info.new_sse) and np.all(np.isfinite(da))
+            if ordered:
+                da = da.reshape(-1, order="F")
+                assert np.abs(da - da_eig).max() <= 1e-6 * np.abs(da_eig).max()
+                assert abs(info.new_sse - sse_eig) <= 1e-9 * sse_eig, (info.new_sse, sse_eig)
+                assert abs(info.new_sse - sse_svd) <= 1e-3 * sse_svd, (info.new_sse, sse_svd)
+
+
+def test_reduced_system_getter_matches_oracle(gpu, oracle):
+    """vlgba_get_reduced_system: ordered mode returns the oracle's S (lower
+    triangle) and e_ bit for bit; the fast path agrees to summation order."""
+    sc = _scene("banded")
+    x, vis = sc.dense()
+    a = np.vstack([sc.w0, sc.T0])
+    b = np.asfortranarray(sc.X0[:3])
+    pb = oracle.SparseProblem(sc.m, sc.n, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.K)
+    L = oracle.sp_linearize(pb, a, b, 6)
+    lam = 1e-3
+    Us = L["U"].copy(order="F")
+    for k in range(6):
+        Us[k, k] = (1 + lam) * L["U"][k, k]
+    Vs = L["V"].copy(order="F")
+    for k in range(3):
+        Vs[k, k] = (1 + lam) * L["V"][k, k]
+    Vi = oracle.pinv3_formula(Vs)
+    Y = oracle.sp_y(pb, L["W"], Vi, 6)
+    S, e_ = oracle.sp_schur(pb, Y, L["W"], Us, L["eA"], L["eB"], 6)
+    St = np.tril(S)
+    for ordered in (True, False):
+        ba = gpu.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, 6, ordered=ordered)
+        ba.set_params(a, b)
+        Sg, eg = ba.reduced_system()
+        ba.close()
+        if ordered:
+            assert np.array_equal(Sg, St) and np.array_equal(eg, e_.reshape(-1))
+        else:
+            assert np.abs(Sg - St).max() <= 1e-12 * np.abs(St).max()
+            assert np.abs(eg - e_.reshape(-1)).max() <= 1e-12 * np.abs(e_).max()
