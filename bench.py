@@ -48,7 +48,15 @@ def main():
     ap.add_argument("--mode", choices=["pass", "solve"], default="pass",
                     help="pass: one LM pass per step (headline); solve: one full LM "
                          "solve to convergence per step (bundle_euclid.m:111-249)")
+    ap.add_argument("--spawn-selftest", action="store_true",
+                    help="launch only: every rank joins the gloo group and reports (no GPU)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # not under torch.distributed.run: start one process per GPU ourselves,
+        # before this process touches the GPU
+        return spawn_ranks(args)
+    if args.spawn_selftest:
+        return spawn_selftest()
     if args.config == "cfg5":
         return bench_incremental(args)
 
@@ -146,7 +154,8 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(sc, a0, b0, num_a, args.cpu_sample_points)
+        cpu = cpu_baseline(sc, a0, b0, num_a, args.cpu_sample_points,
+                           dense=args.config in ("cfg1", "cfg2"))
 
     out = {
         "metric": "LM iterations/sec + observations/sec, 1000-cam/500k-pt synthetic",
@@ -175,6 +184,43 @@ def main():
     ba.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def spawn_ranks(args):
+    """bench.py --gpus N outside torch.distributed.run: N child processes of
+    this script with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT
+    set (the contract torchrun provides); rank 0 prints the JSON line.  The
+    parent never initialises the GPU.  Exit status: the first failing rank's."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    if bad:
+        sys.exit(bad[0])
+
+
+def spawn_selftest():
+    """Each rank joins the gloo process group; rank 0 prints the gathered ranks."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    t = torch.tensor([float(dist.get_rank())])
+    dist.all_reduce(t)
+    world = dist.get_world_size()
+    if dist.get_rank() == 0:
+        print(json.dumps({"world": world, "rank_sum": float(t.item()),
+                          "expected": world * (world - 1) / 2}), flush=True)
+    dist.destroy_process_group()
 
 
 def bench_solve(args, ba, sc, a0, b0, world, rank, barrier, torch, dist):
@@ -349,19 +395,15 @@ def kernel_roofline(name, tot_ms, calls, plan, n_passes):
     return hbm if hbm["frac"] >= fl["frac"] else fl
 
 
-def cpu_baseline(sc, a0, b0, num_a, sample_points):
-    """One LM pass of the multi-threaded CPU port (oracle/ba_cpu_mt.c, OpenMP
-    over the host cores with the reference's per-element arithmetic and
-    reduction orders; SURVEY.md 8.d "ref_sparse_mt") on the GPU box's host,
-    with the reduced solve as a dense LAPACK Cholesky (scipy / OpenBLAS)."""
-    import ctypes
-    import scipy.linalg as sl
+def cpu_baseline(sc, a0, b0, num_a, sample_points, dense=False):
+    """One LM pass of the CPU port on the GPU box's host (oracle/cpu_port.py,
+    SURVEY.md 8.d "ref_sparse_mt"): oracle/ba_cpu_mt.c -- the MEX stages'
+    per-element arithmetic and reduction orders, OpenMP over the host cores --
+    and the reduced solve as LAPACK's banded Cholesky (dpbtrf), the same exact
+    band structure the GPU's cyclic reduction uses.  dense=True adds "ref_dense"
+    (the reference's dense single-thread MEX loops + SVD pinv; configs 1-2)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import bundle_euclid_ref as ref   # builds oracle/build (incl. libba_cpu_mt.so) if needed
-    ref._lib()
-    L = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libba_cpu_mt.so"))
-    L.mt_linearize.restype = ctypes.c_double
-    L.mt_update.restype = ctypes.c_double
+    import cpu_port
     if sample_points and sample_points < sc.n:
         keep = sc.obs_pt < sample_points
         pt, cam, x = sc.obs_pt[keep], sc.obs_cam[keep], sc.obs_x[keep]
@@ -370,42 +412,36 @@ def cpu_baseline(sc, a0, b0, num_a, sample_points):
     else:
         pt, cam, x, n = sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n
         desc = f"1 full LM pass of the scene ({len(pt)} obs)"
-    m, N = sc.m, len(pt)
-    P = lambda arr: arr.ctypes.data_as(ctypes.c_void_p)
-    i32 = lambda arr: np.ascontiguousarray(arr, dtype=np.int32)
-    f64 = lambda arr: np.ascontiguousarray(arr, dtype=np.float64)
-    pt, cam, x = i32(pt), i32(cam), f64(x)
-    pt_ptr = i32(np.concatenate([[0], np.cumsum(np.bincount(pt, minlength=n))]))
-    order = np.argsort(cam, kind="stable")                  # camera-major, points ascending
-    cam_obs = i32(order)
-    cam_ptr = i32(np.concatenate([[0], np.cumsum(np.bincount(cam, minlength=m))]))
-    K = f64(sc.K.T.reshape(-1))
-    a = f64(np.asarray(a0).T.reshape(-1))
-    b = f64(np.asarray(b0)[:, :n].T.reshape(-1))
-    jrec, W, Y = np.empty(20 * N), np.empty(18 * N), np.empty(18 * N)
-    V, eB, Vinv = np.empty(9 * n), np.empty(3 * n), np.empty(9 * n)
-    U, eA = np.empty(36 * m), np.empty(6 * m)
-    ld = 6 * m
-    S, e_ = np.empty((ld, ld), order="F"), np.empty(ld)
-    db, b_new, a_new = np.empty(3 * n), np.empty(3 * n), np.empty(6 * m)
-    lam = 1e-3
-    ref.chol_solve_fixed(np.eye(8) * 2.0, np.ones(8))     # LAPACK / thread-pool start-up
-    t0 = time.perf_counter()
-    old = L.mt_linearize(n, P(pt_ptr), P(cam), P(x), P(K), P(a), P(b), P(jrec), P(W), P(V),
-                         P(eB))
-    L.mt_camera_reduce(m, P(cam_ptr), P(cam_obs), P(jrec), P(U), P(eA))
-    L.mt_damp_y(n, P(pt_ptr), ctypes.c_double(lam), P(V), P(W), P(Vinv), P(Y))
-    L.mt_schur(m, P(cam_ptr), P(cam_obs), P(pt), P(pt_ptr), P(cam), P(Y), P(W), P(U),
-               ctypes.c_double(lam), P(eA), P(eB), P(S), P(e_))
-    da = f64(ref.chol_solve_fixed(S, e_).reshape(-1))     # bundle_euclid.m:193 (dpotrf)
-    new = L.mt_update(m, n, P(pt_ptr), P(cam), P(x), P(K), P(W), P(da), P(eB), P(Vinv), P(a),
-                      P(b), P(db), P(a_new), P(b_new))
-    dt = time.perf_counter() - t0
-    threads = int(L.mt_threads())
-    log(f"[bench] cpu port: old_sse={old:.9g} new_sse={new:.9g} {dt:.2f} s")
-    return {"value": 1.0 / dt, "unit": "LM iterations/s", "cores": threads, "kind": "port",
-            "sample": desc + f"; OpenMP C port of the MEX stages ({threads} threads) + "
-                             f"LAPACK Cholesky of S; {dt:.2f} s"}
+    port = cpu_port.SparsePort(sc.m, n, pt, cam, x, sc.K)
+    b = np.asarray(b0)[:, :n]
+    # warm-up: OpenMP pool, LAPACK / scipy first-call costs
+    cpu_port.band_cholesky_solve(np.eye(12) * 2.0, np.ones(12))
+    port.one_pass(a0, b)
+    r = port.one_pass(a0, b)
+    dt = r["seconds"]["total"]
+    rd = port.one_pass(a0, b, solve="dense")
+    info = cpu_port.host_info()
+    log(f"[bench] cpu port: old_sse={r['old_sse']:.9g} new_sse={r['new_sse']:.9g} {dt:.3f} s "
+        f"(banded solve {r['seconds']['solve']:.4f} s, bandwidth {r['bandwidth']}; dense "
+        f"dpotrf {rd['seconds']['solve']:.3f} s) {info}")
+    out = {"value": 1.0 / dt, "unit": "LM iterations/s", "cores": info["omp_threads"],
+           "kind": "port",
+           "sample": desc + f"; OpenMP C port of the MEX stages ({info['omp_threads']} threads) "
+                            f"+ LAPACK banded Cholesky of S (bandwidth {r['bandwidth']}); "
+                            f"{dt:.3f} s",
+           "phases_s": r["seconds"], "dense_lapack_solve_s": rd["seconds"]["solve"],
+           "host": info, "old_sse": r["old_sse"], "new_sse": r["new_sse"]}
+    if dense:
+        x, vis = sc.dense()
+        a = np.asfortranarray(a0)
+        t, o, nw = cpu_port.dense_pass(sc.K, a, np.asfortranarray(b0), np.asfortranarray(x[0:2]),
+                                       vis.astype(np.float64))
+        out["ref_dense"] = {"value": 1.0 / t, "unit": "LM iterations/s", "cores": 1,
+                            "sample": "1 LM pass of the reference's dense n x m MEX loops "
+                                      "(oracle_mex1/2/3) + SVD pinv, one thread",
+                            "seconds": t, "old_sse": o, "new_sse": nw}
+        log(f"[bench] ref_dense: {t:.3f} s/pass")
+    return out
 
 
 if __name__ == "__main__":

@@ -116,3 +116,21 @@ def test_two_rank_pass_matches_single(tmp_path, oracle):
     assert np.array_equal(r0["da"], r1["da"])         # every rank solves the same system
     b_new = np.concatenate([r0["b_new"], r1["b_new"]], axis=1)
     assert np.allclose(b_new, full["b_new"], rtol=0, atol=1e-9)
+
+
+def test_bench_spawns_ranks():
+    """bench.py --gpus 2 outside torch.distributed.run launches two ranks that
+    rendezvous over gloo on 127.0.0.1 (no GPU touched: --spawn-selftest)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                          "--spawn-selftest"], capture_output=True, text=True, env=env,
+                         timeout=240, check=True)
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, out.stdout + out.stderr
+    rec = json.loads(line[0])
+    assert rec["world"] == 2 and rec["rank_sum"] == rec["expected"] == 1.0
