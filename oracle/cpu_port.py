@@ -67,14 +67,16 @@ def host_info():
             "blas": blas}
 
 
-def band_cholesky_solve(S, e_):
+def band_cholesky_solve(S, e_, bw=None):
     """da = S \\ e_ with LAPACK's banded Cholesky (dpbtrf / dpbtrs) on the band
-    of the lower triangle of S; exactly-zero rows fixed (unit diagonal, rhs 0:
-    the pinv rule of App. A Q2 / Q8).  Returns (da, lower bandwidth)."""
+    of the lower triangle of S (lower bandwidth bw; from S's non-zeros if
+    None); exactly-zero rows fixed (unit diagonal, rhs 0: the pinv rule of
+    App. A Q2 / Q8).  Returns (da, lower bandwidth)."""
     import scipy.linalg as sl
     ld = S.shape[0]
-    rows, cols = np.nonzero(S)
-    bw = int((rows - cols).max()) if rows.size else 0
+    if bw is None:
+        rows, cols = np.nonzero(S)
+        bw = int((rows - cols).max()) if rows.size else 0
     ab = np.zeros((bw + 1, ld))
     for d in range(bw + 1):
         ab[d, :ld - d] = np.diagonal(S, -d)
@@ -108,6 +110,12 @@ class SparsePort:
         self.S = np.empty((6 * m, 6 * m), order="F")
         self.e_ = np.empty(6 * m)
         self.db, self.b_new, self.a_new = np.empty(3 * n), np.empty(3 * n), np.empty(6 * m)
+        # lower bandwidth of S from the co-visibility (the widest camera span of
+        # a point's track): S_jk != 0 only for cameras seen by a common point
+        lo = np.minimum.reduceat(self.cam, self.pt_ptr[:-1]) if n else np.zeros(0, np.int32)
+        hi = np.maximum.reduceat(self.cam, self.pt_ptr[:-1]) if n else np.zeros(0, np.int32)
+        has = np.diff(self.pt_ptr) > 0
+        self.bw = int(6 * (hi[has] - lo[has]).max() + 5) if has.any() else 5
 
     def one_pass(self, a0, b0, lam=1e-3, solve="band"):
         """One LM pass at (a0 6 x m, b0 3 x n): dict of old / new SSE, S, e_,
@@ -132,7 +140,7 @@ class SparsePort:
         t.append(time.perf_counter())
         bw = None
         if solve == "band":
-            da, bw = band_cholesky_solve(self.S, self.e_)
+            da, bw = band_cholesky_solve(self.S, self.e_, self.bw)
         else:
             da = ref.chol_solve_fixed(self.S, self.e_).reshape(-1)
         da = f64(da)
