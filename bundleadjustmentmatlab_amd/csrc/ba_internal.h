@@ -159,7 +159,9 @@ struct ba_dev {
     double *xh_out;    // [N][2] projections (stage 1 and stage 3)
     double *B_out;     // [N][6] point Jacobians (stage 1)
     unsigned char *obs_vis;  // [N] stage 3: 0 = structural-only pair (no projection)
-    int schur_owner;   // this rank adds U* / eA into the reduced system
+    int schur_owner;   // this rank adds U* / eA into the reduced system (every rank
+                       // adds its own partials)
+    int dpg_lambda;    // this rank adds the lambda dp'dp part of the camera dpg
     double scal_host[8];
     struct ba_ktimer *kt;   // NULL unless kernel timing is enabled
     hipStream_t stream;

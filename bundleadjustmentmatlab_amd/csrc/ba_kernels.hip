@@ -1757,8 +1757,10 @@ int ba_launch_update(ba_dev *d, double lambda)
 {
     const int gc = (d->m + 63) / 64;
     KT_B(d);
+    // lambda dp'dp once over the ranks (each adds da' eA of its partial eA)
+    const double lam_dpg = d->dpg_lambda ? lambda : 0.0;
     BA_DISPATCH(d->na, (k_camera_update<NA><<<gc, 64, 0, d->stream>>>(
-                           d->a, d->da, d->eA, d->m, lambda, d->a_new, d->rot_new, d->part)));
+                           d->a, d->da, d->eA, d->m, lam_dpg, d->a_new, d->rot_new, d->part)));
     KT_E(d, KT_CAMUPD);
     if (!d->ordered && d->nch > 0 && !d->obs_vis && !d->xh_out) {
         KT_B(d);

@@ -781,7 +781,12 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
     d.N = (int)(o1 - o0);
     d.ld = (long long)na * p->m;
     d.lds = ((d.ld + 63) / 64) * 64;
-    d.schur_owner = (c->rank == 0);
+    // every rank adds its own partial U* / eA into its partial reduced system
+    // (the damping is linear: sum_r (1 + lambda) U_r = (1 + lambda) sum_r U_r),
+    // so U / eA never need an all-reduce of their own; the camera part of
+    // dp'(lambda dp + g) takes its lambda dp'dp term from rank 0 only
+    d.schur_owner = 1;
+    d.dpg_lambda = c->rank == 0;
     hipStream_t s = d.stream;
 
     // local point-major arrays
@@ -929,8 +934,9 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
     TRY(ctx_alloc(c, &d.blk_jk, 2 * (size_t)d.nb));
     TRY(ctx_alloc(c, &d.blk_ptr, (size_t)d.nb + 1));
     TRY(ctx_alloc(c, &d.term, 2 * (size_t)d.T));
-    TRY(ctx_alloc(c, &d.sblk, (size_t)na * na * d.nb + d.lds));
-    d.rhs = d.sblk + (size_t)na * na * d.nb;  // blocks | rhs contiguous: one all-reduce
+    // blocks | rhs | old SSE contiguous: one all-reduce per pass (world > 1)
+    TRY(ctx_alloc(c, &d.sblk, (size_t)na * na * d.nb + d.lds + 1));
+    d.rhs = d.sblk + (size_t)na * na * d.nb;
     if (!stage_mode) {
         TRY(ctx_alloc(c, &d.S, (size_t)(d.lds * d.lds)));
         TRY(ctx_alloc(c, &d.linv, (size_t)(d.lds / 64) * 64 * 64));
@@ -1105,7 +1111,15 @@ static int schur_phase(vlgba_ctx *c, double lam)
         mark(c, 3);
         TRY(ba_launch_schur_fast(&d, lam));
     }
-    TRY(allreduce(c, d.sblk, (size_t)d.na * d.na * d.nb + d.ld));
+    if (c->world > 1) {
+        // [S blocks | e_ | old SSE] of this rank's points -> the global system
+        double *sse = d.rhs + d.lds;
+        VLGBA_CHECK(hipMemcpyAsync(sse, d.eA + d.ld, sizeof(double), hipMemcpyDeviceToDevice,
+                                   d.stream));
+        TRY(allreduce(c, d.sblk, (size_t)d.na * d.na * d.nb + d.lds + 1));
+        VLGBA_CHECK(hipMemcpyAsync(d.scal + 0, sse, sizeof(double), hipMemcpyDeviceToDevice,
+                                   d.stream));
+    }
     return 0;
 }
 
@@ -1114,14 +1128,8 @@ static int schur_phase(vlgba_ctx *c, double lam)
 static int collect_scalars(vlgba_ctx *c, bool spin, double hs[5])
 {
     ba_dev &d = c->d;
-    if (c->world > 1) {
-        VLGBA_CHECK(hipMemcpyAsync(d.scal + 0, d.eA + d.ld, sizeof(double),
-                                   hipMemcpyDeviceToDevice, d.stream));
-        // global old_sse is already in d.eA[ld]; new_sse and the point part of dpg
-        // are local; the camera part of dpg is identical on every rank.
-        TRY(allreduce(c, d.scal + 1, 1));
-        TRY(allreduce(c, d.scal + 3, 1));
-    }
+    if (c->world > 1)   // new SSE, camera and point parts of dp'(lambda dp + g): local
+        TRY(allreduce(c, d.scal + 1, 3));   // (scal[0] = the global old SSE, schur_phase)
     if (spin) {
         // spin on the host-mapped sequence number written last (by the update's
         // final sums, or k_publish); lower latency than a copy +
@@ -1273,7 +1281,6 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
         if (d.ordered)
             VLGBA_CHECK(hipMemcpyAsync(d.eA + d.ld, d.scal + 0, sizeof(double),
                                        hipMemcpyDeviceToDevice, d.stream));
-        TRY(allreduce(c, d.U, (size_t)d.na * d.na * d.m + d.ld + 1));
         c->lin_valid = 1;
     } else {
         mark(c, 1);
@@ -1454,10 +1461,29 @@ int vlgba_get_linearization(vlgba_ctx *c, double *U, double *eA, double *V, doub
     if (d.ordered)
         VLGBA_CHECK(hipMemcpyAsync(d.eA + d.ld, d.scal + 0, sizeof(double),
                                    hipMemcpyDeviceToDevice, d.stream));
-    TRY(allreduce(c, d.U, (size_t)d.na * d.na * d.m + d.ld + 1));
     c->lin_valid = 1;
-    if (U) TRY(download(U, d.U, (size_t)d.na * d.na * d.m, d.stream));
-    if (eA) TRY(download(eA, d.eA, (size_t)d.ld, d.stream));
+    // U / eA stay per-rank partials on the device (schur_owner); the caller
+    // gets their sum over ranks
+    const size_t nue = (size_t)d.na * d.na * d.m + d.ld + 1;
+    double *ue = d.U;
+    if (c->world > 1) {
+        TRY(dalloc(&ue, nue));
+        VLGBA_CHECK(hipMemcpyAsync(ue, d.U, sizeof(double) * nue, hipMemcpyDeviceToDevice,
+                                   d.stream));
+        const int rc = allreduce(c, ue, nue);
+        if (rc) {
+            ba_dfree(ue);
+            return rc;
+        }
+    }
+    int rc = 0;
+    if (U) rc = download(U, ue, (size_t)d.na * d.na * d.m, d.stream);
+    if (!rc && eA) rc = download(eA, ue + (size_t)d.na * d.na * d.m, (size_t)d.ld, d.stream);
+    if (ue != d.U) {
+        (void)hipStreamSynchronize(d.stream);
+        ba_dfree(ue);
+    }
+    TRY(rc);
     if (V) TRY(download(V, d.V, 9 * (size_t)d.n, d.stream));
     if (eB) TRY(download(eB, d.eB, 3 * (size_t)d.n, d.stream));
     if (W) TRY(download(W, d.W, (size_t)3 * d.na * d.N, d.stream));
@@ -1476,7 +1502,6 @@ int vlgba_get_reduced_system(vlgba_ctx *c, int *blk_jk, double *blocks, double *
         if (d.ordered)
             VLGBA_CHECK(hipMemcpyAsync(d.eA + d.ld, d.scal + 0, sizeof(double),
                                        hipMemcpyDeviceToDevice, d.stream));
-        TRY(allreduce(c, d.U, (size_t)d.na * d.na * d.m + d.ld + 1));
         c->lin_valid = 1;
     }
     TRY(schur_phase(c, c->lambda));

@@ -1,10 +1,10 @@
 """World-size-2 gloo rehearsal (CPU) of the native point-sharded LM pass.
 
 Mirrors ba_solver.cpp's multi-GPU data path with the oracle as the compute:
-each rank linearises its contiguous point range (dist.shard_points), the
-U | eA | old-SSE vector is all-reduced, rank 0 alone adds U* and eA into the
-reduced system (the 'owner' rule of k_schur), the packed S / e_ partials are
-all-reduced, every rank solves the same system, and new-SSE is all-reduced.
+each rank linearises its contiguous point range (dist.shard_points) and adds
+its own partial U* and eA into its partial reduced system (damping is linear
+in U), [S | e_ | old SSE] is all-reduced once, every rank solves the same
+system, and the new SSE is all-reduced (two collectives per pass).
 The result must match the single-process pass (summation order differs, so
 to 1e-12 relative, not bits).
 """
@@ -35,15 +35,9 @@ def _pass(ref, pb_full, lo, hi, a, b, num_a, lam, world, rank):
     bl = np.asfortranarray(b[:, lo:hi])
     L = ref.sp_linearize(pb, a, bl, num_a)
     old = float(L["e"].reshape(-1) @ L["e"].reshape(-1))
-    vec = np.concatenate([L["U"].reshape(-1, order="F"), L["eA"].reshape(-1, order="F"), [old]])
-    if world > 1:
-        t = torch.from_numpy(vec.copy())
-        dist.all_reduce(t)
-        vec = t.numpy()
-    m = pb.m
-    U = vec[: num_a * num_a * m].reshape(num_a, num_a, m, order="F")
-    eA = vec[num_a * num_a * m: num_a * num_a * m + num_a * m].reshape(num_a, m, order="F")
-    old = vec[-1]
+    # every rank adds its own partial U* and eA into its partial reduced system
+    # (damping is linear in U); one all-reduce of [S | e_ | old SSE]
+    U, eA = L["U"], L["eA"]
     Us = U.copy(order="F")
     for k in range(num_a):
         Us[k, k] = (1 + lam) * U[k, k]
@@ -52,15 +46,14 @@ def _pass(ref, pb_full, lo, hi, a, b, num_a, lam, world, rank):
         Vs[k, k] = (1 + lam) * L["V"][k, k]
     Vinv = ref.pinv3_formula(Vs)
     Y = ref.sp_y(pb, L["W"], Vinv, num_a)
-    owner = rank == 0
-    S, e_ = ref.sp_schur(pb, Y, L["W"], Us if owner else np.zeros_like(Us),
-                         eA if owner else np.zeros_like(eA), L["eB"], num_a)
+    S, e_ = ref.sp_schur(pb, Y, L["W"], Us, eA, L["eB"], num_a)
     if world > 1:
-        t = torch.from_numpy(np.concatenate([S.reshape(-1, order="F"), e_.reshape(-1)]))
+        t = torch.from_numpy(np.concatenate([S.reshape(-1, order="F"), e_.reshape(-1), [old]]))
         dist.all_reduce(t)
         v = t.numpy()
         S = v[: S.size].reshape(S.shape, order="F")
-        e_ = v[S.size:].reshape(-1, 1)
+        e_ = v[S.size:S.size + e_.size].reshape(-1, 1)
+        old = float(v[-1])
     da = ref.chol_solve_fixed(S, e_)
     _, a_new, b_new, _, sse = ref.sp_update(pb, L["W"], da, L["eB"], Vinv, a, bl, num_a)
     if world > 1:

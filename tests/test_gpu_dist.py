@@ -1,9 +1,9 @@
 """Point-sharded solver on 2 ranks sharing one GPU (gloo host collective).
 
 Exercises every piece of libvlgba's multi-GPU data path -- contiguous point
-ranges, the owner rule for U* / eA, the all-reduce of U | eA | SSE, of the
-packed reduced system and of the scalars, the replicated solve, the full-b
-gather -- with the collective routed through vlgba_options.allreduce
+ranges, per-rank partial U* / eA in the partial reduced systems, the one
+all-reduce of [S blocks | e_ | old SSE] and the one of the three pass scalars,
+the replicated solve, the full-b gather -- with the collective routed through vlgba_options.allreduce
 (torch.distributed gloo) instead of RCCL, so it runs on a 1-GPU box.  Result:
 equal to the 1-rank solve to summation-order rounding, and identical on both
 ranks.
