@@ -7,7 +7,7 @@ hand-written gfx950 HIP kernels behind the C ABI in include/vlgba.h
 (libvlgba.so, built in-tree).
 """
 from .bundle import (BundleAdjuster, bundle_euclid, bundle_euclid_nomex,  # noqa: F401
-                     bundle_euclid_obs,
+                     bundle_euclid_obs, bundle_euclid_resect,
                      mex_bundle_1_XABeUVWeAeB, mex_bundle_2_Se_, mex_bundle_3_db_new,
                      parse_options)
 from .projective import (bundle_projective, bundle_projective_nomex,  # noqa: F401

@@ -43,6 +43,11 @@ NKERNELS = 16   # VLGBA_NKERNELS
 ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, c_dp, c_ll, ctypes.c_void_p)
 
 
+class VlgbaResectProblem(ctypes.Structure):
+    _fields_ = [("nprob", c_int), ("num_a", c_int), ("obs_ptr", ctypes.POINTER(c_ll)),
+                ("X", c_dp), ("x", c_dp), ("K", c_dp)]
+
+
 class VlgbaStats(ctypes.Structure):
     _fields_ = [("iterations", c_int), ("accepted", c_int), ("num_error", c_int),
                 ("lambda_", c_double), ("seconds", c_double)]
@@ -80,6 +85,8 @@ SIGNATURES = {
     "vlgba_mex_bundle_proj_1": (c_int, [c_int, c_int] + [c_dp] * 13),
     "vlgba_mex_bundle_proj_2": (c_int, [c_int, c_int] + [c_dp] * 7),
     "vlgba_mex_bundle_proj_3": (c_int, [c_int, c_int] + [c_dp] * 12),
+    "vlgba_resect": (c_int, [ctypes.POINTER(VlgbaResectProblem), ctypes.POINTER(VlgbaOptions),
+                             c_dp, c_dp, c_int, c_ip, ctypes.POINTER(VlgbaStats)]),
     "vlgba_version": (c_int, [ctypes.c_char_p, c_int]),
     "vlgba_get_unique_id": (c_int, [ctypes.c_void_p]),
     "vlgba_device_count": (c_int, []),

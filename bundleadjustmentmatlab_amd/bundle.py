@@ -26,10 +26,11 @@ import ctypes
 import numpy as np
 
 from ._lib import (ALLREDUCE_FN, MODEL_EUCLIDEAN, MODEL_PROJECTIVE, NKERNELS, VlgbaOptions,
-                   VlgbaProblem, VlgbaStats,
+                   VlgbaProblem, VlgbaResectProblem, VlgbaStats,
                    VlgbaStepInfo, c_dp, c_ip, c_up, check, lib)
 
 __all__ = ["bundle_euclid", "bundle_euclid_nomex", "bundle_euclid_obs", "BundleAdjuster",
+           "bundle_euclid_resect",
            "parse_options",
            "mex_bundle_1_XABeUVWeAeB", "mex_bundle_2_Se_", "mex_bundle_3_db_new"]
 
@@ -375,6 +376,51 @@ def bundle_euclid_nomex(K, Te, w, Xe, x, *varargin, device=0, return_stats=False
     db from every camera parameter (:268-277), no 'fix_pivot', Xe_(4,:) = 1."""
     return bundle_euclid(K, Te, w, Xe, x, *varargin, device=device,
                          return_stats=return_stats, semantics="nomex", **solver)
+
+
+def bundle_euclid_resect(K, Te, w, Xs, xs, *varargin, device=0, max_iter=0, max_iter2=0,
+                         lambda0=0.0, stop_rel=0.0, return_stats=False):
+    """Batched one-camera refinement with the structure fixed -- the call of
+    estimate_camera.m:247-253,
+
+        [K T Omega] = bundle_euclid(K, T, Omega, X, x0, 'fix_calibration',
+                                    'fix_structure', 'visibility', inlier')
+
+    for every camera q at once on the GPU (vlgba_resect).  K (4 x c), Te, w
+    (3 x c); Xs[q] the fixed points camera q sees (3 or 4 x n_q), xs[q] their
+    measured image points (2 or 3 x n_q; only the inliers).  Options as
+    bundle_euclid.m: 'fix_calibration' (num_a 6), 'fix_principal' (7), neither
+    (10); 'fix_structure' is implied.  Returns K_, Te_, w_ and the list of
+    per-camera error_ (SSE / n_q per accepted step)."""
+    K, Te, w = _F(K), _F(Te), _F(w)
+    c = w.shape[1]
+    o = parse_options(c, 0, varargin)
+    nvk = o["num_variableK"]
+    na = 6 + nvk
+    a = np.ascontiguousarray(pack_a(K, Te, w, nvk).reshape(-1, order="F"))
+    assert len(Xs) == len(xs) == c
+    cnt = [np.shape(X)[1] for X in Xs]
+    assert all(np.shape(x)[1] == k for x, k in zip(xs, cnt))
+    ptr = np.ascontiguousarray(np.concatenate([[0], np.cumsum(cnt)]), dtype=np.int64)
+    Xo = np.ascontiguousarray(np.concatenate([np.asarray(X, dtype=np.float64)[:3].T for X in Xs]
+                                             if c else np.zeros((0, 3))))
+    xo = np.ascontiguousarray(np.concatenate([np.asarray(x, dtype=np.float64)[:2].T for x in xs]
+                                             if c else np.zeros((0, 2))))
+    cap = (max_iter if max_iter > 0 else 20) + 1
+    err = np.zeros((c, cap))
+    nerr = np.zeros(c, dtype=np.int32)
+    pr = VlgbaResectProblem(c, na, ptr.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)),
+                            _dp(Xo), _dp(xo), _dp(np.ascontiguousarray(K.reshape(-1, order="F"))))
+    opt = VlgbaOptions()
+    opt.max_iter, opt.max_iter2, opt.lambda0 = int(max_iter), int(max_iter2), float(lambda0)
+    opt.device, opt.stop_rel = int(device), float(stop_rel)
+    st = VlgbaStats()
+    check(lib().vlgba_resect(ctypes.byref(pr), ctypes.byref(opt), _dp(a), _dp(err), cap,
+                             nerr.ctypes.data_as(c_ip), ctypes.byref(st)), "vlgba_resect")
+    a = a.reshape(na, c, order="F")
+    K_, Te_, w_, _ = unpack(K, a, np.zeros((3, 0)), np.zeros((1, 0)), nvk)
+    errs = [err[q, : nerr[q]].copy() for q in range(c)]
+    return (K_, Te_, w_, errs, st) if return_stats else (K_, Te_, w_, errs)
 
 
 # ---------------------------------------------------------------------------

@@ -3,12 +3,14 @@ toolbox/geometry/incr_reconstruction.m:223-341 (SURVEY.md sec. 8.f rank 2,
 BASELINE.json config 5).
 
 The reference adds cameras one at a time.  Per added camera j it estimates
-the pose (estimate_camera.m), removes outliers, runs ``bundle_euclid`` over
+the pose (estimate_camera.m: DLT + RANSAC, then a one-camera ``bundle_euclid``
+with the structure fixed, :247-253), removes outliers, runs ``bundle_euclid`` over
 the cameras added so far and the points reconstructed so far, aligns the
 scene (align_scene.m), triangulates the points that now have >= 2 views,
 removes outliers again and runs ``bundle_euclid`` a second time.  The BA
-solves are the hot path and run on the GPU here (``bundle_euclid_obs``);
-pose estimation, outlier removal and triangulation are out of scope (SURVEY.md
+solves are the hot path and run on the GPU here (``bundle_euclid_obs``, and
+``bundle_euclid_resect`` for estimate_camera's one-camera refinement); the DLT /
+RANSAC pose, outlier removal and triangulation are out of scope (SURVEY.md
 sec. 2) and are replaced by the synthetic scene's perturbed initial values
 (the new camera's (w0, T0), the point's X0) -- the BA sequence, its growing
 problem sizes and its visibility subsets are the reference's.
@@ -22,7 +24,7 @@ import time
 
 import numpy as np
 
-from .bundle import bundle_euclid_obs
+from .bundle import bundle_euclid_obs, bundle_euclid_resect
 from .evaluation import align_scene, vl_irodr, vl_rodr
 
 __all__ = ["incremental_bundle"]
@@ -47,9 +49,10 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
     reconstruction (VLmvg.m's two_view step); every other camera is added in
     index order (incr_reconstruction.m:223-227).
 
-    Returns dict(solves=[...], K, T, w, X, status) where each solve records the
-    cameras / points / observations it adjusted, its error_ trace, LM passes
-    and wall seconds."""
+    Returns dict(solves=[...], resections=[...], K, T, w, X, status) where each
+    solve records the cameras / points / observations it adjusted, its error_
+    trace, LM passes and wall seconds, and each resection the added camera's
+    one-camera refinement (estimate_camera.m:247-253)."""
     m, n = sc.m, sc.n
     K = np.array(sc.K, dtype=np.float64)
     T = np.array(sc.T0, dtype=np.float64)
@@ -63,7 +66,7 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
     X[:3, tri] = sc.X0[:3, tri]
     X[3, tri] = 1.0
     opts = ("fix_calibration",) if fix_calibration else ()
-    solves = []
+    solves, resections = [], []
 
     def ba(tag, j):
         cams = np.nonzero(status)[0]
@@ -87,14 +90,30 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
             print(f"[incremental] camera {j} {tag}: {len(cams)} cams {len(pts)} pts "
                   f"{len(pt)} obs  error_ {err[0]:.4g} -> {err[-1]:.4g}  {st.iterations} passes")
 
+    def resect(j):
+        """estimate_camera.m:247-253: the new camera refined against the points
+        reconstructed so far that it sees (structure fixed), on the GPU."""
+        sel = (sc.obs_cam == j) & (X[3, sc.obs_pt] == 1)
+        if sel.sum() < 6:
+            return
+        ids = sc.obs_pt[sel]
+        t0 = time.perf_counter()
+        K_, T_, w_, errs = bundle_euclid_resect(K[:, j:j + 1], T[:, j:j + 1], w[:, j:j + 1],
+                                                [X[:, ids]], [sc.obs_x[sel].T], *opts,
+                                                device=device)
+        K[:, j], T[:, j], w[:, j] = K_[:, 0], T_[:, 0], w_[:, 0]
+        resections.append(dict(camera=int(j), observations=int(sel.sum()),
+                               error=errs[0], seconds=time.perf_counter() - t0))
+
     for j in range(m):                                   # :223
         if status[j]:
             continue
         status[j] = True
         s_, R_, t_ = _similarity(sc, X)                  # ground truth -> current frame
-        Rc = vl_rodr(sc.w0[:, j]) @ R_.T                 # estimate_camera stand-in: the
-        w[:, j] = vl_irodr(Rc)                           # perturbed pose in the current frame
+        Rc = vl_rodr(sc.w0[:, j]) @ R_.T                 # DLT stand-in: the perturbed
+        w[:, j] = vl_irodr(Rc)                           # pose in the current frame
         T[:, j] = s_ * sc.T0[:, j] - Rc @ t_
+        resect(j)                                        # :230, estimate_camera.m:247-253
         ba("before-triangulation", j)                    # :250-267
         nvis[:] = 0
         np.add.at(nvis, sc.obs_pt, status[sc.obs_cam])
@@ -103,7 +122,7 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
         X[:3, new] = s_ * R_ @ sc.X0[:3, new] + t_[:, None]
         X[3, new] = 1.0
         ba("after-triangulation", j)                     # :300-318
-    return dict(solves=solves, K=K, T=T, w=w, X=X, status=status)
+    return dict(solves=solves, resections=resections, K=K, T=T, w=w, X=X, status=status)
 
 
 def _similarity(sc, X):

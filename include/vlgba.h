@@ -249,6 +249,32 @@ int vlgba_mex_bundle_proj_3(int m, int n, const double *W, const double *da, con
                             const double *X, const double *vis, double *db, double *a_new,
                             double *b_new, double *X_hat);
 
+/* ---- batched one-camera refinement with the structure fixed ---------------
+ * The bundle_euclid call of estimate_camera.m:247-253,
+ *   bundle_euclid(K, T, Omega, X, x0, ['fix_calibration',] 'fix_structure',
+ *                 'visibility', inlier')
+ * for nprob independent cameras at once (one workgroup per camera and LM
+ * pass; the LM rule of bundle_euclid.m:111-241 per camera on the host).  Each
+ * camera's trajectory equals the parity-mode solver's (and the CPU oracle's)
+ * bit for bit.  Camera q sees observations obs_ptr[q] .. obs_ptr[q+1]-1 of
+ * fixed points X (3 per observation) measured at x (2 per observation);
+ * num_vis = its observation count. */
+typedef struct {
+    int nprob;
+    int num_a;                 /* 6 fix_calibration, 7 fix_principal, 10 free K */
+    const long long *obs_ptr;  /* [nprob + 1], obs_ptr[0] = 0                  */
+    const double *X;           /* [3 * N] world point of each observation      */
+    const double *x;           /* [2 * N] measured (u, v)                       */
+    const double *K;           /* [4 * nprob] fx fy cx cy                       */
+} vlgba_resect_problem;
+
+/* a (num_a x nprob, [w; T; (K)] per camera) is the start point and receives the
+ * result; error_out (nprob x error_cap, row q = camera q's error_) and
+ * num_error (nprob) may be NULL.  opt: max_iter, max_iter2, lambda0,
+ * stop_rel, device are honoured (the rest does not apply). */
+int vlgba_resect(const vlgba_resect_problem *prob, const vlgba_options *opt, double *a,
+                 double *error_out, int error_cap, int *num_error, vlgba_stats *stats);
+
 /* Multi-GPU: rank 0 creates the 128-byte RCCL unique id, the caller
  * broadcasts it (e.g. torch.distributed) and passes it as opt->comm_id. */
 int vlgba_get_unique_id(void *id128);
