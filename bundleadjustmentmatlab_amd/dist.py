@@ -37,3 +37,86 @@ def shard_points(pt_ptr: np.ndarray, world: int, rank: int) -> tuple[int, int]:
     p0 = 0 if rank == 0 else bound(rank)
     p1 = n if rank == world - 1 else bound(rank + 1)
     return p0, p1
+
+
+# ---------------------------------------------------------------------------
+# Elastic shard count (BASELINE.json config 5: "1 -> 8 GPU elastic point
+# shard"): each growing-BA call picks its own number of ranks from its size,
+# and the ranks run as threads of one process, one libvlgba context per rank
+# on device rank % ndev, their collectives through host memory.
+# ---------------------------------------------------------------------------
+OBS_PER_SHARD = 250_000   # below this a rank's pass is launch / latency bound
+
+
+def choose_shards(num_obs: int, ndev: int, obs_per_shard: int = OBS_PER_SHARD) -> int:
+    """Ranks for one solve: the largest power of two <= ndev that keeps at
+    least obs_per_shard observations per rank (1 for the small early solves
+    of a growing reconstruction, up to ndev for the large ones)."""
+    k = 1
+    while k * 2 <= max(1, ndev) and num_obs // (k * 2) >= obs_per_shard:
+        k *= 2
+    return k
+
+
+class HostGroup:
+    """In-process all-reduce for `world` rank threads: each rank's
+    allreduce(buf) blocks until every rank has contributed, then every rank
+    receives the element-wise sum in rank order (deterministic)."""
+
+    def __init__(self, world: int):
+        import threading
+        self.world = world
+        self._bar = threading.Barrier(world)
+        self._bufs = [None] * world
+        self._sum = None
+
+    def allreduce_fn(self, rank: int):
+        def ar(buf: np.ndarray):
+            self._bufs[rank] = buf.copy()
+            if self._bar.wait() == 0:
+                s = self._bufs[0].copy()
+                for r in range(1, self.world):
+                    s += self._bufs[r]
+                self._sum = s
+            self._bar.wait()
+            buf[:] = self._sum
+            self._bar.wait()
+        return ar
+
+
+def run_sharded(K, obs_pt, obs_cam, obs_x, n, num_a, a, b, world, *, devices=None, **kw):
+    """One LM solve (vlgba_run) over `world` rank threads.  Returns
+    (a, b, error_, stats) of rank 0 (every rank holds the same a, b, error_)."""
+    import threading
+    from .bundle import BundleAdjuster
+    if world <= 1:
+        with BundleAdjuster(K, obs_pt, obs_cam, obs_x, n, num_a, **kw) as ba:
+            ba.set_params(a, b)
+            err, st = ba.run()
+            a2, b2 = ba.get_params()
+        return a2, b2, err, st
+    devices = devices or [0]
+    grp = HostGroup(world)
+    out = [None] * world
+    errs = []
+
+    def rank_main(r):
+        try:
+            with BundleAdjuster(K, obs_pt, obs_cam, obs_x, n, num_a, rank=r, world_size=world,
+                                allreduce=grp.allreduce_fn(r), device=devices[r % len(devices)],
+                                **kw) as ba:
+                ba.set_params(a, b)
+                err, st = ba.run()
+                out[r] = ba.get_params() + (err, st)
+        except Exception as e:   # noqa: BLE001 -- re-raised below
+            errs.append(e)
+            grp._bar.abort()
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errs:
+        raise errs[0]
+    return out[0]

@@ -25,6 +25,7 @@ import time
 import numpy as np
 
 from .bundle import bundle_euclid_obs, bundle_euclid_resect
+from .dist import choose_shards, run_sharded
 from .evaluation import align_scene, vl_irodr, vl_rodr
 
 __all__ = ["incremental_bundle"]
@@ -43,11 +44,16 @@ def _subset_obs(sc, cams, pts):
 
 
 def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, device=0,
-                       verbose=False):
+                       verbose=False, devices=None, shards=None):
     """Replay the incremental reconstruction's BA sequence on scene ``sc``
     (scene.Scene).  Cameras ``init_cams`` form the initial two-view
     reconstruction (VLmvg.m's two_view step); every other camera is added in
     index order (incr_reconstruction.m:223-227).
+
+    Elastic sharding (config 5): with ``devices`` (GPU ordinals), each solve
+    picks its rank count with dist.choose_shards from its observation count
+    (or ``shards(num_obs)`` if given) and runs point-sharded over that many
+    rank threads (dist.run_sharded); without it every solve runs on ``device``.
 
     Returns dict(solves=[...], resections=[...], K, T, w, X, status) where each
     solve records the cameras / points / observations it adjusted, its error_
@@ -75,9 +81,22 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
             return
         pt, cam, ox = _subset_obs(sc, cams, pts)
         t0 = time.perf_counter()
-        K_, T_, w_, X_, err, st = bundle_euclid_obs(
-            K[:, cams], T[:, cams], w[:, cams], X[:, pts], pt, cam, ox, *opts,
-            num_vis=float(len(pt)), device=device, return_stats=True)
+        world = 1
+        if devices:
+            world = shards(len(pt)) if shards else choose_shards(len(pt), len(devices))
+        if world > 1:
+            nvk = 0 if fix_calibration else 4
+            Kc, Tc, wc, Xc = K[:, cams], T[:, cams], w[:, cams], X[:, pts]
+            a0 = np.vstack([wc, Tc] + ([Kc] if nvk == 4 else []))
+            a1, b1, err, st = run_sharded(Kc, pt, cam, ox, len(pts), 6 + nvk, a0, Xc[:3],
+                                          world, devices=devices, num_vis=float(len(pt)))
+            K_ = a1[6:10] if nvk == 4 else Kc
+            T_, w_, X_ = a1[3:6], a1[0:3], np.vstack([b1, Xc[3:4]])
+        else:
+            K_, T_, w_, X_, err, st = bundle_euclid_obs(
+                K[:, cams], T[:, cams], w[:, cams], X[:, pts], pt, cam, ox, *opts,
+                num_vis=float(len(pt)), device=devices[0] if devices else device,
+                return_stats=True)
         secs = time.perf_counter() - t0
         if align:                                        # :273 align_scene(T_, Omega_, X_ba_)
             T_, w_, X_ = align_scene(T_, w_, X_)
@@ -85,7 +104,7 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
         X[:, pts] = X_
         solves.append(dict(tag=tag, camera=int(j), cameras=len(cams), points=len(pts),
                            observations=len(pt), error=np.asarray(err), passes=st.iterations,
-                           accepted=st.accepted, seconds=secs))
+                           accepted=st.accepted, seconds=secs, shards=world))
         if verbose:
             print(f"[incremental] camera {j} {tag}: {len(cams)} cams {len(pts)} pts "
                   f"{len(pt)} obs  error_ {err[0]:.4g} -> {err[-1]:.4g}  {st.iterations} passes")
