@@ -34,7 +34,8 @@ class VlgbaOptions(ctypes.Structure):
                 ("world_size", c_int), ("comm_id", ctypes.c_void_p), ("dense_solve", c_int),
                 ("ordered", c_int), ("allreduce", ctypes.c_void_p),
                 ("allreduce_user", ctypes.c_void_p), ("schur_kernel", c_int),
-                ("semantics", c_int), ("stop_rel", c_double)]
+                ("semantics", c_int), ("stop_rel", c_double),
+                ("on_pass", ctypes.c_void_p), ("on_pass_user", ctypes.c_void_p)]
 
 
 NKERNELS = 16   # VLGBA_NKERNELS
@@ -57,6 +58,10 @@ class VlgbaStepInfo(ctypes.Structure):
     _fields_ = [("old_sse", c_double), ("new_sse", c_double), ("dpg", c_double),
                 ("rho", c_double), ("lambda_", c_double), ("accepted", c_int),
                 ("chol_failed", c_int), ("pinv", c_int)]
+
+
+# vlgba_options.on_pass(pass, iter, const vlgba_step_info *, user)
+ON_PASS_FN = ctypes.CFUNCTYPE(None, c_int, c_int, ctypes.POINTER(VlgbaStepInfo), ctypes.c_void_p)
 
 
 # name -> (restype, argtypes); must match include/vlgba.h exactly

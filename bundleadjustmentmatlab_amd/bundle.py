@@ -25,7 +25,8 @@ from __future__ import annotations
 import ctypes
 import numpy as np
 
-from ._lib import (ALLREDUCE_FN, MODEL_EUCLIDEAN, MODEL_PROJECTIVE, NKERNELS, VlgbaOptions,
+from ._lib import (ALLREDUCE_FN, MODEL_EUCLIDEAN, MODEL_PROJECTIVE, NKERNELS, ON_PASS_FN,
+                   VlgbaOptions,
                    VlgbaProblem, VlgbaResectProblem, VlgbaStats,
                    VlgbaStepInfo, c_dp, c_ip, c_up, check, lib)
 
@@ -109,6 +110,53 @@ def unpack(K, a, b, Xe4, nvk):
 
 
 # ---------------------------------------------------------------------------
+# per-pass JSON log ("Tracing")
+# ---------------------------------------------------------------------------
+class _PassLog:
+    """Callable for vlgba_options.on_pass: one JSON line per LM pass."""
+
+    def __init__(self, sink, num_vis, projective):
+        import json
+        self._json = json
+        self._own = False
+        self._fn = None
+        self._fh = None
+        if callable(sink) and not hasattr(sink, "write"):
+            self._fn = sink
+        elif hasattr(sink, "write"):
+            self._fh = sink
+        else:
+            self._fh = open(sink, "a", encoding="utf-8")
+            self._own = True
+        self.num_vis = float(num_vis)
+        self.projective = projective
+        self.records = []
+
+    def __call__(self, npass, it, info_p, _user):
+        i = info_p.contents
+        # bundle_euclid.m:219-220 error_ = SSE / num_vis (projective: SSE * (1 / num_vis))
+        sc = (lambda v: 1 / self.num_vis * v) if self.projective else (lambda v: v / self.num_vis)
+        rec = {"pass": int(npass), "iter": int(it), "lambda": i.lambda_,
+               "old_sse": i.old_sse, "new_sse": i.new_sse, "error_old": sc(i.old_sse),
+               "error_new": sc(i.new_sse), "dpg": i.dpg, "rho": i.rho,
+               "accepted": bool(i.accepted), "chol_failed": bool(i.chol_failed),
+               "pinv": bool(i.pinv)}
+        self.records.append(rec)
+        try:
+            if self._fn is not None:
+                self._fn(rec)
+            else:
+                self._fh.write(self._json.dumps(rec) + "\n")
+        except Exception:   # noqa: BLE001 -- a failing log must not abort the solve
+            pass
+
+    def close(self):
+        if self._own and self._fh is not None:
+            self._fh.close()
+            self._fh = None
+
+
+# ---------------------------------------------------------------------------
 # the GPU solver handle
 # ---------------------------------------------------------------------------
 class BundleAdjuster:
@@ -127,6 +175,9 @@ class BundleAdjuster:
     sums, sequential Cholesky, LM scalars in the reference's flat order --
     the LM trajectory is bit-identical to the CPU oracle's).  ``stop_rel``
     replaces the 1e-3 of the stop rule (bundle_euclid.m:123).
+    ``log`` (a path, a text file or a callable) receives one JSON record per
+    LM pass of run() (vlgba_options.on_pass): pass, iter, lambda, old / new
+    SSE, error_ values (SSE / num_vis), rho, accepted, chol_failed, pinv.
     ``model="projective"`` solves bundle_projective.m instead: num_a = 12
     (a = P(:) per camera), K is None and ``m`` gives the camera count.
     """
@@ -140,7 +191,7 @@ class BundleAdjuster:
                  rank=0, world_size=1, comm_id=None, max_iter=0, max_iter2=0, lambda0=0.0,
                  dense_solve=False, ordered=False, allreduce=None, solver=None,
                  schur_kernel="auto", semantics="mex", model="euclidean", m=None,
-                 parity=False, stop_rel=0.0):
+                 parity=False, stop_rel=0.0, log=None):
         L = lib()
         solve_mode = self.SOLVERS[solver] if solver is not None else int(bool(dense_solve))
         self.K = _F(K) if K is not None else None
@@ -173,6 +224,11 @@ class BundleAdjuster:
                 except Exception:   # noqa: BLE001 -- reported to the library as failure
                     return 1
             self._ar = ALLREDUCE_FN(_cb)
+        self._log = self._log_fn = None
+        if log is not None:
+            self._log = _PassLog(log, num_vis if num_vis > 0 else float(self.num_obs),
+                                 model == "projective")
+            self._log_fn = ON_PASS_FN(self._log)
         opt = VlgbaOptions(int(fix_structure), int(fix_motion),
                            self._pivot.ctypes.data_as(c_up) if self._pivot is not None else None,
                            int(verbose), int(max_iter), int(max_iter2), float(lambda0),
@@ -181,7 +237,9 @@ class BundleAdjuster:
                            solve_mode, 2 if parity else int(ordered),
                            ctypes.cast(self._ar, ctypes.c_void_p) if self._ar else None, None,
                            self.SCHUR_KERNELS[schur_kernel], self.SEMANTICS[semantics],
-                           float(stop_rel))
+                           float(stop_rel),
+                           ctypes.cast(self._log_fn, ctypes.c_void_p) if self._log_fn else None,
+                           None)
         h = ctypes.c_void_p()
         check(L.vlgba_create(ctypes.byref(prob), ctypes.byref(opt), ctypes.byref(h)),
               "vlgba_create")
@@ -192,6 +250,8 @@ class BundleAdjuster:
         if getattr(self, "_h", None):
             self._L.vlgba_destroy(self._h)
             self._h = None
+        if getattr(self, "_log", None) is not None:
+            self._log.close()
 
     def __del__(self):
         try:

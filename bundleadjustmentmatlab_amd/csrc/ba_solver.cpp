@@ -661,6 +661,8 @@ struct vlgba_ctx {
     ba_aux aux;                   // streams / events / host result block (pooled)
     bool has_aux = false;
     double stop_rel = 1e-3;       // bundle_euclid.m:123 relative-decrease stop
+    void (*on_pass)(int, int, const vlgba_step_info *, void *) = nullptr;
+    void *on_pass_user = nullptr;
     // pinv fallback of the reduced solve (allocated on first use)
     double *pinv_S = nullptr, *pinv_ev = nullptr, *pinv_e = nullptr, *pinv_w = nullptr;
     int *pinv_info = nullptr;
@@ -1065,6 +1067,8 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
             break;
         }
         c->stop_rel = o->stop_rel > 0 ? o->stop_rel : 1e-3;
+        c->on_pass = o->on_pass;
+        c->on_pass_user = o->on_pass_user;
         c->d.no_mfma = o->schur_kernel == 1;
         c->d.ndb = o->semantics == 1 ? p->num_a : 6;
         rc = ctx_setup(c, p, h, pt_ptr_all, lower_blocks, all_diag, stage_mode);
@@ -1644,6 +1648,7 @@ int vlgba_run(vlgba_ctx *c, double *error_out, int error_cap, vlgba_stats *stats
             iter2++;
         }
         lm_apply(c, &info);
+        if (c->on_pass && c->rank == 0) c->on_pass(passes, iter, &info, c->on_pass_user);
     }
     VLGBA_CHECK(hipStreamSynchronize(c->d.stream));
     if (error_out)   // at most error_cap entries; stats->num_error is the full count

@@ -214,6 +214,70 @@ def banded_scene(m=50, n=10_000, track=6, depth=(80.0, 120.0), noise=0.5, seed=2
     return Scene(K, T, w, X, pt, cam, x, T0, w0, X0)
 
 
+def ladybug_scene(m=1000, n=200_000, mean_extra=3.0, max_track=60, loop=0.05,
+                  radius=300.0, depth=(80.0, 120.0), noise=0.5, seed=6):
+    """A BAL-"ladybug"-like scene (the plan cliffs): cameras drive
+    (1 + loop) times round a circle of ``radius`` looking at its centre, so
+    the last ``loop`` fraction of the frames revisits the first; every point is
+    tracked by 2 + Geometric(1 / (1 + mean_extra)) consecutive cameras (capped
+    at ``max_track``: long tracks beside short ones), and a point created in
+    the first ``loop`` part is seen again, by 1-3 consecutive cameras, one
+    revolution later (loop-closure observations: S is no longer banded)."""
+    rng = np.random.default_rng(seed)
+    width = height = 500.0
+    f, cx, cy = width, width / 2, height / 2
+    K = np.tile(np.array([[f], [f], [cx], [cy]]), (1, m))
+    per_rev = int(round(m / (1.0 + loop)))
+    ang = 2 * np.pi * np.arange(m) / per_rev
+    C = np.stack([radius * np.cos(ang), radius * np.sin(ang), np.zeros(m)])   # centres
+    Rm = np.zeros((m, 3, 3))
+    for j in range(m):   # rows: camera axes in world coordinates, z towards the centre
+        z = -C[:, j] / np.linalg.norm(C[:, j])
+        x = np.cross(np.array([0.0, 0.0, 1.0]), z)
+        x /= np.linalg.norm(x)
+        Rm[j] = np.stack([x, np.cross(z, x), z])
+    w = np.zeros((3, m))
+    for j in range(m):
+        # rotation vector of Rm[j] (log map), small enough for vl_rodrigues' branch
+        Rj = Rm[j]
+        th = np.arccos(np.clip((np.trace(Rj) - 1) / 2, -1, 1))
+        if th < 1e-12:
+            continue
+        v = np.array([Rj[2, 1] - Rj[1, 2], Rj[0, 2] - Rj[2, 0], Rj[1, 0] - Rj[0, 1]])
+        if np.pi - th < 1e-6:   # ~pi: axis from the symmetric part
+            ax = np.sqrt(np.maximum((np.diag(Rj) + 1) / 2, 0))
+            ax *= np.sign(np.where(v == 0, 1.0, v))
+            w[:, j] = th * ax / np.linalg.norm(ax)
+        else:
+            w[:, j] = th * v / (2 * np.sin(th))
+    R = rodrigues(w)
+    T = -np.einsum("kij,jk->ik", R, C)                     # T = -R C
+    start = np.sort(rng.integers(0, m - 1, size=n))
+    L = 2 + rng.geometric(1.0 / (1.0 + mean_extra), size=n) - 1
+    L = np.minimum(np.minimum(L, max_track), m - start)
+    uv = rng.random((n, 2)) * np.array([width, height])
+    d = rng.uniform(depth[0], depth[1], size=n)
+    ray = np.stack([(uv[:, 0] - cx) / f, (uv[:, 1] - cy) / f, np.ones(n)], 1) * d[:, None]
+    Xw = np.einsum("kji,kj->ki", R[start], ray - T[:, start].T)
+    X = np.vstack([Xw.T, np.ones((1, n))])
+    pt = np.repeat(np.arange(n), L)
+    cam = np.concatenate([np.arange(s0, s0 + k) for s0, k in zip(start, L)])
+    # loop closures: one revolution later, 1-3 cameras
+    lc = np.nonzero(start + per_rev < m)[0]
+    L2 = np.minimum(rng.integers(1, 4, size=lc.size), m - (start[lc] + per_rev))
+    pt = np.concatenate([pt, np.repeat(lc, L2)])
+    cam = np.concatenate([cam, np.concatenate([np.arange(s0 + per_rev, s0 + per_rev + k)
+                                               for s0, k in zip(start[lc], L2)])
+                          if lc.size else np.zeros(0, dtype=int)])
+    x, z = project(K, w, T, X, cam, pt)
+    keep = z > 0.01 * depth[0]
+    pt, cam, x = pt[keep], cam[keep], x[keep]
+    x = x + rng.standard_normal(x.shape) * noise
+    pt, cam, x = _sort_point_major(pt, cam, x)
+    w0, T0, X0 = _perturb(rng, w, T, X, False)
+    return Scene(K, T, w, X, pt, cam, x, T0, w0, X0)
+
+
 def projective_from(sc):
     """Projective BA input (bundle_projective.m:1-8) from a Euclidean scene:
     Pp(:,:,j) = K_j [R(w0_j) | T0_j] / f_j at the perturbed start (a 3 x 4 x m
@@ -237,6 +301,8 @@ CONFIGS = {
     "cfg2": (banded_scene, dict(m=50, n=10_000, track=6, seed=2)),
     "cfg3": (banded_scene, dict(m=1000, n=500_000, track=6, seed=3)),
     "cfg5": (mview_scene, dict(m=50, min_n=100, max_n=200, depth=100.0, seed=5)),
+    # not a BASELINE config: irregular tracks + loop closures
+    "ladybug": (ladybug_scene, dict(m=1000, n=200_000, seed=6)),
 }
 
 

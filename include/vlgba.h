@@ -58,6 +58,8 @@ typedef struct {
                               * 10 on reject); fix_pivot is not an option there */
 } vlgba_problem;
 
+struct vlgba_step_info;
+
 typedef struct {
     int fix_structure;           /* bundle_euclid.m:58-59                      */
     int fix_motion;              /* :60-61                                     */
@@ -112,6 +114,12 @@ typedef struct {
     /* stop rule of bundle_euclid.m:123: stop once the accepted step lowers
      * error_ by no more than stop_rel * error_(previous); 0 -> 1e-3          */
     double stop_rel;
+    /* per-pass log hook (NULL: none): vlgba_run calls on_pass(pass, iter, info,
+     * user) after every LM pass (1-based pass counter, iter = the reference's
+     * iteration counter after the pass, bundle_euclid.m:221), on the calling
+     * thread, rank 0 only; bundle.py writes it as one JSON line per pass */
+    void (*on_pass)(int pass, int iter, const struct vlgba_step_info *info, void *user);
+    void *on_pass_user;
 } vlgba_options;
 
 typedef struct {
@@ -123,7 +131,7 @@ typedef struct {
 } vlgba_stats;
 
 /* One LM pass, for benchmarking / custom drivers. */
-typedef struct {
+typedef struct vlgba_step_info {
     double old_sse;        /* e'e before the step (bundle_euclid.m:209)       */
     double new_sse;        /* e_new'e_new (:210)                              */
     double dpg;            /* dp'(lambda dp + g) (:217)                       */

@@ -205,3 +205,33 @@ def test_reduced_system_getter_matches_oracle(gpu, oracle):
         else:
             assert np.abs(Sg - St).max() <= 1e-12 * np.abs(St).max()
             assert np.abs(eg - e_.reshape(-1)).max() <= 1e-12 * np.abs(e_).max()
+
+
+def test_per_pass_json_log_matches_oracle_trace(gpu, oracle, tmp_path):
+    """vlgba_options.on_pass / BundleAdjuster(log=...): one JSON record per LM
+    pass, accepted and rejected; in parity mode every record's lambda, SSEs,
+    rho and accept flag equal the oracle's trace of the same pass bit for
+    bit, and the file form holds the same records."""
+    import json
+    sc = _scene("small")
+    x, vis = sc.dense()
+    recs = []
+    got = gpu.bundle_euclid(sc.K, sc.T0, sc.w0, sc.X0, x, "visibility", vis, "fix_calibration",
+                            parity=True, log=recs.append, return_stats=True)
+    trace = []
+    ref = oracle.bundle_euclid_ref(sc.K, sc.T0, sc.w0, sc.X0, x, "visibility", vis,
+                                   "fix_calibration", form="sparse", vinv="formula",
+                                   solve="seq", sums="seq", trace=trace)
+    assert np.array_equal(got[4], ref[4])
+    assert len(recs) == len(trace) == got[5].iterations
+    for k, (r, t) in enumerate(zip(recs, trace)):
+        assert r["pass"] == k + 1
+        assert r["lambda"] == t["lam"] and r["accepted"] == t["accepted"]
+        assert r["old_sse"] == t["old"] and r["new_sse"] == t["new"] and r["rho"] == t["rho"]
+    acc = [r for r in recs if r["accepted"]]
+    assert [r["error_new"] for r in acc] == list(got[4][1:])
+    path = tmp_path / "lm.jsonl"
+    gpu.bundle_euclid(sc.K, sc.T0, sc.w0, sc.X0, x, "visibility", vis, "fix_calibration",
+                      parity=True, log=str(path))
+    lines = [json.loads(s) for s in path.read_text().splitlines()]
+    assert lines == recs
