@@ -351,8 +351,10 @@ def kernel_roofline(name, tot_ms, calls, plan, n_passes):
         flops = N * ((1 + NA + 3) * 53 + 2 * (NA + 3) * 2 + 3 * NA * 3)
     elif name == "k_camera_reduce":
         nbytes = plan["chunk_eslots"] * (8 * (NU + NA) + 4) + m * 8 * (NA * NA + NA)
-    elif name == "k_schur_group":
+    elif name in ("k_schur_group", "k_schur_mfma"):
         # W, V, eB, metadata in; V*^-1 out; LDS-accumulated block / camera partials out
+        # (in a mixed plan both kernels run, each over its own groups: the
+        # per-kernel byte split is not tracked, the sum is attributed to each)
         nbytes = (N * WS + n * (72 + 24 + 72) + 4 * plan["blob_words"] +
                   8 * NA * NA * plan["group_slots"] + 8 * NA * plan["group_eslots"])
         # S terms (NA x NA x 3 fma each), Y = W V*^-1, e_ terms

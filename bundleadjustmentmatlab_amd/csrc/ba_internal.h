@@ -35,7 +35,7 @@
 enum {
     KT_ROT, KT_LIN, KT_CAMRED, KT_DAMP, KT_SCHUR, KT_SCHUR_CHUNK, KT_SCHUR_RED,
     KT_ASSEMBLE, KT_FACTOR, KT_SYRK, KT_BACKWARD, KT_CAMUPD, KT_PTUPD, KT_CR_FACTOR,
-    KT_CR_UPDATE, KT_CR_BACK, KT_N
+    KT_CR_UPDATE, KT_CR_BACK, KT_SCHUR_MF, KT_N
 };
 #define KT_MAX_EV 8192
 struct ba_ktimer {
@@ -120,7 +120,8 @@ struct ba_dev {
     int ordered;       // 1: sequential bit-exact kernels (k_damp_point + k_schur)
     int parity;        // ordered = 2: + sequential solve and LM scalars (bit-identical
                        // LM trajectory with the oracle)
-    int mfma;          // fast path: 1 = MFMA Schur chunks (k_schur_mfma), 0 = term lists
+    int mfma;          // fast path: 1 = some MFMA Schur chunks (k_schur_mfma: groups
+                       // [0, ngrp_mf)), 0 = term lists only (k_schur_group)
     int no_mfma;       // option: force the term-list Schur kernel
     int ndb;           // camera parameters in the back substitution: 6 (MEX, App. A
                        // Q3) or NA (bundle_euclid_nomex.m semantics)
@@ -150,7 +151,9 @@ struct ba_dev {
     unsigned *blob;                   // per-chunk metadata records (see build_plan)
     int *ch_blob, *ch_obase;          // [nch+1] record offsets (words), first local obs
     unsigned char *obs_lpt;           // [N] chunk-local point of each observation
-    int max_blob;
+    int max_blob;                     // term groups: largest chunk record
+    int ngrp_mf;                      // leading MFMA groups
+    int mf_max_s, mf_max_e, mf_max_blob;   // MFMA groups' LDS sizes
     int *grp_ch, *grp_gs, *grp_ge;    // [ngrp+1] chunk / group-slot / group-eslot ranges
     unsigned short *cs_g, *ce_g;      // chunk slot / chunk e-slot -> group-local id
     int *blk_gptr, *blk_gslots;       // per block: its group slots in group order

@@ -1542,32 +1542,33 @@ int ba_launch_schur(ba_dev *d, double lambda)
 template <int NA>
 static int launch_schur_fast(ba_dev *d, double lambda)
 {
-    const int gcap = d->grp_max_s, ecap = d->grp_max_e, bcap = d->max_blob;
-    if (d->mfma) {
+    // MFMA groups [0, ngrp_mf), then the per-term groups [ngrp_mf, ngrp)
+    if (d->ngrp_mf > 0) {
         KT_B(d);
         k_point_vinv<NA><<<(d->n + 255) / 256, 256, 0, d->stream>>>(d->V, d->n, lambda, d->Vinv);
         KT_E(d, KT_DAMP);
-        const size_t sm2 = sizeof(double) * (gcap * NA * NA + ecap * NA) +
-                           sizeof(unsigned) * (size_t)bcap;
+        const size_t sm2 = sizeof(double) * (d->mf_max_s * NA * NA + d->mf_max_e * NA) +
+                           sizeof(unsigned) * (size_t)d->mf_max_blob;
         TRY_RC(ba_ensure_dyn_lds((const void *)k_schur_mfma<NA>, sm2));
         KT_B(d);
-        if (d->ngrp > 0)
-            k_schur_mfma<NA><<<d->ngrp, 256, sm2, d->stream>>>(
-                d->grp_ch, d->grp_gs, d->grp_ge, d->ch_pt, d->ch_obase, d->ch_blob, d->blob,
-                d->W, d->Vinv, d->eB, d->N, d->n, gcap, ecap, d->spart, d->epart);
+        k_schur_mfma<NA><<<d->ngrp_mf, 256, sm2, d->stream>>>(
+            d->grp_ch, d->grp_gs, d->grp_ge, d->ch_pt, d->ch_obase, d->ch_blob, d->blob, d->W,
+            d->Vinv, d->eB, d->N, d->n, d->mf_max_s, d->mf_max_e, d->spart, d->epart);
+        KT_E(d, KT_SCHUR_MF);
+    }
+    if (d->ngrp > d->ngrp_mf) {
+        const int gcap = d->grp_max_s, ecap = d->grp_max_e, bcap = d->max_blob;
+        size_t smem = sizeof(double) * (2 * BA_CH_OBS * 3 * NA + BA_CH_PTS * 12 +
+                                        gcap * NA * NA + ecap * NA) +
+                      sizeof(unsigned) * bcap;
+        smem = (smem + 15) & ~(size_t)15;
+        TRY_RC(ba_ensure_dyn_lds((const void *)k_schur_group<NA>, smem));
+        KT_B(d);
+        k_schur_group<NA><<<d->ngrp - d->ngrp_mf, 256, smem, d->stream>>>(
+            d->grp_ch + d->ngrp_mf, d->grp_gs + d->ngrp_mf, d->grp_ge + d->ngrp_mf, d->ch_pt,
+            d->ch_obase, d->ch_blob, d->blob, d->V, d->eB, d->W, lambda, bcap, gcap, ecap,
+            d->Vinv, d->spart, d->epart);
         KT_E(d, KT_SCHUR_CHUNK);
-    } else {
-    size_t smem = sizeof(double) * (2 * BA_CH_OBS * 3 * NA + BA_CH_PTS * 12 + gcap * NA * NA +
-                                    ecap * NA) +
-                  sizeof(unsigned) * bcap;
-    smem = (smem + 15) & ~(size_t)15;
-    TRY_RC(ba_ensure_dyn_lds((const void *)k_schur_group<NA>, smem));
-    KT_B(d);
-    if (d->ngrp > 0)
-        k_schur_group<NA><<<d->ngrp, 256, smem, d->stream>>>(
-            d->grp_ch, d->grp_gs, d->grp_ge, d->ch_pt, d->ch_obase, d->ch_blob, d->blob, d->V,
-            d->eB, d->W, lambda, bcap, gcap, ecap, d->Vinv, d->spart, d->epart);
-    KT_E(d, KT_SCHUR_CHUNK);
     }
     const int bs = ((NA * NA + NA) + 63) / 64 * 64;
     if (d->join_pending) {   // U / eA from the side stream's camera reduction

@@ -275,8 +275,11 @@ void build_blocks(int m, const std::vector<int> &pt_ptr_all, const std::vector<i
 }
 
 // Chunk plan of the fast Schur path for the local points (pt_ptr local,
-// cam local observation cameras).  Returns false when a point has more than
-// BA_CH_OBS observations (the caller then uses the ordered kernels).
+// cam local observation cameras).  Points [0, p_split) form MFMA chunks
+// (k_schur_mfma), points [p_split, n) per-term chunks (k_schur_group); the
+// chunk and group sequences keep that order, so the MFMA groups are
+// [0, ngrp_mf) and the term groups [ngrp_mf, ngrp).  Returns false when a
+// point does not fit its chunk kind (the caller then uses the ordered kernels).
 struct host_plan {
     std::vector<int> ch_pt, ch_slot, ch_eslot, slot_blk, slot_tptr, eslot_optr;
     std::vector<unsigned short> slot_term, eslot_obs;
@@ -288,13 +291,16 @@ struct host_plan {
     std::vector<unsigned short> cs_g, ce_g;        // chunk slot / e-slot -> group-local id
     std::vector<int> gslot_blk, gecam;             // [ngs], [nge]
     std::vector<int> blk_gptr, blk_gslots, cam_gptr, cam_gslots;
-    int grp_max_s = 0, grp_max_e = 0;             // largest accumulated group
+    int grp_max_s = 0, grp_max_e = 0;             // largest accumulated term group
+    int mf_max_s = 0, mf_max_e = 0;               // largest MFMA group
+    int nch_mf = 0, ngrp_mf = 0;                  // leading MFMA chunks / groups
     // per chunk one contiguous metadata record (one coalesced prefetch):
     //   [np | nobs << 16][ns | nes << 16][nterm][neobs] soff[ns+1] eoff[nes+1]
     //   sgl[ns] egl[nes] lpt[nobs] term[nterm] (y | w << 16) eobl[neobs]
     std::vector<unsigned> blob;
     std::vector<int> ch_blob, ch_obase;            // [nch+1]
-    int max_blob = 0;
+    int max_blob = 0;      // term chunks: largest record
+    int mf_max_blob = 0;   // MFMA groups: largest group record block (staged in LDS)
 };
 
 // counting sort of ids by key: ptr[nkey+1], list of ids in ascending id order per key
@@ -309,24 +315,24 @@ static void bucket(const std::vector<int> &key, int nkey, std::vector<int> &ptr,
     for (size_t s = 0; s < key.size(); s++) list[pos[key[s]]++] = (int)s;
 }
 
-// cmax > 0: chunks for the MFMA Schur kernel (k_schur_mfma): at most
-// BA_MF_PTS points and cmax cameras per chunk (the chunk's dense Y / W fit
-// one K = 64 slab of 16 * BA_MF_RT(na) rows); its metadata records are the
-// dense-layout ones described at build of P.blob below.
+// MFMA chunks (points below p_split): at most BA_MF_PTS points and cmax
+// cameras per chunk (the chunk's dense Y / W fit one K = 64 slab of
+// 16 * BA_MF_RT(na) rows); their metadata records are the dense-layout ones
+// described at build of P.blob below.
 bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<int> &lcam,
-                const host_blocks &hb, host_plan &P, int cmax)
+                const host_blocks &hb, host_plan &P, int cmax, int p_split)
 {
     const int n = (int)lptr.size() - 1;
     const int nb = (int)hb.jk.size() / 2;
+    if (cmax <= 0) p_split = 0;
     auto pt_terms = [&](int i) {
         const long long k = lptr[i + 1] - lptr[i];
         return k * (k + 1) / 2;
     };
     for (int i = 0; i < n; i++)
         if (lptr[i + 1] - lptr[i] > BA_CH_OBS || pt_terms(i) > BA_CH_TERMS ||
-            (cmax > 0 && lptr[i + 1] - lptr[i] > cmax))
+            (i < p_split && lptr[i + 1] - lptr[i] > cmax))
             return false;
-    const int pts_max = cmax > 0 ? BA_MF_PTS : BA_CH_PTS;
     std::vector<int> cam_stamp(m, -1);   // chunk camera set (MFMA chunking)
     P.max_terms = P.max_slots = 0;
     std::vector<int> slot_of(nb, -1), eslot_of(m, -1), touched, tcam;
@@ -339,6 +345,9 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
     P.eslot_optr.push_back(0);
     int p = 0;
     while (p < n) {
+        const bool mf = p < p_split;                // chunk kind
+        const int pend = mf ? p_split : n;
+        const int pts_max = mf ? BA_MF_PTS : BA_CH_PTS;
         const int obase = lptr[p];
         int q = p;
         long long nterm = 0;
@@ -350,9 +359,9 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
                 if (lcam[lptr[i1] + a] != lcam[lptr[i2] + a]) return false;
             return true;
         };
-        while (q < n && q - p < pts_max && lptr[q + 1] - obase <= BA_CH_OBS &&
+        while (q < pend && q - p < pts_max && lptr[q + 1] - obase <= BA_CH_OBS &&
                nterm + pt_terms(q) <= BA_CH_TERMS) {
-            if (cmax > 0) {
+            if (mf) {
                 // a run of points with one camera list (video-like tracks) keeps its
                 // chunks to itself: its MFMA sums stay in registers across chunks
                 const bool same = q == p || same_cams(p, q);
@@ -412,6 +421,7 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
         P.ch_pt.push_back(q);
         P.ch_slot.push_back((int)P.slot_blk.size());
         P.ch_eslot.push_back((int)P.eslot_optr.size() - 1);
+        if (mf) P.nch_mf++;
         p = q;
     }
     // per block: its slots in chunk order (counting sort keeps slot order)
@@ -440,11 +450,6 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
     // A chunk with more than gs_cap blocks forms a group of its own whose
     // partials go straight to HBM ("direct" group).
     const int nch = (int)P.ch_pt.size() - 1;
-    // the MFMA kernel has no direct mode: one chunk's blocks must always fit
-    const int gs_cap = cmax > 0 ? std::max(BA_MF_GACC / (na * na), cmax * (cmax + 1) / 2)
-                                : BA_GACC / (na * na);
-    const int gmax = std::min(BA_GROUP_CH, std::max(1, (nch + BA_GROUPS - 1) / BA_GROUPS));
-    const int ge_cap = cmax > 0 ? std::max(BA_MF_GE_CAP, cmax) : BA_GE_CAP;
     std::vector<int> gslot_of(nb, -1), gcam_of(m, -1);
     P.cs_g.assign(ns, 0);
     P.ce_g.assign(nes, 0);
@@ -452,9 +457,16 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
     P.grp_gs.assign(1, 0);
     P.grp_ge.assign(1, 0);
     for (int c = 0; c < nch;) {
+        const bool mf = c < P.nch_mf;
+        const int cend = mf ? P.nch_mf : nch, nseg = mf ? P.nch_mf : nch - P.nch_mf;
+        // the MFMA kernel has no direct mode: one chunk's blocks must always fit
+        const int gs_cap = mf ? std::max(BA_MF_GACC / (na * na), cmax * (cmax + 1) / 2)
+                              : BA_GACC / (na * na);
+        const int gmax = std::min(BA_GROUP_CH, std::max(1, (nseg + BA_GROUPS - 1) / BA_GROUPS));
+        const int ge_cap = mf ? std::max(BA_MF_GE_CAP, cmax) : BA_GE_CAP;
         std::vector<int> gs, ge;
         int d = c;
-        for (; d < nch && d - c < gmax; d++) {
+        for (; d < cend && d - c < gmax; d++) {
             int new_s = 0, new_e = 0;
             for (int s = P.ch_slot[d]; s < P.ch_slot[d + 1]; s++) new_s += gslot_of[P.slot_blk[s]] < 0;
             for (int e = P.ch_eslot[d]; e < P.ch_eslot[d + 1]; e++) new_e += gcam_of[ecam[e]] < 0;
@@ -489,7 +501,11 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
             P.gecam.push_back(j);
             gcam_of[j] = -1;
         }
-        if ((int)gs.size() <= gs_cap) {   // LDS accumulators actually needed
+        if (mf) {
+            P.mf_max_s = std::max(P.mf_max_s, (int)gs.size());
+            P.mf_max_e = std::max(P.mf_max_e, (int)ge.size());
+            P.ngrp_mf++;
+        } else if ((int)gs.size() <= gs_cap) {   // LDS accumulators actually needed
             P.grp_max_s = std::max(P.grp_max_s, (int)gs.size());
             P.grp_max_e = std::max(P.grp_max_e, (int)ge.size());
         }
@@ -502,7 +518,7 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
     bucket(P.gecam, m, P.cam_gptr, P.cam_gslots);
     P.ch_blob.assign(1, 0);
     P.ch_obase.assign(1, lptr[0]);
-    if (cmax > 0) {
+    if (P.nch_mf > 0) {
         // dense-layout record per chunk (k_schur_mfma):
         //   [np | nobs << 16]
         //   [C | flags << 8 | Kc << 16]  C cameras ascending, Kc = 3 np rounded to 4;
@@ -525,8 +541,8 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
             std::sort(cams.begin(), cams.end());
             return cams;
         };
-        std::vector<int> cams = nch > 0 ? cams_of(0) : std::vector<int>();
-        for (int c = 0; c < nch; c++) {
+        std::vector<int> cams = cams_of(0);
+        for (int c = 0; c < P.nch_mf; c++) {
             const int g = ch_grp[c];
             if (c == P.grp_ch[g]) {   // group-local slot / camera ids
                 for (int q = P.grp_gs[g]; q < P.grp_gs[g + 1]; q++)
@@ -539,7 +555,7 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
             const int C = (int)cams.size();
             std::vector<int> next;
             bool flush = true;
-            if (c + 1 < nch) {
+            if (c + 1 < P.nch_mf) {
                 next = cams_of(c + 1);
                 flush = ch_grp[c + 1] != g || next != cams;
             }
@@ -577,16 +593,13 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
             }
             P.ch_blob.push_back((int)B.size());
             P.ch_obase.push_back(lptr[p1]);
-            P.max_blob = std::max(P.max_blob, P.ch_blob[c + 1] - P.ch_blob[c]);
             cams.swap(next);
         }
-        P.max_blob = 0;   // MFMA path: largest group's record block (staged in LDS)
-        for (int g = 0; g + 1 < (int)P.grp_ch.size(); g++)
-            P.max_blob = std::max(P.max_blob,
-                                  P.ch_blob[P.grp_ch[g + 1]] - P.ch_blob[P.grp_ch[g]]);
-        return true;
+        for (int g = 0; g < P.ngrp_mf; g++)
+            P.mf_max_blob = std::max(P.mf_max_blob,
+                                     P.ch_blob[P.grp_ch[g + 1]] - P.ch_blob[P.grp_ch[g]]);
     }
-    for (int c = 0; c < nch; c++) {
+    for (int c = P.nch_mf; c < nch; c++) {
         const int p0 = P.ch_pt[c], p1 = P.ch_pt[c + 1];
         const int nobs = lptr[p1] - lptr[p0];
         const int s0 = P.ch_slot[c], s1 = P.ch_slot[c + 1];
@@ -664,6 +677,11 @@ struct vlgba_ctx {
     void (*on_pass)(int, int, const vlgba_step_info *, void *) = nullptr;
     void *on_pass_user = nullptr;
     // pinv fallback of the reduced solve (allocated on first use)
+    // internal point order (fast path, one rank): the short-track points that
+    // fit the MFMA Schur chunks first, then the rest, each in input order.
+    // pperm[new] = input point, operm[new obs] = input observation (point-major
+    // input order); empty = identity.
+    std::vector<int> pperm, operm;
     double *pinv_S = nullptr, *pinv_ev = nullptr, *pinv_e = nullptr, *pinv_w = nullptr;
     int *pinv_info = nullptr;
     int pinv_used = 0;            // passes that took the pinv fallback
@@ -766,6 +784,51 @@ static int allreduce(vlgba_ctx *c, double *buf, size_t count)
     return 0;
 }
 
+// Fast-path point order: when some but not all tracks fit the MFMA Schur
+// chunks (<= BA_MF_CMAX(na) observations) and every track fits a chunk at all,
+// put the short-track points first (stable), so that the MFMA chunks are runs
+// of consecutive short tracks and the per-term chunks hold the rest.  The
+// summation order of the fast path changes with it (it is not the parity
+// path); set / get_params and the getters map back to the input order.
+static void order_points_by_kind(int na, host_obs &h, std::vector<int> &pt_ptr,
+                                 std::vector<int> &pperm, std::vector<int> &operm)
+{
+    const int n = (int)pt_ptr.size() - 1, cmax = BA_MF_CMAX(na);
+    int nshort = 0;
+    for (int i = 0; i < n; i++) {
+        const long long k = pt_ptr[i + 1] - pt_ptr[i];
+        if (k > BA_CH_OBS || k * (k + 1) / 2 > BA_CH_TERMS) return;   // ordered kernels
+        nshort += k <= cmax;
+    }
+    if (nshort == 0 || nshort == n) return;
+    pperm.clear();
+    pperm.reserve(n);
+    for (int pass = 0; pass < 2; pass++)
+        for (int i = 0; i < n; i++)
+            if ((pt_ptr[i + 1] - pt_ptr[i] <= cmax) == (pass == 0)) pperm.push_back(i);
+    host_obs h2;
+    const size_t N = h.pt.size();
+    h2.pt.resize(N);
+    h2.cam.resize(N);
+    h2.x.resize(2 * N);
+    operm.resize(N);
+    std::vector<int> ptr2(n + 1, 0);
+    size_t q = 0;
+    for (int i2 = 0; i2 < n; i2++) {
+        const int i = pperm[i2];
+        for (int o = pt_ptr[i]; o < pt_ptr[i + 1]; o++, q++) {
+            h2.pt[q] = i2;
+            h2.cam[q] = h.cam[o];
+            h2.x[2 * q] = h.x[2 * (size_t)o];
+            h2.x[2 * q + 1] = h.x[2 * (size_t)o + 1];
+            operm[q] = o;
+        }
+        ptr2[i2 + 1] = (int)q;
+    }
+    h = std::move(h2);
+    pt_ptr.swap(ptr2);
+}
+
 // Device buffers + host-side structure for the observations of points [p0, p1).
 static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
                      const std::vector<int> &pt_ptr_all, bool lower_blocks, bool all_diag,
@@ -810,13 +873,17 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
     host_blocks hb;
     host_plan plan;
     build_blocks(p->m, pt_ptr_all, h.cam, c->p0, c->p1, o0, lower_blocks, all_diag, !fast, hb);
-    // MFMA Schur chunks when every point fits the dense slab, else the term path
+    // MFMA Schur chunks for the leading points whose tracks fit the dense slab
+    // (ctx_create orders the short-track points first), per-term chunks for
+    // the rest; the ordered kernels if some track fits neither
     d.mfma = 0;
-    if (fast && !d.no_mfma && build_plan(p->m, na, lptr, lcam, hb, plan, BA_MF_CMAX(na))) {
-        d.mfma = 1;
-    } else if (fast) {
-        plan = host_plan();
-        if (!build_plan(p->m, na, lptr, lcam, hb, plan, 0)) {
+    if (fast) {
+        int p_split = 0;
+        if (!d.no_mfma)
+            while (p_split < d.n && lptr[p_split + 1] - lptr[p_split] <= BA_MF_CMAX(na)) p_split++;
+        if (build_plan(p->m, na, lptr, lcam, hb, plan, BA_MF_CMAX(na), p_split)) {
+            d.mfma = plan.nch_mf > 0;
+        } else {
             fast = false;
             hb = host_blocks();
             build_blocks(p->m, pt_ptr_all, h.cam, c->p0, c->p1, o0, lower_blocks, all_diag, true,
@@ -868,7 +935,11 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         TRY(ctx_alloc(c, &d.cam_eptr, plan.cam_eptr.size()));
         TRY(ctx_alloc(c, &d.cam_eslots, plan.cam_eslots.size()));
         d.ngrp = (int)plan.grp_ch.size() - 1;
+        d.ngrp_mf = plan.ngrp_mf;
         d.max_blob = plan.max_blob;
+        d.mf_max_blob = plan.mf_max_blob;
+        d.mf_max_s = plan.mf_max_s;
+        d.mf_max_e = plan.mf_max_e;
         TRY(ctx_alloc(c, &d.blob, plan.blob.size()));
         TRY(ctx_alloc(c, &d.ch_blob, plan.ch_blob.size()));
         TRY(ctx_alloc(c, &d.ch_obase, plan.ch_obase.size()));
@@ -1010,6 +1081,8 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
         std::vector<int> pt_ptr_all(p->n + 1, 0);
         for (size_t q = 0; q < h.pt.size(); q++) pt_ptr_all[h.pt[q] + 1]++;
         for (int i = 0; i < p->n; i++) pt_ptr_all[i + 1] += pt_ptr_all[i];
+        if (o->ordered == 0 && !stage_mode && o->schur_kernel != 1 && o->world_size <= 1)
+            order_points_by_kind(p->num_a, h, pt_ptr_all, c->pperm, c->operm);
         c->world = o->world_size > 1 ? o->world_size : 1;
         c->rank = c->world > 1 ? o->rank : 0;
         // contiguous point ranges with balanced observation counts
@@ -1414,12 +1487,33 @@ void vlgba_destroy(vlgba_ctx *ctx)
     ctx_free(ctx);
 }
 
+// per-point device array (k doubles per local point, internal order) -> host,
+// in the input point order (synchronous when a permutation applies)
+static int download_points(vlgba_ctx *c, double *dst, const double *src, int k)
+{
+    const size_t cnt = (size_t)k * c->d.n;
+    if (c->pperm.empty()) return download(dst, src, cnt, c->d.stream);
+    std::vector<double> tmp(cnt);
+    TRY(download(tmp.data(), src, cnt, c->d.stream));
+    VLGBA_CHECK(hipStreamSynchronize(c->d.stream));
+    for (int i = 0; i < c->d.n; i++)
+        std::memcpy(dst + (size_t)k * c->pperm[i], tmp.data() + (size_t)k * i, sizeof(double) * k);
+    return 0;
+}
+
 int vlgba_set_params(vlgba_ctx *c, const double *a, const double *b)
 {
     if (!c || !a || !b) return VLGBA_E_ARG;
     TRY(ctx_enter(c));
     TRY(upload(c->d.a, a, (size_t)c->d.ld, c->d.stream));
-    TRY(upload(c->d.b, b + 3 * (size_t)c->p0, 3 * (size_t)c->d.n, c->d.stream));
+    if (!c->pperm.empty()) {   // input point order -> internal order
+        c->hb_tmp.resize(3 * (size_t)c->d.n);
+        for (int i = 0; i < c->d.n; i++)
+            for (int r = 0; r < 3; r++) c->hb_tmp[3 * (size_t)i + r] = b[3 * (size_t)c->pperm[i] + r];
+        TRY(upload(c->d.b, c->hb_tmp.data(), 3 * (size_t)c->d.n, c->d.stream));
+    } else {
+        TRY(upload(c->d.b, b + 3 * (size_t)c->p0, 3 * (size_t)c->d.n, c->d.stream));
+    }
     TRY(ba_launch_rotations(&c->d, c->d.a, c->d.rot, 1));
     c->lin_valid = 0;
     VLGBA_CHECK(hipStreamSynchronize(c->d.stream));
@@ -1446,7 +1540,7 @@ int vlgba_get_params(vlgba_ctx *c, double *a, double *b)
             ba_dfree(full);
             if (rc) return rc;
         } else {
-            TRY(download(b, c->d.b, 3 * (size_t)c->d.n, c->d.stream));
+            TRY(download_points(c, b, c->d.b, 3));
         }
     }
     VLGBA_CHECK(hipStreamSynchronize(c->d.stream));
@@ -1488,9 +1582,20 @@ int vlgba_get_linearization(vlgba_ctx *c, double *U, double *eA, double *V, doub
         ba_dfree(ue);
     }
     TRY(rc);
-    if (V) TRY(download(V, d.V, 9 * (size_t)d.n, d.stream));
-    if (eB) TRY(download(eB, d.eB, 3 * (size_t)d.n, d.stream));
-    if (W) TRY(download(W, d.W, (size_t)3 * d.na * d.N, d.stream));
+    if (V) TRY(download_points(c, V, d.V, 9));
+    if (eB) TRY(download_points(c, eB, d.eB, 3));
+    if (W) {
+        if (c->operm.empty()) {
+            TRY(download(W, d.W, (size_t)3 * d.na * d.N, d.stream));
+        } else {   // internal observation order -> input order
+            const size_t ws = (size_t)3 * d.na;
+            std::vector<double> tmp(ws * d.N);
+            TRY(download(tmp.data(), d.W, ws * d.N, d.stream));
+            VLGBA_CHECK(hipStreamSynchronize(d.stream));
+            for (int o = 0; o < d.N; o++)
+                std::memcpy(W + ws * c->operm[o], tmp.data() + ws * o, sizeof(double) * ws);
+        }
+    }
     VLGBA_CHECK(hipStreamSynchronize(d.stream));
     return 0;
 }
@@ -1525,7 +1630,7 @@ int vlgba_get_step(vlgba_ctx *c, double *da, double *db)
     if (!c) return VLGBA_E_ARG;
     TRY(ctx_enter(c));
     if (da) TRY(download(da, c->d.da, (size_t)c->d.ld, c->d.stream));
-    if (db) TRY(download(db, c->d.db, 3 * (size_t)c->d.n, c->d.stream));
+    if (db) TRY(download_points(c, db, c->d.db, 3));
     VLGBA_CHECK(hipStreamSynchronize(c->d.stream));
     return 0;
 }
@@ -1566,7 +1671,7 @@ const char *vlgba_kernel_name(int k)
         "k_rotations", "k_linearize", "k_camera_reduce", "k_damp_point", "k_schur",
         "k_schur_group", "k_schur_reduce", "k_assemble", "k_factor_panel", "k_syrk",
         "k_backward", "k_camera_update", "k_point_update", "k_cr_factor", "k_cr_update",
-        "k_cr_back"};
+        "k_cr_back", "k_schur_mfma"};
     return (k >= 0 && k < KT_N) ? names[k] : "";
 }
 
@@ -1580,7 +1685,8 @@ int vlgba_plan_info(vlgba_ctx *c, long long *info, int len)
                                       d.nes, d.ngrp, d.ngs, d.nge,        d.nb,   d.nt,
                                       d.cr_nlev, ne, nk,    d.ordered,    d.ordered ? d.T : d.nterm_fast,
                                       d.blob_words, d.mfma,
-                                      d.cr_nlev ? (d.cr32 ? d.tb32 : 64) : 0};
+                                      d.cr_nlev ? (d.cr32 ? d.tb32 : 64) : 0,
+                                      d.ngrp_mf, c->pperm.empty() ? 0 : 1};
     for (int k = 0; k < len && k < VLGBA_NPLAN; k++) info[k] = v[k];
     return VLGBA_NPLAN;
 }

@@ -192,7 +192,7 @@ int vlgba_phase_ms(vlgba_ctx *ctx, double *ms7);
 /* per-kernel device time accumulated over the passes run with timing on
  * (HIP events around every launch): ms[k], calls[k] for k < VLGBA_NKERNELS,
  * named by vlgba_kernel_name(k); reset = 1 clears the accumulators. */
-#define VLGBA_NKERNELS 16
+#define VLGBA_NKERNELS 17
 int vlgba_kernel_ms(vlgba_ctx *ctx, double *ms, long long *calls, int reset);
 const char *vlgba_kernel_name(int k);
 /* execution-plan sizes of this rank (roofline accounting in bench.py):
@@ -203,9 +203,11 @@ const char *vlgba_kernel_name(int k);
  * [13] eliminated tiles [14] kept-tile updates [15] ordered mode
  * [16] Schur (obs, obs) terms [17] chunk metadata words [18] MFMA Schur
  * chunks in use [19] rows per cyclic-reduction tile (64, or NA * floor(32 /
- * NA) for the camera-aligned tiles; 0 without cyclic reduction).
- * Writes min(len, VLGBA_NPLAN) entries, returns VLGBA_NPLAN. */
-#define VLGBA_NPLAN 20
+ * NA) for the camera-aligned tiles; 0 without cyclic reduction) [20] MFMA
+ * Schur groups (the leading ones; the rest use per-term sums) [21] points
+ * reordered internally (1: short tracks first, input order restored at the
+ * API).  Writes min(len, VLGBA_NPLAN) entries, returns VLGBA_NPLAN. */
+#define VLGBA_NPLAN 22
 int vlgba_plan_info(vlgba_ctx *ctx, long long *info, int len);
 
 /* ---- stage entries with the reference MEX argument layouts ---------------

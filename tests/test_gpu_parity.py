@@ -456,3 +456,48 @@ def test_run_error_capacity(gpu):
     ba.close()
     assert rc == 0 and st2.num_error == st.num_error
     assert np.array_equal(buf[:2], err[:2]) and np.all(buf[2:] == -1.0)
+
+
+@pytest.mark.parametrize("num_a", [6, 7])
+def test_mixed_mfma_and_term_chunks(gpu, oracle, num_a):
+    """Irregular tracks (ladybug-like: 2..30 views, loop closures): the short
+    tracks run in MFMA Schur chunks and the long ones in per-term chunks in one
+    plan (points reordered internally, short tracks first).  One pass matches
+    the ordered kernels and the terms-only plan to summation-order rounding;
+    the stage-1 getters and the accepted parameters come back in the input
+    point / observation order (W, V, eB bit-identical to the oracle)."""
+    from bundleadjustmentmatlab_amd.scene import make_config
+    sc = make_config("ladybug", m=80, n=4000, max_track=30, radius=150.0, seed=23)
+    a = np.zeros((num_a, sc.m), order="F")
+    a[0:3], a[3:6] = sc.w0, sc.T0
+    if num_a == 7:
+        a[6] = sc.K[0]
+    b = np.asfortranarray(sc.X0[:3])
+    res = {}
+    for name, kw in (("ordered", dict(ordered=True)), ("terms", dict(schur_kernel="terms")),
+                     ("mixed", {})):
+        ba = gpu.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, num_a, **kw)
+        ba.set_params(a, b)
+        lin = ba.linearization() if name == "mixed" else None
+        info = ba.step(relinearize=True, update_lm=True)
+        a2, b2 = ba.get_params()
+        da, db = ba.last_step()
+        res[name] = (info, ba.plan_info(), a2, b2, db, lin)
+        ba.close()
+    pl = res["mixed"][1]
+    assert 0 < pl["mfma_groups"] < pl["groups"] and pl["reordered"] == 1
+    assert res["terms"][1]["mfma_groups"] == 0 and res["terms"][1]["reordered"] == 0
+    o = res["ordered"]
+    for nm in ("terms", "mixed"):
+        f = res[nm]
+        assert abs(o[0].old_sse - f[0].old_sse) <= 1e-13 * o[0].old_sse
+        assert abs(o[0].new_sse - f[0].new_sse) <= 1e-8 * o[0].new_sse, nm
+        assert abs(o[0].dpg - f[0].dpg) <= 1e-8 * abs(o[0].dpg), nm
+        assert o[0].accepted == f[0].accepted == 1
+        assert np.max(np.abs(f[3] - o[3])) <= 1e-8 * np.max(np.abs(o[3]))   # b_new
+        assert np.max(np.abs(f[4] - o[4])) <= 1e-6 * np.max(np.abs(o[4]))   # db
+    pb = oracle.SparseProblem(sc.m, sc.n, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.K)
+    ref = oracle.sp_linearize(pb, a, b, num_a)
+    lin = res["mixed"][5]
+    assert np.array_equal(lin["W"].reshape(3 * num_a, -1, order="F").T, ref["W"])
+    assert np.array_equal(lin["V"], ref["V"]) and np.array_equal(lin["eB"], ref["eB"])
