@@ -276,61 +276,71 @@ static __device__ __forceinline__ double rowbcast(double v, int q)
 }
 
 // One wave: Cholesky of the 16x16 diagonal block at (o, o) of As and its
-// inverse (lane r keeps row r of L, then column r of L^-1, in registers;
-// column broadcasts by DPP, pivots by readlane).  L (zero upper) -> As, L^-1 (zero upper) -> Bs.
+// inverse (lane r keeps row r of L and column r of L^-1 in registers; column
+// broadcasts by DPP, pivots by readlane).  L (zero upper) -> As, L^-1 (zero
+// upper) -> Bs.  The inverse's right-looking substitution (x_t /= L_tt,
+// x_q -= L_qt x_t) runs inside the factor loop: its step t needs only column t
+// of L, final at iteration t, and shares that column's DPP broadcasts L_qt with
+// the rank-1 update -- its FMAs fill the latency of the next pivot's rsqrt
+// chain instead of forming a second dependent loop (same operations in the
+// same order as a separate loop: bit-identical).
 __device__ __forceinline__ bool wave_factor16(double *As, double *Bs, int o)
 {
     const int r = threadIdx.x & 63;
-    double d[16], rd[16];
+    double d[16], x[16];
 #pragma unroll
     for (int c = 0; c < 16; c++) d[c] = (r < 16) ? As[(o + r) * LP + o + c] : 0.0;
-    bool ok = true;
-    // 1/sqrt of a pivot: hardware estimate + two Newton steps (full fp64)
+#pragma unroll
+    for (int q = 0; q < 16; q++) x[q] = (q == r) ? 1.0 : 0.0;
+    // 1/sqrt of a pivot: hardware estimate + two Newton steps (full fp64).  No
+    // test on the chain: a pivot <= 0 (or NaN) makes its diagonal entry
+    // piv * rsq(piv) NaN, which the check after the loop finds
     auto rsq = [&](double piv) {
-        if (!(piv > 0.0)) {
-            ok = false;
-            piv = 1.0;
-        }
         double y = __builtin_amdgcn_rsq(piv);
         const double hp = 0.5 * piv;
         y = y * fma(-hp * y, y, 1.5);
         y = y * fma(-hp * y, y, 1.5);
         return y;
     };
-    double pv = rdlane(d[0], 0);
-    double y = rsq(pv);
+    // pivots reach every lane of the row by a DPP broadcast (a VGPR: no
+    // readlane -> SGPR -> VALU hazard wait on the chain)
+    double y = rsq(rowbcast_c<0>(d[0]));
 #pragma unroll
     for (int c = 0; c < 16; c++) {
-        rd[c] = y;
-        d[c] = (r == c) ? pv * y : ((r > c) ? d[c] * y : 0.0);
+        // Unpredicated: lane c's d[c] * y is its pivot times y, the diagonal
+        // of L; lanes r < c scale / update only their upper part, which is
+        // never broadcast (broadcasts read lanes q > c) and is zeroed at the
+        // store below.
+        d[c] = d[c] * y;
+        x[c] = x[c] * y;
         // look-ahead: column c+1 first, so the next pivot's rsqrt chain can
-        // overlap the rest of this column's rank-1 update.  Unpredicated:
-        // lanes r < q only touch their upper part (zeroed below), lanes r < c
-        // hold d[c] = 0 and are unchanged.
+        // overlap the rest of this column's rank-1 update
         if (c + 1 < 16) {
-            d[c + 1] = fma(-d[c], rowbcast(d[c], c + 1), d[c + 1]);
-            pv = rdlane(d[c + 1], c + 1);
-            y = rsq(pv);
+            const double b = rowbcast(d[c], c + 1);
+            d[c + 1] = fma(-d[c], b, d[c + 1]);
+            y = rsq(rowbcast(d[c + 1], c + 1));
+            x[c + 1] = fma(-b, x[c], x[c + 1]);
         }
 #pragma unroll
-        for (int q = c + 2; q < 16; q++) d[q] = fma(-d[c], rowbcast(d[c], q), d[q]);
+        for (int q = c + 2; q < 16; q++) {
+            const double b = rowbcast(d[c], q);
+            d[q] = fma(-d[c], b, d[q]);
+            x[q] = fma(-b, x[c], x[q]);
+        }
+        // keep each column's inverse updates with its broadcasts: left alone,
+        // the compiler sinks them below the loop and parks the 120 broadcasts
+        // in AGPRs until then (an empty asm that "modifies" x pins them here)
+#pragma unroll
+        for (int q = c; q < 16; q++) asm volatile("" : "+v"(x[q]));
     }
+    double dg = 1.0;   // lane r's diagonal entry L_rr = sqrt(pivot r)
+#pragma unroll
+    for (int c = 0; c < 16; c++)
+        if (r == c) dg = d[c];
+    const bool ok = __all(r >= 16 || (dg > 0.0 && dg < __builtin_inf()));
     if (r < 16) {
 #pragma unroll
         for (int c = 0; c < 16; c++) As[(o + r) * LP + o + c] = (c <= r) ? d[c] : 0.0;
-    }
-    // column r of the inverse, right-looking: x_t /= L_tt, x_q -= L_qt x_t, with
-    // L_qt = lane q's d[t] broadcast by DPP (no LDS round trip)
-    double x[16];
-#pragma unroll
-    for (int q = 0; q < 16; q++) x[q] = (q == r) ? 1.0 : 0.0;
-#pragma unroll
-    for (int t = 0; t < 16; t++) {
-        x[t] = x[t] * rd[t];
-#pragma unroll
-        for (int q = t + 1; q < 16; q++) x[q] = fma(-rowbcast(d[t], q), x[t], x[q]);
-    }
-    if (r < 16) {
 #pragma unroll
         for (int c = 0; c < 16; c++) Bs[(o + c) * LP + o + r] = x[c];
     }

@@ -15,6 +15,11 @@ void *ba_dmalloc(size_t bytes)
     return hipMalloc(&p, bytes) == hipSuccess ? p : nullptr;
 }
 void ba_dfree(void *p) { (void)hipFree(p); }
+int ba_ensure_dyn_lds(const void *fn, size_t bytes)
+{
+    return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) ==
+                   hipSuccess ? 0 : -1;
+}
 
 #include <cstdio>
 #include <cstdlib>
