@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="cfg3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-scene", action="store_true",
+                    help="generate the banded configs with numpy instead of on the GPU")
     ap.add_argument("--cpu-sample-points", type=int, default=0,
                     help="points of the CPU-baseline sample (0 = full scene)")
     ap.add_argument("--mode", choices=["pass", "solve"], default="pass",
@@ -74,8 +76,10 @@ def main():
     from bundleadjustmentmatlab_amd.scene import make_config
 
     t0 = time.time()
-    sc = make_config(args.config)
-    log(f"[bench] scene {args.config}: m={sc.m} n={sc.n} N={sc.num_obs} ({time.time()-t0:.1f}s)")
+    sc = make_config(args.config, gpu=not args.host_scene, **({"device": local} if
+                     not args.host_scene and args.config in ("cfg2", "cfg3") else {}))
+    log(f"[bench] scene {args.config}: m={sc.m} n={sc.n} N={sc.num_obs} ({time.time()-t0:.1f}s, "
+        f"{'numpy' if args.host_scene or args.config not in ('cfg2', 'cfg3') else 'GPU'})")
     num_a = 6
     a0 = np.zeros((num_a, sc.m), order="F")
     a0[0:3], a0[3:6] = sc.w0, sc.T0
@@ -170,7 +174,9 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (seeded banded scene, SURVEY.md 8.d)",
+        "data": ("synthetic (seeded banded scene, SURVEY.md 8.d, generated on the GPU: "
+                 "csrc/ba_scene.hip)" if not args.host_scene and args.config in ("cfg2", "cfg3")
+                 else "synthetic (seeded scene, SURVEY.md 8.d, numpy)"),
         "config": {"workload": f"{args.config}: {sc.m} cams x {sc.n} pts x {N} obs, "
                                "fix_calibration (num_a=6), full LM pass per step",
                    "cameras": sc.m, "points": sc.n, "observations": N,

@@ -60,6 +60,18 @@ class VlgbaStepInfo(ctypes.Structure):
                 ("chol_failed", c_int), ("pinv", c_int)]
 
 
+class VlgbaSceneSpec(ctypes.Structure):
+    _fields_ = [("m", c_int), ("n", c_int), ("track", c_int), ("depth_lo", c_double),
+                ("depth_hi", c_double), ("noise", c_double), ("seed", ctypes.c_ulonglong),
+                ("keep_first_rotation", c_int), ("width", c_double), ("height", c_double)]
+
+
+class VlgbaSceneOut(ctypes.Structure):
+    _fields_ = [("K", c_dp), ("w", c_dp), ("T", c_dp), ("X", c_dp), ("w0", c_dp), ("T0", c_dp),
+                ("X0", c_dp), ("obs_pt", c_ip), ("obs_cam", c_ip), ("obs_x", c_dp),
+                ("num_obs_cap", c_ll), ("num_obs", c_ll), ("behind", c_ll)]
+
+
 # vlgba_options.on_pass(pass, iter, const vlgba_step_info *, user)
 ON_PASS_FN = ctypes.CFUNCTYPE(None, c_int, c_int, ctypes.POINTER(VlgbaStepInfo), ctypes.c_void_p)
 
@@ -92,6 +104,8 @@ SIGNATURES = {
     "vlgba_mex_bundle_proj_3": (c_int, [c_int, c_int] + [c_dp] * 12),
     "vlgba_resect": (c_int, [ctypes.POINTER(VlgbaResectProblem), ctypes.POINTER(VlgbaOptions),
                              c_dp, c_dp, c_int, c_ip, ctypes.POINTER(VlgbaStats)]),
+    "vlgba_scene_banded": (c_int, [ctypes.POINTER(VlgbaSceneSpec), c_int,
+                                   ctypes.POINTER(VlgbaSceneOut)]),
     "vlgba_version": (c_int, [ctypes.c_char_p, c_int]),
     "vlgba_get_unique_id": (c_int, [ctypes.c_void_p]),
     "vlgba_device_count": (c_int, []),

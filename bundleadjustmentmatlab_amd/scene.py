@@ -306,7 +306,41 @@ CONFIGS = {
 }
 
 
-def make_config(name, **over):
+def gpu_banded_scene(m=50, n=10_000, track=6, depth=(80.0, 120.0), noise=0.5, seed=2,
+                     keep_first_rotation=False, device=0):
+    """banded_scene's model generated on the GPU (vlgba_scene_banded,
+    csrc/ba_scene.hip: counter-based Philox streams, so the scene is the same
+    for a seed on any device).  Same statistics as banded_scene, a different
+    random stream (and the first cameras as jittered strata: uniform marginal,
+    numbered in camera order)."""
+    import ctypes
+    from ._lib import VlgbaSceneOut, VlgbaSceneSpec, check, lib
+    track = min(track, m)
+    N = n * track
+    out = dict(K=np.zeros((4, m), order="F"), w=np.zeros((3, m), order="F"),
+               T=np.zeros((3, m), order="F"), X=np.zeros((4, n), order="F"),
+               w0=np.zeros((3, m), order="F"), T0=np.zeros((3, m), order="F"),
+               X0=np.zeros((4, n), order="F"), obs_pt=np.zeros(N, np.int32),
+               obs_cam=np.zeros(N, np.int32), obs_x=np.zeros((N, 2)))
+    dp = lambda k: out[k].ctypes.data_as(ctypes.POINTER(ctypes.c_double))   # noqa: E731
+    ip = lambda k: out[k].ctypes.data_as(ctypes.POINTER(ctypes.c_int))      # noqa: E731
+    spec = VlgbaSceneSpec(int(m), int(n), int(track), float(depth[0]), float(depth[1]),
+                          float(noise), int(seed), int(keep_first_rotation), 0.0, 0.0)
+    so = VlgbaSceneOut(dp("K"), dp("w"), dp("T"), dp("X"), dp("w0"), dp("T0"), dp("X0"),
+                       ip("obs_pt"), ip("obs_cam"), dp("obs_x"), N, 0, 0)
+    check(lib().vlgba_scene_banded(ctypes.byref(spec), int(device), ctypes.byref(so)),
+          "vlgba_scene_banded")
+    if so.behind:
+        raise RuntimeError(f"synthetic scene: {so.behind} observations behind their camera")
+    return Scene(out["K"], out["T"], out["w"], out["X"], out["obs_pt"], out["obs_cam"],
+                 out["obs_x"], out["T0"], out["w0"], out["X0"])
+
+
+def make_config(name, gpu=False, **over):
+    """The named config's scene; gpu=True generates the banded configs on the
+    GPU (gpu_banded_scene: same model, counter-based random streams)."""
     fn, kw = CONFIGS[name]
     kw = dict(kw, **over)
+    if gpu and fn is banded_scene:
+        return gpu_banded_scene(**kw)
     return fn(**kw)

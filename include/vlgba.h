@@ -302,6 +302,36 @@ int vlgba_debug_pinv_solve(int ld, const double *S, const double *e_, double *da
 int vlgba_version(char *buf, int len);
 int vlgba_device_count(void);
 
+/* ---- synthetic scenes on the GPU --------------
+ * Configs 2-4's banded model (a restatement of
+ * toolbox/test/generate_scene_and_motion.m:36-117: f = width, c = centre,
+ * damped random-walk cameras, points at depth U(lo, hi) seen by `track`
+ * consecutive cameras, N(0, noise^2) pixel noise) and the perturbation of
+ * toolbox/test/demo_bundle_euclid.m:29-31, generated by counter-based
+ * (Philox4x32-10) kernels: the same seed gives the same scene on any GPU and
+ * launch geometry.  Outputs are host buffers (NULL: not copied); observations
+ * are point-major with cameras ascending, N = n * min(track, m).            */
+typedef struct {
+    int m, n, track;
+    double depth_lo, depth_hi;     /* point depth in front of its first camera  */
+    double noise;                  /* pixel noise sigma                         */
+    unsigned long long seed;
+    int keep_first_rotation;       /* w0(:,1) = w(:,1) (the test_mview path)    */
+    double width, height;          /* image size; 0 -> 500                      */
+} vlgba_scene_spec;
+
+typedef struct {
+    double *K, *w, *T, *X;         /* [4m] [3m] [3m] [4n] ground truth (X(4,:) = 1) */
+    double *w0, *T0, *X0;          /* [3m] [3m] [4n] perturbed initial values       */
+    int *obs_pt, *obs_cam;         /* [N]                                           */
+    double *obs_x;                 /* [2N] measured (u, v)                          */
+    long long num_obs_cap;         /* capacity of the observation arrays (>= N)     */
+    long long num_obs;             /* out: N                                        */
+    long long behind;              /* out: observations at depth <= 0.01 depth_lo   */
+} vlgba_scene_out;
+
+int vlgba_scene_banded(const vlgba_scene_spec *spec, int device, vlgba_scene_out *out);
+
 #ifdef __cplusplus
 }
 #endif
