@@ -30,6 +30,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #define RS_TILE 256
@@ -41,7 +42,7 @@ __global__ __launch_bounds__(256) void k_resect_pass(
     int nprob, const long long *__restrict__ obs_ptr, const double *__restrict__ Xw,
     const double *__restrict__ xo, const double *__restrict__ K4, double *__restrict__ a,
     double *__restrict__ a_new, double *__restrict__ state, const double *__restrict__ lam_p,
-    const int *__restrict__ flags, double *__restrict__ out)
+    const double *__restrict__ flags, double *__restrict__ out)
 {
     constexpr int NUE = NA * NA + NA + 1;
     __shared__ double rot[45], rotn[9], k4[4], av[NA], an[NA];
@@ -50,7 +51,7 @@ __global__ __launch_bounds__(256) void k_resect_pass(
     __shared__ int fail;
     const int pb = blockIdx.x, tid = threadIdx.x;
     if (pb >= nprob) return;
-    const int fl = flags[pb];
+    const int fl = (int)flags[pb];   // staged with lambda as doubles (one copy a pass)
     if (!(fl & 1)) return;                          // problem finished
     const long long o0 = obs_ptr[pb], no = obs_ptr[pb + 1] - o0;
     double *stg = state + (size_t)NUE * pb;
@@ -263,6 +264,52 @@ int dmalloc_n(T **p, size_t n)
     *p = (T *)ba_dmalloc(sizeof(T) * (n ? n : 1));
     return *p ? 0 : -(int)hipErrorOutOfMemory;
 }
+// Per-device pool of a stream and a pinned host block for the per-pass LM
+// scalars: creating a stream and pageable copies cost more than the
+// resection itself (the growing-BA replay calls it once per added camera).
+struct rs_pool {
+    int device;
+    hipStream_t s;
+    double *pin;     // pinned: lam [np] | flags [np] (as doubles) | out [4 np]
+    size_t cap;      // doubles
+};
+std::mutex g_rs_pool_mu;
+std::vector<rs_pool> g_rs_pool;
+
+int rs_acquire(int device, size_t need, rs_pool &r)
+{
+    {
+        std::lock_guard<std::mutex> lk(g_rs_pool_mu);
+        for (size_t q = 0; q < g_rs_pool.size(); q++)
+            if (g_rs_pool[q].device == device) {
+                r = g_rs_pool[q];
+                g_rs_pool.erase(g_rs_pool.begin() + (long)q);
+                break;
+            }
+    }
+    if (!r.s) {
+        r.device = device;
+        if (hipStreamCreateWithFlags(&r.s, hipStreamNonBlocking) != hipSuccess) return -1;
+    }
+    if (r.cap < need) {
+        if (r.pin) (void)hipHostFree(r.pin);
+        r.pin = nullptr;
+        r.cap = 0;
+        const size_t cap = need > 4096 ? need : 4096;
+        if (hipHostMalloc((void **)&r.pin, sizeof(double) * cap, hipHostMallocDefault) !=
+            hipSuccess)
+            return -1;
+        r.cap = cap;
+    }
+    return 0;
+}
+
+void rs_release(const rs_pool &r)
+{
+    (void)hipStreamSynchronize(r.s);
+    std::lock_guard<std::mutex> lk(g_rs_pool_mu);
+    g_rs_pool.push_back(r);
+}
 }   // namespace
 
 extern "C" int vlgba_resect(const vlgba_resect_problem *pr, const vlgba_options *opt, double *a,
@@ -288,13 +335,17 @@ extern "C" int vlgba_resect(const vlgba_resect_problem *pr, const vlgba_options 
     const double stop_rel = opt->stop_rel > 0 ? opt->stop_rel : 1e-3;
     VLGBA_CHECK(hipSetDevice(opt->device));
     const auto t0 = std::chrono::steady_clock::now();
-    hipStream_t s = nullptr;
-    VLGBA_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    rs_pool pool{opt->device, nullptr, nullptr, 0};
+    if (rs_acquire(opt->device, 6 * (size_t)np, pool)) {
+        if (pool.s) rs_release(pool);
+        return -1;
+    }
+    hipStream_t s = pool.s;
+    double *h_lam = pool.pin, *h_fl = pool.pin + np, *h_out = pool.pin + 2 * (size_t)np;
     const int NUE = na * na + na + 1;
     long long *d_ptr = nullptr;
     double *d_X = nullptr, *d_x = nullptr, *d_K = nullptr, *d_a = nullptr, *d_an = nullptr;
-    double *d_st = nullptr, *d_lam = nullptr, *d_out = nullptr;
-    int *d_fl = nullptr;
+    double *d_st = nullptr, *d_lam = nullptr, *d_out = nullptr, *d_fl = nullptr;
     int rc = 0;
     std::vector<double> lam(np, lambda0), nu(np, 2.0), out(4 * (size_t)np);
     std::vector<int> fl(np), iter(np, 1), iter2(np, 0), passes(np, 0), acc(np, 0);
@@ -305,9 +356,10 @@ extern "C" int vlgba_resect(const vlgba_resect_problem *pr, const vlgba_options 
         if ((rc = dmalloc_n(&d_ptr, np + 1)) || (rc = dmalloc_n(&d_X, 3 * (size_t)N)) ||
             (rc = dmalloc_n(&d_x, 2 * (size_t)N)) || (rc = dmalloc_n(&d_K, 4 * (size_t)np)) ||
             (rc = dmalloc_n(&d_a, (size_t)na * np)) || (rc = dmalloc_n(&d_an, (size_t)na * np)) ||
-            (rc = dmalloc_n(&d_st, (size_t)NUE * np)) || (rc = dmalloc_n(&d_lam, np)) ||
-            (rc = dmalloc_n(&d_out, 4 * (size_t)np)) || (rc = dmalloc_n(&d_fl, np)))
+            (rc = dmalloc_n(&d_st, (size_t)NUE * np)) || (rc = dmalloc_n(&d_lam, 2 * (size_t)np)) ||
+            (rc = dmalloc_n(&d_out, 4 * (size_t)np)))
             break;
+        d_fl = d_lam + np;
         if (hipMemcpyAsync(d_ptr, pr->obs_ptr, sizeof(long long) * (np + 1), hipMemcpyHostToDevice,
                            s) != hipSuccess ||
             (N > 0 && (hipMemcpyAsync(d_X, pr->X, sizeof(double) * 3 * N, hipMemcpyHostToDevice,
@@ -337,10 +389,12 @@ extern "C" int vlgba_resect(const vlgba_resect_problem *pr, const vlgba_options 
                 fl[q] = active[q] | (relin[q] ? 2 : 0) | (accepted_prev[q] ? 4 : 0);
             }
             if (!nact) break;
-            if (hipMemcpyAsync(d_lam, lam.data(), sizeof(double) * np, hipMemcpyHostToDevice, s) !=
-                    hipSuccess ||
-                hipMemcpyAsync(d_fl, fl.data(), sizeof(int) * np, hipMemcpyHostToDevice, s) !=
-                    hipSuccess) {
+            for (int q = 0; q < np; q++) {   // pinned staging: one small copy per pass
+                h_lam[q] = lam[q];
+                h_fl[q] = (double)fl[q];
+            }
+            if (hipMemcpyAsync(d_lam, h_lam, sizeof(double) * 2 * np, hipMemcpyHostToDevice, s) !=
+                hipSuccess) {
                 rc = -1;
                 break;
             }
@@ -359,12 +413,13 @@ extern "C" int vlgba_resect(const vlgba_resect_problem *pr, const vlgba_options 
                 break;
             }
             if (hipGetLastError() != hipSuccess ||
-                hipMemcpyAsync(out.data(), d_out, sizeof(double) * 4 * np, hipMemcpyDeviceToHost,
+                hipMemcpyAsync(h_out, d_out, sizeof(double) * 4 * np, hipMemcpyDeviceToHost,
                                s) != hipSuccess ||
                 hipStreamSynchronize(s) != hipSuccess) {
                 rc = -1;
                 break;
             }
+            std::memcpy(out.data(), h_out, sizeof(double) * 4 * np);
             for (int q = 0; q < np; q++) {
                 if (!active[q]) continue;   // a finished problem keeps its last flags
                 accepted_prev[q] = 0;
@@ -418,9 +473,9 @@ extern "C" int vlgba_resect(const vlgba_resect_problem *pr, const vlgba_options 
     } while (0);
     (void)hipStreamSynchronize(s);
     for (void *p : {(void *)d_ptr, (void *)d_X, (void *)d_x, (void *)d_K, (void *)d_a,
-                    (void *)d_an, (void *)d_st, (void *)d_lam, (void *)d_out, (void *)d_fl})
+                    (void *)d_an, (void *)d_st, (void *)d_lam, (void *)d_out})
         if (p) ba_dfree(p);
-    (void)hipStreamDestroy(s);
+    rs_release(pool);
     if (stats) {
         stats->iterations = total_passes;
         stats->accepted = total_acc;
