@@ -127,14 +127,11 @@ struct ba_dev {
                        // Q3) or NA (bundle_euclid_nomex.m semantics)
     int nch;           // chunks
     int *ch_pt;        // [nch+1] local point ranges
-    int *ch_slot;      // [nch+1] slot ranges (slots are numbered chunk-major)
+    // (the per-chunk slot / term lists stay on the host: they are folded into
+    // the chunk records of `blob` and the group-slot lists below)
     int *ch_eslot;     // [nch+1] e-slot ranges
-    int *slot_blk;     // [ns] block id of each slot
-    int *slot_tptr;    // [ns+1] term ranges
-    unsigned short *slot_term;  // [nterm][2] chunk-local obs indices
     int *eslot_optr;   // [nes+1]
     unsigned short *eslot_obs;  // [neo] chunk-local obs indices
-    int *blk_sptr, *blk_slots;  // per block: its slots in chunk order
     int *cam_eptr, *cam_eslots; // per camera: its e-slots in chunk order
     double *spart;     // [ngs][NA*NA] per group slot
     double *epart;     // [nge][NA] per group e-slot

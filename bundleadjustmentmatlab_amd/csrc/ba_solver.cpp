@@ -20,6 +20,8 @@
 #include <rocsolver/rocsolver.h>   // types only: the library is dlopen'ed on first use
 
 #include <dlfcn.h>
+#include <cstdlib>
+#include <string>
 
 #include <algorithm>
 #include <atomic>
@@ -285,6 +287,7 @@ struct host_plan {
     std::vector<unsigned short> slot_term, eslot_obs;
     std::vector<int> blk_sptr, blk_slots, cam_eptr, cam_eslots;
     int max_terms = 0, max_slots = 0;   // per chunk (LDS staging size)
+    long long n_terms = 0;              // (obs, obs) Schur terms of all chunks
     // Schur groups: consecutive chunks whose co-visible blocks ("group slots")
     // and cameras ("group e-slots") are accumulated in LDS across the group
     std::vector<int> grp_ch, grp_gs, grp_ge;      // [ngrp+1] ranges
@@ -335,9 +338,7 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
             return false;
     std::vector<int> cam_stamp(m, -1);   // chunk camera set (MFMA chunking)
     P.max_terms = P.max_slots = 0;
-    std::vector<int> slot_of(nb, -1), eslot_of(m, -1), touched, tcam;
-    std::vector<std::vector<std::pair<int, int>>> terms;   // per local slot
-    std::vector<std::vector<int>> eobs;                     // per local e-slot
+    std::vector<int> slot_of(nb, -1), eslot_of(m, -1), touched, tcam, tcnt, ecnt;
     P.ch_pt.push_back(0);
     P.ch_slot.push_back(0);
     P.ch_eslot.push_back(0);
@@ -376,19 +377,22 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
             nterm += pt_terms(q++);
         }
         P.max_terms = std::max(P.max_terms, (int)nterm);
+        P.n_terms += nterm;
+        // pass 1: the chunk's slots (co-visible blocks, by first touch) and
+        // e-slots (cameras), with their term / observation counts
         touched.clear();
         tcam.clear();
-        terms.clear();
-        eobs.clear();
+        tcnt.clear();
+        ecnt.clear();
         for (int i = p; i < q; i++)
             for (int a = lptr[i]; a < lptr[i + 1]; a++) {
                 const int j = lcam[a];
                 if (eslot_of[j] < 0) {
                     eslot_of[j] = (int)tcam.size();
                     tcam.push_back(j);
-                    eobs.emplace_back();
+                    ecnt.push_back(0);
                 }
-                eobs[eslot_of[j]].push_back(a - obase);
+                ecnt[eslot_of[j]]++;
                 for (int b = lptr[i]; b < lptr[i + 1]; b++) {
                     const int k = lcam[b];
                     if (j < k) continue;
@@ -396,26 +400,42 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
                     if (slot_of[blk] < 0) {
                         slot_of[blk] = (int)touched.size();
                         touched.push_back(blk);
-                        terms.emplace_back();
+                        tcnt.push_back(0);
                     }
-                    terms[slot_of[blk]].push_back({a - obase, b - obase});
+                    tcnt[slot_of[blk]]++;
                 }
             }
         P.max_slots = std::max(P.max_slots, (int)touched.size());
-        for (size_t s = 0; s < touched.size(); s++) {
-            P.slot_blk.push_back(touched[s]);
-            for (auto &t : terms[s]) {
-                P.slot_term.push_back((unsigned short)t.first);
-                P.slot_term.push_back((unsigned short)t.second);
+        // pass 2: the per-term lists (term chunks only: the MFMA records are
+        // dense) and the per-camera observation lists, in the same order
+        const size_t t0 = P.slot_term.size() / 2, u0 = P.eslot_obs.size();
+        for (size_t sl = 0; sl < touched.size(); sl++) {
+            P.slot_blk.push_back(touched[sl]);
+            P.slot_tptr.push_back(P.slot_tptr.back() + (mf ? 0 : tcnt[sl]));
+        }
+        for (size_t e = 0; e < tcam.size(); e++)
+            P.eslot_optr.push_back(P.eslot_optr.back() + ecnt[e]);
+        const int sbase = (int)P.slot_blk.size() - (int)touched.size();
+        const int ebase = (int)P.eslot_optr.size() - 1 - (int)tcam.size();
+        if (!mf) P.slot_term.resize(2 * (size_t)P.slot_tptr.back());
+        P.eslot_obs.resize((size_t)P.eslot_optr.back());
+        for (size_t sl = 0; sl < touched.size(); sl++) tcnt[sl] = P.slot_tptr[sbase + sl] - (int)t0;
+        for (size_t e = 0; e < tcam.size(); e++) ecnt[e] = P.eslot_optr[ebase + e] - (int)u0;
+        for (int i = p; i < q; i++)
+            for (int a = lptr[i]; a < lptr[i + 1]; a++) {
+                const int j = lcam[a];
+                P.eslot_obs[u0 + ecnt[eslot_of[j]]++] = (unsigned short)(a - obase);
+                if (mf) continue;
+                for (int b = lptr[i]; b < lptr[i + 1]; b++) {
+                    const int k = lcam[b];
+                    if (j < k) continue;
+                    const size_t at = t0 + tcnt[slot_of[hb.find(j, k)]]++;
+                    P.slot_term[2 * at] = (unsigned short)(a - obase);
+                    P.slot_term[2 * at + 1] = (unsigned short)(b - obase);
+                }
             }
-            P.slot_tptr.push_back((int)P.slot_term.size() / 2);
-            slot_of[touched[s]] = -1;
-        }
-        for (size_t s = 0; s < tcam.size(); s++) {
-            for (int o : eobs[s]) P.eslot_obs.push_back((unsigned short)o);
-            P.eslot_optr.push_back((int)P.eslot_obs.size());
-            eslot_of[tcam[s]] = -1;
-        }
+        for (int blk : touched) slot_of[blk] = -1;
+        for (int j : tcam) eslot_of[j] = -1;
         // cameras of the chunk, for the per-camera reduction below
         for (size_t s = 0; s < tcam.size(); s++) P.cam_eslots.push_back(tcam[s]);
         P.ch_pt.push_back(q);
@@ -784,6 +804,29 @@ static int allreduce(vlgba_ctx *c, double *buf, size_t count)
     return 0;
 }
 
+// setup timing trace (VLGBA_SETUP_TRACE=1: one stderr line per context)
+struct setup_trace {
+    bool on = std::getenv("VLGBA_SETUP_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    std::string line;
+    void mark(const char *what)
+    {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        char buf[64];
+        std::snprintf(buf, sizeof buf, " %s=%.0fus", what,
+                      std::chrono::duration<double, std::micro>(now - t).count());
+        line += buf;
+        t = now;
+    }
+    ~setup_trace()
+    {
+        if (on && !line.empty()) std::fprintf(stderr, "[vlgba setup]%s\n", line.c_str());
+    }
+};
+static thread_local setup_trace *g_st = nullptr;
+#define ST_MARK(w) do { if (g_st) g_st->mark(w); } while (0)
+
 // Fast-path point order: when some but not all tracks fit the MFMA Schur
 // chunks (<= BA_MF_CMAX(na) observations) and every track fits a chunk at all,
 // put the short-track points first (stable), so that the MFMA chunks are runs
@@ -872,7 +915,9 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
     }
     host_blocks hb;
     host_plan plan;
+    ST_MARK("lists");
     build_blocks(p->m, pt_ptr_all, h.cam, c->p0, c->p1, o0, lower_blocks, all_diag, !fast, hb);
+    ST_MARK("blocks");
     // MFMA Schur chunks for the leading points whose tracks fit the dense slab
     // (ctx_create orders the short-track points first), per-term chunks for
     // the rest; the ordered kernels if some track fits neither
@@ -891,6 +936,7 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         }
     }
     if (!fast) d.ordered = 1;
+    ST_MARK("plan");
     d.nb = (int)hb.jk.size() / 2;
     d.T = (long long)hb.term.size() / 2;
 
@@ -920,18 +966,12 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         d.nes = (int)plan.eslot_optr.size() - 1;
         d.ch_max_terms = plan.max_terms;
         d.ch_max_slots = plan.max_slots;
-        d.nterm_fast = (long long)plan.slot_term.size() / 2;
+        d.nterm_fast = plan.n_terms;
         d.blob_words = (long long)plan.blob.size();
         TRY(ctx_alloc(c, &d.ch_pt, plan.ch_pt.size()));
-        TRY(ctx_alloc(c, &d.ch_slot, plan.ch_slot.size()));
         TRY(ctx_alloc(c, &d.ch_eslot, plan.ch_eslot.size()));
-        TRY(ctx_alloc(c, &d.slot_blk, plan.slot_blk.size()));
-        TRY(ctx_alloc(c, &d.slot_tptr, plan.slot_tptr.size()));
-        TRY(ctx_alloc(c, &d.slot_term, plan.slot_term.size()));
         TRY(ctx_alloc(c, &d.eslot_optr, plan.eslot_optr.size()));
         TRY(ctx_alloc(c, &d.eslot_obs, plan.eslot_obs.size()));
-        TRY(ctx_alloc(c, &d.blk_sptr, plan.blk_sptr.size()));
-        TRY(ctx_alloc(c, &d.blk_slots, plan.blk_slots.size()));
         TRY(ctx_alloc(c, &d.cam_eptr, plan.cam_eptr.size()));
         TRY(ctx_alloc(c, &d.cam_eslots, plan.cam_eslots.size()));
         d.ngrp = (int)plan.grp_ch.size() - 1;
@@ -983,18 +1023,13 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         TRY(ctx_alloc(c, &d.upart, (size_t)(na * (na + 1) / 2 + na) * d.nes));
         TRY(ctx_alloc(c, &d.chsse, 3 * (size_t)d.nch));   // lin SSE | new SSE | dpg
         TRY(upload(d.ch_pt, plan.ch_pt.data(), plan.ch_pt.size(), s));
-        TRY(upload(d.ch_slot, plan.ch_slot.data(), plan.ch_slot.size(), s));
         TRY(upload(d.ch_eslot, plan.ch_eslot.data(), plan.ch_eslot.size(), s));
-        TRY(upload(d.slot_blk, plan.slot_blk.data(), plan.slot_blk.size(), s));
-        TRY(upload(d.slot_tptr, plan.slot_tptr.data(), plan.slot_tptr.size(), s));
-        TRY(upload(d.slot_term, plan.slot_term.data(), plan.slot_term.size(), s));
         TRY(upload(d.eslot_optr, plan.eslot_optr.data(), plan.eslot_optr.size(), s));
         TRY(upload(d.eslot_obs, plan.eslot_obs.data(), plan.eslot_obs.size(), s));
-        TRY(upload(d.blk_sptr, plan.blk_sptr.data(), plan.blk_sptr.size(), s));
-        TRY(upload(d.blk_slots, plan.blk_slots.data(), plan.blk_slots.size(), s));
         TRY(upload(d.cam_eptr, plan.cam_eptr.data(), plan.cam_eptr.size(), s));
         TRY(upload(d.cam_eslots, plan.cam_eslots.data(), plan.cam_eslots.size(), s));
         VLGBA_CHECK(hipStreamSynchronize(s));   // plan vectors are local
+        ST_MARK("plan_upload");
     }
     TRY(ctx_alloc(c, &d.U, (size_t)na * na * p->m + na * (size_t)p->m + 1));
     d.eA = d.U + (size_t)na * na * p->m;     // U | eA | old_sse contiguous: one all-reduce
@@ -1015,7 +1050,9 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         TRY(ctx_alloc(c, &d.linv, (size_t)(d.lds / 64) * 64 * 64));
         TRY(ctx_alloc(c, &d.ywork, (size_t)d.lds + 64));   // + the 32-row CR's last tile
         TRY(ctx_alloc(c, &d.da, (size_t)d.lds));
+        ST_MARK("allocs");
         TRY(ba_chol_setup(&d, hb.jk.data(), d.nb));
+        ST_MARK("chol_setup");
     } else {
         TRY(ctx_alloc(c, &d.da, (size_t)d.lds));
     }
@@ -1062,6 +1099,9 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
     std::memset(&defaults, 0, sizeof defaults);
     if (!o) o = &defaults;
     int rc = 0;
+    setup_trace trace;
+    g_st = &trace;
+    struct st_reset { ~st_reset() { g_st = nullptr; } } st_reset_;
     do {
         if (hipSetDevice(o->device) != hipSuccess) { rc = VLGBA_E_ARG; break; }
         if (aux_acquire(o->device, c->aux)) {
@@ -1075,14 +1115,17 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
         c->d.ev_join = c->aux.ev_join;
         c->d.hres = c->aux.hres_host;
         c->d.hres_dev = c->aux.hres_dev;
+        ST_MARK("aux");
         host_obs h;
         rc = sort_obs(p, h);
         if (rc) break;
+        ST_MARK("sort");
         std::vector<int> pt_ptr_all(p->n + 1, 0);
         for (size_t q = 0; q < h.pt.size(); q++) pt_ptr_all[h.pt[q] + 1]++;
         for (int i = 0; i < p->n; i++) pt_ptr_all[i + 1] += pt_ptr_all[i];
         if (o->ordered == 0 && !stage_mode && o->schur_kernel != 1 && o->world_size <= 1)
             order_points_by_kind(p->num_a, h, pt_ptr_all, c->pperm, c->operm);
+        ST_MARK("order");
         c->world = o->world_size > 1 ? o->world_size : 1;
         c->rank = c->world > 1 ? o->rank : 0;
         // contiguous point ranges with balanced observation counts
@@ -1146,6 +1189,7 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
         c->d.ndb = o->semantics == 1 ? p->num_a : 6;
         rc = ctx_setup(c, p, h, pt_ptr_all, lower_blocks, all_diag, stage_mode);
         if (rc) break;
+        ST_MARK("setup_end");
         if (c->d.parity) {   // new projections for the sequential new-SSE sum
             rc = ctx_alloc(c, &c->d.xh_out, 2 * (size_t)c->d.N + 2);
             if (rc) break;

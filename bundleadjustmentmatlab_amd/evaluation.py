@@ -45,10 +45,20 @@ def vl_rodr(w):
 
 
 def vl_irodr(R):
-    """Inverse Rodrigues map R (3, 3) -> w (3,) (VLFeat vl_irodr): the rotation
-    angle from the trace, the axis from the skew part; the angle-pi case
-    from the symmetric part."""
+    """Inverse Rodrigues map R (3, 3) -> w (3,), or a stack (k, 3, 3) -> (3, k)
+    (VLFeat vl_irodr): the rotation angle from the trace, the axis from the
+    skew part; the angle-pi case from the symmetric part."""
     R = np.asarray(R, dtype=np.float64)
+    if R.ndim == 3:
+        c = np.clip((np.trace(R, axis1=1, axis2=2) - 1.0) / 2.0, -1.0, 1.0)
+        th = np.arccos(c)
+        v = np.stack([R[:, 2, 1] - R[:, 1, 2], R[:, 0, 2] - R[:, 2, 0], R[:, 1, 0] - R[:, 0, 1]])
+        s = np.sin(th)
+        reg = s > 1e-8
+        out = np.where(th < 1e-6, 0.5 * v, th / (2.0 * np.where(reg, s, 1.0)) * v)
+        for k in np.nonzero((th >= 1e-6) & ~reg)[0]:   # theta ~ pi (rare): one by one
+            out[:, k] = vl_irodr(R[k])
+        return out
     c = np.clip((np.trace(R) - 1.0) / 2.0, -1.0, 1.0)
     th = np.arccos(c)
     v = np.array([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]])
@@ -133,13 +143,10 @@ def align_scene(T, Omega, X, TRef=None, OmegaRef=None, XRef=None, ScaleOption="c
         S1 = 1.0 / np.linalg.norm(X1[:, X[3] == 1].mean(1))
     else:
         S1 = 1.0 / np.linalg.norm(R1.T @ T1 - vl_rodr(Omega[:, iref]).T @ T[:, iref])
-    T_ = np.zeros((3, m))
-    Omega_ = np.zeros((3, m))
-    Rj = vl_rodr(Omega)
-    for j in range(m):                                    # :90-97
-        RjR1_ = Rj[j] @ R1.T
-        Omega_[:, j] = vl_irodr(RjR1_ @ Rref1)
-        T_[:, j] = RjR1_ @ Tref1 + S1 / Sref * (-RjR1_ @ T1 + T[:, j])
+    Rj = vl_rodr(Omega).reshape(m, 3, 3)                 # :90-97, all cameras at once
+    RjR1_ = Rj @ R1.T
+    Omega_ = vl_irodr(RjR1_ @ Rref1)
+    T_ = (RjR1_ @ Tref1).T + S1 / Sref * (-(RjR1_ @ T1).T + T)
     X_ = np.zeros((4, n))
     on = X[3] == 1                                        # :98-104
     X_[0:3, on] = Rref1.T @ (S1 / Sref * (R1 @ X[0:3, on] + T1[:, None]) - Tref1[:, None])
