@@ -30,6 +30,9 @@ sys.path.insert(0, ROOT)
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md; fp64 matrix = vendor spec)
 PEAK_HBM_GBS = 8000.0
 PEAK_F64_TFLOPS = 78.6
+# VALU issue: one fp64 wave64 instruction per 4 cycles per SIMD, 4 SIMDs x 256 CUs,
+# 2.4 GHz peak clock (MI355X_MICROARCH.md) -> wave-instructions per second
+PEAK_VALU_WINST = 256 * 4 * 2.4e9 / 4
 
 
 def log(*a):
@@ -146,9 +149,15 @@ def main():
     log("[bench] plan: " + " ".join(f"{k}={v}" for k, v in plan.items()))
     roofs = {k: kernel_roofline(k, tot, calls, plan, n_timed) for k, (tot, calls) in
              kms.items()}
-    traffic = pmc_traffic(args.config, plan)
+    traffic, valu = pmc_traffic(args.config, plan)
     for k, r in roofs.items():
         r["traffic"] = traffic.get(k)
+        if k in valu:   # the VALU-issue roof beside the HBM / MFMA one
+            w = valu[k] / (r["avg_launch_us"] * 1e-6)
+            r["valu_issue"] = {"winst_per_launch": valu[k], "achieved": w,
+                               "peak": PEAK_VALU_WINST, "unit": "wave-instr/s",
+                               "frac": w / PEAK_VALU_WINST,
+                               "source": f"SQ_INSTS_VALU, profiles/pmc_traffic_{args.config}.json"}
     dom = max(kms, key=lambda k: kms[k][0])
     roof = roofs[dom]
     log("[bench] kernels (avg us/launch, launches/pass, roofline frac): " +
@@ -322,19 +331,22 @@ PMC_ALIAS = {"k_linearize": "k_linearize_chunk", "k_camera_reduce": "k_camera_re
 def pmc_traffic(config, plan):
     """HBM bytes per launch of each kernel from the committed PMC passes
     (profiles/pmc_traffic_<config>.json, tools/pmc_traffic.py: FETCH_SIZE x 2 +
-    WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), or {} if absent.
+    WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md) and VALU wave-
+    instructions per launch (SQ_INSTS_VALU), or ({}, {}) if absent.
     Valid for the fast (chunked) single-rank path it was collected on."""
     path = os.path.join(ROOT, "profiles", f"pmc_traffic_{config}.json")
     if plan.get("ordered") or not os.path.exists(path):
-        return {}
+        return {}, {}
     with open(path) as f:
         kern = json.load(f)["kernels"]
-    out = {}
+    out, valu = {}, {}
     for name in list(PMC_ALIAS) + [k for k in kern if k.startswith("k_")]:
         base = PMC_ALIAS.get(name, name)
         if base in kern:
             out[name] = kern[base]["bytes"]
-    return out
+            if "valu_winst" in kern[base]:
+                valu[name] = kern[base]["valu_winst"]
+    return out, valu
 
 
 def kernel_roofline(name, tot_ms, calls, plan, n_passes):

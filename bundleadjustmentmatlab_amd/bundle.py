@@ -355,7 +355,7 @@ class BundleAdjuster:
     PLAN_KEYS = ("obs", "points", "cameras", "num_a", "chunks", "chunk_slots",
                  "chunk_eslots", "groups", "group_slots", "group_eslots", "blocks",
                  "tiles", "cr_levels", "cr_elim", "cr_keep", "ordered", "schur_terms",
-                 "blob_words", "mfma", "cr_rows", "mfma_groups", "reordered")
+                 "blob_words", "mfma", "cr_rows", "mfma_groups", "reordered", "long_points")
 
     def plan_info(self):
         """Execution-plan sizes of this rank (vlgba_plan_info)."""

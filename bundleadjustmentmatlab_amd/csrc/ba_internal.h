@@ -150,6 +150,15 @@ struct ba_dev {
     unsigned char *obs_lpt;           // [N] chunk-local point of each observation
     int max_blob;                     // term groups: largest chunk record
     int ngrp_mf;                      // leading MFMA groups
+    // long tracks (points [p_long, n), ba_solver.cpp build_plan): segment
+    // chunks [nch_reg, nch), their V / eB partials, Schur tiles, update sums
+    int nch_reg, nl, ntile_long, p_long;
+    int *seg_pt, *seg_long;           // [nch - nch_reg] point, long index
+    int *long_pt, *long_o0, *long_seg0;   // [nl], [nl+1] obs range, [nl+1] segments
+    int *long_sbase, *long_ebase;     // [nl] first group slot / group e-slot
+    int *long_tiles;                  // [ntile_long][3] (long, a tile, b tile)
+    double *vseg;                     // [nseg][12] V | eB partials per segment
+    double *dpg_long;                 // [nl] point part of dp'(lambda dp + g)
     int mf_max_s, mf_max_e, mf_max_blob;   // MFMA groups' LDS sizes
     int *grp_ch, *grp_gs, *grp_ge;    // [ngrp+1] chunk / group-slot / group-eslot ranges
     unsigned short *cs_g, *ce_g;      // chunk slot / chunk e-slot -> group-local id
@@ -201,6 +210,13 @@ struct ba_dev {
 #define BA_MF_CMAX(na) ((16 * BA_MF_RT(na)) / (na))
 #define BA_MF_GACC 1536    // doubles of LDS block accumulators per MFMA Schur group
 #define BA_MF_GE_CAP 24    // cameras per MFMA Schur group (LDS budget: 2 groups per CU)
+// long tracks (more observations than a chunk holds): segment chunks of
+// BA_CH_OBS observations, Schur tiles of BA_LONG_TILE x BA_LONG_TILE
+// observation pairs; caps (else the ordered kernels): views per track and
+// (obs, obs) terms of all long tracks (one 8 * NA^2-byte partial each)
+#define BA_LONG_TILE 32
+#define BA_LONG_OBS 65535
+#define BA_LONG_TERMS (1LL << 23)
 
 // ---- ba_kernels.hip ----
 int ba_launch_rotations(ba_dev *d, const double *a, double *rot, int all5);

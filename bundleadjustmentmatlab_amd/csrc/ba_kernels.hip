@@ -291,7 +291,8 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
     const double *__restrict__ a, const double *__restrict__ rot,
     const double *__restrict__ b, ba_flags f, const unsigned char *__restrict__ pivot,
     double *__restrict__ W, double *__restrict__ V, double *__restrict__ eB,
-    double *__restrict__ upart, double *__restrict__ part_sse)
+    double *__restrict__ upart, double *__restrict__ part_sse, int nch_reg,
+    const int *__restrict__ seg_pt, double *__restrict__ vseg)
 {
     constexpr int NC0 = (NA + 4) / 2;       // lane 0: base + FD columns [0, NC0)
     constexpr int RS = 2 * NA + 8;          // LDS row: A (2 NA), B (6), e (2)
@@ -303,7 +304,11 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
     __shared__ unsigned short eobl[BA_CH_OBS];
     __shared__ unsigned char wz[BA_CH_OBS]; // W_ij forced to zero (fix masks, :140-154)
     const int ch = blockIdx.x, tid = threadIdx.x;
-    const int p0 = ch_pt[ch], np = ch_pt[ch + 1] - p0;
+    // a segment chunk (ch >= nch_reg) holds part of one long track: its V / eB
+    // sums are partials (vseg), added up per track by k_long_vsum
+    const bool seg = ch >= nch_reg;
+    const int p0 = seg ? seg_pt[ch - nch_reg] : ch_pt[ch];
+    const int np = seg ? 1 : ch_pt[ch + 1] - p0;
     const int obase = ch_obase[ch], nobs = ch_obase[ch + 1] - obase;
     const int e0 = ch_eslot[ch], nes = ch_eslot[ch + 1] - e0;
     STAMP_DECL;
@@ -312,7 +317,7 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
     // camera loads instead of adding round trips (and a barrier) up front.
     const int u0 = eslot_optr[e0], nu = eslot_optr[e0 + nes] - u0;
     const int m_eoff = tid <= nes ? eslot_optr[e0 + tid] - u0 : 0;
-    const int m_lptr = tid <= np ? pt_ptr[p0 + tid] - obase : 0;
+    const int m_lptr = tid <= np ? (seg ? (tid ? nobs : 0) : pt_ptr[p0 + tid] - obase) : 0;
     const int m_eobl = tid < nu ? eslot_obs[u0 + tid] : 0;
     STAMP(16);
     double sse = 0.0;
@@ -390,7 +395,8 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
             }
         }
         if (f.fix_structure) acc = 0.0;
-        if (e < 9) V[9 * (size_t)i + e] = acc;
+        if (seg) vseg[12 * (size_t)(ch - nch_reg) + e] = acc;
+        else if (e < 9) V[9 * (size_t)i + e] = acc;
         else eB[3 * (size_t)i + e - 9] = acc;
     }
     STAMP(19);
@@ -1308,14 +1314,55 @@ __global__ __launch_bounds__(256) void k_point_update_chunk(
     const double *__restrict__ Vinv, const double *__restrict__ b,
     const double *__restrict__ a_new, const double *__restrict__ rot_new, int ndb,
     double lambda, double *__restrict__ db, double *__restrict__ b_new,
-    double *__restrict__ part_sse, double *__restrict__ part_dpg)
+    double *__restrict__ part_sse, double *__restrict__ part_dpg, int nch_reg,
+    const int *__restrict__ seg_pt, const int *__restrict__ seg_long,
+    const int *__restrict__ long_o0, const double *__restrict__ dpg_long)
 {
     __shared__ double ts[BA_CH_OBS * 3];
     __shared__ double bn[BA_CH_PTS * 3];
     __shared__ int lptr[BA_CH_PTS + 1];
     const int ch = blockIdx.x, tid = threadIdx.x;
-    const int p0 = ch_pt[ch], np = ch_pt[ch + 1] - p0;
+    // segment chunk of a long track: db / b_new come from k_long_db (the sum
+    // over all the track's observations); this chunk projects its part
+    const bool seg = ch >= nch_reg;
+    const int p0 = seg ? seg_pt[ch - nch_reg] : ch_pt[ch];
+    const int np = seg ? 1 : ch_pt[ch + 1] - p0;
     const int obase = ch_obase[ch], nobs = ch_obase[ch + 1] - obase;
+    if (seg) {
+        double dpg = 0.0;
+        if (tid < 3) bn[tid] = b_new[3 * (size_t)p0 + tid];
+        if (tid == 0) {
+            const int l = seg_long[ch - nch_reg];
+            if (obase == long_o0[l]) dpg = dpg_long[l];   // once per track
+        }
+        __syncthreads();
+        double sse = 0.0;
+        if (tid < nobs) {
+            const int o = obase + tid, j = obs_cam[o];
+            const double bl[3] = {bn[0], bn[1], bn[2]};
+            double an[NA], xh[2];
+#pragma unroll
+            for (int c = 0; c < NA; c++) an[c] = a_new[(size_t)NA * j + c];
+            if constexpr (NA == BA_PROJ_NA) {
+                vlg_project_proj(an, bl, xh);
+            } else {
+                double k4[4], Kc[9], R[9];
+#pragma unroll
+                for (int c = 0; c < 4; c++) k4[c] = K4[4 * (size_t)j + c];
+#pragma unroll
+                for (int q = 0; q < 9; q++) R[q] = rot_new[45 * (size_t)j + q];
+                vlg_calib(Kc, k4, an, NA - 6);
+                vlg_project(Kc, R, an + 3, bl, xh);
+            }
+            const double d0 = obs_x[2 * (size_t)o] - xh[0];
+            const double d1 = obs_x[2 * (size_t)o + 1] - xh[1];
+            sse = d0 * d0 + d1 * d1;
+        }
+        block_sum_to<256>(sse, part_sse + ch);
+        __syncthreads();
+        block_sum_to<256>(dpg, part_dpg + ch);
+        return;
+    }
     if (tid <= np) lptr[tid] = pt_ptr[p0 + tid] - obase;
     for (int q = tid; q < nobs * 3; q += 256) {
         const int lo = q / 3, r = q - 3 * lo, o = obase + lo;
@@ -1379,6 +1426,131 @@ __global__ __launch_bounds__(256) void k_point_update_chunk(
     block_sum_to<256>(sse, part_sse + ch);
     __syncthreads();
     block_sum_to<256>(dpg, part_dpg + ch);
+}
+
+// -------------------------------------------------------------------------
+// Long tracks (more observations than a chunk holds; points [p_long, n) of the
+// fast path).  Their observations are linearised by segment chunks of
+// k_linearize_chunk; here:
+//   k_long_vsum  : V_i, eB_i = the sum of the segments' partials (segment order)
+//   k_schur_long : per tile of BA_LONG_TILE^2 (obs a, obs b) pairs, a >= b, the
+//                  block term Y_a W_b^T (mex_bundle_2_Se_.c:80-118, one group
+//                  slot per pair) and, on the diagonal tile column, Y_a eB_i
+//                  (:132-155, one group e-slot per observation)
+//   k_long_db    : db_i = V*^-1 (eB_i - sum_o W_o^T da_j) over all the track's
+//                  observations (mex_bundle_3_db_new.c:99-134), b_new, dp'g
+// -------------------------------------------------------------------------
+__global__ void k_long_vsum(const int *__restrict__ long_pt, const int *__restrict__ long_seg0,
+                            const double *__restrict__ vseg, double *__restrict__ V,
+                            double *__restrict__ eB)
+{
+    const int l = blockIdx.x, e = threadIdx.x;
+    if (e >= 12) return;
+    const int i = long_pt[l];
+    double acc = 0.0;
+    for (int sg = long_seg0[l]; sg < long_seg0[l + 1]; sg++) acc += vseg[12 * (size_t)sg + e];
+    if (e < 9) V[9 * (size_t)i + e] = acc;
+    else eB[3 * (size_t)i + e - 9] = acc;
+}
+
+template <int NA>
+__global__ __launch_bounds__(256) void k_schur_long(
+    const int *__restrict__ tiles, const int *__restrict__ long_pt,
+    const int *__restrict__ long_o0, const int *__restrict__ long_sbase,
+    const int *__restrict__ long_ebase, const double *__restrict__ W,
+    const double *__restrict__ Vinv, const double *__restrict__ eB,
+    double *__restrict__ spart, double *__restrict__ epart)
+{
+    constexpr int WS = 3 * NA, TL = BA_LONG_TILE, NN = NA * NA;
+    __shared__ double Ya[TL * WS], Wb[TL * WS];
+    const int tid = threadIdx.x;
+    const int l = tiles[3 * blockIdx.x], ta = tiles[3 * blockIdx.x + 1],
+              tb = tiles[3 * blockIdx.x + 2];
+    const int i = long_pt[l], o0 = long_o0[l], k = long_o0[l + 1] - o0;
+    const int a0 = TL * ta, na_ = min(TL, k - a0), b0 = TL * tb, nb_ = min(TL, k - b0);
+    double vi[9], eb[3];
+#pragma unroll
+    for (int q = 0; q < 9; q++) vi[q] = Vinv[9 * (size_t)i + q];
+#pragma unroll
+    for (int q = 0; q < 3; q++) eb[q] = eB[3 * (size_t)i + q];
+    // Y_a = W_a V*^-1 (bundle_euclid.m:182; each entry summed left to right)
+    for (int q = tid; q < na_ * WS; q += 256) {
+        const int lo = q / WS, e = q - WS * lo, r = e % NA, c = e / NA;
+        const double *w = W + (size_t)WS * (o0 + a0 + lo);
+        Ya[q] = w[r] * vi[3 * c] + w[r + NA] * vi[1 + 3 * c] + w[r + 2 * NA] * vi[2 + 3 * c];
+    }
+    for (int q = tid; q < nb_ * WS; q += 256) Wb[q] = W[(size_t)WS * (o0 + b0) + q];
+    __syncthreads();
+    const long long sb = long_sbase[l];
+    for (int q = tid; q < na_ * nb_ * NN; q += 256) {
+        const int pr = q / NN, e = q - NN * pr, al = pr / nb_, bl = pr - nb_ * al;
+        const int a = a0 + al, b = b0 + bl;
+        if (a < b) continue;
+        const int r = e % NA, c = e / NA;
+        const double *y = Ya + WS * al, *w = Wb + WS * bl;
+        const long long slot = sb + (long long)a * (a + 1) / 2 + b;
+        spart[(size_t)NN * slot + e] = y[r] * w[c] + y[r + NA] * w[c + NA] + y[r + 2 * NA] * w[c + 2 * NA];
+    }
+    if (tb == 0) {
+        const long long eb0 = long_ebase[l];
+        for (int q = tid; q < na_ * NA; q += 256) {
+            const int al = q / NA, r = q - NA * al;
+            const double *y = Ya + WS * al;
+            epart[(size_t)NA * (eb0 + a0 + al) + r] =
+                y[r] * eb[0] + y[r + NA] * eb[1] + y[r + 2 * NA] * eb[2];
+        }
+    }
+}
+
+template <int NA>
+__global__ __launch_bounds__(256) void k_long_db(
+    const int *__restrict__ long_pt, const int *__restrict__ long_o0,
+    const int *__restrict__ obs_cam, const double *__restrict__ W,
+    const double *__restrict__ da, const double *__restrict__ eB,
+    const double *__restrict__ Vinv, const double *__restrict__ b, int ndb, double lambda,
+    double *__restrict__ db, double *__restrict__ b_new, double *__restrict__ dpg_long)
+{
+    __shared__ double red[3][256];
+    const int l = blockIdx.x, tid = threadIdx.x;
+    const int i = long_pt[l], o0 = long_o0[l], o1 = long_o0[l + 1];
+    double t[3] = {0.0, 0.0, 0.0};
+    for (int o = o0 + tid; o < o1; o += 256) {
+        const double *d = da + (size_t)NA * obs_cam[o];
+        double dl[NA];
+#pragma unroll
+        for (int kk = 0; kk < NA; kk++) dl[kk] = kk < ndb ? d[kk] : 0.0;
+#pragma unroll
+        for (int r = 0; r < 3; r++) {   // the expression of k_point_update_chunk
+            const double *w = W + (size_t)3 * NA * o + NA * r;
+            double v = w[0] * dl[0] + w[1] * dl[1] + w[2] * dl[2] + w[3] * dl[3] + w[4] * dl[4] +
+                       w[5] * dl[5];
+#pragma unroll
+            for (int kk = 6; kk < NA; kk++)
+                if (kk < ndb) v = v + w[kk] * dl[kk];
+            t[r] += v;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 3; r++) red[r][tid] = t[r];
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {   // fixed-order tree: deterministic
+        if (tid < h)
+            for (int r = 0; r < 3; r++) red[r][tid] += red[r][tid + h];
+        __syncthreads();
+    }
+    if (tid == 0) {
+        const double rhs[3] = {eB[3 * (size_t)i] - red[0][0], eB[3 * (size_t)i + 1] - red[1][0],
+                               eB[3 * (size_t)i + 2] - red[2][0]};
+        const double *vi = Vinv + 9 * (size_t)i;
+        double dpg = 0.0;
+        for (int r = 0; r < 3; r++) {
+            const double dbr = vi[r] * rhs[0] + vi[r + 3] * rhs[1] + vi[r + 6] * rhs[2];
+            db[3 * (size_t)i + r] = dbr;
+            b_new[3 * (size_t)i + r] = b[3 * (size_t)i + r] + dbr;
+            dpg += dbr * (lambda * dbr + eB[3 * (size_t)i + r]);
+        }
+        dpg_long[l] = dpg;
+    }
 }
 
 // three fixed-order sums in one launch (block b: part[b] over n[b] -> out[b])
@@ -1483,7 +1655,10 @@ int ba_launch_linearize(ba_dev *d, ba_flags f)
                                    d->ch_pt, d->ch_obase, d->ch_eslot, d->eslot_optr,
                                    d->eslot_obs, d->pt_ptr, d->obs_cam, d->obs_lpt, d->obs_x,
                                    d->K4, d->a, d->rot, d->b, f, d->pivot, d->W, d->V, d->eB,
-                                   d->upart, d->chsse)));
+                                   d->upart, d->chsse, d->nch_reg, d->seg_pt, d->vseg)));
+        if (d->nl > 0)   // long tracks: V / eB = sum of their segments' partials
+            k_long_vsum<<<d->nl, 64, 0, d->stream>>>(d->long_pt, d->long_seg0, d->vseg, d->V,
+                                                     d->eB);
         KT_E(d, KT_LIN);   // the SSE partials are summed by ba_launch_camera_reduce
         return -(int)hipGetLastError();
     }
@@ -1570,6 +1745,17 @@ static int launch_schur_fast(ba_dev *d, double lambda)
             d->Vinv, d->spart, d->epart);
         KT_E(d, KT_SCHUR_CHUNK);
     }
+    if (d->nl > 0) {   // long tracks: their V*^-1, then their (obs, obs) tiles
+        KT_B(d);
+        if (d->ngrp_mf == 0)   // (k_point_vinv above covered every point)
+            k_point_vinv<NA><<<(d->n - d->p_long + 255) / 256, 256, 0, d->stream>>>(
+                d->V + 9 * (size_t)d->p_long, d->n - d->p_long, lambda,
+                d->Vinv + 9 * (size_t)d->p_long);
+        k_schur_long<NA><<<d->ntile_long, 256, 0, d->stream>>>(
+            d->long_tiles, d->long_pt, d->long_o0, d->long_sbase, d->long_ebase, d->W, d->Vinv,
+            d->eB, d->spart, d->epart);
+        KT_E(d, KT_SCHUR_CHUNK);
+    }
     const int bs = ((NA * NA + NA) + 63) / 64 * 64;
     if (d->join_pending) {   // U / eA from the side stream's camera reduction
         VLGBA_CHECK(hipStreamWaitEvent(d->stream, d->ev_join, 0));
@@ -1641,11 +1827,17 @@ int ba_launch_update(ba_dev *d, double lambda)
     KT_E(d, KT_CAMUPD);
     if (!d->ordered && d->nch > 0 && !d->obs_vis && !d->xh_out) {
         KT_B(d);
+        if (d->nl > 0)   // long tracks: db, b_new, dp'g over all their observations
+            BA_DISPATCH(d->na, (k_long_db<NA><<<d->nl, 256, 0, d->stream>>>(
+                                   d->long_pt, d->long_o0, d->obs_cam, d->W, d->da, d->eB,
+                                   d->Vinv, d->b, d->ndb, lambda, d->db, d->b_new,
+                                   d->dpg_long)));
         BA_DISPATCH(d->na, (k_point_update_chunk<NA><<<d->nch, 256, 0, d->stream>>>(
                                d->ch_pt, d->ch_obase, d->pt_ptr, d->obs_cam, d->obs_lpt,
                                d->obs_x, d->K4, d->W, d->da, d->eB, d->Vinv, d->b, d->a_new,
                                d->rot_new, d->ndb, lambda, d->db, d->b_new, d->chsse + d->nch,
-                               d->chsse + 2 * (size_t)d->nch)));
+                               d->chsse + 2 * (size_t)d->nch, d->nch_reg, d->seg_pt,
+                               d->seg_long, d->long_o0, d->dpg_long)));
         KT_E(d, KT_PTUPD);
         // new SSE, point dpg, camera dpg: one launch
         ba_sum3 s3 = {{d->chsse + d->nch, d->chsse + 2 * (size_t)d->nch, d->part},

@@ -297,6 +297,15 @@ struct host_plan {
     int grp_max_s = 0, grp_max_e = 0;             // largest accumulated term group
     int mf_max_s = 0, mf_max_e = 0;               // largest MFMA group
     int nch_mf = 0, ngrp_mf = 0;                  // leading MFMA chunks / groups
+    // long tracks (points [p_long, n)): each split into segment chunks of <=
+    // BA_CH_OBS observations (after the regular chunks: chunk ids
+    // [nch_reg, nch_reg + nseg)); their Schur terms are group slots of their
+    // own, one per (obs, obs) pair, and one group e-slot per observation
+    int nch_reg = 0, nseg = 0;
+    std::vector<int> seg_pt, seg_long;            // [nseg] point / long index
+    std::vector<int> long_pt, long_o0, long_seg0; // [nl], [nl+1], [nl+1]
+    std::vector<int> long_sbase, long_ebase;      // [nl] first group slot / e-slot
+    std::vector<int> long_tiles;                  // [ntile][3] (long, a tile, b tile)
     // per chunk one contiguous metadata record (one coalesced prefetch):
     //   [np | nobs << 16][ns | nes << 16][nterm][neobs] soff[ns+1] eoff[nes+1]
     //   sgl[ns] egl[nes] lpt[nobs] term[nterm] (y | w << 16) eobl[neobs]
@@ -323,9 +332,10 @@ static void bucket(const std::vector<int> &key, int nkey, std::vector<int> &ptr,
 // 16 * BA_MF_RT(na) rows); their metadata records are the dense-layout ones
 // described at build of P.blob below.
 bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<int> &lcam,
-                const host_blocks &hb, host_plan &P, int cmax, int p_split)
+                const host_blocks &hb, host_plan &P, int cmax, int p_split, int p_long)
 {
-    const int n = (int)lptr.size() - 1;
+    const int n_all = (int)lptr.size() - 1;
+    const int n = p_long;   // regular chunks cover points [0, p_long)
     const int nb = (int)hb.jk.size() / 2;
     if (cmax <= 0) p_split = 0;
     auto pt_terms = [&](int i) {
@@ -444,6 +454,29 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
         if (mf) P.nch_mf++;
         p = q;
     }
+    // long tracks: segment chunks (one point each, <= BA_CH_OBS observations;
+    // every observation its own camera slot: a point sees a camera once)
+    P.nch_reg = (int)P.ch_pt.size() - 1;
+    P.long_o0.assign(1, lptr[p_long]);
+    P.long_seg0.assign(1, 0);
+    for (int i = p_long; i < n_all; i++) {
+        const int l = (int)P.long_pt.size();
+        P.long_pt.push_back(i);
+        for (int o = lptr[i]; o < lptr[i + 1]; o += BA_CH_OBS) {
+            const int o1 = std::min(o + BA_CH_OBS, lptr[i + 1]);
+            for (int a = o; a < o1; a++) {
+                P.eslot_obs.push_back((unsigned short)(a - o));
+                P.eslot_optr.push_back((int)P.eslot_obs.size());
+                P.cam_eslots.push_back(lcam[a]);
+            }
+            P.ch_eslot.push_back((int)P.eslot_optr.size() - 1);
+            P.seg_pt.push_back(i);
+            P.seg_long.push_back(l);
+            P.nseg++;
+        }
+        P.long_o0.push_back(lptr[i + 1]);
+        P.long_seg0.push_back(P.nseg);
+    }
     // per block: its slots in chunk order (counting sort keeps slot order)
     const int ns = (int)P.slot_blk.size();
     P.blk_sptr.assign(nb + 1, 0);
@@ -533,6 +566,26 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
         P.grp_gs.push_back((int)P.gslot_blk.size());
         P.grp_ge.push_back((int)P.gecam.size());
         c = d;
+    }
+    // long tracks' Schur terms: one group slot per (a, b), a >= b (cameras
+    // ascending, so block (cam a, cam b) is a lower block), slot a(a+1)/2 + b
+    // of the point; one group e-slot per observation.  After the regular
+    // slots: k_schur_reduce subtracts them last.
+    for (size_t l = 0; l < P.long_pt.size(); l++) {
+        const int o0 = P.long_o0[l], k = P.long_o0[l + 1] - o0;
+        P.long_sbase.push_back((int)P.gslot_blk.size());
+        P.long_ebase.push_back((int)P.gecam.size());
+        for (int a = 0; a < k; a++) {
+            P.gecam.push_back(lcam[o0 + a]);
+            for (int b = 0; b <= a; b++) P.gslot_blk.push_back(hb.find(lcam[o0 + a], lcam[o0 + b]));
+        }
+        const int nt = (k + BA_LONG_TILE - 1) / BA_LONG_TILE;
+        for (int ta = 0; ta < nt; ta++)
+            for (int tb = 0; tb <= ta; tb++) {
+                P.long_tiles.push_back((int)l);
+                P.long_tiles.push_back(ta);
+                P.long_tiles.push_back(tb);
+            }
     }
     bucket(P.gslot_blk, nb, P.blk_gptr, P.blk_gslots);
     bucket(P.gecam, m, P.cam_gptr, P.cam_gslots);
@@ -644,6 +697,11 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
         P.ch_obase.push_back(lptr[p1]);
         P.max_blob = std::max(P.max_blob, P.ch_blob[c + 1] - P.ch_blob[c]);
     }
+    for (size_t l = 0; l < P.long_pt.size(); l++)   // segment chunks: no Schur record
+        for (int o = P.long_o0[l]; o < P.long_o0[l + 1]; o += BA_CH_OBS) {
+            P.ch_blob.push_back(P.ch_blob.back());
+            P.ch_obase.push_back(std::min(o + BA_CH_OBS, P.long_o0[l + 1]));
+        }
     return true;
 }
 
@@ -827,28 +885,43 @@ struct setup_trace {
 static thread_local setup_trace *g_st = nullptr;
 #define ST_MARK(w) do { if (g_st) g_st->mark(w); } while (0)
 
-// Fast-path point order: when some but not all tracks fit the MFMA Schur
-// chunks (<= BA_MF_CMAX(na) observations) and every track fits a chunk at all,
-// put the short-track points first (stable), so that the MFMA chunks are runs
-// of consecutive short tracks and the per-term chunks hold the rest.  The
+// Fast-path point order by track kind (stable within a kind): short tracks
+// (<= BA_MF_CMAX(na) views: MFMA Schur chunks) first, then tracks that fit a
+// per-term chunk, then long tracks (split into chunk-sized segments with the
+// dedicated long-track kernels), so that every kind is one contiguous range.
+// Applied when more than one kind is present and no track exceeds the
+// long-track caps (else the ordered kernels take the problem).  The
 // summation order of the fast path changes with it (it is not the parity
 // path); set / get_params and the getters map back to the input order.
-static void order_points_by_kind(int na, host_obs &h, std::vector<int> &pt_ptr,
+static int track_kind(long long k, int cmax)
+{
+    if (k <= cmax) return 0;                                      // MFMA Schur chunk
+    if (k <= BA_CH_OBS && k * (k + 1) / 2 <= BA_CH_TERMS) return 1;   // per-term chunk
+    return 2;                                                     // long track
+}
+
+static void order_points_by_kind(int cmax, host_obs &h, std::vector<int> &pt_ptr,
                                  std::vector<int> &pperm, std::vector<int> &operm)
 {
-    const int n = (int)pt_ptr.size() - 1, cmax = BA_MF_CMAX(na);
-    int nshort = 0;
+    const int n = (int)pt_ptr.size() - 1;
+    int cnt[3] = {0, 0, 0};
+    long long lterms = 0;
     for (int i = 0; i < n; i++) {
         const long long k = pt_ptr[i + 1] - pt_ptr[i];
-        if (k > BA_CH_OBS || k * (k + 1) / 2 > BA_CH_TERMS) return;   // ordered kernels
-        nshort += k <= cmax;
+        const int kind = track_kind(k, cmax);
+        cnt[kind]++;
+        if (kind == 2) {
+            if (k > BA_LONG_OBS) return;                          // ordered kernels
+            lterms += k * (k + 1) / 2;
+        }
     }
-    if (nshort == 0 || nshort == n) return;
+    if (lterms > BA_LONG_TERMS) return;
+    if ((cnt[0] == 0) + (cnt[1] == 0) + (cnt[2] == 0) >= 2) return;   // one kind: as is
     pperm.clear();
     pperm.reserve(n);
-    for (int pass = 0; pass < 2; pass++)
+    for (int pass = 0; pass < 3; pass++)
         for (int i = 0; i < n; i++)
-            if ((pt_ptr[i + 1] - pt_ptr[i] <= cmax) == (pass == 0)) pperm.push_back(i);
+            if (track_kind(pt_ptr[i + 1] - pt_ptr[i], cmax) == pass) pperm.push_back(i);
     host_obs h2;
     const size_t N = h.pt.size();
     h2.pt.resize(N);
@@ -909,9 +982,21 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         for (int o = 0; o < d.N; o++) cobs[pos[lcam[o]]++] = o;
     }
     bool fast = !d.ordered && !stage_mode;
-    for (int i = 0; fast && i < d.n; i++) {   // very long track: sequential kernels
-        const long long k = lptr[i + 1] - lptr[i];
-        if (k > BA_CH_OBS || k * (k + 1) / 2 > BA_CH_TERMS) fast = false;
+    // long tracks (more than a chunk holds) must form the tail [p_long, n) of
+    // the local points (order_points_by_kind) and stay within the caps; else
+    // the sequential kernels take the problem
+    int p_long = d.n;
+    if (fast) {
+        while (p_long > 0 && track_kind(lptr[p_long] - lptr[p_long - 1], BA_MF_CMAX(na)) == 2)
+            p_long--;
+        long long lterms = 0;
+        for (int i = 0; fast && i < d.n; i++) {
+            const long long k = lptr[i + 1] - lptr[i];
+            const bool lng = track_kind(k, BA_MF_CMAX(na)) == 2;
+            if (lng != (i >= p_long) || k > BA_LONG_OBS) fast = false;
+            if (lng) lterms += k * (k + 1) / 2;
+        }
+        if (lterms > BA_LONG_TERMS) fast = false;
     }
     host_blocks hb;
     host_plan plan;
@@ -925,8 +1010,9 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
     if (fast) {
         int p_split = 0;
         if (!d.no_mfma)
-            while (p_split < d.n && lptr[p_split + 1] - lptr[p_split] <= BA_MF_CMAX(na)) p_split++;
-        if (build_plan(p->m, na, lptr, lcam, hb, plan, BA_MF_CMAX(na), p_split)) {
+            while (p_split < p_long && lptr[p_split + 1] - lptr[p_split] <= BA_MF_CMAX(na))
+                p_split++;
+        if (build_plan(p->m, na, lptr, lcam, hb, plan, BA_MF_CMAX(na), p_split, p_long)) {
             d.mfma = plan.nch_mf > 0;
         } else {
             fast = false;
@@ -961,7 +1047,31 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         TRY(ctx_alloc(c, &d.Y, (size_t)3 * na * d.N));
         TRY(ctx_alloc(c, &d.t, (size_t)na * d.N));
     } else {
-        d.nch = (int)plan.ch_pt.size() - 1;
+        d.nch_reg = plan.nch_reg;
+        d.nch = plan.nch_reg + plan.nseg;
+        d.nl = (int)plan.long_pt.size();
+        d.ntile_long = (int)plan.long_tiles.size() / 3;
+        d.p_long = p_long;
+        if (d.nl > 0) {
+            TRY(ctx_alloc(c, &d.seg_pt, plan.seg_pt.size()));
+            TRY(ctx_alloc(c, &d.seg_long, plan.seg_long.size()));
+            TRY(ctx_alloc(c, &d.long_pt, plan.long_pt.size()));
+            TRY(ctx_alloc(c, &d.long_o0, plan.long_o0.size()));
+            TRY(ctx_alloc(c, &d.long_seg0, plan.long_seg0.size()));
+            TRY(ctx_alloc(c, &d.long_sbase, plan.long_sbase.size()));
+            TRY(ctx_alloc(c, &d.long_ebase, plan.long_ebase.size()));
+            TRY(ctx_alloc(c, &d.long_tiles, plan.long_tiles.size()));
+            TRY(ctx_alloc(c, &d.vseg, 12 * (size_t)plan.nseg));
+            TRY(ctx_alloc(c, &d.dpg_long, (size_t)d.nl));
+            TRY(upload(d.seg_pt, plan.seg_pt.data(), plan.seg_pt.size(), s));
+            TRY(upload(d.seg_long, plan.seg_long.data(), plan.seg_long.size(), s));
+            TRY(upload(d.long_pt, plan.long_pt.data(), plan.long_pt.size(), s));
+            TRY(upload(d.long_o0, plan.long_o0.data(), plan.long_o0.size(), s));
+            TRY(upload(d.long_seg0, plan.long_seg0.data(), plan.long_seg0.size(), s));
+            TRY(upload(d.long_sbase, plan.long_sbase.data(), plan.long_sbase.size(), s));
+            TRY(upload(d.long_ebase, plan.long_ebase.data(), plan.long_ebase.size(), s));
+            TRY(upload(d.long_tiles, plan.long_tiles.data(), plan.long_tiles.size(), s));
+        }
         d.ns = (int)plan.slot_blk.size();
         d.nes = (int)plan.eslot_optr.size() - 1;
         d.ch_max_terms = plan.max_terms;
@@ -1123,8 +1233,9 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
         std::vector<int> pt_ptr_all(p->n + 1, 0);
         for (size_t q = 0; q < h.pt.size(); q++) pt_ptr_all[h.pt[q] + 1]++;
         for (int i = 0; i < p->n; i++) pt_ptr_all[i + 1] += pt_ptr_all[i];
-        if (o->ordered == 0 && !stage_mode && o->schur_kernel != 1 && o->world_size <= 1)
-            order_points_by_kind(p->num_a, h, pt_ptr_all, c->pperm, c->operm);
+        if (o->ordered == 0 && !stage_mode && o->world_size <= 1)
+            order_points_by_kind(o->schur_kernel == 1 ? 0 : BA_MF_CMAX(p->num_a), h, pt_ptr_all,
+                                 c->pperm, c->operm);
         ST_MARK("order");
         c->world = o->world_size > 1 ? o->world_size : 1;
         c->rank = c->world > 1 ? o->rank : 0;
@@ -1730,7 +1841,7 @@ int vlgba_plan_info(vlgba_ctx *c, long long *info, int len)
                                       d.cr_nlev, ne, nk,    d.ordered,    d.ordered ? d.T : d.nterm_fast,
                                       d.blob_words, d.mfma,
                                       d.cr_nlev ? (d.cr32 ? d.tb32 : 64) : 0,
-                                      d.ngrp_mf, c->pperm.empty() ? 0 : 1};
+                                      d.ngrp_mf, c->pperm.empty() ? 0 : 1, d.nl};
     for (int k = 0; k < len && k < VLGBA_NPLAN; k++) info[k] = v[k];
     return VLGBA_NPLAN;
 }

@@ -215,14 +215,18 @@ def banded_scene(m=50, n=10_000, track=6, depth=(80.0, 120.0), noise=0.5, seed=2
 
 
 def ladybug_scene(m=1000, n=200_000, mean_extra=3.0, max_track=60, loop=0.05,
-                  radius=300.0, depth=(80.0, 120.0), noise=0.5, seed=6):
+                  radius=300.0, depth=(80.0, 120.0), noise=0.5, seed=6, long_frac=0.0,
+                  long_len=(100, 200)):
     """A BAL-"ladybug"-like scene (the plan cliffs): cameras drive
     (1 + loop) times round a circle of ``radius`` looking at its centre, so
     the last ``loop`` fraction of the frames revisits the first; every point is
     tracked by 2 + Geometric(1 / (1 + mean_extra)) consecutive cameras (capped
     at ``max_track``: long tracks beside short ones), and a point created in
     the first ``loop`` part is seen again, by 1-3 consecutive cameras, one
-    revolution later (loop-closure observations: S is no longer banded)."""
+    revolution later (loop-closure observations: S is no longer banded).
+    ``long_frac`` of the points are landmarks near the circle's centre (depth
+    ~ radius) tracked by U(long_len) consecutive cameras: tracks longer than a
+    Schur chunk holds."""
     rng = np.random.default_rng(seed)
     width = height = 500.0
     f, cx, cy = width, width / 2, height / 2
@@ -254,9 +258,14 @@ def ladybug_scene(m=1000, n=200_000, mean_extra=3.0, max_track=60, loop=0.05,
     T = -np.einsum("kij,jk->ik", R, C)                     # T = -R C
     start = np.sort(rng.integers(0, m - 1, size=n))
     L = 2 + rng.geometric(1.0 / (1.0 + mean_extra), size=n) - 1
-    L = np.minimum(np.minimum(L, max_track), m - start)
+    L = np.minimum(L, max_track)
     uv = rng.random((n, 2)) * np.array([width, height])
     d = rng.uniform(depth[0], depth[1], size=n)
+    if long_frac > 0:
+        lm = rng.random(n) < long_frac
+        L = np.where(lm, rng.integers(long_len[0], long_len[1] + 1, size=n), L)
+        d = np.where(lm, rng.uniform(0.9 * radius, 1.05 * radius, size=n), d)
+    L = np.minimum(L, m - start)
     ray = np.stack([(uv[:, 0] - cx) / f, (uv[:, 1] - cy) / f, np.ones(n)], 1) * d[:, None]
     Xw = np.einsum("kji,kj->ki", R[start], ray - T[:, start].T)
     X = np.vstack([Xw.T, np.ones((1, n))])

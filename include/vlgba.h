@@ -206,8 +206,10 @@ const char *vlgba_kernel_name(int k);
  * NA) for the camera-aligned tiles; 0 without cyclic reduction) [20] MFMA
  * Schur groups (the leading ones; the rest use per-term sums) [21] points
  * reordered internally (1: short tracks first, input order restored at the
- * API).  Writes min(len, VLGBA_NPLAN) entries, returns VLGBA_NPLAN. */
-#define VLGBA_NPLAN 22
+ * API) [22] long tracks (more views than a Schur chunk holds: segment chunks
+ * + the long-track kernels).  Writes min(len, VLGBA_NPLAN) entries, returns
+ * VLGBA_NPLAN. */
+#define VLGBA_NPLAN 23
 int vlgba_plan_info(vlgba_ctx *ctx, long long *info, int len);
 
 /* ---- stage entries with the reference MEX argument layouts ---------------

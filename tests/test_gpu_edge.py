@@ -6,8 +6,8 @@ code path (bundle_euclid.m + mex_bundle_1/2/3):
   zero rows and the pinv rule of App. A Q2/Q8 applies);
 * a point that no camera sees (V = 0 -> pinv3(0) = 0, db = 0) and points seen
   by a single camera;
-* a track longer than the chunk caps (falls back to the ordered kernels) and
-  tracks longer than the MFMA Schur camera cap (the per-term Schur kernel);
+* a track longer than the chunk caps (the long-track kernels) and tracks
+  longer than the MFMA Schur camera cap (the per-term Schur kernel);
 * the smallest problem (two cameras, one point).
 
 Tolerances as tests/test_gpu_parity.py::test_single_pass_config2: the
@@ -82,8 +82,9 @@ def test_unseen_and_single_view_points(gpu, oracle):
 
 
 def test_track_longer_than_chunk_cap(gpu, oracle):
-    """One point seen by all 140 cameras (> 128 observations in one chunk): the
-    plan falls back to the ordered kernels; result unchanged."""
+    """One point seen by all 140 cameras (> 128 observations in one chunk): it
+    runs as a long track (segment chunks + the long-track kernels, the rest of
+    the plan unchanged: no fallback to the ordered kernels); result unchanged."""
     sc = _scene(140, 2000, seed=5)
     a, b = _params(sc)
     # point 0 observed in every camera: project it with the true cameras
@@ -98,7 +99,7 @@ def test_track_longer_than_chunk_cap(gpu, oracle):
     order = np.lexsort((cam, pt))
     pt, cam, ox = pt[order], cam[order], ox[order]
     plan, _ = _pass_vs_oracle(gpu, oracle, sc.m, sc.n, pt, cam, ox, sc.K, a, b)
-    assert plan["ordered"] == 1
+    assert plan["ordered"] == 0 and plan["long_points"] == 1 and plan["reordered"] == 1
 
 
 def test_tracks_longer_than_mfma_cap(gpu, oracle):

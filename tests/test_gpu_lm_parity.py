@@ -235,3 +235,23 @@ def test_per_pass_json_log_matches_oracle_trace(gpu, oracle, tmp_path):
                       parity=True, log=str(path))
     lines = [json.loads(s) for s in path.read_text().splitlines()]
     assert lines == recs
+
+
+def test_converged_cost_with_long_tracks(gpu, oracle):
+    """Tracks longer than a Schur chunk (the segment-chunk / long-track kernels)
+    in a whole LM solve: the fast GPU path and the reference's MATLAB semantics
+    reach final costs within 1e-6 relative under the tightened stop rule."""
+    from bundleadjustmentmatlab_amd.scene import make_config
+    sc = make_config("ladybug", m=150, n=1500, max_track=20, radius=120.0, seed=31,
+                     long_frac=0.02, long_len=(100, 145))
+    L = np.bincount(sc.obs_pt, minlength=sc.n)
+    assert (L * (L + 1) // 2 > 4096).sum() > 3      # long tracks (more than 90 views)
+    x, vis = sc.dense()
+    kw = dict(stop_rel=1e-9, max_iter=100, max_iter2=30)
+    got = gpu.bundle_euclid(sc.K, sc.T0, sc.w0, sc.X0, x, "visibility", vis, "fix_calibration",
+                            **kw)
+    ref = oracle.bundle_euclid_ref(sc.K, sc.T0, sc.w0, sc.X0, x, "visibility", vis,
+                                   "fix_calibration", form="sparse", vinv="pinv", solve="pinv",
+                                   **kw)
+    e_g, e_r = got[4][-1], ref[4][-1]
+    assert abs(e_g - e_r) <= 1e-6 * e_r, (got[4], ref[4])

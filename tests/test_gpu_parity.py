@@ -501,3 +501,54 @@ def test_mixed_mfma_and_term_chunks(gpu, oracle, num_a):
     lin = res["mixed"][5]
     assert np.array_equal(lin["W"].reshape(3 * num_a, -1, order="F").T, ref["W"])
     assert np.array_equal(lin["V"], ref["V"]) and np.array_equal(lin["eB"], ref["eB"])
+
+
+@pytest.mark.parametrize("kern", ["auto", "terms"])
+def test_long_tracks_fast_path(gpu, oracle, kern):
+    """Tracks longer than a Schur chunk holds (here 100-216 views, > 128 and
+    > 90) no longer switch the whole problem to the ordered kernels: they are
+    split into segment chunks (segmented V / eB sums), their (obs, obs) terms
+    run in the long-track tiles and their db over all their observations.  One
+    pass matches the ordered kernels to summation-order rounding; V / eB of
+    the long tracks to 1e-13 (segment sums), W and the rest bit-exact."""
+    from bundleadjustmentmatlab_amd.scene import make_config
+    sc = make_config("ladybug", m=300, n=5000, max_track=30, radius=150.0, seed=29,
+                     long_frac=0.01, long_len=(100, 220))
+    L = np.bincount(sc.obs_pt, minlength=sc.n)
+    assert (L > 128).sum() > 10
+    num_a = 6
+    a = np.zeros((num_a, sc.m), order="F")
+    a[0:3], a[3:6] = sc.w0, sc.T0
+    b = np.asfortranarray(sc.X0[:3])
+    res = {}
+    for name, kw in (("ordered", dict(ordered=True)), ("fast", dict(schur_kernel=kern))):
+        ba = gpu.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, num_a, **kw)
+        ba.set_params(a, b)
+        lin = ba.linearization()
+        i1 = ba.step(relinearize=True, update_lm=False)
+        db1 = ba.last_step()[1]
+        # the same linearisation again (no relinearisation: the long tracks'
+        # V sums, V*^-1 and tiles from the kept stage-1 outputs)
+        i2 = ba.step(relinearize=False, update_lm=False)
+        res[name] = (i1, i2, ba.plan_info(), db1, ba.last_step()[1], lin)
+        ba.close()
+    pl = res["fast"][2]
+    assert pl["ordered"] == 0 and pl["long_points"] == (L > 128).sum() + ((L <= 128) & (L * (L + 1) // 2 > 4096)).sum()
+    o, f = res["ordered"], res["fast"]
+    for io, jf in ((o[0], f[0]), (o[1], f[1])):
+        assert abs(io.old_sse - jf.old_sse) <= 1e-12 * io.old_sse
+        assert abs(io.new_sse - jf.new_sse) <= 1e-8 * io.new_sse, (io.new_sse, jf.new_sse)
+        assert abs(io.dpg - jf.dpg) <= 1e-8 * abs(io.dpg), (io.dpg, jf.dpg)
+        assert io.accepted == jf.accepted
+    # (a second relinearised pass would differ at the FD noise floor, ~1e-6:
+    # the Jacobians at points one rounding apart; DESIGN.md sec. 3)
+    for q in (3, 4):
+        assert np.max(np.abs(f[q] - o[q])) <= 1e-8 * np.max(np.abs(o[q]))
+    pb = oracle.SparseProblem(sc.m, sc.n, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.K)
+    ref = oracle.sp_linearize(pb, a, b, num_a)
+    lin = f[5]
+    assert np.array_equal(lin["W"].reshape(3 * num_a, -1, order="F").T, ref["W"])
+    for nm in ("V", "eB"):
+        assert np.allclose(lin[nm], ref[nm], rtol=1e-13, atol=1e-13 * np.abs(ref[nm]).max()), nm
+    for nm in ("U", "eA"):
+        assert np.max(np.abs(lin[nm] - ref[nm])) <= 1e-13 * np.max(np.abs(ref[nm])), nm

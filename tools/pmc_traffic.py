@@ -6,7 +6,11 @@ FETCH_SIZE counts half of the bytes of wide coalesced streaming reads, so
 it is doubled; WRITE_SIZE is taken as is.  Kernels are keyed by their base
 name (template arguments and signature dropped).
 
-usage: tools/pmc_traffic.py FETCH_DIR WRITE_DIR [--config cfg3] > profiles/...json
+With --valu DIR (a pass that collected SQ_INSTS_VALU) each kernel also gets
+its VALU wave-instructions per dispatch ("valu_winst"), for the VALU-issue roof
+bench.py reports beside the HBM one.
+
+usage: tools/pmc_traffic.py FETCH_DIR WRITE_DIR [--valu DIR] [--config cfg3] > profiles/...json
 """
 import csv
 import glob
@@ -34,10 +38,14 @@ def main():
     cfg = sys.argv[sys.argv.index("--config") + 1] if "--config" in sys.argv else "cfg3"
     fetch = per_dispatch(fdir, "FETCH_SIZE")
     write = per_dispatch(wdir, "WRITE_SIZE")
+    valu = per_dispatch(sys.argv[sys.argv.index("--valu") + 1], "SQ_INSTS_VALU") \
+        if "--valu" in sys.argv else {}
     out = {}
     for k in sorted(set(fetch) | set(write)):
         f, w = fetch.get(k, 0.0), write.get(k, 0.0)
         out[k] = {"fetch_kb": f, "write_kb": w, "bytes": (2.0 * f + w) * 1024.0}
+        if k in valu:
+            out[k]["valu_winst"] = valu[k]
     json.dump({"config": cfg, "correction": "bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024",
                "kernels": out}, sys.stdout, indent=1, sort_keys=True)
     print()
