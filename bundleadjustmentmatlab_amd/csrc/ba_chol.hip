@@ -13,12 +13,14 @@
 // below visits only tiles inside the envelope, which is exact (the skipped
 // tiles are zero and stay zero).  dense_solve = 1 visits every lower tile.
 //
-// Per tile column k (two launches):
-//   k_factor_panel : WG 0 factors L_kk in registers (one wave), forms
-//                    L_kk^-1 and y_k = L_kk^-1 r_k (forward solve folded in);
-//                    WG b >= 1 redoes that factorisation in LDS and computes
-//                    panel tile L_ik = A_ik L_kk^-T (MFMA), r_i -= L_ik y_k
-//   k_syrk         : A_ij -= L_ik L_jk^T for envelope pairs k < j <= i (MFMA)
+// Per tile column k (one launch, k_factor_step):
+//   WG 0     : applies column k-1's update to A_kk, factors L_kk, forms
+//              L_kk^-1 and y_k = L_kk^-1 r_k (forward solve folded in);
+//   WG b > 0 : applies column k-1's update to A_ik, redoes A_kk's update and
+//              factorisation in LDS and forms the panel tile L_ik = A_ik L_kk^-T
+//              (MFMA), r_i -= L_ik y_k;
+//   the rest : column k-1's trailing update A_ij -= L_i,k-1 L_j,k-1^T of the
+//              envelope pairs below row k (MFMA)
 // then per k descending k_backward: x_k = L_kk^-T z_k, z_j -= L_kj^T x_k.
 #include "ba_internal.h"
 
@@ -440,28 +442,93 @@ __device__ __forceinline__ bool block_potrf_inv(double *As, double *Li, bool zer
 }
 
 // ---------------------------------------------------------------------------
-// factor + panel for tile column k.  blockIdx 0: diagonal; b >= 1: panel tile
-// pan[b-1].
+// One tile column k of the envelope Cholesky, with the trailing update of
+// column k-1 folded in (one launch per column instead of two):
+//   blockIdx 0        : A_kk -= L_{k,k-1} L_{k,k-1}^T (if column k-1 reaches
+//                       row k), factor it, L_kk^-1, y_k = L_kk^-1 r_k
+//   1 .. T            : panel tile i = pan[b-1]: A_ik -= L_{i,k-1} L_{k,k-1}^T,
+//                       the same update + factorisation of A_kk in LDS
+//                       (bit-identical), L_ik = A_ik L_kk^-T, r_i -= L_ik y_k
+//   T+1 ..            : the rest of column k-1's trailing update,
+//                       A_ij -= L_{i,k-1} L_{j,k-1}^T for envelope pairs of
+//                       column k-1 with k < j <= i
+// Every tile receives the same operations in the same order as the two-launch
+// schedule (acc formed from zero, then A + (-1) acc): bit-identical results.
+// pan / prev: the envelope rows below k / below k-1 (ascending), T / Tp their
+// counts (Tp = 0 for k = 0).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_factor_panel(double *__restrict__ S, long long lds,
-                                                      int k, const int *__restrict__ pan,
-                                                      double *__restrict__ linv,
-                                                      double *__restrict__ rhs,
-                                                      double *__restrict__ y,
-                                                      double *__restrict__ status,
-                                                      int fuse_diag)
+__global__ __launch_bounds__(256) void k_factor_step(double *__restrict__ S, long long lds, int k,
+                                                     const int *__restrict__ pan, int T,
+                                                     const int *__restrict__ prev, int Tp,
+                                                     double *__restrict__ linv,
+                                                     double *__restrict__ rhs,
+                                                     double *__restrict__ y,
+                                                     double *__restrict__ status)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double *As = sm, *Bs = sm + NB * LP, *Cs = sm + 2 * NB * LP;
     __shared__ double yk[NB], rk[NB];
     __shared__ double part[4][NB];
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, b = blockIdx.x;
+    const bool kin = Tp > 0 && prev[0] == k;   // column k-1 reaches row k
+    d4 acc[2][2];
+    if (b > T) {
+        // trailing pairs of column k-1 below row k (k_syrk's enumeration over
+        // prev without k)
+        const int *pl = prev + (kin ? 1 : 0);
+        const int Tr = Tp - (kin ? 1 : 0);
+        int q = b - T - 1, jj = 0;
+        while (q >= Tr - jj) {
+            q -= Tr - jj;
+            jj++;
+        }
+        const int j = pl[jj], i = pl[jj + q];
+        load_tile(S, lds, i, k - 1, As);
+        load_tile(S, lds, j, k - 1, Bs);
+        __syncthreads();
+        mfma_64x64(As, Bs, acc);
+        __syncthreads();
+        load_tile(S, lds, i, j, As);
+        __syncthreads();
+        acc_to_lds(acc, As, -1.0, true);
+        __syncthreads();
+        store_tile(S, lds, i, j, As);
+        return;
+    }
+    const int i = b > 0 ? pan[b - 1] : k;
+    bool iin = false;   // column k-1 reaches row i (panel tiles only)
+    if (b > 0 && kin)
+        for (int t = 1; t < Tp && !iin; t++) iin = prev[t] == i;
+    if (b > 0) {   // A_ik and its pending update of column k-1
+        load_tile(S, lds, i, k, Cs);
+        if (iin) {
+            load_tile(S, lds, i, k - 1, As);
+            load_tile(S, lds, k, k - 1, Bs);
+            __syncthreads();
+            mfma_64x64(As, Bs, acc);
+            __syncthreads();
+            acc_to_lds(acc, Cs, -1.0, true);
+        }
+    } else if (kin) {
+        load_tile(S, lds, k, k - 1, Bs);
+    }
+    // A_kk and its pending update
+    if (kin && !iin && b > 0) load_tile(S, lds, k, k - 1, Bs);
+    __syncthreads();
+    if (kin) {
+        mfma_64x64(Bs, Bs, acc);
+        __syncthreads();
+    }
     load_tile(S, lds, k, k, As);
     if (tid < NB) rk[tid] = rhs[(long long)NB * k + tid];
     __syncthreads();
+    if (kin) {
+        acc_to_lds(acc, As, -1.0, true);
+        __syncthreads();
+    }
     const bool ok = block_potrf_inv(As, Bs);
     gemv64(Bs, rk, part, yk, 1.0);            // y_k = L^-1 r_k
-    if (blockIdx.x == 0) {
+    if (b == 0) {
         store_tile(S, lds, k, k, As);
         double *lo = linv + (long long)NB * NB * k;
         for (int q = tid; q < NB * NB; q += blockDim.x) lo[q] = Bs[(q >> 6) * LP + (q & 63)];
@@ -469,54 +536,14 @@ __global__ __launch_bounds__(256) void k_factor_panel(double *__restrict__ S, lo
         if (tid == 0 && !ok) status[0] = 1.0;
         return;
     }
-    const int i = pan[blockIdx.x - 1];
-    load_tile(S, lds, i, k, As);
+    mfma_64x64(Cs, Bs, acc);   // L_ik[r][c] = sum_t A_ik[r][t] Li[c][t]
     __syncthreads();
-    d4 acc[2][2];
-    mfma_64x64(As, Bs, acc);   // L_ik[r][c] = sum_t A_ik[r][t] Li[c][t]
+    acc_to_lds(acc, Cs, 1.0, false);
     __syncthreads();
-    acc_to_lds(acc, As, 1.0, false);
-    __syncthreads();
-    store_tile(S, lds, i, k, As);
+    store_tile(S, lds, i, k, Cs);
     double ri[1];
-    gemv64(As, yk, part, nullptr, 1.0, ri);   // (L_ik y_k)[tid] for tid < 64
+    gemv64(Cs, yk, part, nullptr, 1.0, ri);   // (L_ik y_k)[tid] for tid < 64
     if (tid < NB) rhs[(long long)NB * i + tid] -= ri[0];
-    if (fuse_diag) {
-        // the only panel tile of this step: apply A_ii -= L_ik L_ik^T here
-        mfma_64x64(As, As, acc);
-        load_tile(S, lds, i, i, Cs);
-        __syncthreads();
-        acc_to_lds(acc, Cs, -1.0, true);
-        __syncthreads();
-        store_tile(S, lds, i, i, Cs);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// trailing update A_ij -= L_ik L_jk^T for pan pairs (jj <= ii)
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_syrk(double *__restrict__ S, long long lds, int k,
-                                              const int *__restrict__ pan, int T)
-{
-    extern __shared__ __attribute__((aligned(16))) double sm[];
-    double *As = sm, *Bs = sm + NB * LP;
-    int q = blockIdx.x, jj = 0;
-    while (q >= T - jj) {
-        q -= T - jj;
-        jj++;
-    }
-    const int j = pan[jj], i = pan[jj + q];
-    load_tile(S, lds, i, k, As);
-    load_tile(S, lds, j, k, Bs);
-    __syncthreads();
-    d4 acc[2][2];
-    mfma_64x64(As, Bs, acc);
-    __syncthreads();
-    load_tile(S, lds, i, j, As);
-    __syncthreads();
-    acc_to_lds(acc, As, -1.0, true);
-    __syncthreads();
-    store_tile(S, lds, i, j, As);
 }
 
 // ---------------------------------------------------------------------------
@@ -1559,6 +1586,8 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
     }
     d->pan_ptr_h = new int[nt + 1];
     for (int k = 0; k <= nt; k++) d->pan_ptr_h[k] = ptr[k];
+    d->h_pan_list = new int[list.size() + 1];
+    for (size_t q = 0; q < list.size(); q++) d->h_pan_list[q] = list[q];
     TRY_RC(dev_alloc(&d->pan_list, sizeof(int) * (list.size() + 1)));
     TRY_RC(dev_alloc(&d->env_tiles, sizeof(int) * (env.size() + 1)));
     if (!list.empty())
@@ -1575,6 +1604,8 @@ void ba_chol_free(ba_dev *d)
 {
     delete[] d->h_tfirst;
     delete[] d->pan_ptr_h;
+    delete[] d->h_pan_list;
+    d->h_pan_list = nullptr;
     delete[] d->cr_eptr_h;
     delete[] d->cr_kptr_h;
     d->cr_eptr_h = d->cr_kptr_h = nullptr;
@@ -1622,12 +1653,10 @@ int ba_chol_fix_diag(ba_dev *d)
 int ba_chol_solve(ba_dev *d)
 {
     const int nt = d->nt;
-    const size_t smem = sizeof(double) * 2 * NB * LP;
     const size_t smem3 = sizeof(double) * 3 * NB * LP;
-    TRY_RC(ba_ensure_dyn_lds((const void *)k_factor_panel, smem3));
+    TRY_RC(ba_ensure_dyn_lds((const void *)k_factor_step, smem3));
     TRY_RC(ba_ensure_dyn_lds((const void *)k_cr_factor, smem3));
     TRY_RC(ba_ensure_dyn_lds((const void *)k_cr_update, smem3));
-    TRY_RC(ba_ensure_dyn_lds((const void *)k_syrk, smem));
     if (d->dense_solve == 3) {   // sequential parity solve
         KT_B(d);
         k_chol_seq<<<1, 256, 0, d->stream>>>(d->S, d->lds, (int)d->ld, d->rhs, d->da,
@@ -1698,19 +1727,15 @@ int ba_chol_solve(ba_dev *d)
     }
     for (int k = 0; k < nt; k++) {
         const int p0 = d->pan_ptr_h[k], T = d->pan_ptr_h[k + 1] - p0;
-        // a single panel tile (narrow envelope) applies its own trailing update
-        const int fuse = (T == 1);
+        const int q0 = k > 0 ? d->pan_ptr_h[k - 1] : 0, Tp = k > 0 ? p0 - q0 : 0;
+        // column k-1's trailing pairs below row k (see k_factor_step)
+        const int kin = Tp > 0 && d->h_pan_list[q0] == k;
+        const int Tr = Tp - kin;
         KT_B(d);
-        k_factor_panel<<<1 + T, 256, smem3, d->stream>>>(d->S, d->lds, k, d->pan_list + p0,
-                                                          d->linv, d->rhs, d->ywork,
-                                                          d->scal + 4, fuse);
+        k_factor_step<<<1 + T + Tr * (Tr + 1) / 2, 256, smem3, d->stream>>>(
+            d->S, d->lds, k, d->pan_list + p0, T, d->pan_list + q0, Tp, d->linv, d->rhs,
+            d->ywork, d->scal + 4);
         KT_E(d, KT_FACTOR);
-        if (T > 0 && !fuse) {
-            KT_B(d);
-            k_syrk<<<T * (T + 1) / 2, 256, smem, d->stream>>>(d->S, d->lds, k, d->pan_list + p0,
-                                                              T);
-            KT_E(d, KT_SYRK);
-        }
     }
     for (int k = nt - 1; k >= 0; k--) {
         const int j0 = d->h_tfirst[k];

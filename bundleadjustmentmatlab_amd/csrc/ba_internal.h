@@ -89,6 +89,7 @@ struct ba_dev {
     int nt;
     int *h_tfirst;     // host [nt]
     int *pan_ptr_h;    // host [nt+1]  offsets into pan_list (panel tiles of step k)
+    int *h_pan_list;   // host copy of pan_list
     int *pan_list;     // device: tile rows i > k with tfirst[i] <= k, per k
     int *env_tiles;    // device [n_env][2] (i, k) tiles inside the envelope
     int *tb_ptr, *tb_blk;  // device: per envelope tile, the co-visible blocks overlapping it

@@ -1824,7 +1824,7 @@ const char *vlgba_kernel_name(int k)
 {
     static const char *names[KT_N] = {
         "k_rotations", "k_linearize", "k_camera_reduce", "k_damp_point", "k_schur",
-        "k_schur_group", "k_schur_reduce", "k_assemble", "k_factor_panel", "k_syrk",
+        "k_schur_group", "k_schur_reduce", "k_assemble", "k_factor_step", "k_syrk",
         "k_backward", "k_camera_update", "k_point_update", "k_cr_factor", "k_cr_update",
         "k_cr_back", "k_schur_mfma"};
     return (k >= 0 && k < KT_N) ? names[k] : "";

@@ -291,9 +291,9 @@ def test_cyclic_reduction_matches_envelope(gpu, num_a, m):
     # cameras), 64-row tiles otherwise
     rows = num_a * (32 // num_a) if num_a == 6 else 64
     nt = -(-num_a * m // rows)
-    assert "k_cr_factor" in kcr and "k_factor_panel" not in kcr
+    assert "k_cr_factor" in kcr and "k_factor_step" not in kcr
     assert kcr["k_cr_factor"][1] == nt.bit_length()    # levels: floor(log2 nt) + 1
-    assert "k_factor_panel" in kenv and "k_cr_factor" not in kenv
+    assert "k_factor_step" in kenv and "k_cr_factor" not in kenv
     assert cr.old_sse == env.old_sse
     assert cr.chol_failed == 0 and env.chol_failed == 0
     assert abs(cr.new_sse - env.new_sse) <= 1e-9 * env.new_sse, (cr.new_sse, env.new_sse)

@@ -2,7 +2,7 @@
 // library).  Build: hipcc -O3 --offload-arch=gfx950 -ffp-contract=off
 //   -I include -I bundleadjustmentmatlab_amd/csrc tools/ubench_chol.hip -o ubench_chol
 // Prints in-kernel cycle stamps of the phases of block_potrf_inv and the
-// wall time of k_factor_panel on a 2-tile SPD matrix.
+// wall time of k_factor_step on a 2-tile SPD matrix.
 #include "../bundleadjustmentmatlab_amd/csrc/ba_chol.hip"
 
 // the library's kernel-timer hooks (ba_solver.cpp) are not linked here
@@ -151,7 +151,7 @@ int main()
     int one = 1;
     hipMemcpy(pan, &one, sizeof(int), hipMemcpyHostToDevice);
     const size_t smem3 = sizeof(double) * 3 * NB * LP;
-    hipFuncSetAttribute((const void *)k_factor_panel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipFuncSetAttribute((const void *)k_factor_step, hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)smem3);
     hipFuncSetAttribute((const void *)k_diag, hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)smem3);
@@ -172,14 +172,14 @@ int main()
         for (int it = 0; it < 20; it++) {
             hipMemcpy(S, S0, sizeof(double) * n * n, hipMemcpyDeviceToDevice);
             hipEventRecord(e0);
-            k_factor_panel<<<2, 256, smem3>>>(S, n, 0, pan, linv, rhs, y, st, fuse);
+            k_factor_step<<<2, 256, smem3>>>(S, n, 0, pan, 1, pan, 0, linv, rhs, y, st);
             hipEventRecord(e1);
             hipEventSynchronize(e1);
             float ms;
             hipEventElapsedTime(&ms, e0, e1);
             if (ms < best) best = ms;
         }
-        printf("k_factor_panel (fuse=%d): best %.2f us\n", fuse, best * 1e3);
+        printf("k_factor_step (run %d): best %.2f us\n", fuse, best * 1e3);
     }
     return 0;
 }
