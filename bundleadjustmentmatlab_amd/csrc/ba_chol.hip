@@ -1176,6 +1176,82 @@ __global__ __launch_bounds__(256) void k_cr32_back(const int *__restrict__ elim,
     }
 }
 
+// All levels of the back substitution in ONE launch (the
+// 8 level launches were at the launch floor).  Workgroup b takes elimination
+// record nrec-1-b (the deepest level first); it prefetches its three tiles,
+// then waits for x_p and x_q, which the workgroups of the tiles eliminated
+// above it publish as epoch-tagged 8-byte granules {epoch, 32-bit half}
+// (write-through agent-scope stores: the data is the flag, no fences;
+// MI355X_MICROARCH.md / cdna_hip_programming.md Guideline 16, R2).  One wave
+// sweeps one neighbour's 64 granules until every tag matches.  Every record's
+// neighbours are eliminated at higher levels, so the dependencies form a tree
+// from the top level down; the launch is used only when all n32 workgroups
+// are co-resident (n32 <= 2 x CUs).  A spin that never ends sets
+// status = 2 (the pass then takes the pinv path) instead of hanging.  Same
+// arithmetic as k_cr32_back.
+#define BA_BACK_SPIN_MAX 400000u
+__global__ __launch_bounds__(256) void k_cr32_back_all(const int *__restrict__ elim, int nrec,
+                                                       int nt, int TB, long long ld,
+                                                       const double *__restrict__ linv,
+                                                       const double *__restrict__ crL,
+                                                       const double *__restrict__ y,
+                                                       double *__restrict__ x,
+                                                       unsigned long long *__restrict__ xg,
+                                                       unsigned epoch, double *status)
+{
+    __shared__ __attribute__((aligned(16))) double Lp[T32 * LP], Lq[T32 * LP], Li[T32 * LP];
+    __shared__ __attribute__((aligned(16))) double t[T32], xp[T32], xq[T32], u[T32];
+    __shared__ double part[8][T32];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int rec = nrec - 1 - (int)blockIdx.x;
+    const int e = elim[3 * rec], p = elim[3 * rec + 1], q = elim[3 * rec + 2];
+    const long long T2 = (long long)T32 * T32;
+    // the tiles (written by earlier launches): plain loads, in flight while we wait
+    if (p >= 0) load_rm32(crL + T2 * e, Lp);
+    if (q >= 0) load_rm32(crL + T2 * (nt + e), Lq);
+    load_rm32(linv + T2 * e, Li);
+    if (tid < T32) t[tid] = tid < TB ? y[(long long)TB * e + tid] : 0.0;
+    if (wv < 2) {
+        const int nb = wv == 0 ? p : q;
+        if (nb >= 0) {
+            const unsigned long long *g = xg + 64 * (size_t)nb + lane;
+            unsigned long long v = 0;
+            for (unsigned spins = 0;; spins++) {
+                v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (__all((unsigned)(v >> 32) == epoch)) break;
+                if (spins >= BA_BACK_SPIN_MAX) {
+                    if (lane == 0) status[0] = 2.0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            // lane 2r: low half of x_r, lane 2r + 1: high half
+            reinterpret_cast<unsigned *>(wv == 0 ? xp : xq)[lane] = (unsigned)v;
+        }
+    }
+    __syncthreads();
+    if (p >= 0) {
+        gemv32(Lp, xp, part, u, true);
+        if (tid < T32) t[tid] -= u[tid];
+        __syncthreads();
+    }
+    if (q >= 0) {
+        gemv32(Lq, xq, part, u, true);
+        if (tid < T32) t[tid] -= u[tid];
+        __syncthreads();
+    }
+    gemv32(Li, t, part, u, true);   // x_e = L_e^-T t (ends with a barrier)
+    if (wv == 0) {   // publish x_e: 64 granules, one 8-byte write-through store each
+        const unsigned h = reinterpret_cast<const unsigned *>(u)[lane];
+        __hip_atomic_store(xg + 64 * (size_t)e + lane, ((unsigned long long)epoch << 32) | h,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tid < TB) {
+        const long long g = (long long)TB * e + tid;
+        if (g < ld) x[g] = u[tid];
+    }
+}
+
 __global__ __launch_bounds__(256) void k_cr_back(const int *__restrict__ elim, int nt,
                                                  const double *__restrict__ linv,
                                                  const double *__restrict__ crL,
@@ -1560,6 +1636,10 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
                 d->crf_ptr_h[L] = L >= 1 ? fptr[L] : 0;
                 d->crs_ptr_h[L] = L >= 1 ? sptr[L] : 0;
             }
+            TRY_RC(dev_alloc(&d->xgran, sizeof(unsigned long long) * 64 * (size_t)nt));
+            VLGBA_CHECK(hipMemsetAsync(d->xgran, 0, sizeof(unsigned long long) * 64 * (size_t)nt,
+                                       d->stream));
+            d->back_epoch = 0;
             TRY_RC(dev_alloc(&d->crf, sizeof(int) * (frec.size() + 1)));
             TRY_RC(dev_alloc(&d->crs, sizeof(int) * (srec.size() + 1)));
             if (!frec.empty())
@@ -1609,6 +1689,8 @@ void ba_chol_free(ba_dev *d)
     delete[] d->cr_eptr_h;
     delete[] d->cr_kptr_h;
     d->cr_eptr_h = d->cr_kptr_h = nullptr;
+    if (d->xgran) ba_dfree(d->xgran);
+    d->xgran = nullptr;
     if (d->crf) ba_dfree(d->crf);
     if (d->crs) ba_dfree(d->crs);
     delete[] d->crf_ptr_h;
@@ -1685,6 +1767,16 @@ int ba_chol_solve(ba_dev *d)
                 d->S, d->lds, TB, d->ld, d->crf + 5 * f0, ne, d->crs + 3 * s0, n32, d->linv,
                 d->crL, d->rhs, d->ywork, d->scal + 4);
             KT_E(d, KT_CR_FACTOR);
+        }
+        const int nrec = d->cr_eptr_h[d->cr_nlev];
+        if (d->xgran && nrec <= 2 * d->ncu) {   // every record co-resident: one launch
+            if (++d->back_epoch == 0) d->back_epoch = 1;
+            KT_B(d);
+            k_cr32_back_all<<<nrec, 256, 0, d->stream>>>(d->cr_elim, nrec, n32, TB, d->ld,
+                                                         d->linv, d->crL, d->ywork, d->da,
+                                                         d->xgran, d->back_epoch, d->scal + 4);
+            KT_E(d, KT_CR_BACK);
+            return -(int)hipGetLastError();
         }
         for (int l = d->cr_nlev - 1; l >= 0; l--) {
             const int e0 = d->cr_eptr_h[l], ne = d->cr_eptr_h[l + 1] - e0;

@@ -111,6 +111,10 @@ struct ba_dev {
     // fused levels (L >= 1): records (e, p, q, em, ep) and survivors (k, em, ep)
     int *crf, *crs;               // device
     int *crf_ptr_h, *crs_ptr_h;   // host [nlev + 1], entries per level (level 0 empty)
+    // one-launch back substitution (k_cr32_back_all): x of every tile as
+    // 64 epoch-tagged 8-byte granules, read by the tiles of the level below
+    unsigned long long *xgran;    // [nt32][64]
+    unsigned back_epoch;          // per solve, never 0
     // reductions: partial sums per block of the reducing kernels, in fixed order
     double *part;      // [3][PART_MAX]
     double *scal;      // [8] : 0 old_sse, 1 new_sse, 2 dpg cams, 3 dpg pts, 4 chol status
