@@ -81,17 +81,25 @@ struct scene_dev {
     unsigned *behind;   // per k_scene_obs block: observations behind their camera
 };
 
+// the walk's normals, one thread per camera (the transcendental part)
+__global__ void k_scene_cam_noise(scene_dev s, double *nz)
+{
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < 1 || j >= s.m) return;
+    for (int t = 0; t < 3; t++)
+        normal2(philox(3ull * j + t, ST_CAM, s.seed), nz[6 * (size_t)j + 2 * t],
+                nz[6 * (size_t)j + 2 * t + 1]);
+}
+
 // the camera walk: one lane, sequential over j (m steps of a few flops)
-__global__ void k_scene_cams(scene_dev s)
+__global__ void k_scene_cams(scene_dev s, const double *nzall)
 {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     double vw[3] = {0.0, 0.0, 0.0}, vT[3] = {0.0, 0.0, 0.0};
     double w[3] = {0.0, 0.0, 0.0}, T[3] = {0.0, 0.0, 0.0};
     for (int j = 0; j < s.m; j++) {
         if (j > 0) {
-            double nz[6];
-            for (int t = 0; t < 3; t++)
-                normal2(philox(3ull * j + t, ST_CAM, s.seed), nz[2 * t], nz[2 * t + 1]);
+            const double *nz = nzall + 6 * (size_t)j;
             for (int k = 0; k < 3; k++) {
                 vw[k] = 0.8 * vw[k] + 2e-3 * nz[k];
                 vT[k] = 0.8 * vT[k] + 2e-1 * nz[3 + k];
@@ -243,7 +251,10 @@ extern "C" int vlgba_scene_banded(const vlgba_scene_spec *sp, int device, vlgba_
             break;
         }
         const unsigned nblk = (unsigned)((N + 255) / 256);
-        k_scene_cams<<<1, 64, 0, st>>>(s);
+        // the walk's normals in parallel, then the sequential recurrence (a
+        // single lane evaluating 6m Box-Muller normals took ms)
+        k_scene_cam_noise<<<(s.m + 63) / 64, 64, 0, st>>>(s, s.R);
+        k_scene_cams<<<1, 64, 0, st>>>(s, s.R);
         k_scene_cam_par<<<(s.m + 63) / 64, 64, 0, st>>>(s);
         if (s.n > 0) {
             k_scene_points<<<(s.n + 255) / 256, 256, 0, st>>>(s);

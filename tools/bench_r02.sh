@@ -11,4 +11,5 @@ step cfg3_solve 300 --mode solve --steps 5 --warmup 1 --no-cpu-baseline &&
 step cfg2_solve 300 --config cfg2 --mode solve --steps 20 --warmup 3 --no-cpu-baseline &&
 step cfg5 300 --config cfg5 &&
 step ladybug_pass 300 --config ladybug --steps 10 --warmup 2 &&
-step cfg3_host_scene 300 --host-scene --steps 10 --warmup 2 --no-cpu-baseline
+step cfg3_host_scene 300 --host-scene --steps 10 --warmup 2 --no-cpu-baseline &&
+step cfg3_pass_b 300 --steps 20 --warmup 3 --no-cpu-baseline
