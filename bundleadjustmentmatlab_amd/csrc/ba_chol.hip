@@ -589,6 +589,93 @@ __global__ __launch_bounds__(256) void k_backward(const double *__restrict__ S, 
         z[(long long)NB * j + tid] -= ((part[0][tid] + part[1][tid]) + part[2][tid]) + part[3][tid];
 }
 
+#ifndef BA_BACK_SPIN_MAX
+#define BA_BACK_SPIN_MAX 400000u
+#endif
+// ---------------------------------------------------------------------------
+// The envelope's backward solve in ONE launch (the per-column k_backward
+// launches sat at the launch floor).  Workgroup w takes tile column
+// j = nt-1-w (top first): z_j = y_j - sum over the envelope rows k > j (k
+// descending, the order of the per-column launches: bit-identical) of
+// L_kj^T x_k, then x_j = L_jj^-T z_j, published as 128 epoch-tagged 8-byte
+// write-through granules (cdna_hip_programming.md Guideline 16, R2); each x_k
+// is swept by wave 0 until every tag matches.  Used when every column is
+// co-resident (one workgroup per CU by LDS: nt <= CUs); a spin that never
+// ends sets status = 2 instead of hanging.  Each tile (k, j) is loaded while
+// the wave waits for x_k.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_backward_all(const double *__restrict__ S, long long lds,
+                                                      int nt, const int *__restrict__ pan_ptr,
+                                                      const int *__restrict__ pan,
+                                                      const double *__restrict__ linv,
+                                                      const double *__restrict__ z,
+                                                      double *__restrict__ x,
+                                                      unsigned long long *__restrict__ xg,
+                                                      unsigned epoch, double *status)
+{
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double *Lt = sm, *Li = sm + NB * LP;
+    __shared__ __attribute__((aligned(16))) double zj[NB], xs[NB];
+    __shared__ double part[4][NB];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int j = nt - 1 - (int)blockIdx.x;
+    load_rowmajor(linv + (long long)NB * NB * j, Li);
+    if (tid < NB) zj[tid] = z[(long long)NB * j + tid];
+    const int c = tid & 63, qr = tid >> 6;
+    for (int idx = pan_ptr[j + 1] - 1; idx >= pan_ptr[j]; idx--) {
+        const int k = pan[idx];
+        __syncthreads();   // Lt / xs of the previous k consumed
+        load_tile(S, lds, k, j, Lt);
+        if (wv == 0) {
+            const unsigned long long *g = xg + 128 * (size_t)k;
+            unsigned long long v0 = 0, v1 = 0;
+            for (unsigned spins = 0;; spins++) {
+                v0 = __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                v1 = __hip_atomic_load(g + 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (__all((unsigned)(v0 >> 32) == epoch && (unsigned)(v1 >> 32) == epoch)) break;
+                if (spins >= BA_BACK_SPIN_MAX) {
+                    if (lane == 0) status[0] = 2.0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            unsigned *xu = reinterpret_cast<unsigned *>(xs);
+            xu[lane] = (unsigned)v0;
+            xu[64 + lane] = (unsigned)v1;
+        }
+        __syncthreads();
+        // z_j[c] -= sum_r L_kj[r][c] x_k[r]: thread (c, quarter), as k_backward
+        double s = 0.0;
+#pragma unroll
+        for (int r = 16 * qr; r < 16 * qr + 16; r++) s += Lt[r * LP + c] * xs[r];
+        part[qr][c] = s;
+        __syncthreads();
+        if (tid < NB) zj[tid] -= ((part[0][tid] + part[1][tid]) + part[2][tid]) + part[3][tid];
+    }
+    __syncthreads();
+    {   // x_j[c] = sum_{r >= c} Li[r][c] z_j[r]: thread (c, quarter), as k_backward
+        double s = 0.0;
+        for (int r = 16 * qr; r < 16 * qr + 16; r++)
+            if (r >= c) s += Li[r * LP + c] * zj[r];
+        part[qr][c] = s;
+    }
+    __syncthreads();
+    if (tid < NB) {
+        const double xv = ((part[0][tid] + part[1][tid]) + part[2][tid]) + part[3][tid];
+        xs[tid] = xv;
+        x[(long long)NB * j + tid] = xv;
+    }
+    __syncthreads();
+    if (wv == 0) {
+        const unsigned *xu = reinterpret_cast<const unsigned *>(xs);
+        unsigned long long *g = xg + 128 * (size_t)j;
+        __hip_atomic_store(g + lane, ((unsigned long long)epoch << 32) | xu[lane],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(g + 64 + lane, ((unsigned long long)epoch << 32) | xu[64 + lane],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Block cyclic reduction for a tile-tridiagonal S (co-visibility band narrower
 // than one tile: tile row i couples only with tiles i-1, i+1).  This is the
@@ -1189,7 +1276,6 @@ __global__ __launch_bounds__(256) void k_cr32_back(const int *__restrict__ elim,
 // are co-resident (n32 <= 2 x CUs).  A spin that never ends sets
 // status = 2 (the pass then takes the pinv path) instead of hanging.  Same
 // arithmetic as k_cr32_back.
-#define BA_BACK_SPIN_MAX 400000u
 __global__ __launch_bounds__(256) void k_cr32_back_all(const int *__restrict__ elim, int nrec,
                                                        int nt, int TB, long long ld,
                                                        const double *__restrict__ linv,
@@ -1669,6 +1755,15 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
     d->h_pan_list = new int[list.size() + 1];
     for (size_t q = 0; q < list.size(); q++) d->h_pan_list[q] = list[q];
     TRY_RC(dev_alloc(&d->pan_list, sizeof(int) * (list.size() + 1)));
+    if (!d->cr_nlev && d->dense_solve != 3 && nt <= d->ncu) {   // one-launch backward
+        TRY_RC(dev_alloc(&d->pan_ptr, sizeof(int) * (nt + 1)));
+        VLGBA_CHECK(hipMemcpyAsync(d->pan_ptr, ptr.data(), sizeof(int) * (nt + 1),
+                                   hipMemcpyHostToDevice, d->stream));
+        TRY_RC(dev_alloc(&d->xgran64, sizeof(unsigned long long) * 128 * (size_t)nt));
+        VLGBA_CHECK(hipMemsetAsync(d->xgran64, 0, sizeof(unsigned long long) * 128 * (size_t)nt,
+                                   d->stream));
+        d->back_epoch = 0;
+    }
     TRY_RC(dev_alloc(&d->env_tiles, sizeof(int) * (env.size() + 1)));
     if (!list.empty())
         VLGBA_CHECK(hipMemcpyAsync(d->pan_list, list.data(), sizeof(int) * list.size(),
@@ -1707,6 +1802,10 @@ void ba_chol_free(ba_dev *d)
     if (d->tb_blk) ba_dfree(d->tb_blk);
     d->tb_ptr = d->tb_blk = nullptr;
     if (d->pan_list) ba_dfree(d->pan_list);
+    if (d->pan_ptr) ba_dfree(d->pan_ptr);
+    if (d->xgran64) ba_dfree(d->xgran64);
+    d->pan_ptr = nullptr;
+    d->xgran64 = nullptr;
     if (d->env_tiles) ba_dfree(d->env_tiles);
     d->h_tfirst = d->pan_ptr_h = nullptr;
     d->pan_list = d->env_tiles = nullptr;
@@ -1828,6 +1927,17 @@ int ba_chol_solve(ba_dev *d)
             d->S, d->lds, k, d->pan_list + p0, T, d->pan_list + q0, Tp, d->linv, d->rhs,
             d->ywork, d->scal + 4);
         KT_E(d, KT_FACTOR);
+    }
+    if (d->xgran64) {   // every column co-resident: the backward solve in one launch
+        if (++d->back_epoch == 0) d->back_epoch = 1;
+        const size_t smem2 = sizeof(double) * 2 * NB * LP;
+        TRY_RC(ba_ensure_dyn_lds((const void *)k_backward_all, smem2));
+        KT_B(d);
+        k_backward_all<<<nt, 256, smem2, d->stream>>>(d->S, d->lds, nt, d->pan_ptr, d->pan_list,
+                                                       d->linv, d->ywork, d->da, d->xgran64,
+                                                       d->back_epoch, d->scal + 4);
+        KT_E(d, KT_BACKWARD);
+        return -(int)hipGetLastError();
     }
     for (int k = nt - 1; k >= 0; k--) {
         const int j0 = d->h_tfirst[k];
