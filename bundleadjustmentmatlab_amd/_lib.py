@@ -10,7 +10,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libvlgba.so")
+# VLGBA_LIB: an alternative build of the same library (A/B timing of a kernel
+# variant, tools/ab_build.sh); the package's own build otherwise
+LIB_PATH = os.environ.get("VLGBA_LIB") or os.path.join(_HERE, "libvlgba.so")
 
 c_int, c_double, c_ll = ctypes.c_int, ctypes.c_double, ctypes.c_longlong
 c_dp = ctypes.POINTER(ctypes.c_double)

@@ -909,8 +909,14 @@ __global__ __launch_bounds__(256) void k_point_vinv(const double *__restrict__ V
 // deterministic run to run; only the grouping differs from the term kernel.
 // -------------------------------------------------------------------------
 #define BA_MF_KB 5   // points per K-block (one wave)
+#ifndef BA_MF_PIPE
+#define BA_MF_PIPE 0
+#endif
+#ifndef BA_MF_WAVES
+#define BA_MF_WAVES 3
+#endif
 template <int NA>
-__global__ __launch_bounds__(256, (NA == 6) ? 2 : 1) void k_schur_mfma(
+__global__ __launch_bounds__(256, (NA == 6) ? BA_MF_WAVES : 1) void k_schur_mfma(
     const int *__restrict__ grp_ch, const int *__restrict__ grp_gs,
     const int *__restrict__ grp_ge, const int *__restrict__ ch_pt,
     const int *__restrict__ ch_obase, const int *__restrict__ ch_blob,
@@ -1088,6 +1094,7 @@ __global__ __launch_bounds__(256, (NA == 6) ? 2 : 1) void k_schur_mfma(
     };
     // two register sets, software pipelined: the next chunk's fragments are in
     // flight while this chunk's MFMAs run (no register copies between sets)
+#if BA_MF_PIPE
     double wa[4][RT], da[7], ea[4], wb[4][RT], db[7], eb[4];
     load(0, wa, da, ea);
     for (int k = 0; k < nc; k += 2) {
@@ -1097,6 +1104,13 @@ __global__ __launch_bounds__(256, (NA == 6) ? 2 : 1) void k_schur_mfma(
         load(min(k + 2, nc - 1), wa, da, ea);
         process(k + 1, wb, db, eb);
     }
+#else
+    double wa[4][RT], da[7], ea[4];
+    for (int k = 0; k < nc; k++) {
+        load(k, wa, da, ea);
+        process(k, wa, da, ea);
+    }
+#endif
     __syncthreads();
     for (int q = tid; q < ngs * NA * NA; q += 256) spart[(size_t)NA * NA * gs0 + q] = gacc[q];
     for (int q = tid; q < nge * NA; q += 256) epart[(size_t)NA * ge0 + q] = geacc[q];
@@ -1318,7 +1332,7 @@ __global__ __launch_bounds__(256) void k_point_update_chunk(
     const int *__restrict__ seg_pt, const int *__restrict__ seg_long,
     const int *__restrict__ long_o0, const double *__restrict__ dpg_long)
 {
-    __shared__ double ts[BA_CH_OBS * 3];
+    __shared__ double wl[BA_CH_OBS * 3 * NA];   // the chunk's W rows, then t_o
     __shared__ double bn[BA_CH_PTS * 3];
     __shared__ int lptr[BA_CH_PTS + 1];
     const int ch = blockIdx.x, tid = threadIdx.x;
@@ -1364,22 +1378,54 @@ __global__ __launch_bounds__(256) void k_point_update_chunk(
         return;
     }
     if (tid <= np) lptr[tid] = pt_ptr[p0 + tid] - obase;
-    for (int q = tid; q < nobs * 3; q += 256) {
-        const int lo = q / 3, r = q - 3 * lo, o = obase + lo;
-        const double *wr = W + (size_t)3 * NA * o + NA * r;
-        const double *d = da + (size_t)NA * obs_cam[o];
-        double dl[NA], w[NA];
+    // observation lanes: camera, point slot, x and the da row (zero past ndb)
+    int oj = 0, opl = 0;
+    double ox0 = 0.0, ox1 = 0.0, dl[NA];
 #pragma unroll
-        for (int k = 0; k < NA; k++) {
-            w[k] = wr[k];
-            dl[k] = k < ndb ? d[k] : 0.0;
+    for (int k = 0; k < NA; k++) dl[k] = 0.0;
+    if (tid < nobs) {
+        const int o = obase + tid;
+        oj = obs_cam[o];
+        opl = obs_lpt[o];
+        ox0 = obs_x[2 * (size_t)o];
+        ox1 = obs_x[2 * (size_t)o + 1];
+        const double *d = da + (size_t)NA * oj;
+#pragma unroll
+        for (int k = 0; k < NA; k++) dl[k] = k < ndb ? d[k] : 0.0;
+    }
+    // the chunk's W rows are one contiguous range: read lane by lane (each cache
+    // line requested once, not six times by 48-byte-strided lanes) into LDS
+    {
+        constexpr int MAXE = (BA_CH_OBS * 3 * NA + 255) / 256;
+        const int ne = nobs * 3 * NA;
+        const double *wsrc = W + (size_t)3 * NA * obase;
+        double wr[MAXE];
+#pragma unroll
+        for (int u = 0; u < MAXE; u++) {
+            const int e = tid + 256 * u;
+            wr[u] = wsrc[e < ne ? e : 0];
         }
-        double t = w[0] * dl[0] + w[1] * dl[1] + w[2] * dl[2] + w[3] * dl[3] + w[4] * dl[4] +
-                   w[5] * dl[5];
 #pragma unroll
-        for (int k = 6; k < NA; k++)   // nomex semantics only (ndb = NA)
-            if (k < ndb) t = t + w[k] * dl[k];
-        ts[q] = t;
+        for (int u = 0; u < MAXE; u++) {
+            const int e = tid + 256 * u;
+            if (e < ne) wl[e] = wr[u];
+        }
+    }
+    __syncthreads();
+    // t_o[r] = W_o(:, r)' da_j, into the row's first slot (only this lane reads
+    // the row)
+    if (tid < nobs) {
+        double *wo = wl + 3 * NA * tid;
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            double *w = wo + NA * r;
+            double t = w[0] * dl[0] + w[1] * dl[1] + w[2] * dl[2] + w[3] * dl[3] +
+                       w[4] * dl[4] + w[5] * dl[5];
+#pragma unroll
+            for (int k = 6; k < NA; k++)   // nomex semantics only (ndb = NA)
+                if (k < ndb) t = t + w[k] * dl[k];
+            w[0] = t;
+        }
     }
     __syncthreads();
     double dpg = 0.0, sse = 0.0;
@@ -1388,7 +1434,7 @@ __global__ __launch_bounds__(256) void k_point_update_chunk(
         double rhs[3] = {eB[3 * (size_t)i], eB[3 * (size_t)i + 1], eB[3 * (size_t)i + 2]};
         for (int lo = lptr[tid]; lo < lptr[tid + 1]; lo++) {
 #pragma unroll
-            for (int r = 0; r < 3; r++) rhs[r] -= ts[3 * lo + r];
+            for (int r = 0; r < 3; r++) rhs[r] -= wl[3 * NA * lo + NA * r];
         }
         const double *vi = Vinv + 9 * (size_t)i;
 #pragma unroll
@@ -1403,7 +1449,7 @@ __global__ __launch_bounds__(256) void k_point_update_chunk(
     }
     __syncthreads();
     if (tid < nobs) {
-        const int o = obase + tid, j = obs_cam[o], pl = obs_lpt[o];
+        const int j = oj, pl = opl;
         const double bl[3] = {bn[3 * pl], bn[3 * pl + 1], bn[3 * pl + 2]};
         double an[NA], xh[2];
 #pragma unroll
@@ -1419,8 +1465,8 @@ __global__ __launch_bounds__(256) void k_point_update_chunk(
             vlg_calib(Kc, k4, an, NA - 6);
             vlg_project(Kc, R, an + 3, bl, xh);
         }
-        const double d0 = obs_x[2 * (size_t)o] - xh[0];
-        const double d1 = obs_x[2 * (size_t)o + 1] - xh[1];
+        const double d0 = ox0 - xh[0];
+        const double d1 = ox1 - xh[1];
         sse = d0 * d0 + d1 * d1;
     }
     block_sum_to<256>(sse, part_sse + ch);
