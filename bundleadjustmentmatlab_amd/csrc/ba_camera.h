@@ -112,6 +112,17 @@ struct cam_view<NA, true> {
 // -------------------------------------------------------------------------
 // rotations: R(a), R(a + h e_k) k = 0..2, R(a + 0) per camera (5 x 9)
 // -------------------------------------------------------------------------
+// rotation k of the table alone (k = 0: R(w); k = 1..4: as below)
+__device__ __forceinline__ void rotation_k(const double w[3], int k, double *__restrict__ out)
+{
+    double R[9], w1[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) w1[c] = k == 0 ? w[c] : w[c] + H_FD * ((c == k - 1) ? 1.0 : 0.0);
+    vlg_rodrigues(R, w1);
+#pragma unroll
+    for (int q = 0; q < 9; q++) out[9 * k + q] = R[q];
+}
+
 __device__ __forceinline__ void rotations5(const double w[3], double *__restrict__ out)
 {
     double R[9];

@@ -862,20 +862,37 @@ __global__ __launch_bounds__(256) void k_schur_group(
 // -------------------------------------------------------------------------
 // V*^-1 per point (bundle_euclid.m:168-180) for the MFMA Schur path
 // -------------------------------------------------------------------------
+// (the block's 256 contiguous 9-double rows in and out through LDS, lane by
+// lane: every cache line requested once)
 template <int NA>
 __global__ __launch_bounds__(256) void k_point_vinv(const double *__restrict__ V, int n,
                                                     double lambda, double *__restrict__ Vinv)
 {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    double vs[9], vi[9];
+    __shared__ double vsh[256 * 9];
+    const int i0 = blockIdx.x * 256, tid = threadIdx.x;
+    const int cnt = 9 * min(256, n - i0);
+    const double *src = V + 9 * (size_t)i0;
+    double t[9];
 #pragma unroll
-    for (int q = 0; q < 9; q++) vs[q] = V[9 * (size_t)i + q];
+    for (int u = 0; u < 9; u++) t[u] = tid + 256 * u < cnt ? src[tid + 256 * u] : 0.0;
 #pragma unroll
-    for (int c = 0; c < 3; c++) vs[4 * c] = (1 + lambda) * vs[4 * c];
-    vlg_pinv3(vs, vi);
+    for (int u = 0; u < 9; u++) vsh[tid + 256 * u] = t[u];
+    __syncthreads();
+    if (i0 + tid < n) {
+        double vs[9], vi[9];
 #pragma unroll
-    for (int q = 0; q < 9; q++) Vinv[9 * (size_t)i + q] = vi[q];
+        for (int q = 0; q < 9; q++) vs[q] = vsh[9 * tid + q];
+#pragma unroll
+        for (int c = 0; c < 3; c++) vs[4 * c] = (1 + lambda) * vs[4 * c];
+        vlg_pinv3(vs, vi);
+#pragma unroll
+        for (int q = 0; q < 9; q++) vsh[9 * tid + q] = vi[q];
+    }
+    __syncthreads();
+    double *dst = Vinv + 9 * (size_t)i0;
+#pragma unroll
+    for (int u = 0; u < 9; u++)
+        if (tid + 256 * u < cnt) dst[tid + 256 * u] = vsh[tid + 256 * u];
 }
 
 // -------------------------------------------------------------------------
@@ -1012,11 +1029,9 @@ __global__ __launch_bounds__(256, (NA == 6) ? BA_MF_WAVES : 1) void k_schur_mfma
         const unsigned *r = rec + gbo[k];
         const unsigned h1 = r[1];
         const int C = (int)(h1 & 0xffu), fl = (int)((h1 >> 8) & 0xffu), Rc = NA * C;
-        const int nt = (Rc + 15) >> 4;
         // row tile by row tile: one Y tile live at a time.  Every tile runs (tiles
         // past the chunk's columns multiply exact zeros): no branch between the
         // next chunk's loads and the MFMAs, so their waits stay precise
-        (void)nt;
         // s = 3 first, all column tiles: point 5w + 4 on the matrix pipe
         // (register 0 = A fragment), in flight while the VALU forms the rest
         double y4[RT];
@@ -1208,25 +1223,36 @@ __global__ void k_assemble(const int *__restrict__ blk_jk, const double *__restr
 // (bundle_euclid.m:215-217), one partial per 64-lane workgroup.
 // -------------------------------------------------------------------------
 template <int NA>
-__global__ __launch_bounds__(64) void k_camera_update(
+__global__ __launch_bounds__(320) void k_camera_update(
     const double *__restrict__ a, const double *__restrict__ da,
     const double *__restrict__ eA, int m, double lambda, double *__restrict__ a_new,
     double *__restrict__ rot_new, double *__restrict__ part)
 {
+    // 64 cameras per block; wave k < 5 builds rotation k of each camera's
+    // table (the libm-exact sin / cos chains run side by side), wave 0 also
+    // forms a_new and the camera part of dp'(lambda dp + g) (one wave's sum,
+    // the order of the 64-camera partials)
+    const int lane = threadIdx.x & 63, k = threadIdx.x >> 6;
+    const int j = blockIdx.x * 64 + lane;
+    double an[NA];
     double acc = 0.0;
-    const int j = blockIdx.x * 64 + threadIdx.x;
     if (j < m) {
-        double an[NA];
 #pragma unroll
         for (int c = 0; c < NA; c++) {
             const double d = da[(size_t)NA * j + c];
             an[c] = a[(size_t)NA * j + c] + d;
-            a_new[(size_t)NA * j + c] = an[c];
-            acc += d * (lambda * d + eA[(size_t)NA * j + c]);
+            if (k == 0) {
+                a_new[(size_t)NA * j + c] = an[c];
+                acc += d * (lambda * d + eA[(size_t)NA * j + c]);
+            }
         }
-        if constexpr (NA != BA_PROJ_NA) rotations5(an, rot_new + 45 * (size_t)j);
+        if constexpr (NA != BA_PROJ_NA) rotation_k(an, k, rot_new + 45 * (size_t)j);
     }
-    block_sum_to<64>(acc, part + blockIdx.x);
+    if (k == 0) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+        if (lane == 0) part[blockIdx.x] = acc;
+    }
 }
 
 // -------------------------------------------------------------------------
@@ -1868,7 +1894,7 @@ int ba_launch_update(ba_dev *d, double lambda)
     KT_B(d);
     // lambda dp'dp once over the ranks (each adds da' eA of its partial eA)
     const double lam_dpg = d->dpg_lambda ? lambda : 0.0;
-    BA_DISPATCH(d->na, (k_camera_update<NA><<<gc, 64, 0, d->stream>>>(
+    BA_DISPATCH(d->na, (k_camera_update<NA><<<gc, 320, 0, d->stream>>>(
                            d->a, d->da, d->eA, d->m, lam_dpg, d->a_new, d->rot_new, d->part)));
     KT_E(d, KT_CAMUPD);
     if (!d->ordered && d->nch > 0 && !d->obs_vis && !d->xh_out) {
