@@ -60,6 +60,23 @@ struct ba_flags {
     int has_pivot;      // pivot[m] mask      (:150-154)
 };
 
+// the camera reduction's arguments (k_camera_reduce_chunks, or workgroups
+// appended to the MFMA Schur launch)
+#ifndef BA_FUSE_CAMRED
+#define BA_FUSE_CAMRED 1
+#endif
+struct ba_camred {
+    const int *cam_eptr, *cam_eslots;
+    const double *upart;
+    int m;
+    ba_flags f;
+    const unsigned char *pivot;
+    double *U, *eA;
+    const double *chsse;
+    int nch;
+    double *sse_out, *sse_out2;
+};
+
 struct ba_dev {
     int m, n, na, N, js;
     int device, ncu;   // HIP device ordinal and its CU count
@@ -127,6 +144,9 @@ struct ba_dev {
     int ordered;       // 1: sequential bit-exact kernels (k_damp_point + k_schur)
     int parity;        // ordered = 2: + sequential solve and LM scalars (bit-identical
                        // LM trajectory with the oracle)
+    ba_camred camred;            // this pass's camera reduction
+    int camred_pending;          // ... to run inside the MFMA Schur launch
+    int fuse_camred;             // 1: it may (fast path, MFMA groups)
     int mfma;          // fast path: 1 = some MFMA Schur chunks (k_schur_mfma: groups
                        // [0, ngrp_mf)), 0 = term lists only (k_schur_group)
     int no_mfma;       // option: force the term-list Schur kernel
@@ -228,7 +248,9 @@ struct ba_dev {
 // ---- ba_kernels.hip ----
 int ba_launch_rotations(ba_dev *d, const double *a, double *rot, int all5);
 int ba_launch_linearize(ba_dev *d, ba_flags f);
-int ba_launch_camera_reduce(ba_dev *d, ba_flags f);
+// fuse = 1 (an LM pass whose MFMA Schur launch follows): only records the
+// reduction for that launch when the plan has MFMA groups
+int ba_launch_camera_reduce(ba_dev *d, ba_flags f, int fuse = 0);
 int ba_launch_damp_point(ba_dev *d, double lambda);
 int ba_launch_schur(ba_dev *d, double lambda);
 int ba_launch_assemble(ba_dev *d);

@@ -434,23 +434,26 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
 // p + 2P, ... (P = 256 / (NU + NA) streams, so ~P loads are in flight per
 // entry instead of one dependent chain); the streams are then added in
 // stream order.  Fixed order -> deterministic run to run.
+// workgroup j of the camera reduction (j == m: the SSE)
 template <int NA>
-__global__ __launch_bounds__(256) void k_camera_reduce_chunks(const int *__restrict__ cam_eptr,
-                                                              const int *__restrict__ cam_eslots,
-                                                              const double *__restrict__ upart,
-                                                              int m, ba_flags f,
-                                                              const unsigned char *__restrict__ pivot,
-                                                              double *__restrict__ U,
-                                                              double *__restrict__ eA,
-                                                              const double *__restrict__ chsse,
-                                                              int nch, double *__restrict__ sse_out,
-                                                              double *__restrict__ sse_out2)
+__device__ __forceinline__ void camera_reduce_wg(int j, const ba_camred &a)
 {
+    const int *__restrict__ cam_eptr = a.cam_eptr;
+    const int *__restrict__ cam_eslots = a.cam_eslots;
+    const double *__restrict__ upart = a.upart;
+    const int m = a.m, nch = a.nch;
+    const ba_flags f = a.f;
+    const unsigned char *__restrict__ pivot = a.pivot;
+    double *__restrict__ U = a.U;
+    double *__restrict__ eA = a.eA;
+    const double *__restrict__ chsse = a.chsse;
+    double *__restrict__ sse_out = a.sse_out;
+    double *__restrict__ sse_out2 = a.sse_out2;
     constexpr int NU = NA * (NA + 1) / 2;
     constexpr int NT = NU + NA;
     constexpr int P = 256 / NT;
     __shared__ double part[P][NT];
-    const int j = blockIdx.x, tid = threadIdx.x;
+    const int tid = threadIdx.x;
     if (j == m) {   // extra workgroup: the linearisation SSE (old_error), fixed order
         double v[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         int q = tid;
@@ -486,6 +489,12 @@ __global__ __launch_bounds__(256) void k_camera_reduce_chunks(const int *__restr
     } else {
         eA[(size_t)NA * j + tid - NU] = acc;
     }
+}
+
+template <int NA>
+__global__ __launch_bounds__(256) void k_camera_reduce_chunks(ba_camred a)
+{
+    camera_reduce_wg<NA>(blockIdx.x, a);
 }
 
 // -------------------------------------------------------------------------
@@ -939,8 +948,16 @@ __global__ __launch_bounds__(256, (NA == 6) ? BA_MF_WAVES : 1) void k_schur_mfma
     const int *__restrict__ ch_obase, const int *__restrict__ ch_blob,
     const unsigned *__restrict__ blob, const double *__restrict__ W,
     const double *__restrict__ Vinv, const double *__restrict__ eB, int nobs_all, int n_all,
-    int gcap, int ecap, double *__restrict__ spart, double *__restrict__ epart)
+    int gcap, int ecap, double *__restrict__ spart, double *__restrict__ epart, int ngrp,
+    ba_camred cred)
 {
+    // workgroups past the groups: the camera reduction of a relinearised pass
+    // (independent of the Schur sums, due before k_schur_reduce), filling the
+    // CUs the groups' tail leaves idle -- no side stream, no fork / join
+    if ((int)blockIdx.x >= ngrp) {
+        camera_reduce_wg<NA>((int)blockIdx.x - ngrp, cred);
+        return;
+    }
     constexpr int WS = 3 * NA;
     constexpr int RT = BA_MF_RT(NA);
     constexpr int NTL = RT * (RT + 1) / 2;
@@ -1745,16 +1762,21 @@ int ba_launch_linearize(ba_dev *d, ba_flags f)
     return -(int)hipGetLastError();
 }
 
-int ba_launch_camera_reduce(ba_dev *d, ba_flags f)
+int ba_launch_camera_reduce(ba_dev *d, ba_flags f, int fuse)
 {
     const int bs = ((d->na * (d->na + 1) / 2 + d->na) + 63) / 64 * 64;
     if (!d->ordered) {
-        KT_B(d);
         // m camera workgroups + one for the SSE: scal[0] and the old_sse slot
         // after U | eA (all-reduced together with them)
+        d->camred = ba_camred{d->cam_eptr, d->cam_eslots, d->upart, d->m, f, d->pivot,
+                              d->U, d->eA, d->chsse, d->nch, d->scal + 0, d->eA + d->ld};
+        if (fuse && d->ngrp_mf > 0 && d->fuse_camred) {   // run by this pass's MFMA Schur launch
+            d->camred_pending = 1;
+            return 0;
+        }
+        KT_B(d);
         BA_DISPATCH(d->na, (k_camera_reduce_chunks<NA><<<d->m + 1, 256, 0, d->stream>>>(
-                               d->cam_eptr, d->cam_eslots, d->upart, d->m, f, d->pivot, d->U,
-                               d->eA, d->chsse, d->nch, d->scal + 0, d->eA + d->ld)));
+                               d->camred)));
         KT_E(d, KT_CAMRED);
         return -(int)hipGetLastError();
     }
@@ -1797,10 +1819,13 @@ static int launch_schur_fast(ba_dev *d, double lambda)
         const size_t sm2 = sizeof(double) * (d->mf_max_s * NA * NA + d->mf_max_e * NA) +
                            sizeof(unsigned) * (size_t)d->mf_max_blob;
         TRY_RC(ba_ensure_dyn_lds((const void *)k_schur_mfma<NA>, sm2));
+        const int ncr = d->camred_pending ? d->m + 1 : 0;
+        d->camred_pending = 0;
         KT_B(d);
-        k_schur_mfma<NA><<<d->ngrp_mf, 256, sm2, d->stream>>>(
+        k_schur_mfma<NA><<<d->ngrp_mf + ncr, 256, sm2, d->stream>>>(
             d->grp_ch, d->grp_gs, d->grp_ge, d->ch_pt, d->ch_obase, d->ch_blob, d->blob, d->W,
-            d->Vinv, d->eB, d->N, d->n, d->mf_max_s, d->mf_max_e, d->spart, d->epart);
+            d->Vinv, d->eB, d->N, d->n, d->mf_max_s, d->mf_max_e, d->spart, d->epart,
+            d->ngrp_mf, d->camred);
         KT_E(d, KT_SCHUR_MF);
     }
     if (d->ngrp > d->ngrp_mf) {

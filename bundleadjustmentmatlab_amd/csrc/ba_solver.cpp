@@ -1297,6 +1297,7 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
         c->on_pass = o->on_pass;
         c->on_pass_user = o->on_pass_user;
         c->d.no_mfma = o->schur_kernel == 1;
+        c->d.fuse_camred = BA_FUSE_CAMRED;
         c->d.ndb = o->semantics == 1 ? p->num_a : 6;
         rc = ctx_setup(c, p, h, pt_ptr_all, lower_blocks, all_diag, stage_mode);
         if (rc) break;
@@ -1491,7 +1492,10 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
         // accepted step swaps in the one k_camera_update built for a_new
         TRY(ba_launch_linearize(&d, c->flags));
         mark(c, 1);
-        if (!d.ordered && c->world == 1 && !c->timing) {
+        if (!d.ordered && d.fuse_camred && d.ngrp_mf > 0) {
+            // U / eA / old SSE: workgroups of this pass's MFMA Schur launch
+            TRY(ba_launch_camera_reduce(&d, c->flags, 1));
+        } else if (!d.ordered && c->world == 1 && !c->timing) {
             // U / eA / old SSE on the side stream, overlapping V*^-1 and the
             // Schur chunks (no collective in between at world size 1);
             // launch_schur_fast joins before k_schur_reduce
