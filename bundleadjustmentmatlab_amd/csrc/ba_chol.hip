@@ -24,6 +24,7 @@
 // then per k descending k_backward: x_k = L_kk^-T z_k, z_j -= L_kj^T x_k.
 #include "ba_internal.h"
 
+#include <cstdlib>
 #include <vector>
 
 #define NB 64
@@ -945,6 +946,36 @@ __global__ __launch_bounds__(256) void k_cr_update(double *__restrict__ S, long 
 // ---------------------------------------------------------------------------
 #define T32 32
 
+// In-launch hand-offs of the one-launch cyclic reduction (k_cr32_fused):
+// every byte one workgroup hands to another is stored write-through (sc1,
+// 8-byte agent-scope atomic stores) and every load of it is an sc1 load
+// (8-byte agent-scope atomic loads, L1 bypassed), one workgroup per CU, the
+// flag an sc1 store after each storing wave's vmcnt(0) and a barrier: the
+// first row of MI355X_MICROARCH.md's hand-off table (no acquire fence).
+// SC = false: plain accesses (the per-level kernels, whose hand-offs cross a
+// launch boundary).
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+typedef __attribute__((address_space(1))) unsigned gu32_t;
+
+template <bool SC> __device__ __forceinline__ double ldg(const double *p)
+{
+    if constexpr (SC)
+        return __builtin_bit_cast(
+            double, __hip_atomic_load((gu64_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    else
+        return *p;
+}
+
+template <bool SC> __device__ __forceinline__ void stg(double *p, double v)
+{
+    if constexpr (SC)
+        __hip_atomic_store((gu64_t *)p, __builtin_bit_cast(unsigned long long, v),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        *p = v;
+}
+
+template <bool SC = false>
 __device__ __forceinline__ void load32(const double *__restrict__ S, long long lds, int TB,
                                        long long ld, int ti, int tj, double *T, bool transposed,
                                        bool diag)
@@ -957,7 +988,7 @@ __device__ __forceinline__ void load32(const double *__restrict__ S, long long l
         const int c = c0 + 8 * u;
         const long long gc = (long long)TB * tj + c;
         const bool ok = r < TB && c < TB && gr < ld && gc < ld;
-        v[u] = ok ? S[gr + lds * gc] : ((diag && r == c) ? 1.0 : 0.0);
+        v[u] = ok ? ldg<SC>(S + gr + lds * gc) : ((diag && r == c) ? 1.0 : 0.0);
     }
 #pragma unroll
     for (int u = 0; u < 4; u++) {
@@ -969,6 +1000,7 @@ __device__ __forceinline__ void load32(const double *__restrict__ S, long long l
     }
 }
 
+template <bool SC = false>
 __device__ __forceinline__ void store32(double *__restrict__ S, long long lds, int TB,
                                         long long ld, int ti, int tj, const double *T)
 {
@@ -978,24 +1010,26 @@ __device__ __forceinline__ void store32(double *__restrict__ S, long long lds, i
     for (int u = 0; u < 4; u++) {
         const int c = c0 + 8 * u;
         const long long gc = (long long)TB * tj + c;
-        if (r < TB && c < TB && gr < ld && gc < ld) S[gr + lds * gc] = T[r * LP + c];
+        if (r < TB && c < TB && gr < ld && gc < ld) stg<SC>(S + gr + lds * gc, T[r * LP + c]);
     }
 }
 
 // 32 x 32 LDS tile <-> row-major dst[r * 32 + c]
+template <bool SC = false>
 __device__ __forceinline__ void store_rm32(double *__restrict__ dst, const double *T)
 {
     const int c = threadIdx.x & 31, r0 = threadIdx.x >> 5;
 #pragma unroll
-    for (int u = 0; u < 4; u++) dst[(r0 + 8 * u) * T32 + c] = T[(r0 + 8 * u) * LP + c];
+    for (int u = 0; u < 4; u++) stg<SC>(dst + (r0 + 8 * u) * T32 + c, T[(r0 + 8 * u) * LP + c]);
 }
 
+template <bool SC = false>
 __device__ __forceinline__ void load_rm32(const double *__restrict__ src, double *T)
 {
     const int c = threadIdx.x & 31, r0 = threadIdx.x >> 5;
     double v[4];
 #pragma unroll
-    for (int u = 0; u < 4; u++) v[u] = src[(r0 + 8 * u) * T32 + c];
+    for (int u = 0; u < 4; u++) v[u] = ldg<SC>(src + (r0 + 8 * u) * T32 + c);
 #pragma unroll
     for (int u = 0; u < 4; u++) T[(r0 + 8 * u) * LP + c] = v[u];
 }
@@ -1069,10 +1103,76 @@ __device__ __forceinline__ bool potrf32_inv(double *As, double *Li, double *Xs)
     return bad32 == 0;
 }
 
-// factor step: role 0 factors D_e, writes L_e^-1 (row-major 32 x 32) and
-// y_e = L_e^-1 r_e; role 1 / 2 (split, one workgroup each, redoing the same
-// factorisation) or the same workgroup (no split) form Lp_e = C(p, e) L_e^-T
-// and Lq_e = C(q, e) L_e^-T into crL.
+// LDS of one cyclic-reduction record: five 32-row tiles, the 16-row scratch
+// of potrf32_inv, five 32-vectors and the gemv partials.  The per-level
+// kernels declare it as static LDS; k_cr32_fused carves every record type
+// (factor, fused level, survivor, back substitution) from one pool of this
+// shape (96 KB: one workgroup per CU, which its hand-offs rely on).
+struct cr32_lds {
+    double *As, *Bs, *Cs, *Ds, *Es, *Xs;
+    double *rk, *ym, *yp, *um, *up;
+    double (*part)[T32];
+};
+
+#define CR32_LDS_DECL                                                                      \
+    __shared__ __attribute__((aligned(16))) double cr_As[T32 * LP], cr_Bs[T32 * LP],      \
+        cr_Cs[T32 * LP], cr_Ds[T32 * LP], cr_Es[T32 * LP];                                 \
+    __shared__ __attribute__((aligned(16))) double cr_Xs[16 * LP];                         \
+    __shared__ __attribute__((aligned(16))) double cr_v[5][T32];                           \
+    __shared__ __attribute__((aligned(16))) double cr_part[8][T32];                        \
+    const cr32_lds sh{cr_As, cr_Bs, cr_Cs, cr_Ds, cr_Es, cr_Xs, cr_v[0], cr_v[1], cr_v[2], \
+                      cr_v[3], cr_v[4], cr_part}
+
+// factor step (level 0, on the assembled S): role 0 factors D_e, writes L_e^-1
+// (row-major 32 x 32) and y_e = L_e^-1 r_e; role 1 / 2 (split, one workgroup
+// each, redoing the same factorisation) or the same workgroup (role -1: no
+// split) form Lp_e = C(p, e) L_e^-T and Lq_e = C(q, e) L_e^-T into crL.
+template <bool SC>
+__device__ __forceinline__ void cr32_factor_body(const cr32_lds &sh, double *S, long long lds,
+                                                 int TB, long long ld, int e, int p, int q,
+                                                 int role, int nt, double *linv, double *crL,
+                                                 const double *rhs, double *y, double *status)
+{
+    double *As = sh.As, *Bs = sh.Bs, *Cs = sh.Cs, *Xs = sh.Xs, *rk = sh.rk, *yk = sh.ym;
+    const int tid = threadIdx.x;
+    const long long T2 = (long long)T32 * T32;
+    load32<SC>(S, lds, TB, ld, e, e, As, false, true);
+    if (role == 1) load32<SC>(S, lds, TB, ld, e, p, Cs, true, false);   // C(p, e) = tile(e, p)^T
+    if (role == 2) load32<SC>(S, lds, TB, ld, q, e, Cs, false, false);  // C(q, e) = tile(q, e)
+    if (role <= 0 && tid < T32) {
+        const long long g = (long long)TB * e + tid;
+        rk[tid] = (tid < TB && g < ld) ? ldg<SC>(rhs + g) : 0.0;
+    }
+    __syncthreads();
+    const bool ok = potrf32_inv(As, Bs, Xs);
+    if (role <= 0) {
+        gemv32(Bs, rk, sh.part, yk, false);
+        if (tid < TB) stg<SC>(y + (long long)TB * e + tid, yk[tid]);
+        store_rm32<SC>(linv + T2 * e, Bs);
+        if (tid == 0 && !ok) status[0] = 1.0;
+        if (role == 0) return;   // split: roles 1 and 2 form the panels
+    }
+    for (int side = 1; side <= 2; side++) {
+        if (role > 0 && role != side) continue;
+        const int nb = side == 1 ? p : q;
+        if (nb < 0) continue;
+        if (role < 0) {
+            __syncthreads();
+            if (side == 1)
+                load32<SC>(S, lds, TB, ld, e, p, Cs, true, false);
+            else
+                load32<SC>(S, lds, TB, ld, q, e, Cs, false, false);
+            __syncthreads();
+        }
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        acc = mfma32_nt(Cs, Bs, acc);   // C L^-T: [r][c] = sum_t C[r][t] Li[c][t]
+        __syncthreads();
+        put32(Cs, acc, 1.0, false);
+        __syncthreads();
+        store_rm32<SC>(crL + T2 * (side == 1 ? e : nt + e), Cs);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_cr32_factor(double *__restrict__ S, long long lds,
                                                      int TB, long long ld,
                                                      const int *__restrict__ elim, int nt,
@@ -1086,46 +1186,11 @@ __global__ __launch_bounds__(256) void k_cr32_factor(double *__restrict__ S, lon
     __shared__ __attribute__((aligned(16))) double Xs[16 * LP];
     __shared__ double rk[T32], yk[T32];
     __shared__ double part[8][T32];
-    const int tid = threadIdx.x;
+    const cr32_lds sh{As, Bs, Cs, nullptr, nullptr, Xs, rk, yk, nullptr, nullptr, nullptr, part};
     const int x = split ? blockIdx.x / 3 : blockIdx.x, role = split ? blockIdx.x % 3 : -1;
     const int e = elim[3 * x], p = elim[3 * x + 1], q = elim[3 * x + 2];
     if ((role == 1 && p < 0) || (role == 2 && q < 0)) return;
-    const long long T2 = (long long)T32 * T32;
-    load32(S, lds, TB, ld, e, e, As, false, true);
-    if (role == 1) load32(S, lds, TB, ld, e, p, Cs, true, false);   // C(p, e) = tile(e, p)^T
-    if (role == 2) load32(S, lds, TB, ld, q, e, Cs, false, false);  // C(q, e) = tile(q, e)
-    if (role <= 0 && tid < T32) {
-        const long long g = (long long)TB * e + tid;
-        rk[tid] = (tid < TB && g < ld) ? rhs[g] : 0.0;
-    }
-    __syncthreads();
-    const bool ok = potrf32_inv(As, Bs, Xs);
-    if (role <= 0) {
-        gemv32(Bs, rk, part, yk, false);
-        if (tid < TB) y[(long long)TB * e + tid] = yk[tid];
-        store_rm32(linv + T2 * e, Bs);
-        if (tid == 0 && !ok) status[0] = 1.0;
-        if (role == 0) return;   // split: roles 1 and 2 form the panels
-    }
-    for (int side = 1; side <= 2; side++) {
-        if (role > 0 && role != side) continue;
-        const int nb = side == 1 ? p : q;
-        if (nb < 0) continue;
-        if (role < 0) {
-            __syncthreads();
-            if (side == 1)
-                load32(S, lds, TB, ld, e, p, Cs, true, false);
-            else
-                load32(S, lds, TB, ld, q, e, Cs, false, false);
-            __syncthreads();
-        }
-        d4 acc = {0.0, 0.0, 0.0, 0.0};
-        acc = mfma32_nt(Cs, Bs, acc);   // C L^-T: [r][c] = sum_t C[r][t] Li[c][t]
-        __syncthreads();
-        put32(Cs, acc, 1.0, false);
-        __syncthreads();
-        store_rm32(crL + T2 * (side == 1 ? e : nt + e), Cs);
-    }
+    cr32_factor_body<false>(sh, S, lds, TB, ld, e, p, q, role, nt, linv, crL, rhs, y, status);
 }
 
 // Level L >= 1 of the camera-aligned CR with the previous level's update folded
@@ -1137,8 +1202,74 @@ __global__ __launch_bounds__(256) void k_cr32_factor(double *__restrict__ S, lon
 // the tile e eliminated between them.  Workgroups 3x + role for the tiles
 // eliminated here (role 0: apply the update in LDS, factor, y, L^-1; roles 1 /
 // 2: the same factorisation plus their fill tile C(p, e) / C(q, e), then the
-// panel), then one workgroup per surviving tile (apply the update, write D_k
-// and r_k back).  Records: fused (e, p, q, em, ep), survivor (k, em, ep).
+// panel), then one workgroup per surviving tile (role 3: apply the update,
+// write D_k and r_k back).  Records: fused (e, p, q, em, ep), survivor (k, em, ep).
+template <bool SC>
+__device__ __forceinline__ void cr32_level_body(const cr32_lds &sh, double *S, long long lds,
+                                                int TB, long long ld, int k, int p, int q, int em,
+                                                int ep, int role, int nt, double *linv,
+                                                double *crL, double *rhs, double *y,
+                                                double *status)
+{
+    double *As = sh.As, *Bs = sh.Bs, *Cs = sh.Cs, *Ds = sh.Ds, *Es = sh.Es, *Xs = sh.Xs;
+    double *rk = sh.rk, *ym = sh.ym, *yp = sh.yp, *um = sh.um, *up = sh.up;
+    const int tid = threadIdx.x;
+    const long long T2 = (long long)T32 * T32;
+    const bool surv = role == 3;
+    load32<SC>(S, lds, TB, ld, k, k, As, false, true);
+    load_rm32<SC>(crL + T2 * (nt + em), Bs);            // L(k, em)
+    if (ep >= 0) load_rm32<SC>(crL + T2 * ep, Cs);      // L(k, ep)
+    if (role == 1) load_rm32<SC>(crL + T2 * em, Ds);    // L(p, em)
+    if (role == 2) load_rm32<SC>(crL + T2 * (nt + ep), Ds);   // L(q, ep)
+    const bool rows = surv || role == 0;
+    if (rows && tid < T32) {
+        const long long g = (long long)TB * k + tid;
+        rk[tid] = (tid < TB && g < ld) ? ldg<SC>(rhs + g) : 0.0;
+        ym[tid] = tid < TB ? ldg<SC>(y + (long long)TB * em + tid) : 0.0;
+        yp[tid] = (ep >= 0 && tid < TB) ? ldg<SC>(y + (long long)TB * ep + tid) : 0.0;
+    }
+    __syncthreads();
+    if (role == 1 || role == 2) {   // the fill: C(p, e) = -L(p, em) L(e, em)^T | C(q, e) = -L(q, ep) L(e, ep)^T
+        d4 f = {0.0, 0.0, 0.0, 0.0};
+        f = mfma32_nt(Ds, role == 1 ? Bs : Cs, f);
+        put32(Es, f, -1.0, false);
+    }
+    {
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        acc = mfma32_nt(Bs, Bs, acc);
+        if (ep >= 0) acc = mfma32_nt(Cs, Cs, acc);
+        put32(As, acc, -1.0, true);   // each thread updates the elements it owns
+    }
+    if (rows) {
+        gemv32(Bs, ym, sh.part, um, false);
+        if (ep >= 0) gemv32(Cs, yp, sh.part, up, false);
+        if (tid < T32) rk[tid] = (rk[tid] - um[tid]) - (ep >= 0 ? up[tid] : 0.0);
+    }
+    __syncthreads();
+    if (surv) {
+        store32<SC>(S, lds, TB, ld, k, k, As);
+        if (tid < TB) {
+            const long long g = (long long)TB * k + tid;
+            if (g < ld) stg<SC>(rhs + g, rk[tid]);
+        }
+        return;
+    }
+    const bool ok = potrf32_inv(As, Bs, Xs);   // L^-1 over L(k, em), no longer needed
+    if (role == 0) {
+        gemv32(Bs, rk, sh.part, um, false);
+        if (tid < TB) stg<SC>(y + (long long)TB * k + tid, um[tid]);
+        store_rm32<SC>(linv + T2 * k, Bs);
+        if (tid == 0 && !ok) status[0] = 1.0;
+        return;
+    }
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    acc = mfma32_nt(Es, Bs, acc);   // C L^-T
+    __syncthreads();
+    put32(Es, acc, 1.0, false);
+    __syncthreads();
+    store_rm32<SC>(crL + T2 * (role == 1 ? k : nt + k), Es);
+}
+
 __global__ __launch_bounds__(256) void k_cr32_level(double *__restrict__ S, long long lds, int TB,
                                                     long long ld, const int *__restrict__ frec,
                                                     int ne, const int *__restrict__ srec, int nt,
@@ -1148,15 +1279,9 @@ __global__ __launch_bounds__(256) void k_cr32_level(double *__restrict__ S, long
                                                     double *__restrict__ y,
                                                     double *__restrict__ status)
 {
-    __shared__ __attribute__((aligned(16))) double As[T32 * LP], Bs[T32 * LP], Cs[T32 * LP];
-    __shared__ __attribute__((aligned(16))) double Ds[T32 * LP], Es[T32 * LP];
-    __shared__ __attribute__((aligned(16))) double Xs[16 * LP];
-    __shared__ double rk[T32], ym[T32], yp[T32], um[T32], up[T32];
-    __shared__ double part[8][T32];
-    const int tid = threadIdx.x;
-    const long long T2 = (long long)T32 * T32;
+    CR32_LDS_DECL;
     const bool surv = (int)blockIdx.x >= 3 * ne;
-    int k, p = -1, q = -1, em, ep, role = 0;
+    int k, p = -1, q = -1, em, ep, role = 3;
     if (surv) {
         const int *r = srec + 3 * (blockIdx.x - 3 * ne);
         k = r[0];
@@ -1172,58 +1297,8 @@ __global__ __launch_bounds__(256) void k_cr32_level(double *__restrict__ S, long
         ep = r[4];
         if ((role == 1 && p < 0) || (role == 2 && q < 0)) return;
     }
-    load32(S, lds, TB, ld, k, k, As, false, true);
-    load_rm32(crL + T2 * (nt + em), Bs);            // L(k, em)
-    if (ep >= 0) load_rm32(crL + T2 * ep, Cs);      // L(k, ep)
-    if (role == 1) load_rm32(crL + T2 * em, Ds);    // L(p, em)
-    if (role == 2) load_rm32(crL + T2 * (nt + ep), Ds);   // L(q, ep)
-    const bool rows = surv || role == 0;
-    if (rows && tid < T32) {
-        const long long g = (long long)TB * k + tid;
-        rk[tid] = (tid < TB && g < ld) ? rhs[g] : 0.0;
-        ym[tid] = tid < TB ? y[(long long)TB * em + tid] : 0.0;
-        yp[tid] = (ep >= 0 && tid < TB) ? y[(long long)TB * ep + tid] : 0.0;
-    }
-    __syncthreads();
-    if (role > 0) {   // the fill: C(p, e) = -L(p, em) L(e, em)^T | C(q, e) = -L(q, ep) L(e, ep)^T
-        d4 f = {0.0, 0.0, 0.0, 0.0};
-        f = mfma32_nt(Ds, role == 1 ? Bs : Cs, f);
-        put32(Es, f, -1.0, false);
-    }
-    {
-        d4 acc = {0.0, 0.0, 0.0, 0.0};
-        acc = mfma32_nt(Bs, Bs, acc);
-        if (ep >= 0) acc = mfma32_nt(Cs, Cs, acc);
-        put32(As, acc, -1.0, true);   // each thread updates the elements it owns
-    }
-    if (rows) {
-        gemv32(Bs, ym, part, um, false);
-        if (ep >= 0) gemv32(Cs, yp, part, up, false);
-        if (tid < T32) rk[tid] = (rk[tid] - um[tid]) - (ep >= 0 ? up[tid] : 0.0);
-    }
-    __syncthreads();
-    if (surv) {
-        store32(S, lds, TB, ld, k, k, As);
-        if (tid < TB) {
-            const long long g = (long long)TB * k + tid;
-            if (g < ld) rhs[g] = rk[tid];
-        }
-        return;
-    }
-    const bool ok = potrf32_inv(As, Bs, Xs);   // L^-1 over L(k, em), no longer needed
-    if (role == 0) {
-        gemv32(Bs, rk, part, um, false);
-        if (tid < TB) y[(long long)TB * k + tid] = um[tid];
-        store_rm32(linv + T2 * k, Bs);
-        if (tid == 0 && !ok) status[0] = 1.0;
-        return;
-    }
-    d4 acc = {0.0, 0.0, 0.0, 0.0};
-    acc = mfma32_nt(Es, Bs, acc);   // C L^-T
-    __syncthreads();
-    put32(Es, acc, 1.0, false);
-    __syncthreads();
-    store_rm32(crL + T2 * (role == 1 ? k : nt + k), Es);
+    cr32_level_body<false>(sh, S, lds, TB, ld, k, p, q, em, ep, role, nt, linv, crL, rhs, y,
+                           status);
 }
 
 // back substitution: x_e = L_e^-T (y_e - Lp_e^T x_p - Lq_e^T x_q)
@@ -1263,40 +1338,30 @@ __global__ __launch_bounds__(256) void k_cr32_back(const int *__restrict__ elim,
     }
 }
 
-// All levels of the back substitution in ONE launch (VERDICT r1 item 6: the
-// 8 level launches were at the launch floor).  Workgroup b takes elimination
-// record nrec-1-b (the deepest level first); it prefetches its three tiles,
-// then waits for x_p and x_q, which the workgroups of the tiles eliminated
+// One record of the one-launch back substitution: it prefetches its three
+// tiles, then waits for x_p and x_q, which the records of the tiles eliminated
 // above it publish as epoch-tagged 8-byte granules {epoch, 32-bit half}
 // (write-through agent-scope stores: the data is the flag, no fences;
 // MI355X_MICROARCH.md / cdna_hip_programming.md Guideline 16, R2).  One wave
-// sweeps one neighbour's 64 granules until every tag matches.  Every record's
-// neighbours are eliminated at higher levels, so the dependencies form a tree
-// from the top level down; the launch is used only when all n32 workgroups
-// are co-resident (n32 <= 2 x CUs).  A spin that never ends sets
-// status = 2 (the pass then takes the pinv path) instead of hanging.  Same
-// arithmetic as k_cr32_back.
-__global__ __launch_bounds__(256) void k_cr32_back_all(const int *__restrict__ elim, int nrec,
-                                                       int nt, int TB, long long ld,
-                                                       const double *__restrict__ linv,
-                                                       const double *__restrict__ crL,
-                                                       const double *__restrict__ y,
-                                                       double *__restrict__ x,
-                                                       unsigned long long *__restrict__ xg,
-                                                       unsigned epoch, double *status)
+// sweeps one neighbour's 64 granules until every tag matches; a spin that
+// never ends sets status = 2 (the pass then takes the pinv path) instead of
+// hanging.  Same arithmetic as k_cr32_back.
+template <bool SC>
+__device__ __forceinline__ void cr32_back_body(const cr32_lds &sh, int e, int p, int q, int nt,
+                                               int TB, long long ld, const double *linv,
+                                               const double *crL, const double *y, double *x,
+                                               unsigned long long *xg, unsigned epoch,
+                                               double *status)
 {
-    __shared__ __attribute__((aligned(16))) double Lp[T32 * LP], Lq[T32 * LP], Li[T32 * LP];
-    __shared__ __attribute__((aligned(16))) double t[T32], xp[T32], xq[T32], u[T32];
-    __shared__ double part[8][T32];
+    double *Lp = sh.As, *Lq = sh.Bs, *Li = sh.Cs;
+    double *t = sh.rk, *xp = sh.ym, *xq = sh.yp, *u = sh.um;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int rec = nrec - 1 - (int)blockIdx.x;
-    const int e = elim[3 * rec], p = elim[3 * rec + 1], q = elim[3 * rec + 2];
     const long long T2 = (long long)T32 * T32;
-    // the tiles (written by earlier launches): plain loads, in flight while we wait
-    if (p >= 0) load_rm32(crL + T2 * e, Lp);
-    if (q >= 0) load_rm32(crL + T2 * (nt + e), Lq);
-    load_rm32(linv + T2 * e, Li);
-    if (tid < T32) t[tid] = tid < TB ? y[(long long)TB * e + tid] : 0.0;
+    // the tiles: loads in flight while we wait
+    if (p >= 0) load_rm32<SC>(crL + T2 * e, Lp);
+    if (q >= 0) load_rm32<SC>(crL + T2 * (nt + e), Lq);
+    load_rm32<SC>(linv + T2 * e, Li);
+    if (tid < T32) t[tid] = tid < TB ? ldg<SC>(y + (long long)TB * e + tid) : 0.0;
     if (wv < 2) {
         const int nb = wv == 0 ? p : q;
         if (nb >= 0) {
@@ -1317,16 +1382,16 @@ __global__ __launch_bounds__(256) void k_cr32_back_all(const int *__restrict__ e
     }
     __syncthreads();
     if (p >= 0) {
-        gemv32(Lp, xp, part, u, true);
+        gemv32(Lp, xp, sh.part, u, true);
         if (tid < T32) t[tid] -= u[tid];
         __syncthreads();
     }
     if (q >= 0) {
-        gemv32(Lq, xq, part, u, true);
+        gemv32(Lq, xq, sh.part, u, true);
         if (tid < T32) t[tid] -= u[tid];
         __syncthreads();
     }
-    gemv32(Li, t, part, u, true);   // x_e = L_e^-T t (ends with a barrier)
+    gemv32(Li, t, sh.part, u, true);   // x_e = L_e^-T t (ends with a barrier)
     if (wv == 0) {   // publish x_e: 64 granules, one 8-byte write-through store each
         const unsigned h = reinterpret_cast<const unsigned *>(u)[lane];
         __hip_atomic_store(xg + 64 * (size_t)e + lane, ((unsigned long long)epoch << 32) | h,
@@ -1336,6 +1401,157 @@ __global__ __launch_bounds__(256) void k_cr32_back_all(const int *__restrict__ e
         const long long g = (long long)TB * e + tid;
         if (g < ld) x[g] = u[tid];
     }
+}
+
+// All levels of the back substitution in ONE launch (VERDICT r1 item 6: the
+// 8 level launches were at the launch floor).  Workgroup b takes elimination
+// record nrec-1-b (the deepest level first).  Every record's neighbours are
+// eliminated at higher levels, so the dependencies form a tree from the top
+// level down; the launch is used only when all workgroups are co-resident
+// (nrec <= 2 x CUs).
+__global__ __launch_bounds__(256) void k_cr32_back_all(const int *__restrict__ elim, int nrec,
+                                                       int nt, int TB, long long ld,
+                                                       const double *__restrict__ linv,
+                                                       const double *__restrict__ crL,
+                                                       const double *__restrict__ y,
+                                                       double *__restrict__ x,
+                                                       unsigned long long *__restrict__ xg,
+                                                       unsigned epoch, double *status)
+{
+    __shared__ __attribute__((aligned(16))) double Lp[T32 * LP], Lq[T32 * LP], Li[T32 * LP];
+    __shared__ __attribute__((aligned(16))) double t[T32], xp[T32], xq[T32], u[T32];
+    __shared__ double part[8][T32];
+    const cr32_lds sh{Lp, Lq, Li, nullptr, nullptr, nullptr, t, xp, xq, u, nullptr, part};
+    const int rec = nrec - 1 - (int)blockIdx.x;
+    const int e = elim[3 * rec], p = elim[3 * rec + 1], q = elim[3 * rec + 2];
+    cr32_back_body<false>(sh, e, p, q, nt, TB, ld, linv, crL, y, x, xg, epoch, status);
+}
+
+// ---------------------------------------------------------------------------
+// The whole camera-aligned cyclic reduction in ONE launch: the level-0
+// factor records (3 per eliminated tile), then per level L >= 1 the fused
+// records (3 per eliminated tile) and the survivor records, then the back
+// substitution records deepest level first -- the schedule and arithmetic of
+// k_cr32_factor + k_cr32_level x (nl - 1) + k_cr32_back_all, record for record
+// (bit-identical), with the launch boundaries replaced by per-record
+// dependencies: a record waits only for the records whose outputs it reads,
+//   level L >= 1, tile k (neighbours em / ep eliminated at L-1):
+//     roles 0..2 of em and ep at L-1 (L(k, em), L(k, ep), y, the fill panels)
+//     and k's own survivor record at L-1 (D_k, r_k) when L >= 2;
+//   back record of e (eliminated at Le): roles 0..2 of e at Le, then the
+//     x granules of its neighbours (as k_cr32_back_all).
+// Hand-offs: payload stored sc1 (stg<true>), every storing wave's vmcnt(0),
+// a barrier, one lane's sc1 flag store {epoch} per (level, tile, role); the
+// consumer's wave 0 polls its <= 7 flags (relaxed agent loads), a barrier,
+// then sc1 loads (ldg<true>) of every handed-off byte.  The 96 KB LDS pool
+// keeps one workgroup per CU (the row of MI355X_MICROARCH.md's hand-off table
+// this protocol follows).  Records wait only on records with lower block
+// indices, so in-order dispatch makes progress without co-residency; every
+// spin is bounded (status = 2: the pass takes the pinv path).
+// ---------------------------------------------------------------------------
+#define BA_CR_MAXLEV 30
+struct cr32_fplan {
+    int nl, nrec;
+    int b0[BA_CR_MAXLEV + 2];      // first block of level L; b0[nl] = first back block
+    int fofs[BA_CR_MAXLEV + 1];    // level L >= 1: first fused record in crf
+    int sofs[BA_CR_MAXLEV + 1];    //               first survivor record in crs
+    int eofs[BA_CR_MAXLEV + 2];    // elimination records of level L in cr_elim
+};
+
+__device__ __forceinline__ void cr32_wait_flags(const unsigned *flag, int nw, const int w[8],
+                                                unsigned epoch, double *status)
+{
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        int idx = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+            if (lane == q) idx = w[q];
+        for (unsigned spins = 0;; spins++) {
+            const bool ok = lane >= nw || __hip_atomic_load((const gu32_t *)(flag + idx),
+                                                            __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT) == epoch;
+            if (__all(ok)) break;
+            if (spins >= BA_BACK_SPIN_MAX) {
+                if (lane == 0) status[0] = 2.0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void cr32_publish(unsigned *flag, unsigned epoch)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store((gu32_t *)flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, int TB, long long ld,
+                                                    const int *__restrict__ elim,
+                                                    const int *__restrict__ frec,
+                                                    const int *__restrict__ srec, int nt,
+                                                    double *linv, double *crL, double *rhs,
+                                                    double *y, double *x, unsigned *flag,
+                                                    unsigned long long *xg, unsigned epoch,
+                                                    double *status, cr32_fplan P)
+{
+    CR32_LDS_DECL;
+    const int b = blockIdx.x;
+    int L = 0;
+    while (L < P.nl && b >= P.b0[L + 1]) L++;
+    // flag word of (level, tile, role): role 3 = survivor
+    auto fw = [&](int lev, int t, int r) { return 4 * (lev * nt + t) + r; };
+    if (L == 0) {
+        const int xr = b / 3, role = b % 3;
+        const int e = elim[3 * xr], p = elim[3 * xr + 1], q = elim[3 * xr + 2];
+        if (!((role == 1 && p < 0) || (role == 2 && q < 0)))
+            cr32_factor_body<true>(sh, S, lds, TB, ld, e, p, q, role, nt, linv, crL, rhs, y,
+                                   status);
+        cr32_publish(flag + fw(0, e, role), epoch);
+        return;
+    }
+    if (L < P.nl) {
+        const int r = b - P.b0[L];
+        const int ne = (P.b0[L + 1] - P.b0[L]) - (P.sofs[L + 1] - P.sofs[L]);   // 3 x fused
+        int k, p = -1, q = -1, em, ep, role = 3;
+        if (r >= ne) {
+            const int *sr = srec + 3 * (P.sofs[L] + r - ne);
+            k = sr[0];
+            em = sr[1];
+            ep = sr[2];
+        } else {
+            const int *fr = frec + 5 * (P.fofs[L] + r / 3);
+            role = r % 3;
+            k = fr[0];
+            p = fr[1];
+            q = fr[2];
+            em = fr[3];
+            ep = fr[4];
+        }
+        int w[8] = {0, 0, 0, 0, 0, 0, 0, 0}, nw = 0;
+        for (int rr = 0; rr < 3; rr++) w[nw++] = fw(L - 1, em, rr);
+        if (ep >= 0)
+            for (int rr = 0; rr < 3; rr++) w[nw++] = fw(L - 1, ep, rr);
+        if (L >= 2) w[nw++] = fw(L - 1, k, 3);
+        cr32_wait_flags(flag, nw, w, epoch, status);
+        if (!((role == 1 && p < 0) || (role == 2 && q < 0)))
+            cr32_level_body<true>(sh, S, lds, TB, ld, k, p, q, em, ep, role, nt, linv, crL, rhs,
+                                  y, status);
+        cr32_publish(flag + fw(L, k, role), epoch);
+        return;
+    }
+    // back substitution, deepest record first
+    const int rec = P.nrec - 1 - (b - P.b0[P.nl]);
+    int Le = 0;
+    while (Le + 1 < P.nl && rec >= P.eofs[Le + 1]) Le++;
+    const int e = elim[3 * rec], p = elim[3 * rec + 1], q = elim[3 * rec + 2];
+    const int w[8] = {fw(Le, e, 0), fw(Le, e, 1), fw(Le, e, 2), 0, 0, 0, 0, 0};
+    cr32_wait_flags(flag, 3, w, epoch, status);
+    cr32_back_body<true>(sh, e, p, q, nt, TB, ld, linv, crL, y, x, xg, epoch, status);
 }
 
 __global__ __launch_bounds__(256) void k_cr_back(const int *__restrict__ elim, int nt,
@@ -1726,6 +1942,15 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
             VLGBA_CHECK(hipMemsetAsync(d->xgran, 0, sizeof(unsigned long long) * 64 * (size_t)nt,
                                        d->stream));
             d->back_epoch = 0;
+            {   // one-launch CR (k_cr32_fused) unless VLGBA_CR_FUSED=0
+                const char *ev = std::getenv("VLGBA_CR_FUSED");
+                d->cr_fused = !(ev && ev[0] == '0') && nl <= BA_CR_MAXLEV;
+            }
+            if (d->cr_fused) {
+                const size_t nfl = (size_t)4 * nl * nt;
+                TRY_RC(dev_alloc(&d->crflag, sizeof(unsigned) * nfl));
+                VLGBA_CHECK(hipMemsetAsync(d->crflag, 0, sizeof(unsigned) * nfl, d->stream));
+            }
             TRY_RC(dev_alloc(&d->crf, sizeof(int) * (frec.size() + 1)));
             TRY_RC(dev_alloc(&d->crs, sizeof(int) * (srec.size() + 1)));
             if (!frec.empty())
@@ -1786,6 +2011,9 @@ void ba_chol_free(ba_dev *d)
     d->cr_eptr_h = d->cr_kptr_h = nullptr;
     if (d->xgran) ba_dfree(d->xgran);
     d->xgran = nullptr;
+    if (d->crflag) ba_dfree(d->crflag);
+    d->crflag = nullptr;
+    d->cr_fused = 0;
     if (d->crf) ba_dfree(d->crf);
     if (d->crs) ba_dfree(d->crs);
     delete[] d->crf_ptr_h;
@@ -1843,6 +2071,30 @@ int ba_chol_solve(ba_dev *d)
         k_chol_seq<<<1, 256, 0, d->stream>>>(d->S, d->lds, (int)d->ld, d->rhs, d->da,
                                              d->scal + 4);
         KT_E(d, KT_FACTOR);
+        return -(int)hipGetLastError();
+    }
+    if (d->cr_nlev > 0 && d->cr32 && d->cr_fused && d->crflag) {   // one launch
+        const int nl = d->cr_nlev, nrec = d->cr_eptr_h[nl];
+        cr32_fplan P{};
+        P.nl = nl;
+        P.nrec = nrec;
+        P.b0[0] = 0;
+        P.b0[1] = 3 * d->cr_eptr_h[1];
+        for (int l = 1; l < nl; l++) {
+            const int nf = d->crf_ptr_h[l + 1] - d->crf_ptr_h[l];
+            const int ns = d->crs_ptr_h[l + 1] - d->crs_ptr_h[l];
+            P.fofs[l] = d->crf_ptr_h[l];
+            P.sofs[l] = d->crs_ptr_h[l];
+            P.b0[l + 1] = P.b0[l] + 3 * nf + ns;
+        }
+        P.sofs[nl] = d->crs_ptr_h[nl];
+        for (int l = 0; l <= nl; l++) P.eofs[l] = d->cr_eptr_h[l];
+        if (++d->back_epoch == 0) d->back_epoch = 1;
+        KT_B(d);
+        k_cr32_fused<<<P.b0[nl] + nrec, 256, 0, d->stream>>>(
+            d->S, d->lds, d->tb32, d->ld, d->cr_elim, d->crf, d->crs, d->nt32, d->linv, d->crL,
+            d->rhs, d->ywork, d->da, d->crflag, d->xgran, d->back_epoch, d->scal + 4, P);
+        KT_E(d, KT_CR_FACTOR);
         return -(int)hipGetLastError();
     }
     if (d->cr_nlev > 0 && d->cr32) {   // camera-aligned 32-row tiles

@@ -134,6 +134,11 @@ struct ba_dev {
     // 64 epoch-tagged 8-byte granules, read by the tiles of the level below
     unsigned long long *xgran;    // [nt32][64]
     unsigned back_epoch;          // per solve, never 0
+    // the whole CR in one launch (k_cr32_fused): epoch flags per (level, tile,
+    // role 0..2 | survivor); cr_fused = 0 (VLGBA_CR_FUSED=0) keeps the
+    // per-level launches
+    unsigned *crflag;             // [nlev][nt32][4]
+    int cr_fused;
     // reductions: partial sums per block of the reducing kernels, in fixed order
     double *part;      // [3][PART_MAX]
     double *scal;      // [8] : 0 old_sse, 1 new_sse, 2 dpg cams, 3 dpg pts, 4 chol status

@@ -292,7 +292,9 @@ def test_cyclic_reduction_matches_envelope(gpu, num_a, m):
     rows = num_a * (32 // num_a) if num_a == 6 else 64
     nt = -(-num_a * m // rows)
     assert "k_cr_factor" in kcr and "k_factor_step" not in kcr
-    assert kcr["k_cr_factor"][1] == nt.bit_length()    # levels: floor(log2 nt) + 1
+    # levels: floor(log2 nt) + 1 launches, or ONE (k_cr32_fused) for the
+    # camera-aligned tiles
+    assert kcr["k_cr_factor"][1] == (1 if rows <= 32 else nt.bit_length())
     assert "k_factor_step" in kenv and "k_cr_factor" not in kenv
     assert cr.old_sse == env.old_sse
     assert cr.chol_failed == 0 and env.chol_failed == 0
@@ -554,14 +556,46 @@ def test_long_tracks_fast_path(gpu, oracle, kern):
         assert np.max(np.abs(lin[nm] - ref[nm])) <= 1e-13 * np.max(np.abs(ref[nm])), nm
 
 
+def _cr_pass(gpu, sc, num_a, fused, **kw):
+    """One LM pass with the one-launch CR (k_cr32_fused) or the per-level
+    launches (VLGBA_CR_FUSED=0, read when the context is set up): pass info,
+    kernel timers, the step (da, db)."""
+    import os
+    old = os.environ.get("VLGBA_CR_FUSED")
+    os.environ["VLGBA_CR_FUSED"] = "1" if fused else "0"
+    try:
+        a = np.zeros((num_a, sc.m), order="F")
+        a[0:3], a[3:6] = sc.w0, sc.T0
+        if num_a == 7:
+            a[6] = sc.K[0]
+        elif num_a == 10:
+            a[6:10] = sc.K
+        b = np.asfortranarray(sc.X0[:3])
+        ba = gpu.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, num_a, **kw)
+        ba.set_params(a, b)
+        ba.set_timing(True)
+        info = ba.step(relinearize=True, update_lm=False)
+        km = ba.kernel_ms()
+        da, db = ba.last_step()
+        plan = ba.plan_info()
+        ba.close()
+    finally:
+        if old is None:
+            del os.environ["VLGBA_CR_FUSED"]
+        else:
+            os.environ["VLGBA_CR_FUSED"] = old
+    return info, km, np.array(da, copy=True), np.array(db, copy=True), plan
+
+
 def test_cr_back_substitution_one_launch_and_fallback(gpu):
-    """The cyclic reduction's back substitution runs as one launch with in-kernel
-    hand-offs while every elimination record is co-resident (<= 2 x CUs), and
-    as one launch per level beyond; both agree with the envelope Cholesky."""
+    """Per-level CR launches (VLGBA_CR_FUSED=0): the back substitution runs as
+    one launch with in-kernel hand-offs while every elimination record is
+    co-resident (<= 2 x CUs), and as one launch per level beyond; both agree
+    with the envelope Cholesky."""
     from bundleadjustmentmatlab_amd.scene import make_config
     for m, launches in ((200, 1), (3000, None)):
         sc = make_config("cfg2", m=m, n=10 * m, seed=37)
-        cr, kcr = _one_pass(gpu, sc, 6)
+        cr, kcr, _, _, _ = _cr_pass(gpu, sc, 6, fused=False)
         env, _ = _one_pass(gpu, sc, 6, solver="envelope")
         nrec = -(-6 * m // 30)                          # 30-row camera-aligned tiles
         calls = kcr["k_cr_back"][1]
@@ -572,3 +606,26 @@ def test_cr_back_substitution_one_launch_and_fallback(gpu):
         assert cr.chol_failed == 0
         assert abs(cr.new_sse - env.new_sse) <= 1e-9 * env.new_sse, (m, cr.new_sse, env.new_sse)
         assert abs(cr.dpg - env.dpg) <= 1e-9 * abs(env.dpg), (m, cr.dpg, env.dpg)
+
+
+@pytest.mark.parametrize("num_a,m,track", [(6, 200, 6), (6, 11, 6), (6, 3000, 6), (6, 6, 2),
+                                           (7, 75, 5), (10, 64, 4)])
+def test_cr_one_launch_bit_identical(gpu, num_a, m, track):
+    """The whole cyclic reduction in ONE launch (k_cr32_fused: factor levels
+    and back substitution as records with in-kernel hand-offs) performs the
+    per-level kernels' arithmetic record for record: the step da / db and the
+    pass scalars are bit-identical to the per-level launches', for odd / even /
+    power-of-two tile counts, tile heights 30 / 28, and more records than
+    CUs (m = 3000: 600 tiles, ~2000 records on 256 CUs at one per CU)."""
+    from bundleadjustmentmatlab_amd.scene import make_config
+    sc = make_config("cfg2", m=m, n=max(40, 10 * m), track=track, seed=43 + m)
+    f_info, f_km, f_da, f_db, plan = _cr_pass(gpu, sc, num_a, fused=True)
+    l_info, l_km, l_da, l_db, _ = _cr_pass(gpu, sc, num_a, fused=False)
+    assert plan["cr_levels"] > 0 and plan["cr_rows"] > 0
+    assert f_km["k_cr_factor"][1] == 1 and "k_cr_back" not in {k for k, v in f_km.items()
+                                                                if v[1] > 0}
+    assert l_km["k_cr_factor"][1] == plan["cr_levels"]
+    assert f_info.chol_failed == 0 and l_info.chol_failed == 0
+    assert np.array_equal(f_da, l_da)
+    assert np.array_equal(f_db, l_db)
+    assert f_info.new_sse == l_info.new_sse and f_info.dpg == l_info.dpg
