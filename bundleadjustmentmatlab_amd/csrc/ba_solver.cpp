@@ -845,7 +845,7 @@ static int ctx_alloc(vlgba_ctx *c, T **p, size_t count)
 
 static int allreduce(vlgba_ctx *c, double *buf, size_t count)
 {
-    if (c->world <= 1 || count == 0) return 0;
+    if ((c->world <= 1 && !c->comm) || count == 0) return 0;
     if (c->comm) {
         ncclResult_t r =
             ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c->comm, c->d.stream);
@@ -1266,6 +1266,15 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
         } else {
             c->p0 = 0;
             c->p1 = p->n;
+            if (o->comm_id) {   // a one-rank RCCL communicator: every collective
+                                // of the pass runs through RCCL (identity sums)
+                ncclUniqueId id;
+                std::memcpy(&id, o->comm_id, sizeof id);
+                if (ncclCommInitRank(&c->comm, 1, id, 0) != ncclSuccess) {
+                    rc = VLGBA_E_COMM;
+                    break;
+                }
+            }
         }
         c->n_global = p->n;
         c->N_global = p->num_obs;
@@ -1344,7 +1353,7 @@ static int schur_phase(vlgba_ctx *c, double lam)
         mark(c, 3);
         TRY(ba_launch_schur_fast(&d, lam));
     }
-    if (c->world > 1) {
+    if (c->world > 1 || c->comm) {
         // [S blocks | e_ | old SSE] of this rank's points -> the global system
         double *sse = d.rhs + d.lds;
         VLGBA_CHECK(hipMemcpyAsync(sse, d.eA + d.ld, sizeof(double), hipMemcpyDeviceToDevice,
@@ -1361,7 +1370,7 @@ static int schur_phase(vlgba_ctx *c, double lam)
 static int collect_scalars(vlgba_ctx *c, bool spin, double hs[5])
 {
     ba_dev &d = c->d;
-    if (c->world > 1)   // new SSE, camera and point parts of dp'(lambda dp + g): local
+    if (c->world > 1 || c->comm)   // new SSE, camera and point parts of dp'(lambda dp + g)
         TRY(allreduce(c, d.scal + 1, 3));   // (scal[0] = the global old SSE, schur_phase)
     if (spin) {
         // spin on the host-mapped sequence number written last (by the update's
@@ -1527,8 +1536,10 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
     mark(c, 5);
     TRY(ba_chol_solve(&d));
     mark(c, 6);
-    const bool spin = c->world == 1 && !c->timing;
-    d.publish_req = spin;   // the fast update's final-sums launch publishes
+    // RCCL ranks spin as well: their collectives are stream-ordered, and the
+    // publish then follows the scalars' all-reduce (collect_scalars)
+    const bool spin = (c->world == 1 || c->comm) && !c->timing;
+    d.publish_req = spin && !c->comm;   // the fast update's final-sums launch publishes
     d.published = 0;
     TRY(ba_launch_update(&d, lam));
     d.publish_req = 0;

@@ -86,3 +86,36 @@ def test_two_rank_sharded_solve_matches_single(tmp_path):
     assert np.allclose(r0["new"], r0["new1"], rtol=1e-4, atol=0)
     # parameters are compared through the cost above: they drift along the
     # 7-dof similarity gauge that only the damping constrains (~1e-3 here)
+
+
+def test_rccl_one_rank_communicator():
+    """The RCCL data path on real hardware with a one-rank communicator
+    (vlgba_get_unique_id -> ncclCommInitRank, the in-place ncclAllReduce of
+    [S blocks | e_ | old SSE] and of the pass scalars on the library stream,
+    the publish after the scalars' all-reduce, ncclCommDestroy): a box with
+    one GPU cannot hold two RCCL ranks (RCCL refuses two ranks on one device),
+    so this pins everything but the inter-GPU transfer.  Sums over one rank
+    are identities: the whole LM solve is bit-identical to the
+    communicator-free one."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bundleadjustmentmatlab_amd as pkg
+    from bundleadjustmentmatlab_amd.dist import unique_id_bytes
+    from bundleadjustmentmatlab_amd.scene import make_config
+    sc = make_config("cfg2", m=30, n=3000, seed=17)
+    a = np.zeros((6, sc.m), order="F")
+    a[0:3], a[3:6] = sc.w0, sc.T0
+    b = np.asfortranarray(sc.X0[:3])
+    out = []
+    for comm in (None, unique_id_bytes()):
+        with pkg.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, 6,
+                                comm_id=comm) as ba:
+            ba.set_params(a, b)
+            err, st = ba.run()
+            a1, b1 = ba.get_params()
+            out.append((np.array(err, copy=True), st.iterations, a1.copy(), b1.copy()))
+    (e0, n0, a0, b0), (e1, n1, a1, b1) = out
+    assert n0 == n1 and n0 > 2
+    assert np.array_equal(e0, e1)
+    assert np.array_equal(a0, a1) and np.array_equal(b0, b1)
