@@ -1126,7 +1126,8 @@ struct cr32_lds {
 // factor step (level 0, on the assembled S): role 0 factors D_e, writes L_e^-1
 // (row-major 32 x 32) and y_e = L_e^-1 r_e; role 1 / 2 (split, one workgroup
 // each, redoing the same factorisation) or the same workgroup (role -1: no
-// split) form Lp_e = C(p, e) L_e^-T and Lq_e = C(q, e) L_e^-T into crL.
+// split) form Lp_e = C(p, e) L_e^-T and Lq_e = C(q, e) L_e^-T into crL;
+// role 4 = roles 0 and 1 in one workgroup.
 template <bool SC>
 __device__ __forceinline__ void cr32_factor_body(const cr32_lds &sh, double *S, long long lds,
                                                  int TB, long long ld, int e, int p, int q,
@@ -1136,16 +1137,18 @@ __device__ __forceinline__ void cr32_factor_body(const cr32_lds &sh, double *S, 
     double *As = sh.As, *Bs = sh.Bs, *Cs = sh.Cs, *Xs = sh.Xs, *rk = sh.rk, *yk = sh.ym;
     const int tid = threadIdx.x;
     const long long T2 = (long long)T32 * T32;
+    const bool rows = role <= 0 || role == 4;
     load32<SC>(S, lds, TB, ld, e, e, As, false, true);
-    if (role == 1) load32<SC>(S, lds, TB, ld, e, p, Cs, true, false);   // C(p, e) = tile(e, p)^T
+    if ((role == 1 || role == 4) && p >= 0)
+        load32<SC>(S, lds, TB, ld, e, p, Cs, true, false);   // C(p, e) = tile(e, p)^T
     if (role == 2) load32<SC>(S, lds, TB, ld, q, e, Cs, false, false);  // C(q, e) = tile(q, e)
-    if (role <= 0 && tid < T32) {
+    if (rows && tid < T32) {
         const long long g = (long long)TB * e + tid;
         rk[tid] = (tid < TB && g < ld) ? ldg<SC>(rhs + g) : 0.0;
     }
     __syncthreads();
     const bool ok = potrf32_inv(As, Bs, Xs);
-    if (role <= 0) {
+    if (rows) {
         gemv32(Bs, rk, sh.part, yk, false);
         if (tid < TB) stg<SC>(y + (long long)TB * e + tid, yk[tid]);
         store_rm32<SC>(linv + T2 * e, Bs);
@@ -1153,7 +1156,7 @@ __device__ __forceinline__ void cr32_factor_body(const cr32_lds &sh, double *S, 
         if (role == 0) return;   // split: roles 1 and 2 form the panels
     }
     for (int side = 1; side <= 2; side++) {
-        if (role > 0 && role != side) continue;
+        if (role > 0 && role != side && !(role == 4 && side == 1)) continue;
         const int nb = side == 1 ? p : q;
         if (nb < 0) continue;
         if (role < 0) {
@@ -1452,6 +1455,7 @@ __global__ __launch_bounds__(256) void k_cr32_back_all(const int *__restrict__ e
 #define BA_CR_MAXLEV 30
 struct cr32_fplan {
     int nl, nrec;
+    int l0two;                     // level 0 in 2 records per tile (roles 4 | 2), else 3
     int b0[BA_CR_MAXLEV + 2];      // first block of level L; b0[nl] = first back block
     int fofs[BA_CR_MAXLEV + 1];    // level L >= 1: first fused record in crf
     int sofs[BA_CR_MAXLEV + 1];    //               first survivor record in crs
@@ -1482,12 +1486,13 @@ __device__ __forceinline__ void cr32_wait_flags(const unsigned *flag, int nw, co
     __syncthreads();
 }
 
-__device__ __forceinline__ void cr32_publish(unsigned *flag, unsigned epoch)
+__device__ __forceinline__ void cr32_publish(unsigned *flag, unsigned epoch, int nflags = 1)
 {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave
     __syncthreads();
-    if (threadIdx.x == 0)
-        __hip_atomic_store((gu32_t *)flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < nflags)   // consecutive flag words (role 4: roles 0 and 1)
+        __hip_atomic_store((gu32_t *)(flag + threadIdx.x), epoch, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, int TB, long long ld,
@@ -1506,12 +1511,18 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
     // flag word of (level, tile, role): role 3 = survivor
     auto fw = [&](int lev, int t, int r) { return 4 * (lev * nt + t) + r; };
     if (L == 0) {
-        const int xr = b / 3, role = b % 3;
+        // three records per tile, or two (roles 0 + 1 merged) when three would
+        // not all fit on the CUs at once (one workgroup per CU)
+        const int xr = P.l0two ? b / 2 : b / 3;
+        const int role = P.l0two ? ((b & 1) ? 2 : 4) : b % 3;
         const int e = elim[3 * xr], p = elim[3 * xr + 1], q = elim[3 * xr + 2];
         if (!((role == 1 && p < 0) || (role == 2 && q < 0)))
             cr32_factor_body<true>(sh, S, lds, TB, ld, e, p, q, role, nt, linv, crL, rhs, y,
                                    status);
-        cr32_publish(flag + fw(0, e, role), epoch);
+        if (role == 4)
+            cr32_publish(flag + fw(0, e, 0), epoch, 2);
+        else
+            cr32_publish(flag + fw(0, e, role), epoch);
         return;
     }
     if (L < P.nl) {
@@ -2078,8 +2089,9 @@ int ba_chol_solve(ba_dev *d)
         cr32_fplan P{};
         P.nl = nl;
         P.nrec = nrec;
+        P.l0two = 3 * d->cr_eptr_h[1] > d->ncu;
         P.b0[0] = 0;
-        P.b0[1] = 3 * d->cr_eptr_h[1];
+        P.b0[1] = (P.l0two ? 2 : 3) * d->cr_eptr_h[1];
         for (int l = 1; l < nl; l++) {
             const int nf = d->crf_ptr_h[l + 1] - d->crf_ptr_h[l];
             const int ns = d->crs_ptr_h[l + 1] - d->crs_ptr_h[l];
