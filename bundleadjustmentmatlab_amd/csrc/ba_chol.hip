@@ -1495,6 +1495,29 @@ __device__ __forceinline__ void cr32_publish(unsigned *flag, unsigned epoch, int
                            __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Diagnostic build only (make stamps): per record of k_cr32_fused, the
+// s_memrealtime (100 MHz) at entry, after its wait, before and after its
+// publish (tools/cr_timeline.py)
+#ifdef BA_STAMPS
+#define CR_ST_MAX 8192
+__device__ unsigned long long g_crst[CR_ST_MAX][4];
+extern "C" int vlgba_debug_crstamps(unsigned long long *out, int nrec)
+{
+    if (nrec > CR_ST_MAX) nrec = CR_ST_MAX;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_crst), sizeof(unsigned long long) * 4 * nrec) ==
+                   hipSuccess
+               ? 0
+               : -1;
+}
+#define CR_ST(k)                                                                          \
+    do {                                                                                  \
+        if (threadIdx.x == 0 && blockIdx.x < CR_ST_MAX)                                   \
+            g_crst[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();                     \
+    } while (0)
+#else
+#define CR_ST(k)
+#endif
+
 __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, int TB, long long ld,
                                                     const int *__restrict__ elim,
                                                     const int *__restrict__ frec,
@@ -1505,6 +1528,7 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
                                                     double *status, cr32_fplan P)
 {
     CR32_LDS_DECL;
+    CR_ST(0);
     const int b = blockIdx.x;
     int L = 0;
     while (L < P.nl && b >= P.b0[L + 1]) L++;
@@ -1516,13 +1540,16 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
         const int xr = P.l0two ? b / 2 : b / 3;
         const int role = P.l0two ? ((b & 1) ? 2 : 4) : b % 3;
         const int e = elim[3 * xr], p = elim[3 * xr + 1], q = elim[3 * xr + 2];
+        CR_ST(1);
         if (!((role == 1 && p < 0) || (role == 2 && q < 0)))
             cr32_factor_body<true>(sh, S, lds, TB, ld, e, p, q, role, nt, linv, crL, rhs, y,
                                    status);
+        CR_ST(2);
         if (role == 4)
             cr32_publish(flag + fw(0, e, 0), epoch, 2);
         else
             cr32_publish(flag + fw(0, e, role), epoch);
+        CR_ST(3);
         return;
     }
     if (L < P.nl) {
@@ -1549,10 +1576,13 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
             for (int rr = 0; rr < 3; rr++) w[nw++] = fw(L - 1, ep, rr);
         if (L >= 2) w[nw++] = fw(L - 1, k, 3);
         cr32_wait_flags(flag, nw, w, epoch, status);
+        CR_ST(1);
         if (!((role == 1 && p < 0) || (role == 2 && q < 0)))
             cr32_level_body<true>(sh, S, lds, TB, ld, k, p, q, em, ep, role, nt, linv, crL, rhs,
                                   y, status);
+        CR_ST(2);
         cr32_publish(flag + fw(L, k, role), epoch);
+        CR_ST(3);
         return;
     }
     // back substitution, deepest record first
@@ -1562,7 +1592,10 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
     const int e = elim[3 * rec], p = elim[3 * rec + 1], q = elim[3 * rec + 2];
     const int w[8] = {fw(Le, e, 0), fw(Le, e, 1), fw(Le, e, 2), 0, 0, 0, 0, 0};
     cr32_wait_flags(flag, 3, w, epoch, status);
+    CR_ST(1);
     cr32_back_body<true>(sh, e, p, q, nt, TB, ld, linv, crL, y, x, xg, epoch, status);
+    CR_ST(2);
+    CR_ST(3);
 }
 
 __global__ __launch_bounds__(256) void k_cr_back(const int *__restrict__ elim, int nt,
