@@ -88,6 +88,7 @@ SIGNATURES = {
     "vlgba_get_params": (c_int, [ctypes.c_void_p, c_dp, c_dp]),
     "vlgba_step": (c_int, [ctypes.c_void_p, c_int, c_int, ctypes.POINTER(VlgbaStepInfo)]),
     "vlgba_run": (c_int, [ctypes.c_void_p, c_dp, c_int, ctypes.POINTER(VlgbaStats)]),
+    "vlgba_run_passes": (c_int, [ctypes.c_void_p, c_int, ctypes.POINTER(VlgbaStepInfo)]),
     "vlgba_get_step": (c_int, [ctypes.c_void_p, c_dp, c_dp]),
     "vlgba_get_reduced_system": (c_int, [ctypes.c_void_p, c_ip, c_dp, c_dp]),
     "vlgba_get_linearization": (c_int, [ctypes.c_void_p, c_dp, c_dp, c_dp, c_dp, c_dp]),

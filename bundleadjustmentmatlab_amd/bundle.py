@@ -283,6 +283,14 @@ class BundleAdjuster:
               "vlgba_step")
         return info
 
+    def passes(self, n):
+        """n full passes at the current parameters and lambda, each
+        relinearising, none changing the state (vlgba_run_passes: enqueued back
+        to back, the decisions on the device as in run()); the last pass's info."""
+        info = VlgbaStepInfo()
+        check(self._L.vlgba_run_passes(self._h, int(n), ctypes.byref(info)), "vlgba_run_passes")
+        return info
+
     def run(self):
         """The LM loop (vlgba_run): (error_, stats).  error_ has at most
         max_iter entries (bundle_euclid.m:117-123)."""

@@ -1525,8 +1525,10 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
                                                     double *linv, double *crL, double *rhs,
                                                     double *y, double *x, unsigned *flag,
                                                     unsigned long long *xg, unsigned epoch,
-                                                    double *status, cr32_fplan P)
+                                                    double *status, cr32_fplan P,
+                                                    const ba_lm *lm)
 {
+    if (lm && lm_flag(&lm->done)) return;   // a pass enqueued past the device LM's end
     CR32_LDS_DECL;
     CR_ST(0);
     const int b = blockIdx.x;
@@ -1645,8 +1647,9 @@ __global__ __launch_bounds__(256) void k_assemble_tiles(
     double *__restrict__ S, long long lds, const int *__restrict__ env,
     const int *__restrict__ tb_ptr, const int *__restrict__ tb_blk,
     const int *__restrict__ blk_jk, const double *__restrict__ sblk, int na, long long ld,
-    double *__restrict__ rhs, double *__restrict__ status)
+    double *__restrict__ rhs, double *__restrict__ status, const ba_lm *lm)
 {
+    if (lm && lm_flag(&lm->done)) return;   // a pass enqueued past the device LM's end
     __shared__ double T[NB * (NB + 1)];
     const int ti = env[2 * blockIdx.x], tk = env[2 * blockIdx.x + 1], tid = threadIdx.x;
     for (int q = tid; q < NB * (NB + 1); q += 256) T[q] = 0.0;
@@ -2087,7 +2090,7 @@ int ba_assemble_tiles(ba_dev *d)
 {
     k_assemble_tiles<<<d->n_env, 256, 0, d->stream>>>(d->S, d->lds, d->env_tiles, d->tb_ptr,
                                                       d->tb_blk, d->blk_jk, d->sblk, d->na, d->ld,
-                                                      d->rhs, d->scal + 4);
+                                                      d->rhs, d->scal + 4, d->lm);
     return -(int)hipGetLastError();
 }
 
@@ -2138,7 +2141,7 @@ int ba_chol_solve(ba_dev *d)
         KT_B(d);
         k_cr32_fused<<<P.b0[nl] + nrec, 256, 0, d->stream>>>(
             d->S, d->lds, d->tb32, d->ld, d->cr_elim, d->crf, d->crs, d->nt32, d->linv, d->crL,
-            d->rhs, d->ywork, d->da, d->crflag, d->xgran, d->back_epoch, d->scal + 4, P);
+            d->rhs, d->ywork, d->da, d->crflag, d->xgran, d->back_epoch, d->scal + 4, P, d->lm);
         KT_E(d, KT_CR_FACTOR);
         return -(int)hipGetLastError();
     }

@@ -77,6 +77,39 @@ struct ba_camred {
     double *sse_out, *sse_out2;
 };
 
+// Device-side Levenberg-Marquardt state (vlgba_run without host round trips):
+// the accept / lambda / stop decisions of bundle_euclid.m:205-241 taken by
+// k_lm_decide after each pass; the pass kernels read lambda, whether to
+// relinearise and which parameter buffers are current from here.
+struct ba_lm {
+    double lambda, nu, num_vis, stop_rel;
+    int iter, iter2, passes, acc;
+    int done;      // 1: stop rule / caps met; 2: non-positive pivot (the host takes the pinv step)
+    int relin;     // the next pass relinearises
+    int sel;       // current parameters: 0 = (a, b, rot), 1 = (a_new, b_new, rot_new)
+    int nerr;      // error_ entries
+    int max_iter, max_iter2, proj, force;   // force: passes that relinearise and never commit
+    int cap;       // error_ capacity
+    int pad;
+    double seq;    // decisions taken (published to the host as hres[7])
+};
+
+static_assert(sizeof(ba_lm) % 8 == 0, "ba_lm moves as 8-byte words");
+
+// Kernels read the LM state with vector loads at device scope: it was written
+// by an earlier kernel (k_lm_decide), and a scalar load of such a word was
+// seen to return a stale value (the scalar cache)
+#ifdef __HIPCC__
+__device__ __forceinline__ double lm_lambda(const ba_lm *lm)
+{
+    return __hip_atomic_load(&lm->lambda, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int lm_flag(const int *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#endif
+
 struct ba_dev {
     int m, n, na, N, js;
     int device, ncu;   // HIP device ordinal and its CU count
@@ -146,6 +179,10 @@ struct ba_dev {
     // ---- fast (chunked) Schur path: points in chunks of <= CH_OBS observations;
     // per chunk the co-visible blocks it touches ("slots") and the cameras it
     // sees ("e-slots") get one partial each, reduced per block in chunk order.
+    ba_lm *lm;         // device LM state of the running vlgba_run, else NULL (host loop)
+    double *lm_err;    // its error_ [cap]
+    ba_lm *lm_mem;     // allocation behind lm
+    int lm_cap;
     int ordered;       // 1: sequential bit-exact kernels (k_damp_point + k_schur)
     int parity;        // ordered = 2: + sequential solve and LM scalars (bit-identical
                        // LM trajectory with the oracle)
@@ -262,6 +299,8 @@ int ba_launch_assemble(ba_dev *d);
 int ba_launch_update(ba_dev *d, double lambda);
 int ba_launch_yeb(ba_dev *d);
 int ba_launch_publish(ba_dev *d);
+// the pass's LM decision on the device (d->lm), published to hres with seq
+int ba_launch_lm_decide(ba_dev *d);
 void *ba_dmalloc(size_t bytes);   // per-device caching allocator (ba_solver.cpp)
 // raise kernel fn's dynamic-LDS limit to >= bytes on the current device (cached
 // per (kernel, device), thread-safe; ba_solver.cpp)

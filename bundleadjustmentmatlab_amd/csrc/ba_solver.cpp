@@ -744,6 +744,8 @@ struct vlgba_ctx {
     double lambda = 1e-3, lambda0 = 1e-3, nu = 2.0;
     int model = VLGBA_MODEL_EUCLIDEAN;
     int lin_valid = 0;
+    int device_lm = 1;   // VLGBA_DEVICE_LM=0: the LM decisions on the host every pass
+    ba_lm lm_host{};     // staging of the device LM state (async upload / download)
     int timing = 0;
     hipEvent_t ev[8] = {};
     double phase_ms[7] = {};
@@ -1287,6 +1289,10 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
         c->flags.has_pivot = o->pivot != nullptr && o->semantics == 0 &&
                              p->model == VLGBA_MODEL_EUCLIDEAN;
         c->model = p->model;
+        {
+            const char *ev = std::getenv("VLGBA_DEVICE_LM");
+            c->device_lm = !(ev && ev[0] == '0');
+        }
         c->max_iter = o->max_iter > 0 ? o->max_iter : 20;
         c->max_iter2 = o->max_iter2 > 0 ? o->max_iter2 : 10;
         c->lambda0 = c->lambda = o->lambda0 > 0 ? o->lambda0 : 1e-3;
@@ -1887,6 +1893,178 @@ int vlgba_step(vlgba_ctx *c, int relinearize, int update_lm, vlgba_step_info *in
     return 0;
 }
 
+// ---------------------------------------------------------------------------
+// The LM loop without host round trips: the passes are enqueued one ahead and
+// k_lm_decide takes each pass's decision on the device (ba_lm: lambda, nu,
+// error_, the current parameter buffers, relinearise or not, the stop test);
+// the host only watches the published decision count and stops enqueueing
+// once the device says done.  A pass enqueued after the last decision runs but
+// commits nothing.  Fast path, single rank or RCCL ranks, no per-pass host
+// hooks (timing, verbose, on_pass), no long tracks; otherwise the host loop.
+// ---------------------------------------------------------------------------
+static bool device_lm_ok(const vlgba_ctx *c)
+{
+    const ba_dev &d = c->d;
+    return c->device_lm && !d.ordered && !d.parity && d.nl == 0 && d.nch > 0 && !d.obs_vis &&
+           !d.xh_out && !c->timing && !c->verbose && !c->on_pass &&
+           (c->world == 1 || c->comm);
+}
+
+// every launch of one pass (lm_pass's), the decision on the device
+static int lm_pass_device(vlgba_ctx *c)
+{
+    ba_dev &d = c->d;
+    const double lam = c->lambda;   // the kernels read d.lm->lambda
+    TRY(ba_launch_linearize(&d, c->flags));   // returns at once unless d.lm->relin
+    // U / eA / old SSE re-formed from the chunk partials every pass (the same
+    // values after a rejected step), inside the MFMA Schur launch
+    TRY(ba_launch_camera_reduce(&d, c->flags, 1));
+    TRY(schur_phase(c, lam));
+    TRY(ba_launch_assemble(&d));
+    TRY(ba_chol_solve(&d));
+    d.publish_req = 0;
+    d.published = 0;
+    TRY(ba_launch_update(&d, lam));
+    if (c->world > 1 || c->comm) TRY(allreduce(c, d.scal + 1, 3));
+    TRY(ba_launch_lm_decide(&d));
+    return 0;
+}
+
+// wait until the device has taken `want` decisions (host-mapped hres[7])
+static int wait_decisions(vlgba_ctx *c, double want)
+{
+    ba_dev &d = c->d;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (long it = 0;; it++) {
+        if (d.hres[7] >= want) break;
+        if ((it & 1023) == 1023 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+            VLGBA_CHECK(hipStreamSynchronize(d.stream));   // reports a failed kernel
+            if (d.hres[7] >= want) break;
+            return VLGBA_E_ARG;
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return 0;
+}
+
+static int lm_device_begin(vlgba_ctx *c, int force)
+{
+    ba_dev &d = c->d;
+    const int cap = c->max_iter + 2;
+    if (!d.lm_mem || d.lm_cap < cap) {
+        TRY(ctx_alloc(c, &d.lm_mem, 1));
+        TRY(ctx_alloc(c, &d.lm_err, (size_t)cap));
+        d.lm_cap = cap;
+    }
+    ba_lm &L = c->lm_host;
+    L = ba_lm{};
+    L.lambda = c->lambda;
+    L.nu = c->nu;
+    L.num_vis = c->num_vis;
+    L.stop_rel = c->stop_rel;
+    L.iter = 1;
+    L.relin = (force || !c->lin_valid) ? 1 : 0;
+    L.max_iter = c->max_iter;
+    L.max_iter2 = c->max_iter2;
+    L.proj = c->model == VLGBA_MODEL_PROJECTIVE;
+    L.force = force;
+    L.cap = cap;
+    L.seq = (double)d.seq;
+    VLGBA_CHECK(hipMemcpyAsync(d.lm_mem, &L, sizeof L, hipMemcpyHostToDevice, d.stream));
+    d.lm = d.lm_mem;
+    return 0;
+}
+
+// after the device loop: the state back to the context (parameter buffers,
+// lambda, nu, the linearisation's validity); error_ into err
+static int lm_device_end(vlgba_ctx *c, std::vector<double> *err)
+{
+    ba_dev &d = c->d;
+    d.lm = nullptr;
+    ba_lm &L = c->lm_host;
+    VLGBA_CHECK(hipMemcpyAsync(&L, d.lm_mem, sizeof L, hipMemcpyDeviceToHost, d.stream));
+    std::vector<double> e((size_t)d.lm_cap);
+    VLGBA_CHECK(hipMemcpyAsync(e.data(), d.lm_err, sizeof(double) * d.lm_cap,
+                               hipMemcpyDeviceToHost, d.stream));
+    VLGBA_CHECK(hipStreamSynchronize(d.stream));
+    d.seq = (unsigned long long)L.seq;
+    if (L.force) return 0;
+    c->lambda = L.lambda;
+    c->nu = L.nu;
+    if (L.sel) {   // the current parameters are the "new" buffers
+        std::swap(d.a, d.a_new);
+        std::swap(d.b, d.b_new);
+        std::swap(d.rot, d.rot_new);
+    }
+    c->lin_valid = L.relin ? 0 : 1;
+    if (err) err->assign(e.begin(), e.begin() + std::min(L.nerr, d.lm_cap));
+    return 0;
+}
+
+static int run_device(vlgba_ctx *c, std::vector<double> &err, int &iter, int &iter2,
+                      int &passes, int &acc, bool &handoff)
+{
+    ba_dev &d = c->d;
+    TRY(lm_device_begin(c, 0));
+    const double seq0 = c->lm_host.seq;
+    const int max_enq = c->max_iter * (c->max_iter2 + 1) + 4;
+    int enq = 0, rc = 0;
+    for (;;) {
+        if ((rc = lm_pass_device(c))) break;
+        enq++;
+        if (enq >= 2) {   // one pass ahead: wait for the previous one's decision
+            if ((rc = wait_decisions(c, seq0 + enq - 1))) break;
+            if (d.hres[5] != 0.0) break;
+        }
+        if (enq >= max_enq) break;
+    }
+    if (!rc && d.hres[5] == 0.0) rc = wait_decisions(c, seq0 + enq);
+    const int rc2 = lm_device_end(c, &err);
+    TRY(rc);
+    TRY(rc2);
+    const ba_lm &L = c->lm_host;
+    iter = L.iter;
+    iter2 = L.iter2;
+    passes = L.passes;
+    acc = L.acc;
+    handoff = L.done == 2;   // a non-positive pivot: the host takes that pass (pinv)
+    return 0;
+}
+
+int vlgba_run_passes(vlgba_ctx *c, int npass, vlgba_step_info *info)
+{
+    if (!c || npass < 0) return VLGBA_E_ARG;
+    TRY(ctx_enter(c));
+    vlgba_step_info tmp;
+    if (!info) info = &tmp;
+    std::memset(info, 0, sizeof *info);
+    if (npass == 0) return 0;
+    ba_dev &d = c->d;
+    if (!device_lm_ok(c)) {   // host-decided passes
+        for (int q = 0; q < npass; q++) TRY(lm_pass(c, 1, info));
+        return 0;
+    }
+    TRY(lm_device_begin(c, 1));
+    const double seq0 = c->lm_host.seq;
+    int rc = 0;
+    for (int q = 0; q < npass && !rc; q++) rc = lm_pass_device(c);
+    if (!rc) rc = wait_decisions(c, seq0 + npass);
+    double hs[7];
+    for (int q = 0; q < 7; q++) hs[q] = d.hres[q];
+    const int rc2 = lm_device_end(c, nullptr);
+    TRY(rc);
+    TRY(rc2);
+    info->old_sse = hs[0];
+    info->new_sse = hs[1];
+    info->dpg = hs[2] + hs[3];
+    info->lambda = c->lambda;
+    info->pinv = info->chol_failed = hs[4] != 0.0;
+    info->rho = (hs[0] - hs[1]) / info->dpg;
+    info->accepted = (hs[0] - hs[1]) > 0;
+    return 0;
+}
+
 // bundle_euclid.m:111-249
 int vlgba_run(vlgba_ctx *c, double *error_out, int error_cap, vlgba_stats *stats)
 {
@@ -1898,7 +2076,13 @@ int vlgba_run(vlgba_ctx *c, double *error_out, int error_cap, vlgba_stats *stats
     c->lin_valid = 0;
     std::vector<double> err;   // error_, 1-based in the reference
     int iter = 1, iter2 = 0, passes = 0, acc = 0;
-    for (;;) {
+    bool host_loop = true;
+    if (device_lm_ok(c) && iter < c->max_iter && iter2 < c->max_iter2) {
+        bool handoff = false;
+        TRY(run_device(c, err, iter, iter2, passes, acc, handoff));
+        host_loop = handoff;   // the host continues only to take a pinv step
+    }
+    for (; host_loop;) {
         if (!(iter < c->max_iter && iter2 < c->max_iter2)) break;
         if (iter >= 3) {
             const double e1 = err[iter - 1], e0 = err[iter - 2];
