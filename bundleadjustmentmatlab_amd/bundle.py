@@ -285,8 +285,9 @@ class BundleAdjuster:
 
     def passes(self, n):
         """n full passes at the current parameters and lambda, each
-        relinearising, none changing the state (vlgba_run_passes: enqueued back
-        to back, the decisions on the device as in run()); the last pass's info."""
+        relinearising, none changing the state (vlgba_run_passes; enqueued back
+        to back with the decisions on the device when VLGBA_DEVICE_LM=1); the
+        last pass's info."""
         info = VlgbaStepInfo()
         check(self._L.vlgba_run_passes(self._h, int(n), ctypes.byref(info)), "vlgba_run_passes")
         return info

@@ -1445,7 +1445,10 @@ __global__ __launch_bounds__(256) void k_point_update_chunk(
         if (tid < 3) bn[tid] = b_new[3 * (size_t)p0 + tid];
         if (tid == 0) {
             const int l = seg_long[ch - nch_reg];
-            if (obase == long_o0[l]) dpg = dpg_long[l];   // once per track
+            // once per track; written by k_long_db in this pass: a vector load
+            // (a uniform-address load could come from the stale scalar cache)
+            if (obase == long_o0[l])
+                dpg = __hip_atomic_load(dpg_long + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
         double sse = 0.0;

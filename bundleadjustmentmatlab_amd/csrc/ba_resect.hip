@@ -51,7 +51,10 @@ __global__ __launch_bounds__(256) void k_resect_pass(
     __shared__ int fail;
     const int pb = blockIdx.x, tid = threadIdx.x;
     if (pb >= nprob) return;
-    const int fl = (int)flags[pb];   // staged with lambda as doubles (one copy a pass)
+    // staged with lambda as doubles (one copy a pass): read with a vector load
+    // at device scope -- a uniform-address (scalar-cache) load can return the
+    // previous pass's value
+    const int fl = (int)__hip_atomic_load(flags + pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (!(fl & 1)) return;                          // problem finished
     const long long o0 = obs_ptr[pb], no = obs_ptr[pb + 1] - o0;
     double *stg = state + (size_t)NUE * pb;
@@ -111,7 +114,7 @@ __global__ __launch_bounds__(256) void k_resect_pass(
     __syncthreads();
     if (tid < NUE) st[tid] = stg[tid];
     __syncthreads();
-    const double lambda = lam_p[pb];
+    const double lambda = __hip_atomic_load(lam_p + pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid == 0) {
         // S = U* (damped diagonal), e_ = eA - 0: fix_structure zeroes V, W, eB,
         // so V*^-1 = pinv(0) = 0 and Y = 0 (bundle_euclid.m:140-193)

@@ -744,7 +744,7 @@ struct vlgba_ctx {
     double lambda = 1e-3, lambda0 = 1e-3, nu = 2.0;
     int model = VLGBA_MODEL_EUCLIDEAN;
     int lin_valid = 0;
-    int device_lm = 1;   // VLGBA_DEVICE_LM=0: the LM decisions on the host every pass
+    int device_lm = 0;   // VLGBA_DEVICE_LM=1: the LM decisions on the device (run_device)
     ba_lm lm_host{};     // staging of the device LM state (async upload / download)
     int timing = 0;
     hipEvent_t ev[8] = {};
@@ -1290,8 +1290,11 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
                              p->model == VLGBA_MODEL_EUCLIDEAN;
         c->model = p->model;
         {
+            // opt-in: measured (tools/ab_lm.sh) the one-ahead pass that ends
+            // every device-decided solve costs what the saved host round
+            // trips gain (cfg3 and cfg2 whole solves within noise)
             const char *ev = std::getenv("VLGBA_DEVICE_LM");
-            c->device_lm = !(ev && ev[0] == '0');
+            c->device_lm = ev && ev[0] == '1';
         }
         c->max_iter = o->max_iter > 0 ? o->max_iter : 20;
         c->max_iter2 = o->max_iter2 > 0 ? o->max_iter2 : 10;
@@ -1901,6 +1904,7 @@ int vlgba_step(vlgba_ctx *c, int relinearize, int update_lm, vlgba_step_info *in
 // once the device says done.  A pass enqueued after the last decision runs but
 // commits nothing.  Fast path, single rank or RCCL ranks, no per-pass host
 // hooks (timing, verbose, on_pass), no long tracks; otherwise the host loop.
+// Opt-in (VLGBA_DEVICE_LM=1): it does not beat the host loop, see device_lm.
 // ---------------------------------------------------------------------------
 static bool device_lm_ok(const vlgba_ctx *c)
 {

@@ -172,13 +172,13 @@ int vlgba_get_linearization(vlgba_ctx *ctx, double *U, double *eA, double *V, do
                             double *W);
 /* the LM loop from the context's parameters; error_out / error_cap as
  * vlgba_solve.  Every handle entry point makes the context's device current.
- * On the fast path the accept / lambda / stop decisions are taken on the
- * device after every pass (no host round trip between passes). */
+ * With VLGBA_DEVICE_LM=1 (fast path) the accept / lambda / stop decisions are
+ * taken on the device after every pass (no host round trip between passes). */
 int vlgba_run(vlgba_ctx *ctx, double *error_out, int error_cap, vlgba_stats *stats);
 /* npass full passes at the context's parameters and lambda, each
- * relinearising, none changing the context (measurement; vlgba_step(ctx, 1,
- * 0, .) npass times, enqueued back to back with the decisions on the device
- * where vlgba_run takes them there); info: the last pass */
+ * relinearising, none changing the context (vlgba_step(ctx, 1, 0, .) npass
+ * times; enqueued back to back with the decisions on the device when
+ * VLGBA_DEVICE_LM=1); info: the last pass */
 int vlgba_run_passes(vlgba_ctx *ctx, int npass, vlgba_step_info *info);
 /* the last pass's step: da (num_a * m, the reduced solve) and db (3 x
  * n_local, this rank's points); either may be NULL */

@@ -4,8 +4,9 @@ k_lm_decide takes every pass's accept / lambda / error_ / stop decision
 (bundle_euclid.m:205-241, bundle_projective.m:182-207, the stop test of
 :111-123) and the pass kernels read lambda, "relinearise or not" and the
 current parameter buffers from that device state, so the host enqueues passes
-one ahead instead of waiting for each pass's scalars.  Checked against the
-host-decided loop (VLGBA_DEVICE_LM=0, read when the context is created): the
+one ahead instead of waiting for each pass's scalars (opt-in:
+VLGBA_DEVICE_LM=1, read when the context is created).  Checked against the
+host-decided loop (VLGBA_DEVICE_LM=0): the
 same passes, accepts, error_ and parameters -- the only arithmetic that may
 differ is (2 rho - 1)^3 (a double-double cube on the device, glibc pow on the
 host), so the comparison allows the rounding that 1-ulp lambda difference
@@ -109,12 +110,13 @@ def test_device_lm_pinv_handoff(gpu):
     assert np.array_equal(da, ha) and np.array_equal(db, hb)
 
 
-def test_passes_equal_host_steps(gpu):
+def test_passes_equal_host_steps(gpu, monkeypatch):
     """vlgba_run_passes (K relinearising passes enqueued back to back, the
     decisions on the device, nothing committed) = K host-decided
     vlgba_step(relinearize=1, update_lm=0): the same last-pass scalars bit for
     bit, and the parameters unchanged."""
     from bundleadjustmentmatlab_amd.scene import make_config
+    monkeypatch.setenv("VLGBA_DEVICE_LM", "1")
     sc = make_config("cfg2", m=60, n=6000, seed=5)
     a = np.zeros((6, sc.m), order="F")
     a[0:3], a[3:6] = sc.w0, sc.T0
