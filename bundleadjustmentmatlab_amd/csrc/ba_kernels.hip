@@ -957,6 +957,29 @@ __global__ __launch_bounds__(256) void k_point_vinv(const double *__restrict__ V
 // deterministic run to run; only the grouping differs from the term kernel.
 // -------------------------------------------------------------------------
 #define BA_MF_KB 5   // points per K-block (one wave)
+#ifndef BA_MF_ROW4
+#define BA_MF_ROW4 1
+#endif
+// lane (lk, 4 b + i) <- lane (lk, 4 rg + i) within each 16-lane row (ds_swizzle
+// bit mask mode on 32-lane halves: and 0x13 keeps bit 4 and the row i, or sets
+// the row group)
+template <int RG> __device__ __forceinline__ double row4_bcast_c(double v)
+{
+    constexpr int pat = 0x13 | ((RG << 2) << 5);
+    const long long u = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_ds_swizzle((int)(u & 0xffffffffLL), pat);
+    const int hi = __builtin_amdgcn_ds_swizzle((int)(u >> 32), pat);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double row4_bcast(double v, int rg)
+{
+    switch (rg) {
+    case 0: return row4_bcast_c<0>(v);
+    case 1: return row4_bcast_c<1>(v);
+    case 2: return row4_bcast_c<2>(v);
+    default: return row4_bcast_c<3>(v);
+    }
+}
 #ifndef BA_MF_PIPE
 #define BA_MF_PIPE 0
 #endif
@@ -1075,10 +1098,21 @@ __global__ __launch_bounds__(256, (NA == 6) ? BA_MF_WAVES : 1) void k_schur_mfma
         // s = 3 first, all column tiles: point 5w + 4 on the matrix pipe
         // (register 0 = A fragment), in flight while the VALU forms the rest
         double y4[RT];
+        if (BA_MF_ROW4) {
+            // v_mfma_f64_4x4x4: block b = li >> 2 takes V*^-1 rows (li & 3) (the
+            // A fragment's first block, swizzled to all four) against columns
+            // 16 ti + li and leaves row lk, column 16 ti + li: register 0 of
+            // the 16x16x4 form, at a sixth of its matrix-pipe time
+            const double va = row4_bcast(vc[6], 0);
 #pragma unroll
-        for (int ti = 0; ti < RT; ti++)
-            y4[ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(vc[6], wc[3][ti],
-                                                          d4{0.0, 0.0, 0.0, 0.0}, 0, 0, 0)[0];
+            for (int ti = 0; ti < RT; ti++)
+                y4[ti] = __builtin_amdgcn_mfma_f64_4x4x4f64(va, wc[3][ti], 0.0, 0, 0, 0);
+        } else {
+#pragma unroll
+            for (int ti = 0; ti < RT; ti++)
+                y4[ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(vc[6], wc[3][ti],
+                                                              d4{0.0, 0.0, 0.0, 0.0}, 0, 0, 0)[0];
+        }
 #pragma unroll
         for (int ti = 0; ti < RT; ti++) {
             {
@@ -1090,12 +1124,37 @@ __global__ __launch_bounds__(256, (NA == 6) ? BA_MF_WAVES : 1) void k_schur_mfma
                 y[2] = fma(wc[2][ti], vc[5], fma(wc[1][ti], vc[4], wc[0][ti] * vc[2]));
                 eacc[ti] = fma(y[3], ec[3], fma(y[2], ec[2], fma(y[1], ec[1],
                                                                  fma(y[0], ec[0], eacc[ti]))));
+                if (BA_MF_ROW4 && NA == 6 && ti == RT - 1) {
+                    // the last row tile holds NA C - 32 real rows (4 for the usual
+                    // six-camera chunk): v_mfma_f64_4x4x4 per group of 4 rows
+                    // (tools/ubench_mfma4x4.hip: a sixth of the 16x16x4 time).
+                    // Its blocks b = li >> 2 take rows 4 rg + (li & 3) (the A
+                    // operand swizzled within each 16-lane row) against columns
+                    // 16 tj + li (the B fragment as is) and leave row 4 rg + lk,
+                    // column 16 tj + li -- component rg of the 16x16 tile's
+                    // accumulator, same lane: the flush below is unchanged
 #pragma unroll
-                for (int s = 0; s < 4; s++) {   // K step outer: neighbours independent
+                    for (int rg = 0; rg < 4; rg++) {
+                        if (16 * ti + 4 * rg >= Rc) continue;   // (uniform) rows past the chunk
 #pragma unroll
-                    for (int tj = 0; tj <= ti; tj++)
-                        accS[ti * (ti + 1) / 2 + tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(
-                            y[s], wc[s][tj], accS[ti * (ti + 1) / 2 + tj], 0, 0, 0);
+                        for (int s = 0; s < 4; s++) {
+                            const double ya = row4_bcast(y[s], rg);
+#pragma unroll
+                            for (int tj = 0; tj <= ti; tj++) {
+                                d4 &t = accS[ti * (ti + 1) / 2 + tj];
+                                t[rg] = __builtin_amdgcn_mfma_f64_4x4x4f64(ya, wc[s][tj], t[rg], 0,
+                                                                           0, 0);
+                            }
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int s = 0; s < 4; s++) {   // K step outer: neighbours independent
+#pragma unroll
+                        for (int tj = 0; tj <= ti; tj++)
+                            accS[ti * (ti + 1) / 2 + tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+                                y[s], wc[s][tj], accS[ti * (ti + 1) / 2 + tj], 0, 0, 0);
+                    }
                 }
             }
         }
