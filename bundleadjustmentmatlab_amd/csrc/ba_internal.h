@@ -96,9 +96,13 @@ struct ba_lm {
 
 static_assert(sizeof(ba_lm) % 8 == 0, "ba_lm moves as 8-byte words");
 
-// Kernels read the LM state with vector loads at device scope: it was written
-// by an earlier kernel (k_lm_decide), and a scalar load of such a word was
-// seen to return a stale value (the scalar cache)
+// Kernels read the LM state with vector loads at device scope.  Why not plain
+// reads: hipcc turns a uniform-address read into a scalar load, and in
+// k_lm_decide (which reads the status word and then clears it) the scalar
+// load and the vector store of the same word were issued back to back with
+// no wait between them (the scalar and vector memory paths are not ordered):
+// the load returned the cleared value.  Vector loads are ordered before a
+// later vector store of the same address.
 #ifdef __HIPCC__
 __device__ __forceinline__ double lm_lambda(const ba_lm *lm)
 {

@@ -1504,8 +1504,8 @@ __global__ __launch_bounds__(256) void k_point_update_chunk(
         if (tid < 3) bn[tid] = b_new[3 * (size_t)p0 + tid];
         if (tid == 0) {
             const int l = seg_long[ch - nch_reg];
-            // once per track; written by k_long_db in this pass: a vector load
-            // (a uniform-address load could come from the stale scalar cache)
+            // once per track (written by k_long_db in this pass; a vector load,
+            // as every word an earlier launch of the pass writes, ba_internal.h)
             if (obase == long_o0[l])
                 dpg = __hip_atomic_load(dpg_long + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -2035,8 +2035,8 @@ __global__ void k_lm_decide(ba_lm *__restrict__ lm, double *__restrict__ err,
                             double *__restrict__ scal, double *hres)
 {
     if (threadIdx.x != 0) return;
-    // the state and error_ (written by earlier launches) by vector loads at
-    // device scope, never the scalar cache
+    // the state, error_ and the pass scalars by vector loads at device scope:
+    // a scalar load of scal[4] raced the clearing store below (ba_internal.h)
     constexpr int NW = sizeof(ba_lm) / 8;
     unsigned long long w[NW];
 #pragma unroll
@@ -2048,8 +2048,7 @@ __global__ void k_lm_decide(ba_lm *__restrict__ lm, double *__restrict__ err,
     auto err_at = [&](int k) {
         return __hip_atomic_load(err + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
-    // vector loads at device scope (not the scalar cache: the status was
-    // written by another workgroup of an earlier kernel)
+    // vector loads at device scope: ordered before the clearing store below
     double sv[5];
 #pragma unroll
     for (int q = 0; q < 5; q++)

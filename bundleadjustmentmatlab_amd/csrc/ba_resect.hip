@@ -51,9 +51,8 @@ __global__ __launch_bounds__(256) void k_resect_pass(
     __shared__ int fail;
     const int pb = blockIdx.x, tid = threadIdx.x;
     if (pb >= nprob) return;
-    // staged with lambda as doubles (one copy a pass): read with a vector load
-    // at device scope -- a uniform-address (scalar-cache) load can return the
-    // previous pass's value
+    // staged with lambda as doubles (one copy a pass); a vector load at device
+    // scope, as every per-pass word (ba_internal.h)
     const int fl = (int)__hip_atomic_load(flags + pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (!(fl & 1)) return;                          // problem finished
     const long long o0 = obs_ptr[pb], no = obs_ptr[pb + 1] - o0;
