@@ -281,6 +281,9 @@ __global__ __launch_bounds__(256) void k_linearize(
 // -------------------------------------------------------------------------
 // 7 waves per SIMD for NA = 6: the LDS rows (21.7 KB) allow 7 workgroups per
 // CU; the bound keeps the register allocation from costing one of them
+#ifndef BA_LIN_W2_ON
+#define BA_LIN_W2_ON 1
+#endif
 template <int NA>
 __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
     const int *__restrict__ ch_pt, const int *__restrict__ ch_obase,
@@ -376,8 +379,24 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
     __syncthreads();
     STAMP(17);
     // W_ij = A^T B onto a zeroed output (:305-314): the chunk's W rows are one
-    // contiguous HBM range, written lane by lane (coalesced)
-    {
+    // contiguous HBM range, written lane by lane (coalesced), two entries
+    // (rows r, r + 1 of one column) per lane
+    if constexpr (BA_LIN_W2_ON && NA % 2 == 0) {
+        double2 *wdst = reinterpret_cast<double2 *>(W + (size_t)3 * NA * obase);
+        constexpr int NP = 3 * NA / 2;         // entry pairs per observation
+        for (int q = tid; q < nobs * NP; q += 256) {
+            const int lo = q / NP, e = q - NP * lo, c = e / (NA / 2), r = 2 * (e - (NA / 2) * c);
+            const double *row = rows + RS * lo;
+            const double2 a0 = *reinterpret_cast<const double2 *>(row + 2 * r);
+            const double2 a1 = *reinterpret_cast<const double2 *>(row + 2 * r + 2);
+            const double2 bc = *reinterpret_cast<const double2 *>(row + 2 * NA + 2 * c);
+            const long long keep = wz[lo] ? 0 : -1;   // forced zeros by a mask, no branch
+            const double v0 = 0.0 + (a0.x * bc.x + a0.y * bc.y);
+            const double v1 = 0.0 + (a1.x * bc.x + a1.y * bc.y);
+            wdst[q] = make_double2(__builtin_bit_cast(double, __builtin_bit_cast(long long, v0) & keep),
+                                   __builtin_bit_cast(double, __builtin_bit_cast(long long, v1) & keep));
+        }
+    } else {
         double *wdst = W + (size_t)3 * NA * obase;
         for (int q = tid; q < nobs * 3 * NA; q += 256) {
             const int lo = q / (3 * NA), e = q - 3 * NA * lo, c = e / NA, r = e - NA * c;
@@ -392,19 +411,13 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
     for (int q = tid; q < np * 12; q += 256) {
         const int pl = q / 12, e = q % 12, i = p0 + pl;
         const int lo0 = lptr[pl], lo1 = lptr[pl + 1];
+        // one loop for both kinds (no divergent pair of loops in a wave): e
+        // is the column after B's three, B[6], B[7]
+        const int r = (e < 9) ? e % 3 : e - 9, c = (e < 9) ? e / 3 : 3;
         double acc = 0.0;
-        if (e < 9) {
-            const int r = e % 3, c = e / 3;
-            for (int lo = lo0; lo < lo1; lo++) {
-                const double *B = rows + RS * lo + 2 * NA;
-                acc += B[2 * r] * B[2 * c] + B[2 * r + 1] * B[2 * c + 1];
-            }
-        } else {
-            const int r = e - 9;
-            for (int lo = lo0; lo < lo1; lo++) {
-                const double *B = rows + RS * lo + 2 * NA;
-                acc += B[2 * r] * B[6] + B[2 * r + 1] * B[7];
-            }
+        for (int lo = lo0; lo < lo1; lo++) {
+            const double *B = rows + RS * lo + 2 * NA;
+            acc += B[2 * r] * B[2 * c] + B[2 * r + 1] * B[2 * c + 1];
         }
         if (f.fix_structure) acc = 0.0;
         if (seg) vseg[12 * (size_t)(ch - nch_reg) + e] = acc;
@@ -426,8 +439,22 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
             c = NA;   // e occupies the column after B: row[2 NA + 6]
         }
         const int cc = (c < NA) ? 2 * c : 2 * NA + 6;
+        // four observations a step: their index and data reads in flight
+        // together, the sum still taken one observation at a time in order
         double acc = 0.0;
-        for (int u = eoff[s]; u < eoff[s + 1]; u++) {
+        int u = eoff[s];
+        const int u1 = eoff[s + 1];
+        for (; u + 3 < u1; u += 4) {
+            double p[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const double *rw = rows + RS * eobl[u + k];
+                p[k] = rw[2 * r] * rw[cc] + rw[2 * r + 1] * rw[cc + 1];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) acc += p[k];
+        }
+        for (; u < u1; u++) {
             const double *row = rows + RS * eobl[u];
             acc += row[2 * r] * row[cc] + row[2 * r + 1] * row[cc + 1];
         }
