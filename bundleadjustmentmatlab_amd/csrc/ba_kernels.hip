@@ -314,8 +314,11 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
     constexpr int NU = NA * (NA + 1) / 2;
     static_assert(BA_CH_OBS + 1 <= 256 && BA_CH_PTS + 1 <= 256, "one metadata word per lane");
     __shared__ __attribute__((aligned(16))) double rows[BA_CH_OBS * RS];
-    __shared__ int lptr[BA_CH_PTS + 1];     // chunk-local observation offsets per point
-    __shared__ int eoff[BA_CH_OBS + 1];
+    // pt_ptr[p0 + t] (t <= np) and eslot_optr[e0 + t] (t <= nes) as they are
+    // in memory, written by LDS-DMA (no registers, no wait until the barrier)
+    // from the waves whose lanes cover them
+    __shared__ int lptr_raw[64 * (BA_CH_PTS / 64 + 1)];
+    __shared__ int eoff_raw[64 * (BA_CH_OBS / 64 + 1)];
     __shared__ unsigned short eobl[BA_CH_OBS];
     __shared__ unsigned char wz[BA_CH_OBS]; // W_ij forced to zero (fix masks, :140-154)
     const int ch = blockIdx.x, tid = threadIdx.x;
@@ -330,16 +333,33 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
     // Metadata of the reduction phases: loaded now, stored to LDS after the
     // projections, so its dependent loads ride along with the observation and
     // camera loads instead of adding round trips (and a barrier) up front.
+    // Every load of this prologue and of the projections' operands is
+    // issued by every lane at a clamped, valid index (no divergent branch
+    // around a load: the compiler then waits on each one before the next
+    // block), so the dependent chains overlap.
     const int u0 = eslot_optr[e0], nu = eslot_optr[e0 + nes] - u0;
-    const int m_eoff = tid <= nes ? eslot_optr[e0 + tid] - u0 : 0;
-    const int m_lptr = tid <= np ? (seg ? (tid ? nobs : 0) : pt_ptr[p0 + tid] - obase) : 0;
-    const int m_eobl = tid < nu ? eslot_obs[u0 + tid] : 0;
+    {
+        const int wv = tid >> 6;   // uniform per wave
+        if (wv <= (nes >> 6))
+            __builtin_amdgcn_global_load_lds(eslot_optr + e0 + min(tid, nes), eoff_raw + 64 * wv,
+                                             4, 0, 0);
+        if (!seg && wv <= (np >> 6))
+            __builtin_amdgcn_global_load_lds(pt_ptr + p0 + min(tid, np), lptr_raw + 64 * wv, 4, 0,
+                                             0);
+    }
+    int m_eobl = 0;
     STAMP(16);
     double sse = 0.0;
-    {
+    if (nobs > 0) {   // (nu > 0 too)
+        m_eobl = __hip_atomic_load(eslot_obs + u0 + min(tid, nu - 1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+        // lanes past the chunk's observations project its last one again
+        // into rows nobs .. BA_CH_OBS - 1, which nothing reads
         const int lo = tid >> 1, half = tid & 1;
-        if (lo < nobs) {
-            const int o = obase + lo, j = obs_cam[o], i = p0 + obs_lpt[o];
+        const bool live = lo < nobs;
+        {
+            const int o = obase + min(lo, nobs - 1);
+            const int j = obs_cam[o], i = p0 + obs_lpt[o];
             const double bi[3] = {b[3 * (size_t)i], b[3 * (size_t)i + 1],
                                   b[3 * (size_t)i + 2]};
             cam_view<NA> cv(a, K4, rot, j);
@@ -368,13 +388,11 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
                 const double e1 = obs_x[2 * (size_t)o + 1] - xh[1];
                 row[2 * NA + 6] = e0;
                 row[2 * NA + 7] = e1;
-                sse = e0 * e0 + e1 * e1;
+                if (live) sse = e0 * e0 + e1 * e1;
                 wz[lo] = f.fix_structure || f.fix_motion || (f.has_pivot && pivot[j]);
             }
         }
     }
-    if (tid <= nes) eoff[tid] = m_eoff;
-    if (tid <= np) lptr[tid] = m_lptr;
     if (tid < nu) eobl[tid] = (unsigned short)m_eobl;
     __syncthreads();
     STAMP(17);
@@ -410,7 +428,8 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
     // V_i += B^T B, eB_i += B^T e over the point's cameras (:293-302, :326-332)
     for (int q = tid; q < np * 12; q += 256) {
         const int pl = q / 12, e = q % 12, i = p0 + pl;
-        const int lo0 = lptr[pl], lo1 = lptr[pl + 1];
+        const int lo0 = seg ? 0 : lptr_raw[pl] - obase;
+        const int lo1 = seg ? nobs : lptr_raw[pl + 1] - obase;
         // one loop for both kinds (no divergent pair of loops in a wave): e
         // is the column after B's three, B[6], B[7]
         const int r = (e < 9) ? e % 3 : e - 9, c = (e < 9) ? e / 3 : 3;
@@ -442,8 +461,8 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
         // four observations a step: their index and data reads in flight
         // together, the sum still taken one observation at a time in order
         double acc = 0.0;
-        int u = eoff[s];
-        const int u1 = eoff[s + 1];
+        int u = eoff_raw[s] - u0;
+        const int u1 = eoff_raw[s + 1] - u0;
         for (; u + 3 < u1; u += 4) {
             double p[4];
 #pragma unroll
