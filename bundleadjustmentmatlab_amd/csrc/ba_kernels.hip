@@ -94,7 +94,7 @@ __device__ __forceinline__ void fd_columns_6(const cam_view<6> &cv, const double
                                              const double xh[2], int half, double *row)
 {
     const double *t0 = cv.a0 + 3;
-#pragma unroll 1
+#pragma unroll
     for (int t = 0; t < 3; t++) {
         const double *Rs = cv.R + 9 * (half ? 0 : 1 + t);
         double Rk[9], tt[3], bb[3], x1[2];
@@ -528,8 +528,22 @@ __device__ __forceinline__ void camera_reduce_wg(int j, const ba_camred &a)
     const int l = tid % NT, p = tid / NT;
     if (p < P) {
         const int q0 = cam_eptr[j], q1 = cam_eptr[j + 1];
+        // four partials of the stream a step: their index and value loads in
+        // flight together (a dependent pair of L2 round trips per partial
+        // otherwise), added in stream order
         double acc = 0.0;
-        for (int q = q0 + p; q < q1; q += P) acc += upart[(size_t)NT * cam_eslots[q] + l];
+        int q = q0 + p;
+        for (; q + 3 * P < q1; q += 4 * P) {
+            int ix[4];
+            double v[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) ix[k] = cam_eslots[q + k * P];
+#pragma unroll
+            for (int k = 0; k < 4; k++) v[k] = upart[(size_t)NT * ix[k] + l];
+#pragma unroll
+            for (int k = 0; k < 4; k++) acc += v[k];
+        }
+        for (; q < q1; q += P) acc += upart[(size_t)NT * cam_eslots[q] + l];
         part[p][l] = acc;
     }
     __syncthreads();
