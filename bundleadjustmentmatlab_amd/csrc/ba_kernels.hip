@@ -1551,7 +1551,7 @@ __global__ __launch_bounds__(256) void k_point_update_chunk(
     }
     __shared__ double wl[BA_CH_OBS * 3 * NA];   // the chunk's W rows, then t_o
     __shared__ double bn[BA_CH_PTS * 3];
-    __shared__ int lptr[BA_CH_PTS + 1];
+    __shared__ int lptr_raw[BA_CH_PTS];   // pt_ptr[p0 + t], t < np (wave 0: np <= 64)
     const int ch = blockIdx.x, tid = threadIdx.x;
     // segment chunk of a long track: db / b_new come from k_long_db (the sum
     // over all the track's observations); this chunk projects its part
@@ -1597,34 +1597,42 @@ __global__ __launch_bounds__(256) void k_point_update_chunk(
         block_sum_to<256>(dpg, part_dpg + ch);
         return;
     }
-    if (tid <= np) lptr[tid] = pt_ptr[p0 + tid] - obase;
-    // observation lanes: camera, point slot, x and the da row (zero past ndb)
+    // Load order = dependence depth: the chunk's W rows (HBM, the bulk) first,
+    // the point offsets by LDS-DMA, the observations, then their da rows; no
+    // load sits in a branch (the compiler would wait on it before the next)
+    constexpr int MAXE = (BA_CH_OBS * 3 * NA + 255) / 256;
+    const int ne = nobs * 3 * NA;
+    double wr[MAXE];
     int oj = 0, opl = 0;
     double ox0 = 0.0, ox1 = 0.0, dl[NA];
+    if (nobs > 0) {
+        // the chunk's W rows are one contiguous range: read lane by lane (each
+        // cache line requested once, not six times by 48-byte-strided lanes)
+        const double *wsrc = W + (size_t)3 * NA * obase;
 #pragma unroll
-    for (int k = 0; k < NA; k++) dl[k] = 0.0;
-    if (tid < nobs) {
-        const int o = obase + tid;
+        for (int u = 0; u < MAXE; u++) {
+            const int e = tid + 256 * u;
+            wr[u] = wsrc[e < ne ? e : 0];
+        }
+        static_assert(BA_CH_PTS <= 64, "one wave loads the point offsets");
+        if (tid < 64)   // wave 0
+            // (&lptr_raw[0], not the bare array: the builtin does not decay an
+            // array argument and would read its first element as the address)
+            __builtin_amdgcn_global_load_lds(pt_ptr + p0 + min(tid, np - 1), &lptr_raw[0], 4, 0,
+                                             0);
+        // observation lanes: camera, point slot, x and the da row (zero past
+        // ndb); lanes past the chunk's observations read its last one
+        const int o = obase + min(tid, nobs - 1);
         oj = obs_cam[o];
         opl = obs_lpt[o];
         ox0 = obs_x[2 * (size_t)o];
         ox1 = obs_x[2 * (size_t)o + 1];
         const double *d = da + (size_t)NA * oj;
 #pragma unroll
-        for (int k = 0; k < NA; k++) dl[k] = k < ndb ? d[k] : 0.0;
-    }
-    // the chunk's W rows are one contiguous range: read lane by lane (each cache
-    // line requested once, not six times by 48-byte-strided lanes) into LDS
-    {
-        constexpr int MAXE = (BA_CH_OBS * 3 * NA + 255) / 256;
-        const int ne = nobs * 3 * NA;
-        const double *wsrc = W + (size_t)3 * NA * obase;
-        double wr[MAXE];
+        for (int k = 0; k < NA; k++) dl[k] = d[k];
 #pragma unroll
-        for (int u = 0; u < MAXE; u++) {
-            const int e = tid + 256 * u;
-            wr[u] = wsrc[e < ne ? e : 0];
-        }
+        for (int k = 0; k < NA; k++)
+            if (k >= ndb) dl[k] = 0.0;
 #pragma unroll
         for (int u = 0; u < MAXE; u++) {
             const int e = tid + 256 * u;
@@ -1652,7 +1660,8 @@ __global__ __launch_bounds__(256) void k_point_update_chunk(
     if (tid < np) {
         const int i = p0 + tid;
         double rhs[3] = {eB[3 * (size_t)i], eB[3 * (size_t)i + 1], eB[3 * (size_t)i + 2]};
-        for (int lo = lptr[tid]; lo < lptr[tid + 1]; lo++) {
+        const int lo1 = tid + 1 < np ? lptr_raw[tid + 1] - obase : nobs;
+        for (int lo = lptr_raw[tid] - obase; lo < lo1; lo++) {
 #pragma unroll
             for (int r = 0; r < 3; r++) rhs[r] -= wl[3 * NA * lo + NA * r];
         }
