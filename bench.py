@@ -62,7 +62,7 @@ def main():
         return spawn_ranks(args)
     if args.spawn_selftest:
         return spawn_selftest()
-    if args.config == "cfg5":
+    if args.config in ("cfg5", "cfg5x"):
         return bench_incremental(args)
 
     import torch
@@ -73,10 +73,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo")
-    torch.cuda.set_device(local)
-
     import bundleadjustmentmatlab_amd as pkg
+    from bundleadjustmentmatlab_amd.dist import rank_collective
     from bundleadjustmentmatlab_amd.scene import make_config
+    # one GPU per rank with RCCL; more ranks than GPUs share them over gloo
+    ndev = torch.cuda.device_count()   # (counting does not initialise the GPU)
+    comm_id, host_ar, local = (rank_collective(dist, rank, world, ndev) if world > 1
+                               else (None, None, local))
+    torch.cuda.set_device(local)
 
     t0 = time.time()
     sc = make_config(args.config, gpu=not args.host_scene, **({"device": local} if
@@ -88,15 +92,9 @@ def main():
     a0[0:3], a0[3:6] = sc.w0, sc.T0
     b0 = np.asfortranarray(sc.X0[:3])
 
-    comm_id = None
-    if world > 1:
-        from bundleadjustmentmatlab_amd.dist import unique_id_bytes
-        buf = [unique_id_bytes() if rank == 0 else None]
-        dist.broadcast_object_list(buf, src=0)
-        comm_id = buf[0]
     t0 = time.time()
     ba = pkg.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, num_a, device=local,
-                            rank=rank, world_size=world, comm_id=comm_id)
+                            rank=rank, world_size=world, comm_id=comm_id, allreduce=host_ar)
     ba.set_params(a0, b0)
     log(f"[bench] setup {time.time()-t0:.1f}s")
 
@@ -189,7 +187,10 @@ def main():
         "config": {"workload": f"{args.config}: {sc.m} cams x {sc.n} pts x {N} obs, "
                                "fix_calibration (num_a=6), full LM pass per step",
                    "cameras": sc.m, "points": sc.n, "observations": N,
-                   "parallelism": f"point-shard x{world}"},
+                   "parallelism": f"point-shard x{world}",
+                   "collective": "rccl" if comm_id is not None else
+                                 ("gloo host all-reduce (ranks share a GPU)" if world > 1 else
+                                  None)},
         "phases_ms": ph,
         "roofline": roof,
         "cpu_baseline": cpu,
@@ -286,23 +287,31 @@ def bench_solve(args, ba, sc, a0, b0, world, rank, barrier, torch, dist):
 def bench_incremental(args):
     """--config cfg5 (BASELINE.json configs[4]): replay the growing-BA call
     sequence of incr_reconstruction.m:223-341 (two bundle_euclid solves per
-    added camera) on the seeded 50-camera test_incremental scene.  A step is
-    one whole replay; value = BA solves/s."""
+    added camera) on the seeded 50-camera test_incremental scene; --config
+    cfg5x: the same on the scaled 1000-camera variant (scene.growing_scene).
+    Each solve picks its shard count with dist.choose_shards over the GPUs
+    present (1 -> 8 elastic point sharding: rank threads, RCCL between
+    distinct GPUs).  A step is one whole replay; value = BA solves/s."""
     import torch
     from bundleadjustmentmatlab_amd.incremental import incremental_bundle
     from bundleadjustmentmatlab_amd.scene import make_config
+    ndev = max(1, torch.cuda.device_count())
     torch.cuda.set_device(0)
-    sc = make_config("cfg5")
+    sc = make_config(args.config)
+    devices = list(range(ndev))
     for _ in range(args.warmup):
-        incremental_bundle(sc)
+        incremental_bundle(sc, devices=devices)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     res = None
     for _ in range(args.steps):
-        res = incremental_bundle(sc)
+        res = incremental_bundle(sc, devices=devices)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     sol = res["solves"]
+    shards = {}
+    for q in sol:
+        shards[str(q["shards"])] = shards.get(str(q["shards"]), 0) + 1
     passes = sum(q["passes"] for q in sol)
     obs_passes = sum(q["passes"] * q["observations"] for q in sol)
     out = {
@@ -314,11 +323,13 @@ def bench_incremental(args):
         "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (seeded generate_scene_and_motion restatement, SURVEY.md 8.d)",
-        "config": {"workload": f"cfg5: {sc.m} cams x {sc.n} pts x {sc.num_obs} obs, "
+        "config": {"workload": f"{args.config}: {sc.m} cams x {sc.n} pts x {sc.num_obs} obs, "
                                f"{len(sol)} growing solves per replay",
                    "cameras": sc.m, "points": sc.n, "observations": sc.num_obs,
-                   "parallelism": "x1"},
+                   "parallelism": f"elastic point shard over {ndev} GPU(s)",
+                   "solves_by_shard_count": shards},
         "final": {"cameras": sol[-1]["cameras"], "points": sol[-1]["points"],
+                  "observations": sol[-1]["observations"],
                   "error_final": float(sol[-1]["error"][-1])},
     }
     print(json.dumps(out), flush=True)

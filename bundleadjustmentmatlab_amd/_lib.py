@@ -53,13 +53,14 @@ class VlgbaResectProblem(ctypes.Structure):
 
 class VlgbaStats(ctypes.Structure):
     _fields_ = [("iterations", c_int), ("accepted", c_int), ("num_error", c_int),
-                ("lambda_", c_double), ("seconds", c_double)]
+                ("lambda_", c_double), ("seconds", c_double), ("pinv_passes", c_int),
+                ("spin_retries", c_int)]
 
 
 class VlgbaStepInfo(ctypes.Structure):
     _fields_ = [("old_sse", c_double), ("new_sse", c_double), ("dpg", c_double),
                 ("rho", c_double), ("lambda_", c_double), ("accepted", c_int),
-                ("chol_failed", c_int), ("pinv", c_int)]
+                ("chol_failed", c_int), ("pinv", c_int), ("spin_retry", c_int)]
 
 
 class VlgbaSceneSpec(ctypes.Structure):

@@ -32,7 +32,7 @@ from ._lib import (ALLREDUCE_FN, MODEL_EUCLIDEAN, MODEL_PROJECTIVE, NKERNELS, ON
 
 __all__ = ["bundle_euclid", "bundle_euclid_nomex", "bundle_euclid_obs", "BundleAdjuster",
            "bundle_euclid_resect",
-           "parse_options",
+           "parse_options", "pivot_mask",
            "mex_bundle_1_XABeUVWeAeB", "mex_bundle_2_Se_", "mex_bundle_3_db_new"]
 
 
@@ -47,9 +47,35 @@ def _dp(a):
 # ---------------------------------------------------------------------------
 # options (bundle_euclid.m:44-82)
 # ---------------------------------------------------------------------------
+def pivot_mask(pivot, m):
+    """The cameras ``U(:,:,pivot) = 0`` fixes (bundle_euclid.m:150-153), read
+    the way MATLAB indexes with ``pivot``: a logical mask (bool dtype) of any
+    length -- entries past m must be false -- or a list of 1-based camera
+    numbers (``'fix_pivot', 1`` or ``[1 3]``; duplicates allowed).  MATLAB
+    would grow U / W / eA for a true entry or an index past m, and errors on
+    an index that is not a positive integer; both are errors here.  Returns
+    the (m,) bool mask."""
+    p = np.asarray(pivot)
+    mask = np.zeros(m, dtype=bool)
+    flat = p.reshape(-1)
+    if p.dtype == bool:
+        if flat[m:].any():
+            raise ValueError("fix_pivot: logical index past the camera count")
+        mask[:min(flat.size, m)] = flat[:m]
+        return mask
+    if flat.size == 0:
+        return mask
+    v = flat.astype(np.float64)
+    if not np.all(np.isfinite(v)) or np.any(v != np.floor(v)) or v.min() < 1 or v.max() > m:
+        raise ValueError("fix_pivot: camera indices must be integers in 1..m")
+    mask[v.astype(np.int64) - 1] = True
+    return mask
+
+
 def parse_options(m, n, varargin, x=None, nomex=False):
     """Name/value options of bundle_euclid.m:53-78.  Unknown names are
-    ignored, as the reference's switch statement ignores them.  nomex=True
+    ignored, as the reference's switch statement ignores them.  'fix_pivot'
+    takes a logical mask or 1-based camera numbers (pivot_mask).  nomex=True
     parses bundle_euclid_nomex.m:50-70 instead, which has no 'fix_pivot': the
     name and its argument fall through its switch and are ignored."""
     o = dict(fix_structure=False, fix_motion=False, fix_pivot=False,
@@ -66,7 +92,7 @@ def parse_options(m, n, varargin, x=None, nomex=False):
         elif name == "fix_pivot":
             if not nomex:
                 o["fix_pivot"] = True
-                o["pivot"] = np.asarray(varargin[k + 1], dtype=bool).reshape(-1)
+                o["pivot"] = pivot_mask(varargin[k + 1], m)
             k += 1
         elif name == "fix_calibration":
             o["num_variableK"] = 0
@@ -140,7 +166,7 @@ class _PassLog:
                "old_sse": i.old_sse, "new_sse": i.new_sse, "error_old": sc(i.old_sse),
                "error_new": sc(i.new_sse), "dpg": i.dpg, "rho": i.rho,
                "accepted": bool(i.accepted), "chol_failed": bool(i.chol_failed),
-               "pinv": bool(i.pinv)}
+               "pinv": bool(i.pinv), "spin_retry": bool(i.spin_retry)}
         self.records.append(rec)
         try:
             if self._fn is not None:
@@ -285,9 +311,8 @@ class BundleAdjuster:
 
     def passes(self, n):
         """n full passes at the current parameters and lambda, each
-        relinearising, none changing the state (vlgba_run_passes; enqueued back
-        to back with the decisions on the device when VLGBA_DEVICE_LM=1); the
-        last pass's info."""
+        relinearising, none changing the state (vlgba_run_passes); the last
+        pass's info."""
         info = VlgbaStepInfo()
         check(self._L.vlgba_run_passes(self._h, int(n), ctypes.byref(info)), "vlgba_run_passes")
         return info

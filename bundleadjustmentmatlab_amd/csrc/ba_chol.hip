@@ -5,7 +5,8 @@
 // symmetric positive definite once its exactly-zero rows (fixed parameters,
 // App. A Q2/Q8) are given a unit diagonal (k_fix_diag), and on that matrix
 // pinv and the Cholesky solve agree to conditioning-limited rounding.  A
-// non-positive pivot sets *status (the host treats the step as rejected).
+// non-positive pivot sets status[0]; the host then takes da = pinv(S) e_
+// (rocSOLVER dsyevd, ba_solver.cpp pinv_fallback), as bundle_euclid.m:193 does.
 //
 // Storage: S column major, leading dimension lds (multiple of NB = 64), lower
 // triangle.  Tile envelope: tile row i of S (hence of L: the profile is
@@ -602,7 +603,7 @@ __global__ __launch_bounds__(256) void k_backward(const double *__restrict__ S, 
 // write-through granules (cdna_hip_programming.md Guideline 16, R2); each x_k
 // is swept by wave 0 until every tag matches.  Used when every column is
 // co-resident (one workgroup per CU by LDS: nt <= CUs); a spin that never
-// ends sets status = 2 instead of hanging.  Each tile (k, j) is loaded while
+// ends sets the timeout word status[1] instead of hanging.  Each tile (k, j) is loaded while
 // the wave waits for x_k.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_backward_all(const double *__restrict__ S, long long lds,
@@ -635,7 +636,7 @@ __global__ __launch_bounds__(256) void k_backward_all(const double *__restrict__
                 v1 = __hip_atomic_load(g + 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (__all((unsigned)(v0 >> 32) == epoch && (unsigned)(v1 >> 32) == epoch)) break;
                 if (spins >= BA_BACK_SPIN_MAX) {
-                    if (lane == 0) status[0] = 2.0;
+                    if (lane == 0) status[1] = 1.0;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(2);
@@ -1347,7 +1348,8 @@ __global__ __launch_bounds__(256) void k_cr32_back(const int *__restrict__ elim,
 // (write-through agent-scope stores: the data is the flag, no fences;
 // MI355X_MICROARCH.md / cdna_hip_programming.md Guideline 16, R2).  One wave
 // sweeps one neighbour's 64 granules until every tag matches; a spin that
-// never ends sets status = 2 (the pass then takes the pinv path) instead of
+// never ends sets the timeout word status[1] (the host then re-solves the pass
+// with the per-level launches, which never spin) instead of
 // hanging.  Same arithmetic as k_cr32_back.
 template <bool SC>
 __device__ __forceinline__ void cr32_back_body(const cr32_lds &sh, int e, int p, int q, int nt,
@@ -1374,7 +1376,7 @@ __device__ __forceinline__ void cr32_back_body(const cr32_lds &sh, int e, int p,
                 v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (__all((unsigned)(v >> 32) == epoch)) break;
                 if (spins >= BA_BACK_SPIN_MAX) {
-                    if (lane == 0) status[0] = 2.0;
+                    if (lane == 0) status[1] = 1.0;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(2);
@@ -1450,7 +1452,8 @@ __global__ __launch_bounds__(256) void k_cr32_back_all(const int *__restrict__ e
 // keeps one workgroup per CU (the row of MI355X_MICROARCH.md's hand-off table
 // this protocol follows).  Records wait only on records with lower block
 // indices, so in-order dispatch makes progress without co-residency; every
-// spin is bounded (status = 2: the pass takes the pinv path).
+// spin is bounded (timeout word status[1]: the host re-solves with the per-level
+// launches).
 // ---------------------------------------------------------------------------
 #define BA_CR_MAXLEV 30
 struct cr32_fplan {
@@ -1477,7 +1480,7 @@ __device__ __forceinline__ void cr32_wait_flags(const unsigned *flag, int nw, co
                                                             __HIP_MEMORY_SCOPE_AGENT) == epoch;
             if (__all(ok)) break;
             if (spins >= BA_BACK_SPIN_MAX) {
-                if (lane == 0) status[0] = 2.0;
+                if (lane == 0) status[1] = 1.0;
                 break;
             }
             __builtin_amdgcn_s_sleep(2);
@@ -1525,10 +1528,8 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
                                                     double *linv, double *crL, double *rhs,
                                                     double *y, double *x, unsigned *flag,
                                                     unsigned long long *xg, unsigned epoch,
-                                                    double *status, cr32_fplan P,
-                                                    const ba_lm *lm)
+                                                    double *status, cr32_fplan P)
 {
-    if (lm && lm_flag(&lm->done)) return;   // a pass enqueued past the device LM's end
     CR32_LDS_DECL;
     CR_ST(0);
     const int b = blockIdx.x;
@@ -1647,13 +1648,15 @@ __global__ __launch_bounds__(256) void k_assemble_tiles(
     double *__restrict__ S, long long lds, const int *__restrict__ env,
     const int *__restrict__ tb_ptr, const int *__restrict__ tb_blk,
     const int *__restrict__ blk_jk, const double *__restrict__ sblk, int na, long long ld,
-    double *__restrict__ rhs, double *__restrict__ status, const ba_lm *lm)
+    double *__restrict__ rhs, double *__restrict__ status)
 {
-    if (lm && lm_flag(&lm->done)) return;   // a pass enqueued past the device LM's end
     __shared__ double T[NB * (NB + 1)];
     const int ti = env[2 * blockIdx.x], tk = env[2 * blockIdx.x + 1], tid = threadIdx.x;
     for (int q = tid; q < NB * (NB + 1); q += 256) T[q] = 0.0;
-    if (blockIdx.x == 0 && tid == 0) status[0] = 0.0;
+    if (blockIdx.x == 0 && tid == 0) {
+        status[0] = 0.0;   // non-positive pivot
+        status[1] = 0.0;   // bounded hand-off spin gave up
+    }
     __syncthreads();
     const long long r0 = (long long)NB * ti, c0 = (long long)NB * tk;
     const int na2 = na * na;
@@ -2090,7 +2093,7 @@ int ba_assemble_tiles(ba_dev *d)
 {
     k_assemble_tiles<<<d->n_env, 256, 0, d->stream>>>(d->S, d->lds, d->env_tiles, d->tb_ptr,
                                                       d->tb_blk, d->blk_jk, d->sblk, d->na, d->ld,
-                                                      d->rhs, d->scal + 4, d->lm);
+                                                      d->rhs, d->scal + 4);
     return -(int)hipGetLastError();
 }
 
@@ -2106,7 +2109,7 @@ int ba_chol_fix_diag(ba_dev *d)
     return -(int)hipGetLastError();
 }
 
-int ba_chol_solve(ba_dev *d)
+int ba_chol_solve(ba_dev *d, int nospin)
 {
     const int nt = d->nt;
     const size_t smem3 = sizeof(double) * 3 * NB * LP;
@@ -2120,7 +2123,7 @@ int ba_chol_solve(ba_dev *d)
         KT_E(d, KT_FACTOR);
         return -(int)hipGetLastError();
     }
-    if (d->cr_nlev > 0 && d->cr32 && d->cr_fused && d->crflag) {   // one launch
+    if (d->cr_nlev > 0 && d->cr32 && d->cr_fused && d->crflag && !nospin) {   // one launch
         const int nl = d->cr_nlev, nrec = d->cr_eptr_h[nl];
         cr32_fplan P{};
         P.nl = nl;
@@ -2141,7 +2144,7 @@ int ba_chol_solve(ba_dev *d)
         KT_B(d);
         k_cr32_fused<<<P.b0[nl] + nrec, 256, 0, d->stream>>>(
             d->S, d->lds, d->tb32, d->ld, d->cr_elim, d->crf, d->crs, d->nt32, d->linv, d->crL,
-            d->rhs, d->ywork, d->da, d->crflag, d->xgran, d->back_epoch, d->scal + 4, P, d->lm);
+            d->rhs, d->ywork, d->da, d->crflag, d->xgran, d->back_epoch, d->scal + 4, P);
         KT_E(d, KT_CR_FACTOR);
         return -(int)hipGetLastError();
     }
@@ -2168,7 +2171,7 @@ int ba_chol_solve(ba_dev *d)
             KT_E(d, KT_CR_FACTOR);
         }
         const int nrec = d->cr_eptr_h[d->cr_nlev];
-        if (d->xgran && nrec <= 2 * d->ncu) {   // every record co-resident: one launch
+        if (d->xgran && nrec <= 2 * d->ncu && !nospin) {   // every record co-resident: one launch
             if (++d->back_epoch == 0) d->back_epoch = 1;
             KT_B(d);
             k_cr32_back_all<<<nrec, 256, 0, d->stream>>>(d->cr_elim, nrec, n32, TB, d->ld,
@@ -2228,7 +2231,7 @@ int ba_chol_solve(ba_dev *d)
             d->ywork, d->scal + 4);
         KT_E(d, KT_FACTOR);
     }
-    if (d->xgran64) {   // every column co-resident: the backward solve in one launch
+    if (d->xgran64 && !nospin) {   // every column co-resident: the backward solve in one launch
         if (++d->back_epoch == 0) d->back_epoch = 1;
         const size_t smem2 = sizeof(double) * 2 * NB * LP;
         TRY_RC(ba_ensure_dyn_lds((const void *)k_backward_all, smem2));

@@ -77,43 +77,6 @@ struct ba_camred {
     double *sse_out, *sse_out2;
 };
 
-// Device-side Levenberg-Marquardt state (vlgba_run without host round trips):
-// the accept / lambda / stop decisions of bundle_euclid.m:205-241 taken by
-// k_lm_decide after each pass; the pass kernels read lambda, whether to
-// relinearise and which parameter buffers are current from here.
-struct ba_lm {
-    double lambda, nu, num_vis, stop_rel;
-    int iter, iter2, passes, acc;
-    int done;      // 1: stop rule / caps met; 2: non-positive pivot (the host takes the pinv step)
-    int relin;     // the next pass relinearises
-    int sel;       // current parameters: 0 = (a, b, rot), 1 = (a_new, b_new, rot_new)
-    int nerr;      // error_ entries
-    int max_iter, max_iter2, proj, force;   // force: passes that relinearise and never commit
-    int cap;       // error_ capacity
-    int pad;
-    double seq;    // decisions taken (published to the host as hres[7])
-};
-
-static_assert(sizeof(ba_lm) % 8 == 0, "ba_lm moves as 8-byte words");
-
-// Kernels read the LM state with vector loads at device scope.  Why not plain
-// reads: hipcc turns a uniform-address read into a scalar load, and in
-// k_lm_decide (which reads the status word and then clears it) the scalar
-// load and the vector store of the same word were issued back to back with
-// no wait between them (the scalar and vector memory paths are not ordered):
-// the load returned the cleared value.  Vector loads are ordered before a
-// later vector store of the same address.
-#ifdef __HIPCC__
-__device__ __forceinline__ double lm_lambda(const ba_lm *lm)
-{
-    return __hip_atomic_load(&lm->lambda, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int lm_flag(const int *p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-#endif
-
 struct ba_dev {
     int m, n, na, N, js;
     int device, ncu;   // HIP device ordinal and its CU count
@@ -178,15 +141,12 @@ struct ba_dev {
     int cr_fused;
     // reductions: partial sums per block of the reducing kernels, in fixed order
     double *part;      // [3][PART_MAX]
-    double *scal;      // [8] : 0 old_sse, 1 new_sse, 2 dpg cams, 3 dpg pts, 4 chol status
+    double *scal;      // [8] : 0 old_sse, 1 new_sse, 2 dpg cams, 3 dpg pts, 4 non-positive
+                       // pivot, 5 hand-off spin timeout (the solve's status words)
     int *chol_cnt;     // arrival counters for the triangular solves
     // ---- fast (chunked) Schur path: points in chunks of <= CH_OBS observations;
     // per chunk the co-visible blocks it touches ("slots") and the cameras it
     // sees ("e-slots") get one partial each, reduced per block in chunk order.
-    ba_lm *lm;         // device LM state of the running vlgba_run, else NULL (host loop)
-    double *lm_err;    // its error_ [cap]
-    ba_lm *lm_mem;     // allocation behind lm
-    int lm_cap;
     int ordered;       // 1: sequential bit-exact kernels (k_damp_point + k_schur)
     int parity;        // ordered = 2: + sequential solve and LM scalars (bit-identical
                        // LM trajectory with the oracle)
@@ -253,7 +213,7 @@ struct ba_dev {
     hipStream_t side;
     hipEvent_t ev_fork, ev_join;
     int join_pending;
-    // host-mapped pass results: [0..4] the scal slots, [7] the pass sequence
+    // host-mapped pass results: [0..5] the scal slots, [7] the pass sequence
     // number written last (k_publish); the host spins on it instead of a
     // device-to-host copy + stream synchronisation
     volatile double *hres;     // host view
@@ -302,14 +262,12 @@ int ba_launch_schur(ba_dev *d, double lambda);
 int ba_launch_assemble(ba_dev *d);
 int ba_launch_update(ba_dev *d, double lambda);
 int ba_launch_yeb(ba_dev *d);
-int ba_launch_publish(ba_dev *d);
-// the pass's LM decision on the device (d->lm), published to hres with seq
-int ba_launch_lm_decide(ba_dev *d);
+int ba_launch_publish(ba_dev *d);   // scal[0..5] + ++seq -> hres (host-mapped)
 void *ba_dmalloc(size_t bytes);   // per-device caching allocator (ba_solver.cpp)
 // raise kernel fn's dynamic-LDS limit to >= bytes on the current device (cached
 // per (kernel, device), thread-safe; ba_solver.cpp)
 int ba_ensure_dyn_lds(const void *fn, size_t bytes);
-void ba_dfree(void *p);   // scal[0..4] + ++seq -> hres (host-mapped)
+void ba_dfree(void *p);
 int ba_launch_schur_fast(ba_dev *d, double lambda);   // fused damp + Vinv + Y + S + e_
 int ba_launch_assemble_plain(ba_dev *d, double *S, long long ld, int lower_only);
 // parity mode (ordered = 2): sequential LM scalars in the reference's flat order
@@ -321,7 +279,9 @@ void ba_chol_free(ba_dev *d);
 int ba_chol_prepare(ba_dev *d);
 int ba_assemble_tiles(ba_dev *d);   // envelope tiles of S + pinv rule + status, one launch
 int ba_chol_fix_diag(ba_dev *d);
-int ba_chol_solve(ba_dev *d);
+// nospin = 1: only launches that never wait on other workgroups (the
+// per-level / per-column paths) -- the re-solve after a hand-off timeout
+int ba_chol_solve(ba_dev *d, int nospin = 0);
 // da = pinv(S) rhs from the eigen-decomposition S = V diag(ev) V^T (ev
 // ascending, V column major ld x ld): MATLAB's tolerance ld * eps(max |ev|)
 int ba_pinv_apply(ba_dev *d, const double *V, const double *ev, long long ld, const double *rhs,

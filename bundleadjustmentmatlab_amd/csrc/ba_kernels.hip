@@ -295,20 +295,8 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
     const double *__restrict__ b, ba_flags f, const unsigned char *__restrict__ pivot,
     double *__restrict__ W, double *__restrict__ V, double *__restrict__ eB,
     double *__restrict__ upart, double *__restrict__ part_sse, int nch_reg,
-    const int *__restrict__ seg_pt, double *__restrict__ vseg, const ba_lm *lm,
-    const double *__restrict__ a1, const double *__restrict__ rot1,
-    const double *__restrict__ b1)
+    const int *__restrict__ seg_pt, double *__restrict__ vseg)
 {
-    // device LM (vlgba_run): a rejected step keeps the linearisation; the
-    // current parameters are the buffers lm->sel names
-    if (lm) {
-        if (!lm_flag(&lm->relin) || lm_flag(&lm->done)) return;
-        if (lm_flag(&lm->sel)) {
-            a = a1;
-            rot = rot1;
-            b = b1;
-        }
-    }
     constexpr int NC0 = (NA + 4) / 2;       // lane 0: base + FD columns [0, NC0)
     constexpr int RS = 2 * NA + 8;          // LDS row: A (2 NA), B (6), e (2)
     constexpr int NU = NA * (NA + 1) / 2;
@@ -564,9 +552,8 @@ __device__ __forceinline__ void camera_reduce_wg(int j, const ba_camred &a)
 }
 
 template <int NA>
-__global__ __launch_bounds__(256) void k_camera_reduce_chunks(ba_camred a, const ba_lm *lm)
+__global__ __launch_bounds__(256) void k_camera_reduce_chunks(ba_camred a)
 {
-    if (lm && lm_flag(&lm->done)) return;   // a pass enqueued past the device LM's end
     camera_reduce_wg<NA>(blockIdx.x, a);
 }
 
@@ -745,12 +732,8 @@ __global__ __launch_bounds__(256) void k_schur_group(
     const unsigned *__restrict__ blob, const double *__restrict__ V,
     const double *__restrict__ eB, const double *__restrict__ W, double lambda, int bcap,
     int gcap, int ecap, double *__restrict__ Vinv, double *__restrict__ spart,
-    double *__restrict__ epart, const ba_lm *lm)
+    double *__restrict__ epart)
 {
-    if (lm) {
-        if (lm_flag(&lm->done)) return;   // a pass enqueued past the device LM's end
-        lambda = lm_lambda(lm);
-    }
     constexpr int WS = 3 * NA;
     constexpr int NR = (NA + 1) / 2;          // rows per half
     constexpr int NCP = (NA + 1) / 2;         // column pairs
@@ -952,13 +935,8 @@ __global__ __launch_bounds__(256) void k_schur_group(
 // lane: every cache line requested once)
 template <int NA>
 __global__ __launch_bounds__(256) void k_point_vinv(const double *__restrict__ V, int n,
-                                                    double lambda, double *__restrict__ Vinv,
-                                                    const ba_lm *lm = nullptr)
+                                                    double lambda, double *__restrict__ Vinv)
 {
-    if (lm) {
-        if (lm_flag(&lm->done)) return;
-        lambda = lm_lambda(lm);
-    }
     __shared__ double vsh[256 * 9];
     const int i0 = blockIdx.x * 256, tid = threadIdx.x;
     const int cnt = 9 * min(256, n - i0);
@@ -1054,9 +1032,8 @@ __global__ __launch_bounds__(256, (NA == 6) ? BA_MF_WAVES : 1) void k_schur_mfma
     const unsigned *__restrict__ blob, const double *__restrict__ W,
     const double *__restrict__ Vinv, const double *__restrict__ eB, int nobs_all, int n_all,
     int gcap, int ecap, double *__restrict__ spart, double *__restrict__ epart, int ngrp,
-    ba_camred cred, const ba_lm *lm)
+    ba_camred cred)
 {
-    if (lm && lm_flag(&lm->done)) return;   // a pass enqueued past the device LM's end
     // workgroups past the groups: the camera reduction of a relinearised pass
     // (independent of the Schur sums, due before k_schur_reduce), filling the
     // CUs the groups' tail leaves idle -- no side stream, no fork / join
@@ -1299,13 +1276,8 @@ __global__ void k_schur_reduce(const int *__restrict__ blk_jk, const int *__rest
                                const double *__restrict__ spart,
                                const double *__restrict__ epart, const double *__restrict__ U,
                                const double *__restrict__ eA, int nb, double lambda, int owner,
-                               double *__restrict__ sblk, double *__restrict__ rhs,
-                               const ba_lm *lm = nullptr)
+                               double *__restrict__ sblk, double *__restrict__ rhs)
 {
-    if (lm) {
-        if (lm_flag(&lm->done)) return;   // a pass enqueued past the device LM's end
-        lambda = lm_lambda(lm);
-    }
     const int bk = blockIdx.x, l = threadIdx.x;
     if (bk >= nb) return;
     const int j = blk_jk[2 * bk], k = blk_jk[2 * bk + 1];
@@ -1390,21 +1362,8 @@ template <int NA>
 __global__ __launch_bounds__(320) void k_camera_update(
     const double *__restrict__ a, const double *__restrict__ da,
     const double *__restrict__ eA, int m, double lambda, double *__restrict__ a_new,
-    double *__restrict__ rot_new, double *__restrict__ part, const ba_lm *lm, int dpg_lambda,
-    double *__restrict__ rot)
+    double *__restrict__ rot_new, double *__restrict__ part)
 {
-    // device LM: this pass's lambda (its dp'dp share on the dpg_lambda rank);
-    // current / new parameter buffers as lm->sel names them
-    if (lm) {
-        if (lm_flag(&lm->done)) return;
-        lambda = dpg_lambda ? lm_lambda(lm) : 0.0;
-        if (lm_flag(&lm->sel)) {
-            double *t = a_new;
-            a_new = const_cast<double *>(a);
-            a = t;
-            rot_new = rot;
-        }
-    }
     // 64 cameras per block; wave k < 5 builds rotation k of each camera's
     // table (the libm-exact sin / cos chains run side by side), wave 0 also
     // forms a_new and the camera part of dp'(lambda dp + g) (one wave's sum,
@@ -1533,22 +1492,8 @@ __global__ __launch_bounds__(256) void k_point_update_chunk(
     double lambda, double *__restrict__ db, double *__restrict__ b_new,
     double *__restrict__ part_sse, double *__restrict__ part_dpg, int nch_reg,
     const int *__restrict__ seg_pt, const int *__restrict__ seg_long,
-    const int *__restrict__ long_o0, const double *__restrict__ dpg_long, const ba_lm *lm,
-    const double *__restrict__ a0, const double *__restrict__ rot0)
+    const int *__restrict__ long_o0, const double *__restrict__ dpg_long)
 {
-    // device LM: lambda and the current (b) / new (b_new, a_new, rot_new)
-    // buffers as lm->sel names them
-    if (lm) {
-        if (lm_flag(&lm->done)) return;
-        lambda = lm_lambda(lm);
-        if (lm_flag(&lm->sel)) {
-            double *t = b_new;
-            b_new = const_cast<double *>(b);
-            b = t;
-            a_new = a0;
-            rot_new = rot0;
-        }
-    }
     __shared__ double wl[BA_CH_OBS * 3 * NA];   // the chunk's W rows, then t_o
     __shared__ double bn[BA_CH_PTS * 3];
     __shared__ int lptr_raw[BA_CH_PTS];   // pt_ptr[p0 + t], t < np (wave 0: np <= 64)
@@ -1834,17 +1779,15 @@ struct ba_sum3 {
     int n[3];
     double *out[3];
     // optional publish (k_publish folded in): the last block to finish copies
-    // scal[0..4] to the host-mapped hres, then the sequence number
+    // scal[0..5] to the host-mapped hres, then the sequence number
     const double *scal;
     double *hres;
     double seq;
     unsigned *cnt;   // zero between launches (the last block resets it)
-    const ba_lm *lm; // device LM: nothing to sum in a pass enqueued past its end
 };
 
 __global__ __launch_bounds__(1024) void k_sum_parts3(ba_sum3 a)
 {
-    if (a.lm && lm_flag(&a.lm->done)) return;
     const double *part = a.part[blockIdx.x];
     const int nparts = a.n[blockIdx.x];
     double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
@@ -1862,7 +1805,7 @@ __global__ __launch_bounds__(1024) void k_sum_parts3(ba_sum3 a)
         if (atomicAdd(a.cnt, 1u) == 2u) {   // the three sums are in scal
             __threadfence();
             const volatile double *sc = a.scal;
-            for (int k = 0; k < 5; k++) a.hres[k] = sc[k];
+            for (int k = 0; k < 6; k++) a.hres[k] = sc[k];
             __threadfence_system();
             *a.cnt = 0u;
             __atomic_store_n((unsigned long long *)(a.hres + 7), __double_as_longlong(a.seq),
@@ -1932,8 +1875,7 @@ int ba_launch_linearize(ba_dev *d, ba_flags f)
                                    d->ch_pt, d->ch_obase, d->ch_eslot, d->eslot_optr,
                                    d->eslot_obs, d->pt_ptr, d->obs_cam, d->obs_lpt, d->obs_x,
                                    d->K4, d->a, d->rot, d->b, f, d->pivot, d->W, d->V, d->eB,
-                                   d->upart, d->chsse, d->nch_reg, d->seg_pt, d->vseg, d->lm,
-                                   d->a_new, d->rot_new, d->b_new)));
+                                   d->upart, d->chsse, d->nch_reg, d->seg_pt, d->vseg)));
         if (d->nl > 0)   // long tracks: V / eB = sum of their segments' partials
             k_long_vsum<<<d->nl, 64, 0, d->stream>>>(d->long_pt, d->long_seg0, d->vseg, d->V,
                                                      d->eB);
@@ -1965,7 +1907,7 @@ int ba_launch_camera_reduce(ba_dev *d, ba_flags f, int fuse)
         }
         KT_B(d);
         BA_DISPATCH(d->na, (k_camera_reduce_chunks<NA><<<d->m + 1, 256, 0, d->stream>>>(
-                               d->camred, d->lm)));
+                               d->camred)));
         KT_E(d, KT_CAMRED);
         return -(int)hipGetLastError();
     }
@@ -2003,8 +1945,7 @@ static int launch_schur_fast(ba_dev *d, double lambda)
     // MFMA groups [0, ngrp_mf), then the per-term groups [ngrp_mf, ngrp)
     if (d->ngrp_mf > 0) {
         KT_B(d);
-        k_point_vinv<NA><<<(d->n + 255) / 256, 256, 0, d->stream>>>(d->V, d->n, lambda, d->Vinv,
-                                                                   d->lm);
+        k_point_vinv<NA><<<(d->n + 255) / 256, 256, 0, d->stream>>>(d->V, d->n, lambda, d->Vinv);
         KT_E(d, KT_DAMP);
         const size_t sm2 = sizeof(double) * (d->mf_max_s * NA * NA + d->mf_max_e * NA) +
                            sizeof(unsigned) * (size_t)d->mf_max_blob;
@@ -2015,7 +1956,7 @@ static int launch_schur_fast(ba_dev *d, double lambda)
         k_schur_mfma<NA><<<d->ngrp_mf + ncr, 256, sm2, d->stream>>>(
             d->grp_ch, d->grp_gs, d->grp_ge, d->ch_pt, d->ch_obase, d->ch_blob, d->blob, d->W,
             d->Vinv, d->eB, d->N, d->n, d->mf_max_s, d->mf_max_e, d->spart, d->epart,
-            d->ngrp_mf, d->camred, d->lm);
+            d->ngrp_mf, d->camred);
         KT_E(d, KT_SCHUR_MF);
     }
     if (d->ngrp > d->ngrp_mf) {
@@ -2029,7 +1970,7 @@ static int launch_schur_fast(ba_dev *d, double lambda)
         k_schur_group<NA><<<d->ngrp - d->ngrp_mf, 256, smem, d->stream>>>(
             d->grp_ch + d->ngrp_mf, d->grp_gs + d->ngrp_mf, d->grp_ge + d->ngrp_mf, d->ch_pt,
             d->ch_obase, d->ch_blob, d->blob, d->V, d->eB, d->W, lambda, bcap, gcap, ecap,
-            d->Vinv, d->spart, d->epart, d->lm);
+            d->Vinv, d->spart, d->epart);
         KT_E(d, KT_SCHUR_CHUNK);
     }
     if (d->nl > 0) {   // long tracks: their V*^-1, then their (obs, obs) tiles
@@ -2051,7 +1992,7 @@ static int launch_schur_fast(ba_dev *d, double lambda)
     KT_B(d);
     k_schur_reduce<NA><<<d->nb, bs, 0, d->stream>>>(
         d->blk_jk, d->blk_gptr, d->blk_gslots, d->cam_gptr, d->cam_gslots, d->spart, d->epart,
-        d->U, d->eA, d->nb, lambda, d->schur_owner, d->sblk, d->rhs, d->lm);
+        d->U, d->eA, d->nb, lambda, d->schur_owner, d->sblk, d->rhs);
     KT_E(d, KT_SCHUR_RED);
     return -(int)hipGetLastError();
 }
@@ -2071,135 +2012,13 @@ int ba_launch_schur_fast(ba_dev *d, double lambda)
 // (system-scope release): the host reads them without a copy or a stream sync
 __global__ void k_publish(const double *__restrict__ scal, double *hres, double seq)
 {
-    if (threadIdx.x < 5) hres[threadIdx.x] = scal[threadIdx.x];
+    if (threadIdx.x < 6) hres[threadIdx.x] = scal[threadIdx.x];
     __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) {
         __atomic_store_n((unsigned long long *)(hres + 7), __double_as_longlong(seq),
                          __ATOMIC_RELEASE);
     }
-}
-
-// ---------------------------------------------------------------------------
-// The LM decision of one pass on the device (vlgba_run's loop body,
-// bundle_euclid.m:205-241 / bundle_projective.m:182-207): accept or reject,
-// error_, lambda / nu, the parameter buffers (lm->sel), whether the next pass
-// relinearises, and the stop test of the next iteration (:111-123).  A
-// non-positive pivot (status) stops the device loop (done = 2) without
-// committing: the host then takes that pass's pinv step.  Decisions arriving
-// after done (passes enqueued ahead) change nothing.  Publishes the pass
-// scalars, done and the decision count to the host-mapped hres.
-// ---------------------------------------------------------------------------
-// (2 rho - 1)^3 rounded once: the square exactly as a double-double, then
-// times t with the error terms added (pow(t, 3) of the host loop up to the
-// rare halfway case)
-__device__ __forceinline__ double cube_rn(double t)
-{
-    const double h = t * t, l = fma(t, t, -h);   // t^2 = h + l exactly
-    const double p = h * t, e = fma(h, t, -p);   // h t = p + e exactly
-    return p + (e + l * t);
-}
-
-__global__ void k_lm_decide(ba_lm *__restrict__ lm, double *__restrict__ err,
-                            double *__restrict__ scal, double *hres)
-{
-    if (threadIdx.x != 0) return;
-    // the state, error_ and the pass scalars by vector loads at device scope:
-    // a scalar load of scal[4] raced the clearing store below (ba_internal.h)
-    constexpr int NW = sizeof(ba_lm) / 8;
-    unsigned long long w[NW];
-#pragma unroll
-    for (int q = 0; q < NW; q++)
-        w[q] = __hip_atomic_load(reinterpret_cast<unsigned long long *>(lm) + q, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-    ba_lm L;
-    __builtin_memcpy(&L, w, sizeof L);
-    auto err_at = [&](int k) {
-        return __hip_atomic_load(err + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
-    // vector loads at device scope: ordered before the clearing store below
-    double sv[5];
-#pragma unroll
-    for (int q = 0; q < 5; q++)
-        sv[q] = __hip_atomic_load(scal + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const double old = sv[0], nw = sv[1], dpg = sv[2] + sv[3], st = sv[4];
-    scal[4] = 0.0;   // the factorisation status, for the next pass
-    if (!L.done) {
-        if (st != 0.0) {
-            L.done = 2;
-        } else if (L.force) {   // measurement passes: relinearise, never commit
-            L.passes++;
-            L.relin = 1;
-        } else {
-            L.passes++;
-            const double rho = (old - nw) / dpg;
-            const double iv = 1 / L.num_vis;
-            const bool acc = L.proj ? iv * nw < iv * old : (old - nw) > 0;
-            if (acc) {
-                const double olde = L.proj ? iv * old : old / L.num_vis;
-                const double newe = L.proj ? iv * nw : nw / L.num_vis;
-                auto put = [&](int k, double v) {
-                    if (k < L.cap)
-                        __hip_atomic_store(err + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                };
-                if (L.nerr < L.iter) {
-                    put(L.nerr, olde);
-                    L.nerr++;
-                } else {
-                    put(L.iter - 1, olde);
-                }
-                L.iter++;
-                put(L.nerr, newe);
-                L.nerr++;
-                L.iter2 = 0;
-                L.acc++;
-                L.sel ^= 1;
-                L.relin = 1;
-                if (L.proj)
-                    L.lambda = L.lambda / 10;
-                else
-                    L.lambda = L.lambda * fmax(1.0 / 3.0, 1.0 - cube_rn(2.0 * rho - 1.0));
-                L.nu = 2.0;
-            } else {
-                L.iter2++;
-                L.relin = 0;
-                if (L.proj) {
-                    L.lambda = L.lambda * 10;
-                } else {
-                    L.lambda = L.lambda * L.nu;
-                    L.nu = 2.0 * L.nu;
-                }
-            }
-            if (!(L.iter < L.max_iter && L.iter2 < L.max_iter2)) {
-                L.done = 1;
-            } else if (L.iter >= 3) {
-                const double e1 = err_at(L.iter - 1), e0 = err_at(L.iter - 2);
-                if (!(e1 > 1e-20 && e0 - e1 > L.stop_rel * e0)) L.done = 1;
-            }
-        }
-    }
-    L.seq = L.seq + 1.0;
-    __builtin_memcpy(w, &L, sizeof L);
-#pragma unroll
-    for (int q = 0; q < NW; q++)
-        __hip_atomic_store(reinterpret_cast<unsigned long long *>(lm) + q, w[q], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    hres[0] = old;
-    hres[1] = nw;
-    hres[2] = sv[2];
-    hres[3] = sv[3];
-    hres[4] = st;
-    hres[5] = (double)L.done;
-    hres[6] = (double)L.passes;
-    __threadfence_system();
-    __atomic_store_n((unsigned long long *)(hres + 7), __double_as_longlong(L.seq),
-                     __ATOMIC_RELEASE);
-}
-
-int ba_launch_lm_decide(ba_dev *d)
-{
-    k_lm_decide<<<1, 64, 0, d->stream>>>(d->lm, d->lm_err, d->scal, d->hres_dev);
-    return -(int)hipGetLastError();
 }
 
 int ba_launch_publish(ba_dev *d)
@@ -2232,8 +2051,8 @@ int ba_launch_update(ba_dev *d, double lambda)
     // lambda dp'dp once over the ranks (each adds da' eA of its partial eA)
     const double lam_dpg = d->dpg_lambda ? lambda : 0.0;
     BA_DISPATCH(d->na, (k_camera_update<NA><<<gc, 320, 0, d->stream>>>(
-                           d->a, d->da, d->eA, d->m, lam_dpg, d->a_new, d->rot_new, d->part,
-                           d->lm, d->dpg_lambda, d->rot)));
+                           d->a, d->da, d->eA, d->m, lam_dpg, d->a_new, d->rot_new,
+                           d->part)));
     KT_E(d, KT_CAMUPD);
     if (!d->ordered && d->nch > 0 && !d->obs_vis && !d->xh_out) {
         KT_B(d);
@@ -2247,13 +2066,13 @@ int ba_launch_update(ba_dev *d, double lambda)
                                d->obs_x, d->K4, d->W, d->da, d->eB, d->Vinv, d->b, d->a_new,
                                d->rot_new, d->ndb, lambda, d->db, d->b_new, d->chsse + d->nch,
                                d->chsse + 2 * (size_t)d->nch, d->nch_reg, d->seg_pt,
-                               d->seg_long, d->long_o0, d->dpg_long, d->lm, d->a, d->rot)));
+                               d->seg_long, d->long_o0, d->dpg_long)));
         KT_E(d, KT_PTUPD);
         // new SSE, point dpg, camera dpg: one launch
         ba_sum3 s3 = {{d->chsse + d->nch, d->chsse + 2 * (size_t)d->nch, d->part},
                       {d->nch, d->nch, gc},
                       {d->scal + 1, d->scal + 3, d->scal + 2},
-                      d->scal, nullptr, 0.0, d->pub_cnt, d->lm};
+                      d->scal, nullptr, 0.0, d->pub_cnt};
         if (d->publish_req) {
             d->seq++;
             s3.hres = d->hres_dev;

@@ -247,6 +247,30 @@ void build_blocks(int m, const std::vector<int> &pt_ptr_all, const std::vector<i
                 if (lower && j < k) continue;
                 hb.insert(j, k);
             }
+    // canonical block ids, (k, j) ascending: independent of the point order,
+    // so ranks that order their own points differently (order_points_by_kind)
+    // agree on the packed layout of the all-reduced blocks
+    {
+        const int nb0 = (int)hb.jk.size() / 2;
+        std::vector<int> ord(nb0);
+        std::iota(ord.begin(), ord.end(), 0);
+        std::sort(ord.begin(), ord.end(), [&](int u, int v) {
+            const int ku = hb.jk[2 * u + 1], kv = hb.jk[2 * v + 1];
+            return ku != kv ? ku < kv : hb.jk[2 * u] < hb.jk[2 * v];
+        });
+        std::vector<int> jk2(2 * (size_t)nb0);
+        for (int q = 0; q < nb0; q++) {
+            jk2[2 * q] = hb.jk[2 * ord[q]];
+            jk2[2 * q + 1] = hb.jk[2 * ord[q] + 1];
+        }
+        hb.jk.swap(jk2);
+        if (hb.dense_tab) {
+            for (int q = 0; q < nb0; q++) hb.tab[(size_t)hb.jk[2 * q] * m + hb.jk[2 * q + 1]] = q;
+        } else {
+            for (auto &r : hb.rows) r.clear();
+            for (int q = 0; q < nb0; q++) hb.rows[hb.jk[2 * q]].push_back({hb.jk[2 * q + 1], q});
+        }
+    }
     const int nb = (int)hb.jk.size() / 2;
     if (!need_terms) {
         hb.ptr.assign(nb + 1, 0);
@@ -744,8 +768,6 @@ struct vlgba_ctx {
     double lambda = 1e-3, lambda0 = 1e-3, nu = 2.0;
     int model = VLGBA_MODEL_EUCLIDEAN;
     int lin_valid = 0;
-    int device_lm = 0;   // VLGBA_DEVICE_LM=1: the LM decisions on the device (run_device)
-    ba_lm lm_host{};     // staging of the device LM state (async upload / download)
     int timing = 0;
     hipEvent_t ev[8] = {};
     double phase_ms[7] = {};
@@ -760,11 +782,14 @@ struct vlgba_ctx {
     // internal point order (fast path, one rank): the short-track points that
     // fit the MFMA Schur chunks first, then the rest, each in input order.
     // pperm[new] = input point, operm[new obs] = input observation (point-major
-    // input order); empty = identity.
+    // input order), both relative to this rank's first point / observation;
+    // empty = identity.
     std::vector<int> pperm, operm;
     double *pinv_S = nullptr, *pinv_ev = nullptr, *pinv_e = nullptr, *pinv_w = nullptr;
     int *pinv_info = nullptr;
     int pinv_used = 0;            // passes that took the pinv fallback
+    int spin_retries = 0;         // passes re-solved after a hand-off timeout
+    int debug_timeouts = 0;       // test hook: passes whose timeout word is forced
 };
 
 // Per-device pool of the context's streams, fork/join events and host-mapped
@@ -902,13 +927,15 @@ static int track_kind(long long k, int cmax)
     return 2;                                                     // long track
 }
 
-static void order_points_by_kind(int cmax, host_obs &h, std::vector<int> &pt_ptr,
-                                 std::vector<int> &pperm, std::vector<int> &operm)
+static void order_points_by_kind(int cmax, host_obs &h, std::vector<int> &pt_ptr, int p0,
+                                 int p1, std::vector<int> &pperm, std::vector<int> &operm)
 {
-    const int n = (int)pt_ptr.size() - 1;
+    // points [p0, p1) of the global point-major arrays (this rank's range);
+    // pperm / operm are relative to p0 / the range's first observation
+    const int n = p1 - p0;
     int cnt[3] = {0, 0, 0};
     long long lterms = 0;
-    for (int i = 0; i < n; i++) {
+    for (int i = p0; i < p1; i++) {
         const long long k = pt_ptr[i + 1] - pt_ptr[i];
         const int kind = track_kind(k, cmax);
         cnt[kind]++;
@@ -923,28 +950,33 @@ static void order_points_by_kind(int cmax, host_obs &h, std::vector<int> &pt_ptr
     pperm.reserve(n);
     for (int pass = 0; pass < 3; pass++)
         for (int i = 0; i < n; i++)
-            if (track_kind(pt_ptr[i + 1] - pt_ptr[i], cmax) == pass) pperm.push_back(i);
-    host_obs h2;
-    const size_t N = h.pt.size();
-    h2.pt.resize(N);
-    h2.cam.resize(N);
-    h2.x.resize(2 * N);
+            if (track_kind(pt_ptr[p0 + i + 1] - pt_ptr[p0 + i], cmax) == pass) pperm.push_back(i);
+    const int o0 = pt_ptr[p0];
+    const size_t N = (size_t)(pt_ptr[p1] - o0);
+    std::vector<int> cam2(N);
+    std::vector<double> x2(2 * N);
     operm.resize(N);
     std::vector<int> ptr2(n + 1, 0);
     size_t q = 0;
     for (int i2 = 0; i2 < n; i2++) {
-        const int i = pperm[i2];
+        const int i = p0 + pperm[i2];
         for (int o = pt_ptr[i]; o < pt_ptr[i + 1]; o++, q++) {
-            h2.pt[q] = i2;
-            h2.cam[q] = h.cam[o];
-            h2.x[2 * q] = h.x[2 * (size_t)o];
-            h2.x[2 * q + 1] = h.x[2 * (size_t)o + 1];
-            operm[q] = o;
+            cam2[q] = h.cam[o];
+            x2[2 * q] = h.x[2 * (size_t)o];
+            x2[2 * q + 1] = h.x[2 * (size_t)o + 1];
+            operm[q] = o - o0;
         }
         ptr2[i2 + 1] = (int)q;
     }
-    h = std::move(h2);
-    pt_ptr.swap(ptr2);
+    for (size_t o = 0; o < N; o++) {
+        h.cam[o0 + o] = cam2[o];
+        h.x[2 * (o0 + o)] = x2[2 * o];
+        h.x[2 * (o0 + o) + 1] = x2[2 * o + 1];
+    }
+    for (int i2 = 0; i2 < n; i2++) {
+        pt_ptr[p0 + i2 + 1] = o0 + ptr2[i2 + 1];
+        for (int o = ptr2[i2]; o < ptr2[i2 + 1]; o++) h.pt[o0 + o] = p0 + i2;
+    }
 }
 
 // Device buffers + host-side structure for the observations of points [p0, p1).
@@ -1235,10 +1267,6 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
         std::vector<int> pt_ptr_all(p->n + 1, 0);
         for (size_t q = 0; q < h.pt.size(); q++) pt_ptr_all[h.pt[q] + 1]++;
         for (int i = 0; i < p->n; i++) pt_ptr_all[i + 1] += pt_ptr_all[i];
-        if (o->ordered == 0 && !stage_mode && o->world_size <= 1)
-            order_points_by_kind(o->schur_kernel == 1 ? 0 : BA_MF_CMAX(p->num_a), h, pt_ptr_all,
-                                 c->pperm, c->operm);
-        ST_MARK("order");
         c->world = o->world_size > 1 ? o->world_size : 1;
         c->rank = c->world > 1 ? o->rank : 0;
         // contiguous point ranges with balanced observation counts
@@ -1278,6 +1306,14 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
                 }
             }
         }
+        // fast path: this rank's points by track kind (short tracks for the MFMA
+        // Schur chunks first, per-term tracks, long tracks last); the ranges
+        // of the other ranks are left as they are (the block set, the only
+        // global structure a rank builds, is order independent: build_blocks)
+        if (o->ordered == 0 && !stage_mode)
+            order_points_by_kind(o->schur_kernel == 1 ? 0 : BA_MF_CMAX(p->num_a), h, pt_ptr_all,
+                                 c->p0, c->p1, c->pperm, c->operm);
+        ST_MARK("order");
         c->n_global = p->n;
         c->N_global = p->num_obs;
         c->num_vis = p->num_vis > 0 ? p->num_vis : (double)p->num_obs;
@@ -1289,13 +1325,6 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
         c->flags.has_pivot = o->pivot != nullptr && o->semantics == 0 &&
                              p->model == VLGBA_MODEL_EUCLIDEAN;
         c->model = p->model;
-        {
-            // opt-in: measured (tools/ab_lm.sh) the one-ahead pass that ends
-            // every device-decided solve costs what the saved host round
-            // trips gain (cfg3 and cfg2 whole solves within noise)
-            const char *ev = std::getenv("VLGBA_DEVICE_LM");
-            c->device_lm = ev && ev[0] == '1';
-        }
         c->max_iter = o->max_iter > 0 ? o->max_iter : 20;
         c->max_iter2 = o->max_iter2 > 0 ? o->max_iter2 : 10;
         c->lambda0 = c->lambda = o->lambda0 > 0 ? o->lambda0 : 1e-3;
@@ -1312,6 +1341,11 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
             break;
         }
         c->stop_rel = o->stop_rel > 0 ? o->stop_rel : 1e-3;
+        if (const char *ev = std::getenv("VLGBA_DEBUG_SPIN_TIMEOUT")) {
+            // "R:K": rank R's first K passes report a hand-off timeout (tests)
+            int r = -1, k = 0;
+            if (std::sscanf(ev, "%d:%d", &r, &k) == 2 && r == c->rank) c->debug_timeouts = k;
+        }
         c->on_pass = o->on_pass;
         c->on_pass_user = o->on_pass_user;
         c->d.no_mfma = o->schur_kernel == 1;
@@ -1376,11 +1410,13 @@ static int schur_phase(vlgba_ctx *c, double lam)
 
 // the pass scalars after the update: cross-rank sums, then to the host (spin
 // on the host-mapped block when single-rank and untimed, else a copy)
-static int collect_scalars(vlgba_ctx *c, bool spin, double hs[5])
+static int collect_scalars(vlgba_ctx *c, bool spin, double hs[6])
 {
     ba_dev &d = c->d;
-    if (c->world > 1 || c->comm)   // new SSE, camera and point parts of dp'(lambda dp + g)
-        TRY(allreduce(c, d.scal + 1, 3));   // (scal[0] = the global old SSE, schur_phase)
+    // new SSE, camera and point parts of dp'(lambda dp + g), and the solve's
+    // two status words (every rank then takes the same pinv / re-solve
+    // decision; scal[0] = the global old SSE, schur_phase)
+    if (c->world > 1 || c->comm) TRY(allreduce(c, d.scal + 1, 5));
     if (spin) {
         // spin on the host-mapped sequence number written last (by the update's
         // final sums, or k_publish); lower latency than a copy +
@@ -1401,13 +1437,34 @@ static int collect_scalars(vlgba_ctx *c, bool spin, double hs[5])
         }
         std::atomic_thread_fence(std::memory_order_acquire);
         if (got) {
-            for (int q = 0; q < 5; q++) hs[q] = d.hres[q];
+            for (int q = 0; q < 6; q++) hs[q] = d.hres[q];
             return 0;
         }
         VLGBA_CHECK(hipStreamSynchronize(d.stream));
     }
-    TRY(download(hs, d.scal, 5, d.stream));
+    TRY(download(hs, d.scal, 6, d.stream));
     VLGBA_CHECK(hipStreamSynchronize(d.stream));
+    return 0;
+}
+
+// A hand-off spin of the one-launch solve gave up (timeout word scal[5]):
+// nothing is wrong with S, the launch just did not finish in time.  Re-form
+// S and e_ (the solve works in place), solve with the launches that never
+// wait on other workgroups, then the same update.  Every rank gets here
+// together (the status words travel in the scalars' all-reduce), so the
+// collectives of schur_phase pair up.
+static int resolve_nospin(vlgba_ctx *c, double lam, double hs[6])
+{
+    ba_dev &d = c->d;
+    TRY(schur_phase(c, lam));
+    TRY(ba_launch_assemble(&d));
+    TRY(ba_chol_solve(&d, 1));
+    d.publish_req = 0;
+    d.published = 0;
+    TRY(ba_launch_update(&d, lam));
+    if (d.parity) TRY(ba_launch_parity_new_sums(&d, lam));
+    TRY(collect_scalars(c, false, hs));
+    c->spin_retries++;
     return 0;
 }
 
@@ -1446,9 +1503,10 @@ std::map<int, rocblas_handle> g_rs_handle;   // per device
 // in place), the lower triangle of S assembled densely, rocSOLVER dsyevd,
 // then V diag(1/ev, |ev| > tol) V^T e_ (ba_pinv_apply), and the update with
 // that da.  Every rank runs it on the identical all-reduced system.
-static int pinv_fallback(vlgba_ctx *c, double lam, double hs[5])
+static int pinv_fallback(vlgba_ctx *c, double lam, double hs[6])
 {
     ba_dev &d = c->d;
+    const auto t0 = std::chrono::steady_clock::now();
     rs_api *rs = rs_load();
     if (!rs) return VLGBA_E_ARG;
     const long long ld = d.ld;
@@ -1497,6 +1555,12 @@ static int pinv_fallback(vlgba_ctx *c, double lam, double hs[5])
     if (d.parity) TRY(ba_launch_parity_new_sums(&d, lam));
     TRY(collect_scalars(c, false, hs));
     c->pinv_used++;
+    if (c->rank == 0 && !std::getenv("VLGBA_QUIET"))
+        std::fprintf(stderr,
+                     "[vlgba] non-positive pivot: da = pinv(S) e_ by dsyevd on the dense "
+                     "%lld x %lld S (%.1f MB of device memory), %.3f s\n",
+                     ld, ld, 8e-6 * (double)ld * (double)ld,
+                     std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     return 0;
 }
 
@@ -1544,6 +1608,12 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
     TRY(ba_launch_assemble(&d));
     mark(c, 5);
     TRY(ba_chol_solve(&d));
+    if (c->debug_timeouts > 0) {   // test hook (VLGBA_DEBUG_SPIN_TIMEOUT): as if a spin gave up
+        static const double one = 1.0;
+        VLGBA_CHECK(hipMemcpyAsync(d.scal + 5, &one, sizeof one, hipMemcpyHostToDevice,
+                                   d.stream));
+        c->debug_timeouts--;
+    }
     mark(c, 6);
     // RCCL ranks spin as well: their collectives are stream-ordered, and the
     // publish then follows the scalars' all-reduce (collect_scalars)
@@ -1554,10 +1624,16 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
     d.publish_req = 0;
     if (d.parity) TRY(ba_launch_parity_new_sums(&d, lam));
     mark(c, 7);
-    // scalars: [0] old_sse(local) [1] new_sse [2] dpg cameras [3] dpg points [4] chol status
-    double hs[5];
+    // scalars: [0] old_sse [1] new_sse [2] dpg cameras [3] dpg points
+    // [4] non-positive pivot [5] hand-off spin timeout (summed over ranks)
+    double hs[6];
     TRY(collect_scalars(c, spin, hs));
     info->pinv = 0;
+    info->spin_retry = 0;
+    if (hs[5] != 0.0) {   // the solve did not finish: again, without spins
+        TRY(resolve_nospin(c, lam, hs));
+        info->spin_retry = 1;
+    }
     if (hs[4] != 0.0) {
         // non-positive pivot: bundle_euclid.m:193 takes pinv(S)*e_ whatever S is
         // (App. A Q8), so does the fallback -- then the same update
@@ -1688,7 +1764,8 @@ int vlgba_set_params(vlgba_ctx *c, const double *a, const double *b)
     if (!c->pperm.empty()) {   // input point order -> internal order
         c->hb_tmp.resize(3 * (size_t)c->d.n);
         for (int i = 0; i < c->d.n; i++)
-            for (int r = 0; r < 3; r++) c->hb_tmp[3 * (size_t)i + r] = b[3 * (size_t)c->pperm[i] + r];
+            for (int r = 0; r < 3; r++)
+                c->hb_tmp[3 * (size_t)i + r] = b[3 * ((size_t)c->p0 + c->pperm[i]) + r];
         TRY(upload(c->d.b, c->hb_tmp.data(), 3 * (size_t)c->d.n, c->d.stream));
     } else {
         TRY(upload(c->d.b, b + 3 * (size_t)c->p0, 3 * (size_t)c->d.n, c->d.stream));
@@ -1710,9 +1787,18 @@ int vlgba_get_params(vlgba_ctx *c, double *a, double *b)
             double *full = nullptr;
             TRY(dalloc(&full, 3 * (size_t)c->n_global));
             VLGBA_CHECK(hipMemsetAsync(full, 0, sizeof(double) * 3 * c->n_global, c->d.stream));
-            VLGBA_CHECK(hipMemcpyAsync(full + 3 * (size_t)c->p0, c->d.b,
-                                       sizeof(double) * 3 * c->d.n, hipMemcpyDeviceToDevice,
-                                       c->d.stream));
+            if (c->pperm.empty()) {
+                VLGBA_CHECK(hipMemcpyAsync(full + 3 * (size_t)c->p0, c->d.b,
+                                           sizeof(double) * 3 * c->d.n, hipMemcpyDeviceToDevice,
+                                           c->d.stream));
+            } else {   // internal -> input order inside this rank's range
+                c->hb_tmp.resize(3 * (size_t)c->d.n);
+                TRY(download_points(c, c->hb_tmp.data(), c->d.b, 3));
+                VLGBA_CHECK(hipMemcpyAsync(full + 3 * (size_t)c->p0, c->hb_tmp.data(),
+                                           sizeof(double) * 3 * c->d.n, hipMemcpyHostToDevice,
+                                           c->d.stream));
+                VLGBA_CHECK(hipStreamSynchronize(c->d.stream));
+            }
             int rc = allreduce(c, full, 3 * (size_t)c->n_global);
             if (!rc) rc = download(b, full, 3 * (size_t)c->n_global, c->d.stream);
             (void)hipStreamSynchronize(c->d.stream);
@@ -1896,146 +1982,6 @@ int vlgba_step(vlgba_ctx *c, int relinearize, int update_lm, vlgba_step_info *in
     return 0;
 }
 
-// ---------------------------------------------------------------------------
-// The LM loop without host round trips: the passes are enqueued one ahead and
-// k_lm_decide takes each pass's decision on the device (ba_lm: lambda, nu,
-// error_, the current parameter buffers, relinearise or not, the stop test);
-// the host only watches the published decision count and stops enqueueing
-// once the device says done.  A pass enqueued after the last decision runs but
-// commits nothing.  Fast path, single rank or RCCL ranks, no per-pass host
-// hooks (timing, verbose, on_pass), no long tracks; otherwise the host loop.
-// Opt-in (VLGBA_DEVICE_LM=1): it does not beat the host loop, see device_lm.
-// ---------------------------------------------------------------------------
-static bool device_lm_ok(const vlgba_ctx *c)
-{
-    const ba_dev &d = c->d;
-    return c->device_lm && !d.ordered && !d.parity && d.nl == 0 && d.nch > 0 && !d.obs_vis &&
-           !d.xh_out && !c->timing && !c->verbose && !c->on_pass &&
-           (c->world == 1 || c->comm);
-}
-
-// every launch of one pass (lm_pass's), the decision on the device
-static int lm_pass_device(vlgba_ctx *c)
-{
-    ba_dev &d = c->d;
-    const double lam = c->lambda;   // the kernels read d.lm->lambda
-    TRY(ba_launch_linearize(&d, c->flags));   // returns at once unless d.lm->relin
-    // U / eA / old SSE re-formed from the chunk partials every pass (the same
-    // values after a rejected step), inside the MFMA Schur launch
-    TRY(ba_launch_camera_reduce(&d, c->flags, 1));
-    TRY(schur_phase(c, lam));
-    TRY(ba_launch_assemble(&d));
-    TRY(ba_chol_solve(&d));
-    d.publish_req = 0;
-    d.published = 0;
-    TRY(ba_launch_update(&d, lam));
-    if (c->world > 1 || c->comm) TRY(allreduce(c, d.scal + 1, 3));
-    TRY(ba_launch_lm_decide(&d));
-    return 0;
-}
-
-// wait until the device has taken `want` decisions (host-mapped hres[7])
-static int wait_decisions(vlgba_ctx *c, double want)
-{
-    ba_dev &d = c->d;
-    const auto t0 = std::chrono::steady_clock::now();
-    for (long it = 0;; it++) {
-        if (d.hres[7] >= want) break;
-        if ((it & 1023) == 1023 &&
-            std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
-            VLGBA_CHECK(hipStreamSynchronize(d.stream));   // reports a failed kernel
-            if (d.hres[7] >= want) break;
-            return VLGBA_E_ARG;
-        }
-    }
-    std::atomic_thread_fence(std::memory_order_acquire);
-    return 0;
-}
-
-static int lm_device_begin(vlgba_ctx *c, int force)
-{
-    ba_dev &d = c->d;
-    const int cap = c->max_iter + 2;
-    if (!d.lm_mem || d.lm_cap < cap) {
-        TRY(ctx_alloc(c, &d.lm_mem, 1));
-        TRY(ctx_alloc(c, &d.lm_err, (size_t)cap));
-        d.lm_cap = cap;
-    }
-    ba_lm &L = c->lm_host;
-    L = ba_lm{};
-    L.lambda = c->lambda;
-    L.nu = c->nu;
-    L.num_vis = c->num_vis;
-    L.stop_rel = c->stop_rel;
-    L.iter = 1;
-    L.relin = (force || !c->lin_valid) ? 1 : 0;
-    L.max_iter = c->max_iter;
-    L.max_iter2 = c->max_iter2;
-    L.proj = c->model == VLGBA_MODEL_PROJECTIVE;
-    L.force = force;
-    L.cap = cap;
-    L.seq = (double)d.seq;
-    VLGBA_CHECK(hipMemcpyAsync(d.lm_mem, &L, sizeof L, hipMemcpyHostToDevice, d.stream));
-    d.lm = d.lm_mem;
-    return 0;
-}
-
-// after the device loop: the state back to the context (parameter buffers,
-// lambda, nu, the linearisation's validity); error_ into err
-static int lm_device_end(vlgba_ctx *c, std::vector<double> *err)
-{
-    ba_dev &d = c->d;
-    d.lm = nullptr;
-    ba_lm &L = c->lm_host;
-    VLGBA_CHECK(hipMemcpyAsync(&L, d.lm_mem, sizeof L, hipMemcpyDeviceToHost, d.stream));
-    std::vector<double> e((size_t)d.lm_cap);
-    VLGBA_CHECK(hipMemcpyAsync(e.data(), d.lm_err, sizeof(double) * d.lm_cap,
-                               hipMemcpyDeviceToHost, d.stream));
-    VLGBA_CHECK(hipStreamSynchronize(d.stream));
-    d.seq = (unsigned long long)L.seq;
-    if (L.force) return 0;
-    c->lambda = L.lambda;
-    c->nu = L.nu;
-    if (L.sel) {   // the current parameters are the "new" buffers
-        std::swap(d.a, d.a_new);
-        std::swap(d.b, d.b_new);
-        std::swap(d.rot, d.rot_new);
-    }
-    c->lin_valid = L.relin ? 0 : 1;
-    if (err) err->assign(e.begin(), e.begin() + std::min(L.nerr, d.lm_cap));
-    return 0;
-}
-
-static int run_device(vlgba_ctx *c, std::vector<double> &err, int &iter, int &iter2,
-                      int &passes, int &acc, bool &handoff)
-{
-    ba_dev &d = c->d;
-    TRY(lm_device_begin(c, 0));
-    const double seq0 = c->lm_host.seq;
-    const int max_enq = c->max_iter * (c->max_iter2 + 1) + 4;
-    int enq = 0, rc = 0;
-    for (;;) {
-        if ((rc = lm_pass_device(c))) break;
-        enq++;
-        if (enq >= 2) {   // one pass ahead: wait for the previous one's decision
-            if ((rc = wait_decisions(c, seq0 + enq - 1))) break;
-            if (d.hres[5] != 0.0) break;
-        }
-        if (enq >= max_enq) break;
-    }
-    if (!rc && d.hres[5] == 0.0) rc = wait_decisions(c, seq0 + enq);
-    const int rc2 = lm_device_end(c, &err);
-    TRY(rc);
-    TRY(rc2);
-    const ba_lm &L = c->lm_host;
-    iter = L.iter;
-    iter2 = L.iter2;
-    passes = L.passes;
-    acc = L.acc;
-    handoff = L.done == 2;   // a non-positive pivot: the host takes that pass (pinv)
-    return 0;
-}
-
 int vlgba_run_passes(vlgba_ctx *c, int npass, vlgba_step_info *info)
 {
     if (!c || npass < 0) return VLGBA_E_ARG;
@@ -2043,29 +1989,7 @@ int vlgba_run_passes(vlgba_ctx *c, int npass, vlgba_step_info *info)
     vlgba_step_info tmp;
     if (!info) info = &tmp;
     std::memset(info, 0, sizeof *info);
-    if (npass == 0) return 0;
-    ba_dev &d = c->d;
-    if (!device_lm_ok(c)) {   // host-decided passes
-        for (int q = 0; q < npass; q++) TRY(lm_pass(c, 1, info));
-        return 0;
-    }
-    TRY(lm_device_begin(c, 1));
-    const double seq0 = c->lm_host.seq;
-    int rc = 0;
-    for (int q = 0; q < npass && !rc; q++) rc = lm_pass_device(c);
-    if (!rc) rc = wait_decisions(c, seq0 + npass);
-    double hs[7];
-    for (int q = 0; q < 7; q++) hs[q] = d.hres[q];
-    const int rc2 = lm_device_end(c, nullptr);
-    TRY(rc);
-    TRY(rc2);
-    info->old_sse = hs[0];
-    info->new_sse = hs[1];
-    info->dpg = hs[2] + hs[3];
-    info->lambda = c->lambda;
-    info->pinv = info->chol_failed = hs[4] != 0.0;
-    info->rho = (hs[0] - hs[1]) / info->dpg;
-    info->accepted = (hs[0] - hs[1]) > 0;
+    for (int q = 0; q < npass; q++) TRY(lm_pass(c, 1, info));
     return 0;
 }
 
@@ -2080,13 +2004,8 @@ int vlgba_run(vlgba_ctx *c, double *error_out, int error_cap, vlgba_stats *stats
     c->lin_valid = 0;
     std::vector<double> err;   // error_, 1-based in the reference
     int iter = 1, iter2 = 0, passes = 0, acc = 0;
-    bool host_loop = true;
-    if (device_lm_ok(c) && iter < c->max_iter && iter2 < c->max_iter2) {
-        bool handoff = false;
-        TRY(run_device(c, err, iter, iter2, passes, acc, handoff));
-        host_loop = handoff;   // the host continues only to take a pinv step
-    }
-    for (; host_loop;) {
+    const int pinv0 = c->pinv_used, retry0 = c->spin_retries;
+    for (;;) {
         if (!(iter < c->max_iter && iter2 < c->max_iter2)) break;
         if (iter >= 3) {
             const double e1 = err[iter - 1], e0 = err[iter - 2];
@@ -2122,6 +2041,8 @@ int vlgba_run(vlgba_ctx *c, double *error_out, int error_cap, vlgba_stats *stats
         stats->accepted = acc;
         stats->num_error = (int)err.size();
         stats->lambda = c->lambda;
+        stats->pinv_passes = c->pinv_used - pinv0;
+        stats->spin_retries = c->spin_retries - retry0;
         stats->seconds =
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     }

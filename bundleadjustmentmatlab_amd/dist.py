@@ -39,6 +39,26 @@ def shard_points(pt_ptr: np.ndarray, world: int, rank: int) -> tuple[int, int]:
     return p0, p1
 
 
+def rank_collective(pg, rank: int, world: int, ndev: int):
+    """The collective of one process per rank (torch.distributed group pg
+    already initialised): RCCL when every rank has a GPU of its own (world <=
+    ndev; rank 0 makes the unique id and the group broadcasts it), else --
+    ranks sharing a device, where RCCL refuses a second rank -- the host
+    all-reduce over pg (gloo).  Returns (comm_id, allreduce, device): pass
+    comm_id / allreduce to BundleAdjuster and run on `device`."""
+    if world <= 1:
+        return None, None, 0
+    if world <= ndev:
+        buf = [unique_id_bytes() if rank == 0 else None]
+        pg.broadcast_object_list(buf, src=0)
+        return buf[0], None, rank
+    import torch
+
+    def allreduce(arr):
+        pg.all_reduce(torch.from_numpy(arr))
+    return None, allreduce, rank % max(1, ndev)
+
+
 # ---------------------------------------------------------------------------
 # Elastic shard count (BASELINE.json config 5: "1 -> 8 GPU elastic point
 # shard"): each growing-BA call picks its own number of ranks from its size,
@@ -85,8 +105,12 @@ class HostGroup:
 
 
 def run_sharded(K, obs_pt, obs_cam, obs_x, n, num_a, a, b, world, *, devices=None, **kw):
-    """One LM solve (vlgba_run) over `world` rank threads.  Returns
-    (a, b, error_, stats) of rank 0 (every rank holds the same a, b, error_)."""
+    """One LM solve (vlgba_run) over `world` rank threads, rank r on device
+    devices[r % len(devices)].  Ranks on distinct GPUs share one RCCL
+    communicator (the unique id made here, ncclCommInitRank per thread);
+    ranks that share a GPU (RCCL refuses two ranks on one device) use the
+    host-memory all-reduce (HostGroup).  Returns (a, b, error_, stats) of
+    rank 0 (every rank holds the same a, b, error_)."""
     import threading
     from .bundle import BundleAdjuster
     if world <= 1:
@@ -96,21 +120,24 @@ def run_sharded(K, obs_pt, obs_cam, obs_x, n, num_a, a, b, world, *, devices=Non
             a2, b2 = ba.get_params()
         return a2, b2, err, st
     devices = devices or [0]
-    grp = HostGroup(world)
+    devs = [devices[r % len(devices)] for r in range(world)]
+    comm = unique_id_bytes() if len(set(devs)) == world else None
+    grp = None if comm else HostGroup(world)
     out = [None] * world
     errs = []
 
     def rank_main(r):
         try:
             with BundleAdjuster(K, obs_pt, obs_cam, obs_x, n, num_a, rank=r, world_size=world,
-                                allreduce=grp.allreduce_fn(r), device=devices[r % len(devices)],
-                                **kw) as ba:
+                                comm_id=comm, allreduce=grp.allreduce_fn(r) if grp else None,
+                                device=devs[r], **kw) as ba:
                 ba.set_params(a, b)
                 err, st = ba.run()
                 out[r] = ba.get_params() + (err, st)
         except Exception as e:   # noqa: BLE001 -- re-raised below
             errs.append(e)
-            grp._bar.abort()
+            if grp:
+                grp._bar.abort()
 
     th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
     for t in th:

@@ -44,7 +44,7 @@ def _subset_obs(sc, cams, pts):
 
 
 def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, device=0,
-                       verbose=False, devices=None, shards=None):
+                       verbose=False, devices=None, shards=None, obs_per_shard=None):
     """Replay the incremental reconstruction's BA sequence on scene ``sc``
     (scene.Scene).  Cameras ``init_cams`` form the initial two-view
     reconstruction (VLmvg.m's two_view step); every other camera is added in
@@ -52,8 +52,11 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
 
     Elastic sharding (config 5): with ``devices`` (GPU ordinals), each solve
     picks its rank count with dist.choose_shards from its observation count
-    (or ``shards(num_obs)`` if given) and runs point-sharded over that many
-    rank threads (dist.run_sharded); without it every solve runs on ``device``.
+    (``obs_per_shard``: choose_shards' threshold, default dist.OBS_PER_SHARD;
+    or ``shards(num_obs)`` if given) and runs point-sharded over that many
+    rank threads (dist.run_sharded: RCCL across distinct GPUs, host
+    collectives between ranks sharing one); without it every solve runs on
+    ``device``.
 
     Returns dict(solves=[...], resections=[...], K, T, w, X, status) where each
     solve records the cameras / points / observations it adjusted, its error_
@@ -83,7 +86,9 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
         t0 = time.perf_counter()
         world = 1
         if devices:
-            world = shards(len(pt)) if shards else choose_shards(len(pt), len(devices))
+            world = (shards(len(pt)) if shards else
+                     choose_shards(len(pt), len(devices),
+                                   **({"obs_per_shard": obs_per_shard} if obs_per_shard else {})))
         if world > 1:
             nvk = 0 if fix_calibration else 4
             Kc, Tc, wc, Xc = K[:, cams], T[:, cams], w[:, cams], X[:, pts]

@@ -177,6 +177,88 @@ def mview_scene(m=10, min_n=100, max_n=200, depth=100.0, noise=0.5, seed=1,
     return Scene(K, T, w, X, pt, cam, x, T0, w0, X0)
 
 
+def growing_scene(m=1000, min_n=300, max_n=500, depth=100.0, noise=0.5, seed=15,
+                  keep_first_rotation=True):
+    """generate_scene_and_motion.m:36-117's model (mview_scene) with every
+    per-frame step vectorised over the points, for long sequences (config 5's
+    scaled 1000-camera variant): frame j keeps the points tracked from frame
+    j-1 that still project inside the image in front of the camera, re-detects
+    stored points in index order while fewer than min_n are seen (up to max_n),
+    and creates max_n - tracked new points when still below min_n.  Same model
+    and parameters as mview_scene, not the same random stream."""
+    rng = np.random.default_rng(seed)
+    width = height = 500.0
+    f, cx, cy = width, width / 2, height / 2
+    Kmat = np.array([[f, 0, cx], [0, f, cy], [0, 0, 1.0]])
+    K = np.tile(np.array([[f], [f], [cx], [cy]]), (1, m))
+    w = np.zeros((3, m))
+    T = np.zeros((3, m))
+    vw, vT = np.zeros(3), np.zeros(3)
+    for j in range(1, m):
+        vw = vw + 1e-2 * rng.standard_normal(3)
+        vT = vT + 1e-0 * rng.standard_normal(3)
+        w[:, j] = w[:, j - 1] + vw
+        T[:, j] = T[:, j - 1] + vT
+    R = rodrigues(w)
+    Kinv = np.linalg.inv(Kmat)
+    cap = 1 << 16
+    Xs = np.zeros((3, cap))
+    n = 0
+    prev = np.zeros(0, dtype=np.int64)                # points seen in frame j-1
+    obs_pt, obs_cam, obs_x = [], [], []
+
+    def inside(j, idx):
+        P = Kmat @ (R[j] @ Xs[:, idx] + T[:, j:j + 1])
+        z = P[2]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            u, v = P[0] / z, P[1] / z
+        ok = (z > 0.01 * depth) & (u > 1) & (u < width) & (v > 1) & (v < height)
+        return ok, np.stack([u, v], 1)
+
+    for j in range(m):
+        ok, uv = inside(j, prev)
+        vis_idx, vis_uv = [prev[ok]], [uv[ok]]
+        tracked = int(ok.sum())
+        if tracked < min_n and n > 0:                 # re-detect stored points, in order
+            seen = np.zeros(n, dtype=bool)
+            seen[prev[ok]] = True
+            cand = np.nonzero(~seen)[0]
+            ok2, uv2 = inside(j, cand)
+            take = np.nonzero(ok2)[0][:max_n - tracked]
+            vis_idx.append(cand[take])
+            vis_uv.append(uv2[take])
+            tracked += len(take)
+        if tracked < min_n:                           # new points
+            n_new = max_n - tracked
+            xi = rng.random((2, n_new)) * np.array([[width], [height]])
+            d = (1 + 0.5 * rng.standard_normal(n_new)) * depth
+            keep = d > 0
+            xi, d = xi[:, keep], d[keep]
+            ray = (Kinv @ np.vstack([xi, np.ones(xi.shape[1])])) * d
+            Xn = R[j].T @ (ray - T[:, j:j + 1])
+            k = Xn.shape[1]
+            while n + k > Xs.shape[1]:
+                Xs = np.hstack([Xs, np.zeros_like(Xs)])
+            Xs[:, n:n + k] = Xn
+            vis_idx.append(np.arange(n, n + k))
+            vis_uv.append(xi.T)
+            n += k
+        idx = np.concatenate(vis_idx)
+        uvs = np.concatenate(vis_uv)
+        order = np.argsort(idx, kind="stable")
+        prev = idx[order]
+        obs_pt.append(prev)
+        obs_cam.append(np.full(len(prev), j))
+        obs_x.append(uvs[order])
+    X = np.vstack([Xs[:, :n], np.ones((1, n))])
+    pt = np.concatenate(obs_pt)
+    cam = np.concatenate(obs_cam)
+    x = np.concatenate(obs_x) + rng.standard_normal((len(pt), 2)) * noise
+    pt, cam, x = _sort_point_major(pt, cam, x)
+    w0, T0, X0 = _perturb(rng, w, T, X, keep_first_rotation)
+    return Scene(K, T, w, X, pt, cam, x, T0, w0, X0)
+
+
 def banded_scene(m=50, n=10_000, track=6, depth=(80.0, 120.0), noise=0.5, seed=2,
                  keep_first_rotation=False):
     """Configs 2-4: point i is seen by ``track`` consecutive
@@ -310,6 +392,8 @@ CONFIGS = {
     "cfg2": (banded_scene, dict(m=50, n=10_000, track=6, seed=2)),
     "cfg3": (banded_scene, dict(m=1000, n=500_000, track=6, seed=3)),
     "cfg5": (mview_scene, dict(m=50, min_n=100, max_n=200, depth=100.0, seed=5)),
+    # config 5's scaled 1000-camera variant
+    "cfg5x": (growing_scene, dict(m=1000, min_n=300, max_n=500, depth=100.0, seed=15)),
     # not a BASELINE config: irregular tracks + loop closures
     "ladybug": (ladybug_scene, dict(m=1000, n=200_000, seed=6)),
 }

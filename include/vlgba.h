@@ -128,6 +128,8 @@ typedef struct {
     int num_error;         /* entries written to error_out                    */
     double lambda;         /* final damping                                   */
     double seconds;        /* wall time of the solve (setup excluded)         */
+    int pinv_passes;       /* passes whose step came from the pinv fallback   */
+    int spin_retries;      /* passes re-solved after a hand-off spin timeout  */
 } vlgba_stats;
 
 /* One LM pass, for benchmarking / custom drivers. */
@@ -140,7 +142,16 @@ typedef struct vlgba_step_info {
     int accepted;
     int chol_failed;       /* non-positive pivot in the reduced solve: the
                               step came from the pinv fallback (= pinv)       */
-    int pinv;              /* da = pinv(S) e_ by eigen-decomposition          */
+    int pinv;              /* da = pinv(S) e_ by eigen-decomposition: a dense
+                              (num_a m)^2 copy of S + rocSOLVER dsyevd, i.e.
+                              8 (num_a m)^2 bytes of device memory and
+                              O((num_a m)^3) flops (cfg3: 288 MB); the library
+                              notes each such pass on stderr (ld, seconds)    */
+    int spin_retry;        /* the one-launch solve gave up waiting on a
+                              hand-off (a bounded spin): the pass was solved
+                              again with the per-level launches (every rank
+                              takes the same decision: the status words are
+                              all-reduced with the pass scalars)              */
 } vlgba_step_info;
 
 typedef struct vlgba_ctx vlgba_ctx;
@@ -172,13 +183,12 @@ int vlgba_get_linearization(vlgba_ctx *ctx, double *U, double *eA, double *V, do
                             double *W);
 /* the LM loop from the context's parameters; error_out / error_cap as
  * vlgba_solve.  Every handle entry point makes the context's device current.
- * With VLGBA_DEVICE_LM=1 (fast path) the accept / lambda / stop decisions are
- * taken on the device after every pass (no host round trip between passes). */
+ * The accept / lambda / stop decisions are the host's (a handful of scalars
+ * per pass, as bundle_euclid.m keeps them in MATLAB). */
 int vlgba_run(vlgba_ctx *ctx, double *error_out, int error_cap, vlgba_stats *stats);
 /* npass full passes at the context's parameters and lambda, each
  * relinearising, none changing the context (vlgba_step(ctx, 1, 0, .) npass
- * times; enqueued back to back with the decisions on the device when
- * VLGBA_DEVICE_LM=1); info: the last pass */
+ * times); info: the last pass */
 int vlgba_run_passes(vlgba_ctx *ctx, int npass, vlgba_step_info *info);
 /* the last pass's step: da (num_a * m, the reduced solve) and db (3 x
  * n_local, this rank's points); either may be NULL */

@@ -6,7 +6,8 @@ function [K_, Te_, w_, Xe_, error_] = bundle_euclid(K, Te, w, Xe, x, varargin)
 %   Same signature, options and outputs as VLG's toolbox/bundle/bundle_euclid.m:
 %     K (4xm) fx fy cx cy, Te (3xm), w (3xm) Rodrigues vectors, Xe (4xn)
 %     homogeneous points (Xe(4,:) passed through), x (3xnxm) image points.
-%   Options: 'fix_structure', 'fix_motion', 'fix_pivot' pivot (1xm logical),
+%   Options: 'fix_structure', 'fix_motion', 'fix_pivot' pivot (a logical mask
+%   or camera numbers, as U(:,:,pivot) indexes in VLG's bundle_euclid.m),
 %   'fix_calibration', 'fix_principal', 'visibility' V (nxm), 'verbose'.
 %   error_ is the SSE / sum(visibility) before the first and after every
 %   accepted step.
@@ -29,7 +30,7 @@ end
 m = size(w, 2);
 n = size(x, 2);
 
-opts = struct('fix_structure', 0, 'fix_motion', 0, 'verbose', 0, 'pivot', [], ...
+opts = struct('fix_structure', 0, 'fix_motion', 0, 'verbose', 0, 'pivot', [], 'pivot_mask', [], ...
               'semantics', 0, 'max_iter', 0, 'stop_rel', 0, 'device', 0, 'ordered', 0);
 nvk = 4;                                    % free fx fy cx cy
 vis = [];
@@ -38,7 +39,10 @@ while k <= numel(varargin)
     name = lower(varargin{k});
     if strcmp(name, 'fix_structure'),      opts.fix_structure = 1;
     elseif strcmp(name, 'fix_motion'),     opts.fix_motion = 1;
-    elseif strcmp(name, 'fix_pivot'),      opts.pivot = double(varargin{k+1}(:)'); k = k + 1;
+    elseif strcmp(name, 'fix_pivot')
+        pv = varargin{k+1}; k = k + 1;      % mask or index list (bundle_euclid.m:150-153)
+        if islogical(pv), opts.pivot_mask = double(pv(:)');
+        else,             opts.pivot = double(pv(:)'); end
     elseif strcmp(name, 'fix_calibration'), nvk = 0;
     elseif strcmp(name, 'fix_principal'),  nvk = 1;
     elseif strcmp(name, 'visibility'),     vis = varargin{k+1}; k = k + 1;
@@ -57,6 +61,7 @@ if isempty(vis)
 end
 if opts.semantics
     opts.pivot = [];                        % bundle_euclid_nomex has no fix_pivot
+    opts.pivot_mask = [];
 end
 
 % parameters as VLG packs them: a = [w; T; (fx) | (fx fy cx cy)], b = Xe(1:3,:)

@@ -6,7 +6,13 @@
  * options struct (every field optional; the drop-in bundle_euclid.m /
  * bundle_projective.m fill it from their name / value arguments):
  *   fix_structure, fix_motion, verbose   0 / 1   (bundle_euclid.m:58-61,73-74)
- *   pivot        1 x m, non-zero = fixed camera  ('fix_pivot', :62-65)
+ *   pivot        'fix_pivot' as camera numbers: 1-based indices (any count,
+ *                duplicates allowed), as U(:,:,pivot) reads a numeric pivot
+ *                (bundle_euclid.m:62-65,150-153)
+ *   pivot_mask   'fix_pivot' as a logical mask (sent as double): 1 x k,
+ *                non-zero = fixed; entries past m must be zero
+ *   (an index outside 1..m or a mask entry past m is an error: MATLAB would
+ *   grow U / W / eA there)
  *   semantics    0 bundle_euclid.m, 1 bundle_euclid_nomex.m
  *   max_iter, max_iter2, lambda0        0 = the reference's 20 / 10 / 1e-3
  *   device                              HIP device
@@ -72,16 +78,42 @@ static void vm_lm(const char *who, int model, const double *K, const mxArray *pa
     max_iter = o.max_iter > 0 ? o.max_iter : 20;
     {
         const mxArray *pv = popt ? mxGetField(popt, 0, "pivot") : NULL;
-        if (pv && !mxIsEmpty(pv)) {
-            const double *v;
-            if (!mxIsDouble(pv) || mxGetNumberOfElements(pv) != (size_t)m)
-                vm_fail(who, "pivot must be a double 1 x m vector");
-            v = mxGetPr(pv);
+        const mxArray *pm = popt ? mxGetField(popt, 0, "pivot_mask") : NULL;
+        const int has_pv = pv && !mxIsEmpty(pv), has_pm = pm && !mxIsEmpty(pm);
+        if (has_pv || has_pm) {
+            const char *bad = NULL;
+            size_t k, cnt;
+            if ((has_pv && !mxIsDouble(pv)) || (has_pm && !mxIsDouble(pm)))
+                vm_fail(who, "pivot / pivot_mask must be double");
             pivot = (unsigned char *)calloc((size_t)m, 1);
             if (!pivot)
                 mexErrMsgIdAndTxt("vlgba:nomem", "out of memory");
-            for (j = 0; j < m; j++)
-                pivot[j] = v[j] != 0.0;
+            if (has_pm) {   /* logical mask */
+                const double *v = mxGetPr(pm);
+                cnt = mxGetNumberOfElements(pm);
+                for (k = 0; k < cnt && !bad; k++)
+                    if (v[k] != 0.0) {
+                        if (k >= (size_t)m)
+                            bad = "fix_pivot: logical index past the camera count";
+                        else
+                            pivot[k] = 1;
+                    }
+            }
+            if (has_pv) {   /* 1-based camera numbers */
+                const double *v = mxGetPr(pv);
+                cnt = mxGetNumberOfElements(pv);
+                for (k = 0; k < cnt && !bad; k++) {
+                    const double x = v[k];
+                    if (!(x >= 1.0 && x <= (double)m) || x != (double)(long long)x)
+                        bad = "fix_pivot: camera indices must be integers in 1..m";
+                    else
+                        pivot[(long long)x - 1] = 1;
+                }
+            }
+            if (bad) {
+                free(pivot);
+                vm_fail(who, bad);
+            }
             o.pivot = pivot;
         }
     }

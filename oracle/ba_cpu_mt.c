@@ -25,6 +25,7 @@
 #define MT_NA 6   /* fix_calibration (num_a = 6), the config-3 workload */
 
 int mt_threads(void) { return omp_get_max_threads(); }
+void mt_set_threads(int n) { omp_set_num_threads(n); }
 
 /* reproject_point (num_variableK = 0): Rodrigues per call, as the reference */
 static void proj6(const double *K4, const double *a, const double *b, double x[2])
@@ -114,6 +115,33 @@ void mt_damp_y(int n, const int *pt_ptr, double lambda, const double *V, const d
         memcpy(vs, V + 9 * (size_t)i, sizeof vs);
         for (k = 0; k < 3; k++) vs[4 * k] = (1 + lambda) * V[9 * (size_t)i + 4 * k];
         orc_pinv3_formula(vs, vi);
+        for (o = pt_ptr[i]; o < pt_ptr[i + 1]; o++) {
+            const double *w = W + 18 * (size_t)o;
+            double *y = Y + 18 * (size_t)o;
+            for (c = 0; c < 3; c++)
+                for (r = 0; r < MT_NA; r++)
+                    y[r + MT_NA * c] = w[r] * vi[3 * c] + w[r + MT_NA] * vi[1 + 3 * c] +
+                                       w[r + 2 * MT_NA] * vi[2 + 3 * c];
+        }
+    }
+}
+
+/* mt_damp_y with MATLAB's pinv of each damped V*_i (bundle_euclid.m:180):
+ * the symmetric block's eigen-decomposition (cyclic Jacobi, orc_pinv3_eig)
+ * with MATLAB's tolerance 3 * eps(max |eigenvalue|) -- for a symmetric
+ * matrix the singular values are the absolute eigenvalues, so this is
+ * pinv's SVD rule -- instead of the closed-form inverse */
+void mt_damp_y_pinv(int n, const int *pt_ptr, double lambda, const double *V,
+                    const double *W, double *Vinv, double *Y)
+{
+    int i;
+#pragma omp parallel for schedule(static)
+    for (i = 0; i < n; i++) {
+        double vs[9], *vi = Vinv + 9 * (size_t)i;
+        int o, r, c, k;
+        memcpy(vs, V + 9 * (size_t)i, sizeof vs);
+        for (k = 0; k < 3; k++) vs[4 * k] = (1 + lambda) * V[9 * (size_t)i + 4 * k];
+        orc_pinv3_eig(vs, vi);
         for (o = pt_ptr[i]; o < pt_ptr[i + 1]; o++) {
             const double *w = W + 18 * (size_t)o;
             double *y = Y + 18 * (size_t)o;

@@ -276,6 +276,22 @@ def sp_update(pb, W, da, eB, Vinv, a, b, num_a, lib=None, ndb=6):
 # --------------------------------------------------------------------------
 # The driver: bundle_euclid.m restated
 # --------------------------------------------------------------------------
+def _matlab_index_mask(idx, m):
+    """Which pages of an m-page array MATLAB's X(:,:,idx) = 0 addresses
+    (bundle_euclid.m:151): logical idx -> its true positions (any length, none
+    past m), numeric idx -> the 1-based positions it lists.  Positions past m
+    (MATLAB would grow the array) and non-positive / fractional indices
+    (MATLAB errors) raise."""
+    a = np.asarray(idx)
+    pos = np.flatnonzero(a.reshape(-1)) if a.dtype == bool else a.reshape(-1) - 1
+    pos = np.asarray(pos, dtype=np.float64)
+    if pos.size and (np.any(pos != np.round(pos)) or pos.min() < 0 or pos.max() >= m):
+        raise ValueError("pivot index outside 1..m")
+    out = np.zeros(m, dtype=bool)
+    out[pos.astype(np.int64)] = True
+    return out
+
+
 def parse_options(m, n, x, varargin):
     """bundle_euclid.m:44-82."""
     o = dict(fix_structure=False, fix_motion=False, fix_pivot=False,
@@ -289,7 +305,7 @@ def parse_options(m, n, x, varargin):
             o["fix_motion"] = True
         elif name == "fix_pivot":
             o["fix_pivot"] = True
-            o["pivot"] = np.asarray(varargin[k + 1], dtype=bool).reshape(-1)
+            o["pivot"] = _matlab_index_mask(varargin[k + 1], m)
             k += 1
         elif name == "fix_calibration":
             o["num_variableK"] = 0

@@ -63,7 +63,17 @@ def host_info():
                 break
     except Exception:   # noqa: BLE001 -- informational only
         pass
-    return {"nproc": os.cpu_count(), "cpu_model": model, "omp_threads": int(mt_lib().mt_threads()),
+    quota = None   # the cgroup's CPU bandwidth limit, in CPUs (None = unlimited / unknown)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
+            "cgroup_cpus": quota, "omp_threads": int(mt_lib().mt_threads()),
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"), "cpu_model": model,
             "blas": blas}
 
 
@@ -117,23 +127,30 @@ class SparsePort:
         has = np.diff(self.pt_ptr) > 0
         self.bw = int(6 * (hi[has] - lo[has]).max() + 5) if has.any() else 5
 
-    def one_pass(self, a0, b0, lam=1e-3, solve="band"):
+    def one_pass(self, a0, b0, lam=1e-3, solve="band", vinv="formula", relin=True):
         """One LM pass at (a0 6 x m, b0 3 x n): dict of old / new SSE, S, e_,
         da, db and the seconds of each phase (the timed region is the whole
-        pass: stage 1, damping + Schur, the reduced solve, stage 3)."""
+        pass: stage 1, damping + Schur, the reduced solve, stage 3).
+        vinv="pinv": V*_i^-1 by MATLAB's pinv rule (mt_damp_y_pinv) instead of
+        the closed form; relin=False reuses the last pass's stage 1 (a
+        rejected step's identical linearisation, App. A Q12)."""
         L = mt_lib()
         f64 = lambda a: np.ascontiguousarray(a, dtype=np.float64)   # noqa: E731
         a = f64(np.asarray(a0).T.reshape(-1))
         b = f64(np.asarray(b0).T.reshape(-1))
         m, n = self.m, self.n
         t = [time.perf_counter()]
-        old = L.mt_linearize(n, _P(self.pt_ptr), _P(self.cam), _P(self.x), _P(self.K), _P(a),
-                             _P(b), _P(self.jrec), _P(self.W), _P(self.V), _P(self.eB))
-        L.mt_camera_reduce(m, _P(self.cam_ptr), _P(self.cam_obs), _P(self.jrec), _P(self.U),
-                           _P(self.eA))
+        if relin or not hasattr(self, "_old"):
+            self._old = L.mt_linearize(n, _P(self.pt_ptr), _P(self.cam), _P(self.x), _P(self.K),
+                                       _P(a), _P(b), _P(self.jrec), _P(self.W), _P(self.V),
+                                       _P(self.eB))
+            L.mt_camera_reduce(m, _P(self.cam_ptr), _P(self.cam_obs), _P(self.jrec), _P(self.U),
+                               _P(self.eA))
+        old = self._old
         t.append(time.perf_counter())
-        L.mt_damp_y(n, _P(self.pt_ptr), ctypes.c_double(lam), _P(self.V), _P(self.W),
-                    _P(self.Vinv), _P(self.Y))
+        damp = L.mt_damp_y_pinv if vinv == "pinv" else L.mt_damp_y
+        damp(n, _P(self.pt_ptr), ctypes.c_double(lam), _P(self.V), _P(self.W), _P(self.Vinv),
+             _P(self.Y))
         L.mt_schur(m, _P(self.cam_ptr), _P(self.cam_obs), _P(self.pt), _P(self.pt_ptr),
                    _P(self.cam), _P(self.Y), _P(self.W), _P(self.U), ctypes.c_double(lam),
                    _P(self.eA), _P(self.eB), _P(self.S), _P(self.e_))
@@ -150,9 +167,82 @@ class SparsePort:
                           _P(self.db), _P(self.a_new), _P(self.b_new))
         t.append(time.perf_counter())
         return {"old_sse": old, "new_sse": new, "S": self.S, "e_": self.e_, "da": da,
-                "db": self.db.reshape(n, 3).T, "bandwidth": bw,
+                "db": self.db.reshape(n, 3).T, "bandwidth": bw, "a_new": self.a_new,
+                "b_new": self.b_new,
                 "seconds": {"linearize": t[1] - t[0], "schur": t[2] - t[1],
                             "solve": t[3] - t[2], "update": t[4] - t[3], "total": t[4] - t[0]}}
+
+
+    def lm(self, a0, b0, *, stop_rel=1e-3, max_iter=20, max_iter2=10, lambda0=1e-3,
+           vinv="pinv", solve="band", check_pinv=1):
+        """The whole LM loop of bundle_euclid.m:111-249 (fix_calibration) with
+        the reference's MATLAB semantics: V*_i^-1 = pinv(V*_i) (mt_damp_y_pinv)
+        and da = pinv(S) e_.  The reduced solve is LAPACK's banded Cholesky on
+        S with its exactly-zero rows fixed (App. A Q2 / Q8); that IS pinv(S) e_
+        when no eigenvalue of S falls below pinv's tolerance ld * eps(max
+        eigenvalue) (none is truncated), which check_pinv verifies on every
+        check_pinv-th pass and the last (sparse shift-invert Lanczos for the
+        extreme eigenvalues of the band; 0 = never).  Returns (error_, a, b, info) with info = passes, accepted and
+        the smallest lambda_min / tol seen."""
+        a = np.array(a0, dtype=np.float64, order="F")
+        b = np.array(b0, dtype=np.float64, order="F")
+        lam, nu, it, it2 = lambda0, 2.0, 1, 0
+        err, passes, acc, relin = [], 0, 0, True
+        worst = np.inf
+
+        def cont():
+            if not (it < max_iter and it2 < max_iter2):
+                return False
+            if it < 3:
+                return True
+            return err[it - 1] > 1e-20 and err[it - 2] - err[it - 1] > stop_rel * err[it - 2]
+
+        while cont():
+            r = self.one_pass(a, b, lam, solve=solve, vinv=vinv, relin=relin)
+            passes += 1
+            if check_pinv and (passes - 1) % check_pinv == 0:
+                worst = min(worst, pinv_margin(self.S))
+            old, new = r["old_sse"], r["new_sse"]
+            g = np.concatenate([self.eA, self.eB])
+            dp = np.concatenate([r["da"], self.db])
+            rho = (old - new) / float(dp @ (lam * dp + g))
+            if old - new > 0:                         # bundle_euclid.m:218-232
+                a = r["a_new"].reshape(self.m, 6).T.copy(order="F")
+                b = r["b_new"].reshape(self.n, 3).T.copy(order="F")
+                lam = lam * max(1.0 / 3.0, 1.0 - (2.0 * rho - 1.0) ** 3)
+                nu = 2.0
+                if len(err) < it:
+                    err.append(old / self.N)
+                else:
+                    err[it - 1] = old / self.N
+                it += 1
+                err.append(new / self.N)
+                it2 = 0
+                acc += 1
+                relin = True
+            else:                                     # :233-241
+                lam, nu = lam * nu, 2.0 * nu
+                it2 += 1
+                relin = False
+        if check_pinv:   # the last pass's system
+            worst = min(worst, pinv_margin(self.S))
+        return np.array(err), a, b, {"passes": passes, "accepted": acc, "pinv_margin": worst}
+
+
+def pinv_margin(S):
+    """lambda_min / tol of S restricted to its non-zero rows, tol = MATLAB
+    pinv's ld * eps(sigma_max): > 1 means pinv(S) e_ equals the Cholesky
+    solve with the zero rows fixed (no singular value is truncated).  S is
+    symmetric; sparse shift-invert Lanczos on the band."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as sla
+    d = np.diag(S)
+    keep = d != 0.0
+    A = sp.csc_matrix(S[np.ix_(keep, keep)])
+    lmax = sla.eigsh(A, k=1, which="LA", return_eigenvectors=False, tol=1e-6)[0]
+    lmin = sla.eigsh(A, k=1, sigma=0.0, which="LM", return_eigenvectors=False, tol=1e-6)[0]
+    tol = S.shape[0] * np.spacing(lmax)
+    return float(lmin / tol)
 
 
 def dense_pass(K, a, b, X, vis, lam=1e-3):

@@ -119,3 +119,95 @@ def test_rccl_one_rank_communicator():
     assert n0 == n1 and n0 > 2
     assert np.array_equal(e0, e1)
     assert np.array_equal(a0, a1) and np.array_equal(b0, b1)
+
+
+@pytest.mark.timeout(600)
+def test_cfg3_eight_rank_threads_one_pass(gpu):
+    """Config 4's data path at full size on one GPU: the config-3 scene (1000
+    cameras, 500k points, 3M observations) point-sharded over 8 rank threads
+    (dist.HostGroup host collective, every rank on device 0), one relinearising
+    pass, against the one-rank pass.  Exercises every shard boundary of the
+    8-GPU layout: the contiguous point ranges, the per-rank partial U* / eA in
+    the partial reduced systems, the one all-reduce of [S blocks | e_ | old
+    SSE], the replicated CR solve, the per-rank update and the scalars'
+    all-reduce.  Bars: old SSE 1e-12, every co-visible S block and e_ 1e-12 of
+    their largest entry (sums grouped per rank), da 1e-6 of its largest entry
+    (cond(S), as tests/test_gpu_full_configs.py), db 1e-6, new SSE 1e-9; and
+    every rank holds the identical system, step and decision."""
+    import threading
+    from bundleadjustmentmatlab_amd.dist import HostGroup
+    from bundleadjustmentmatlab_amd.scene import make_config
+    sc = make_config("cfg3", gpu=True)
+    a = np.vstack([sc.w0, sc.T0])
+    b = np.asfortranarray(sc.X0[:3])
+    args = (sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, 6)
+
+    def one_pass(ba):
+        ba.set_params(a, b)
+        jk, blk, e_ = ba.reduced_system(dense=False)
+        info = ba.step(relinearize=True, update_lm=False)
+        da, db = ba.last_step()
+        return dict(jk=jk, blk=blk, e_=e_, old=info.old_sse, new=info.new_sse,
+                    acc=info.accepted, da=da, db=db, plan=ba.plan_info())
+
+    with gpu.BundleAdjuster(*args) as ba:
+        ref = one_pass(ba)
+    world = 8
+    grp = HostGroup(world)
+    out, errs = [None] * world, []
+
+    def rank_main(r):
+        try:
+            with gpu.BundleAdjuster(*args, rank=r, world_size=world,
+                                    allreduce=grp.allreduce_fn(r)) as ba:
+                out[r] = one_pass(ba)
+        except Exception as e:   # noqa: BLE001 -- re-raised below
+            errs.append(e)
+            grp._bar.abort()
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    o0 = out[0]
+    assert sum(o["plan"]["points"] for o in out) == sc.n
+    assert sum(o["plan"]["obs"] for o in out) == sc.num_obs
+    assert all(not o["plan"]["ordered"] for o in out)          # every rank on the fast path
+    for o in out[1:]:   # replicated: identical system, step and decision on every rank
+        assert np.array_equal(o["jk"], o0["jk"]) and np.array_equal(o["blk"], o0["blk"])
+        assert np.array_equal(o["da"], o0["da"]) and o["acc"] == o0["acc"]
+        assert o["old"] == o0["old"] and o["new"] == o0["new"]
+    assert np.array_equal(o0["jk"], ref["jk"])                # one packed block layout
+    smax = np.abs(ref["blk"]).max()
+    assert np.abs(o0["blk"] - ref["blk"]).max() <= 1e-12 * smax
+    assert np.abs(o0["e_"] - ref["e_"]).max() <= 1e-12 * np.abs(ref["e_"]).max()
+    assert abs(o0["old"] - ref["old"]) <= 1e-12 * ref["old"]
+    rel = np.abs(o0["da"] - ref["da"]).max() / np.abs(ref["da"]).max()
+    assert rel <= 1e-6, rel
+    # last_step's db: this rank's points first (the rest of the n columns 0)
+    db = np.concatenate([o["db"][:, :o["plan"]["points"]] for o in out], axis=1)
+    assert np.abs(db - ref["db"]).max() <= 1e-6 * np.abs(ref["db"]).max()
+    assert abs(o0["new"] - ref["new"]) <= 1e-9 * ref["new"], (o0["new"], ref["new"])
+    assert o0["acc"] == ref["acc"]
+
+
+@pytest.mark.timeout(300)
+def test_bench_two_ranks_share_one_gpu(tmp_path):
+    """bench.py --gpus 2 on a one-GPU box: two processes, both on device 0;
+    RCCL refuses a second rank on a device, so dist.rank_collective hands
+    them the gloo host all-reduce.  The bench line reports both ranks' work
+    (config 2, point-sharded x2)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--config", "cfg2", "--steps", "5", "--warmup", "1",
+                        "--no-cpu-baseline"], capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([q for q in r.stdout.splitlines() if q.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    assert line["config"]["collective"].startswith("gloo")
+    assert line["config"]["observations"] == 60_000

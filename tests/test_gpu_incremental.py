@@ -112,3 +112,45 @@ def test_run_sharded_matches_single(gpu):
     assert abs(r1[2][0] - r4[2][0]) <= 1e-12 * r1[2][0]
     assert abs(r1[2][1] - r4[2][1]) <= 1e-7 * r1[2][1]
     assert abs(r1[2][-1] - r4[2][-1]) <= 1e-4 * r1[2][-1]
+
+
+@pytest.mark.timeout(600)
+def test_scaled_replay_elastic_shards_from_choose_shards(gpu):
+    """Config 5's scaled variant (scene.growing_scene, the generate_scene_and_
+    motion model vectorised) replayed with 8 virtual devices on GPU 0: every
+    solve's rank count comes from dist.choose_shards (its threshold lowered to
+    the test scene's size, so the replay walks 1 -> 2 -> 4 -> 8 ranks as it
+    grows; ranks sharing a GPU use host collectives).  Every sharded solve is
+    re-run on one rank from the same inputs: error_(1) equal to 1e-12
+    (summation order) and the first step's error_(2) to 1e-7; the final
+    reconstruction reprojects at the noise level."""
+    from bundleadjustmentmatlab_amd import incremental as inc
+    from bundleadjustmentmatlab_amd.dist import choose_shards
+    from bundleadjustmentmatlab_amd.scene import make_config
+    sc = make_config("cfg5x", m=120, seed=16)
+    thr = max(1000, sc.num_obs // 12)
+    pairs = []
+    orig = inc.run_sharded
+
+    def spy(K, pt, cam, ox, n, na, a0, b0, world, **kw):
+        out = orig(K, pt, cam, ox, n, na, a0, b0, world, **kw)
+        one = orig(K, pt, cam, ox, n, na, a0, b0, 1, **{k: v for k, v in kw.items()
+                                                        if k != "devices"})
+        pairs.append((world, out[2], one[2]))
+        return out
+
+    inc.run_sharded = spy
+    try:
+        el = inc.incremental_bundle(sc, devices=[0] * 8, obs_per_shard=thr)
+    finally:
+        inc.run_sharded = orig
+    ks = [q["shards"] for q in el["solves"]]
+    assert ks == [choose_shards(q["observations"], 8, thr) for q in el["solves"]]
+    assert {1, 2, 4} <= set(ks), ks
+    assert len(pairs) == sum(k > 1 for k in ks)
+    for world, e, e1 in pairs:
+        assert abs(e[0] - e1[0]) <= 1e-12 * e1[0], world
+        assert abs(e[1] - e1[1]) <= 1e-7 * e1[1], (world, e[1], e1[1])
+    assert el["solves"][-1]["error"][-1] < 0.6
+    print(f"scaled replay: {len(ks)} solves, {len(pairs)} sharded (rank counts "
+          f"{sorted(set(ks))}), each equal to its one-rank solve")

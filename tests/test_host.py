@@ -25,6 +25,31 @@ def test_parse_options_defaults_and_names():
     assert parse_options(m, n, ["fix_principal"], x=x)["num_variableK"] == 1
 
 
+def test_pivot_mask_matlab_indexing():
+    """'fix_pivot' as bundle_euclid.m:150-153 indexes with it: a logical mask
+    of any length (none true past m) or 1-based camera numbers."""
+    from bundleadjustmentmatlab_amd.bundle import pivot_mask
+    m = 5
+    assert pivot_mask(np.array([True, False, True]), m).tolist() == [1, 0, 1, 0, 0]
+    assert pivot_mask(np.array([True, False, False, False, False, False]), m).tolist() == \
+        [1, 0, 0, 0, 0]
+    assert pivot_mask(1, m).tolist() == [1, 0, 0, 0, 0]
+    assert pivot_mask([1, 3, 3], m).tolist() == [1, 0, 1, 0, 0]
+    assert pivot_mask(np.array([[2.0], [5.0]]), m).tolist() == [0, 1, 0, 0, 1]
+    assert not pivot_mask(np.zeros(0), m).any()
+    for bad in (0, 6, 1.5, [-1], np.array([False] * 5 + [True])):
+        with pytest.raises(ValueError):
+            pivot_mask(bad, m)
+    o = parse_options(m, 2, ["fix_pivot", [2, 4]])
+    assert o["fix_pivot"] and o["pivot"].tolist() == [0, 1, 0, 1, 0]
+
+
+def test_oracle_pivot_matches_host(oracle):
+    from bundleadjustmentmatlab_amd.bundle import pivot_mask
+    for pv in ([1, 3], np.array([True, False]), 2, np.array([1.0, 1.0, 4.0])):
+        assert np.array_equal(oracle._matlab_index_mask(pv, 4), pivot_mask(pv, 4))
+
+
 @pytest.mark.parametrize("nvk", [0, 1, 4])
 def test_pack_unpack_roundtrip(nvk):
     rng = np.random.default_rng(0)

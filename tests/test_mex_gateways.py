@@ -65,7 +65,7 @@ def test_gateway_shape_errors():
     with pytest.raises(mexhost.MexError, match="options must be a struct"):
         mexhost.call("mex_bundle_euclid_lm", 3, K, a, b, X, vis, np.zeros(2))
     with pytest.raises(mexhost.MexError, match="pivot"):
-        mexhost.call("mex_bundle_euclid_lm", 3, K, a, b, X, vis, {"pivot": np.ones(2)})
+        mexhost.call("mex_bundle_euclid_lm", 3, K, a, b, X, vis, {"pivot": np.ones(2) * 9})
 
 
 # ------------------------------------------------------------------ GPU -----
@@ -130,9 +130,28 @@ def _dropin_euclid(sc, x, vis, nvk, opts):
     return mexhost.call("mex_bundle_euclid_lm", 3, sc.K, a, sc.X0[0:3], x[0:2], vis, opts)
 
 
+@pytest.mark.parametrize("opts,msg", [
+    ({"pivot": np.array([[0.0]])}, "integers in 1..m"),
+    ({"pivot": np.array([[1.0, 4.0]])}, "integers in 1..m"),
+    ({"pivot": np.array([[1.5]])}, "integers in 1..m"),
+    ({"pivot_mask": np.array([[1.0, 0.0, 0.0, 1.0]])}, "past the camera count"),
+])
+def test_fused_gateway_pivot_errors(opts, msg):
+    """'fix_pivot' outside the cameras is an error before any device work
+    (MATLAB errors on index 0 / 1.5 and would grow U / W / eA past m)."""
+    m, n = 3, 4
+    K = np.tile([[500.0], [500.0], [250.0], [250.0]], (1, m))
+    a = np.zeros((6, m))
+    b = np.zeros((3, n))
+    X = np.ones((2, n, m))
+    vis = np.ones((n, m))
+    with pytest.raises(mexhost.MexError, match=msg):
+        mexhost.call("mex_bundle_euclid_lm", 3, K, a, b, X, vis, opts)
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["fix_calibration", "fix_pivot", "nomex", "free_K",
-                                  "max_iter"])
+@pytest.mark.parametrize("case", ["fix_calibration", "fix_pivot", "pivot_index",
+                                  "pivot_short_mask", "nomex", "free_K", "max_iter"])
 def test_fused_euclid_gateway_matches_python_dropin(gpu, case):
     """mex_bundle_euclid_lm (options struct really parsed) == the Python drop-in
     bundle_euclid over the same library, bit for bit; error_ sized from
@@ -148,7 +167,13 @@ def test_fused_euclid_gateway_matches_python_dropin(gpu, case):
         args += ["fix_calibration"]
     elif case == "fix_pivot":
         args += ["fix_calibration", "fix_pivot", pv.astype(bool)]
-        opts["pivot"] = pv
+        opts["pivot_mask"] = pv
+    elif case == "pivot_index":   # 'fix_pivot', [1 3]: MATLAB camera numbers
+        args += ["fix_calibration", "fix_pivot", np.array([1.0, 3.0])]
+        opts["pivot"] = np.array([[1.0, 3.0, 3.0]])   # duplicates index the same page
+    elif case == "pivot_short_mask":   # logical(1:2) on m = 6 cameras
+        args += ["fix_calibration", "fix_pivot", np.array([True, True])]
+        opts["pivot_mask"] = np.array([[1.0, 1.0]])
     elif case == "nomex":
         args += ["fix_calibration"]
         opts["semantics"] = 1.0
@@ -179,8 +204,11 @@ def test_fused_euclid_gateway_matches_python_dropin(gpu, case):
     assert np.array_equal(b_g, Xe_[0:3])
     if nvk == 4:
         assert np.array_equal(a_g[6:10], K_)
-    if case == "fix_pivot":
+    if case in ("fix_pivot", "pivot_short_mask"):
         assert np.array_equal(a_g[0:3, :2], sc.w0[:, :2])
+    if case == "pivot_index":
+        assert np.array_equal(a_g[0:3, [0, 2]], sc.w0[:, [0, 2]])
+        assert not np.array_equal(a_g[0:3, 1], sc.w0[:, 1])
 
 
 @pytest.mark.gpu

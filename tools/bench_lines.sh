@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-2 bench lines (GPU box, repo root): every line under its own limit
+# the bench lines of a round (GPU box, repo root): every line under its own limit
 set -o pipefail
 out=${1:-gpurun_out/r02b}
 mkdir -p "$out"
