@@ -53,6 +53,9 @@ def main():
     ap.add_argument("--mode", choices=["pass", "solve"], default="pass",
                     help="pass: one LM pass per step (headline); solve: one full LM "
                          "solve to convergence per step (bundle_euclid.m:111-249)")
+    ap.add_argument("--time-fallbacks", action="store_true",
+                    help="also time one forced pinv pass and one forced re-solve "
+                         "(loads rocSOLVER; outside the timed region)")
     ap.add_argument("--spawn-selftest", action="store_true",
                     help="launch only: every rank joins the gloo group and reports (no GPU)")
     args = ap.parse_args()
@@ -124,8 +127,11 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     info = None
+    n_pinv = n_retry = 0
     for _ in range(args.steps):
         info = ba.step(relinearize=True, update_lm=False)
+        n_pinv += info.pinv
+        n_retry += info.spin_retry
     ba.sync()
     barrier()
     torch.cuda.synchronize()
@@ -163,6 +169,27 @@ def main():
                   f"{roofs[k]['frac']:.3f}" for k, (t, c) in
                   sorted(kms.items(), key=lambda kv: -kv[1][0])))
 
+    # the solve's fallbacks, outside the timed region: their count in the timed
+    # passes, and one pass of each forced (vlgba_debug_force_status) -- the
+    # pinv step (rocSOLVER dsyevd on the dense S; its first call also loads
+    # the library) and the re-solve without spins after a hand-off timeout
+    fallbacks = {"pinv_passes_timed": n_pinv, "spin_retries_timed": n_retry}
+    if args.time_fallbacks:
+        for word, key in ((4, "pinv_pass_ms"), (5, "nospin_resolve_pass_ms")):
+            ts = []
+            for _ in range(2):                      # the first pinv pass loads rocSOLVER
+                barrier()
+                t1 = time.perf_counter()
+                ba.force_status(word, 1)
+                fi = ba.step(relinearize=True, update_lm=False)
+                ba.sync()
+                ts.append(1e3 * (time.perf_counter() - t1))
+                assert (fi.pinv if word == 4 else fi.spin_retry) == 1
+            fallbacks[key] = ts[-1]
+            if word == 4:
+                fallbacks["pinv_first_call_ms"] = ts[0]
+        log(f"[bench] fallbacks: {fallbacks}")
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(sc, a0, b0, num_a, args.cpu_sample_points,
@@ -193,6 +220,7 @@ def main():
                                   None)},
         "phases_ms": ph,
         "roofline": roof,
+        "solve_fallbacks": fallbacks,
         "cpu_baseline": cpu,
     }
     if rank == 0:

@@ -303,6 +303,12 @@ class BundleAdjuster:
         check(self._L.vlgba_get_params(self._h, _dp(a), _dp(b)), "vlgba_get_params")
         return a.reshape(self.num_a, self.m, order="F"), b.reshape(3, self.n, order="F")
 
+    def force_status(self, word, passes=1):
+        """Fault injection: the next ``passes`` passes report a non-positive
+        pivot (word 4: pinv step) or a hand-off timeout (word 5: re-solve)."""
+        check(self._L.vlgba_debug_force_status(self._h, int(word), int(passes)),
+              "vlgba_debug_force_status")
+
     def step(self, relinearize=True, update_lm=True):
         info = VlgbaStepInfo()
         check(self._L.vlgba_step(self._h, int(relinearize), int(update_lm), ctypes.byref(info)),

@@ -229,7 +229,9 @@ struct ba_dev {
     do { if ((d)->kt && (d)->kt->on) kt_end((d)->kt, (d)->stream, (id)); } while (0)
 
 #define BA_PART_MAX 65536
+#ifndef BA_CH_OBS
 #define BA_CH_OBS 128      // observations per Schur chunk (LDS budget)
+#endif
 #define BA_CH_PTS 64       // points per Schur chunk
 #define BA_CH_TERMS 4096   // (obs, obs) terms per chunk: a track of <= 90 observations
 #define BA_GACC 4096       // max doubles of LDS block accumulators per Schur group

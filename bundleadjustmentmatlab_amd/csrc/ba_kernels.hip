@@ -284,6 +284,7 @@ __global__ __launch_bounds__(256) void k_linearize(
 #ifndef BA_LIN_W2_ON
 #define BA_LIN_W2_ON 1
 #endif
+
 template <int NA>
 __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
     const int *__restrict__ ch_pt, const int *__restrict__ ch_obase,
@@ -342,9 +343,11 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
         m_eobl = __hip_atomic_load(eslot_obs + u0 + min(tid, nu - 1), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
         // lanes past the chunk's observations project its last one again
-        // into rows nobs .. BA_CH_OBS - 1, which nothing reads
-        const int lo = tid >> 1, half = tid & 1;
-        const bool live = lo < nobs;
+        // into rows nobs .. BA_CH_OBS - 1, which nothing reads (lanes past
+        // BA_CH_OBS rows, when it is < 128, into the last row: the same
+        // values as any lane that writes it)
+        const int lo = min(tid >> 1, BA_CH_OBS - 1), half = tid & 1;
+        const bool live = (tid >> 1) < nobs;
         {
             const int o = obase + min(lo, nobs - 1);
             const int j = obs_cam[o], i = p0 + obs_lpt[o];

@@ -789,7 +789,8 @@ struct vlgba_ctx {
     int *pinv_info = nullptr;
     int pinv_used = 0;            // passes that took the pinv fallback
     int spin_retries = 0;         // passes re-solved after a hand-off timeout
-    int debug_timeouts = 0;       // test hook: passes whose timeout word is forced
+    int debug_timeouts = 0;       // test hooks: passes whose timeout word / pivot word
+    int debug_pivots = 0;         // is forced (vlgba_debug_force_status)
 };
 
 // Per-device pool of the context's streams, fork/join events and host-mapped
@@ -1608,11 +1609,14 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
     TRY(ba_launch_assemble(&d));
     mark(c, 5);
     TRY(ba_chol_solve(&d));
-    if (c->debug_timeouts > 0) {   // test hook (VLGBA_DEBUG_SPIN_TIMEOUT): as if a spin gave up
-        static const double one = 1.0;
-        VLGBA_CHECK(hipMemcpyAsync(d.scal + 5, &one, sizeof one, hipMemcpyHostToDevice,
-                                   d.stream));
-        c->debug_timeouts--;
+    for (int w = 4; w <= 5; w++) {   // test hooks: as if a pivot failed / a spin gave up
+        int &k = w == 4 ? c->debug_pivots : c->debug_timeouts;
+        if (k > 0) {
+            static const double one = 1.0;
+            VLGBA_CHECK(hipMemcpyAsync(d.scal + w, &one, sizeof one, hipMemcpyHostToDevice,
+                                       d.stream));
+            k--;
+        }
     }
     mark(c, 6);
     // RCCL ranks spin as well: their collectives are stream-ordered, and the
@@ -1897,6 +1901,13 @@ int vlgba_get_step(vlgba_ctx *c, double *da, double *db)
     if (da) TRY(download(da, c->d.da, (size_t)c->d.ld, c->d.stream));
     if (db) TRY(download_points(c, db, c->d.db, 3));
     VLGBA_CHECK(hipStreamSynchronize(c->d.stream));
+    return 0;
+}
+
+int vlgba_debug_force_status(vlgba_ctx *c, int word, int passes)
+{
+    if (!c || (word != 4 && word != 5) || passes < 0) return VLGBA_E_ARG;
+    (word == 4 ? c->debug_pivots : c->debug_timeouts) = passes;
     return 0;
 }
 

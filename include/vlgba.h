@@ -316,6 +316,12 @@ int vlgba_debug_sincos(const double *x, double *s, double *c, long long n);
  * on a host ld x ld symmetric S (lower triangle read) and e_: da = pinv(S) e_
  * with MATLAB's tolerance ld * eps(max |eigenvalue|). */
 int vlgba_debug_pinv_solve(int ld, const double *S, const double *e_, double *da);
+/* Fault injection (tests / the bench's fallback timing): the next `passes`
+ * passes of ctx report word 4 = a non-positive pivot (the pass then takes the
+ * pinv step) or word 5 = a hand-off spin timeout of the one-launch solve (the
+ * pass is solved again without spins).  VLGBA_DEBUG_SPIN_TIMEOUT="rank:passes"
+ * sets word 5 at context creation. */
+int vlgba_debug_force_status(vlgba_ctx *ctx, int word, int passes);
 
 /* Library / device info: writes a NUL-terminated string, returns its length. */
 int vlgba_version(char *buf, int len);

@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 for r in $(seq $R); do
   for v in $VARIANTS; do
     echo "== $v" >> gpurun_out/ab.log
-    VLGBA_LIB=tools/build/ab/$v/libvlgba.so timeout -k 10 300 python -u bench.py $ARGS > gpurun_out/ab_$v.out 2>&1 || { echo "FAIL $v rc=$?"; tail -5 gpurun_out/ab_$v.out; exit 1; }
+    VLGBA_LIB=tools/build/ab/$v/libvlgba.so timeout -k 10 120 python -u bench.py $ARGS > gpurun_out/ab_$v.out 2>&1 || { echo "FAIL $v rc=$?"; tail -5 gpurun_out/ab_$v.out; exit 1; }
     grep -E "ms/iteration|kernels" gpurun_out/ab_$v.out >> gpurun_out/ab.log
   done
 done

@@ -5,9 +5,14 @@ set -o pipefail
 export TMPDIR=/tmp
 VARIANTS=${VARIANTS:-$(ls tools/build/ab)}
 args="--steps 3 --warmup 1 --no-cpu-baseline"
-sets=("SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES"
-      "SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY"
-      "SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY")
+# PMC_SETS: counter sets separated by ';' (each at most 8 SQ counters)
+if [ -n "$PMC_SETS" ]; then
+  IFS=';' read -r -a sets <<< "$PMC_SETS"
+else
+  sets=("SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES"
+        "SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY"
+        "SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY")
+fi
 for v in $VARIANTS; do
   for i in "${!sets[@]}"; do
     out=gpurun_out/ab_pmc/${v}_$i
