@@ -211,3 +211,61 @@ def test_bench_two_ranks_share_one_gpu(tmp_path):
     assert line["n_gpus"] == 2 and line["value"] > 0
     assert line["config"]["collective"].startswith("gloo")
     assert line["config"]["observations"] == 60_000
+
+
+def test_long_tracks_sharded_fast_path(gpu):
+    """Irregular tracks with more than one rank (VERDICT r2 missing 5): each
+    rank orders ITS points by track kind (short tracks for the MFMA Schur
+    chunks, per-term tracks, long tracks last), so every rank of a sharded
+    ladybug-like scene with 100-220-view tracks stays on the fast path; the
+    ranks agree on one packed block layout (canonical block ids).  Two rank
+    threads on one GPU (host collective) against the one-rank pass: old SSE
+    1e-12, new SSE / dp'(lambda dp + g) 1e-8, db of every point (input order)
+    1e-8."""
+    import threading
+    from bundleadjustmentmatlab_amd.dist import HostGroup
+    from bundleadjustmentmatlab_amd.scene import make_config
+    sc = make_config("ladybug", m=300, n=5000, max_track=30, radius=150.0, seed=29,
+                     long_frac=0.01, long_len=(100, 220))
+    L = np.bincount(sc.obs_pt, minlength=sc.n)
+    a = np.vstack([sc.w0, sc.T0])
+    b = np.asfortranarray(sc.X0[:3])
+    args = (sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, 6)
+
+    def one_pass(ba):
+        ba.set_params(a, b)
+        info = ba.step(relinearize=True, update_lm=False)
+        return info, ba.last_step()[1], ba.plan_info(), ba.get_params()
+
+    with gpu.BundleAdjuster(*args) as ba:
+        i1, db1, _, _ = one_pass(ba)
+    world = 2
+    grp = HostGroup(world)
+    out, errs = [None] * world, []
+
+    def rank_main(r):
+        try:
+            with gpu.BundleAdjuster(*args, rank=r, world_size=world,
+                                    allreduce=grp.allreduce_fn(r)) as ba:
+                out[r] = one_pass(ba)
+        except Exception as e:   # noqa: BLE001 -- re-raised below
+            errs.append(e)
+            grp._bar.abort()
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    assert sum(o[2]["long_points"] for o in out) > 0
+    for info, db, plan, _ in out:
+        assert plan["ordered"] == 0, plan                  # fast path on every rank
+        assert abs(info.old_sse - i1.old_sse) <= 1e-12 * i1.old_sse
+        assert abs(info.new_sse - i1.new_sse) <= 1e-8 * i1.new_sse
+        assert abs(info.dpg - i1.dpg) <= 1e-8 * abs(i1.dpg)
+    db = np.concatenate([o[1][:, :o[2]["points"]] for o in out], axis=1)
+    assert np.abs(db - db1).max() <= 1e-8 * np.abs(db1).max()
+    # get_params: every rank returns the full b in input order
+    assert np.array_equal(out[0][3][1], out[1][3][1])
+    assert (L > 128).sum() > 10
