@@ -327,13 +327,21 @@ def bench_incremental(args):
     torch.cuda.set_device(0)
     sc = make_config(args.config)
     devices = list(range(ndev))
+    t_start = time.perf_counter()
+
+    def progress(solves):   # a line every 200 solves (long replays)
+        if len(solves) % 200 == 0:
+            q = solves[-1]
+            log(f"[bench] {len(solves)} solves, {time.perf_counter() - t_start:.1f} s: "
+                f"{q['cameras']} cams {q['observations']} obs, solve {1e3 * q['seconds']:.1f} ms "
+                f"(solve time so far {sum(s['seconds'] for s in solves):.1f} s)")
     for _ in range(args.warmup):
-        incremental_bundle(sc, devices=devices)
+        incremental_bundle(sc, devices=devices, progress=progress)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     res = None
     for _ in range(args.steps):
-        res = incremental_bundle(sc, devices=devices)
+        res = incremental_bundle(sc, devices=devices, progress=progress)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     sol = res["solves"]
@@ -358,7 +366,13 @@ def bench_incremental(args):
                    "solves_by_shard_count": shards},
         "final": {"cameras": sol[-1]["cameras"], "points": sol[-1]["points"],
                   "observations": sol[-1]["observations"],
-                  "error_final": float(sol[-1]["error"][-1])},
+                  # (a solve whose every step is rejected returns an empty error_,
+                  # as bundle_euclid.m does: the last solve that moved)
+                  "error_final": float(next(q["error"][-1] for q in reversed(sol)
+                                            if len(q["error"])))},
+        "time_split_s": {"solves": sum(q["seconds"] for q in sol),
+                         "resections": sum(q["seconds"] for q in res["resections"]),
+                         "replay": dt / args.steps},
     }
     print(json.dumps(out), flush=True)
 

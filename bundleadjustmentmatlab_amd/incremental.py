@@ -44,7 +44,8 @@ def _subset_obs(sc, cams, pts):
 
 
 def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, device=0,
-                       verbose=False, devices=None, shards=None, obs_per_shard=None):
+                       verbose=False, devices=None, shards=None, obs_per_shard=None,
+                       progress=None):
     """Replay the incremental reconstruction's BA sequence on scene ``sc``
     (scene.Scene).  Cameras ``init_cams`` form the initial two-view
     reconstruction (VLmvg.m's two_view step); every other camera is added in
@@ -61,7 +62,8 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
     Returns dict(solves=[...], resections=[...], K, T, w, X, status) where each
     solve records the cameras / points / observations it adjusted, its error_
     trace, LM passes and wall seconds, and each resection the added camera's
-    one-camera refinement (estimate_camera.m:247-253)."""
+    one-camera refinement (estimate_camera.m:247-253).  ``progress(solves)``,
+    if given, is called after every solve with the solve log so far."""
     m, n = sc.m, sc.n
     K = np.array(sc.K, dtype=np.float64)
     T = np.array(sc.T0, dtype=np.float64)
@@ -113,6 +115,8 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
         if verbose:
             print(f"[incremental] camera {j} {tag}: {len(cams)} cams {len(pts)} pts "
                   f"{len(pt)} obs  error_ {err[0]:.4g} -> {err[-1]:.4g}  {st.iterations} passes")
+        if progress is not None:
+            progress(solves)
 
     def resect(j):
         """estimate_camera.m:247-253: the new camera refined against the points

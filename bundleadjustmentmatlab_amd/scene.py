@@ -393,7 +393,8 @@ CONFIGS = {
     "cfg3": (banded_scene, dict(m=1000, n=500_000, track=6, seed=3)),
     "cfg5": (mview_scene, dict(m=50, min_n=100, max_n=200, depth=100.0, seed=5)),
     # config 5's scaled 1000-camera variant
-    "cfg5x": (growing_scene, dict(m=1000, min_n=300, max_n=500, depth=100.0, seed=15)),
+    # (test_incremental.m's 100 .. 200 tracked features per frame, 1000 frames)
+    "cfg5x": (growing_scene, dict(m=1000, min_n=100, max_n=200, depth=100.0, seed=15)),
     # not a BASELINE config: irregular tracks + loop closures
     "ladybug": (ladybug_scene, dict(m=1000, n=200_000, seed=6)),
 }

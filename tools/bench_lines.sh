@@ -1,7 +1,7 @@
 #!/bin/bash
 # the bench lines of a round (GPU box, repo root): every line under its own limit
 set -o pipefail
-out=${1:-gpurun_out/r02b}
+out=${1:-gpurun_out/bench}
 mkdir -p "$out"
 step() { local name=$1 secs=$2; shift 2
   timeout -k 10 "$secs" python3 -u bench.py "$@" > "$out/$name.log" 2>&1
@@ -10,6 +10,7 @@ step cfg3_pass 300 --steps 20 --warmup 3 &&
 step cfg3_solve 300 --mode solve --steps 5 --warmup 1 --no-cpu-baseline &&
 step cfg2_solve 300 --config cfg2 --mode solve --steps 20 --warmup 3 --no-cpu-baseline &&
 step cfg5 300 --config cfg5 &&
+step cfg5x 600 --config cfg5x --steps 1 --warmup 0 &&
 step ladybug_pass 300 --config ladybug --steps 10 --warmup 2 &&
-step cfg3_host_scene 300 --host-scene --steps 10 --warmup 2 --no-cpu-baseline &&
+step cfg3_fallbacks 300 --steps 10 --warmup 2 --no-cpu-baseline --time-fallbacks &&
 step cfg3_pass_b 300 --steps 20 --warmup 3 --no-cpu-baseline
