@@ -60,7 +60,10 @@ def _project(Kp, a, b, nvk):
     return np.stack([x0 / Xc[:, 2], x1 / Xc[:, 2]], 1)
 
 
-def bundle_euclid_nomex(K, Te, w, Xe, x, *varargin):
+def bundle_euclid_nomex(K, Te, w, Xe, x, *varargin, stop_rel=1e-3, max_iter=20, max_iter2=10):
+    """stop_rel / max_iter / max_iter2: the stop rule's constants
+    (bundle_euclid_nomex.m:106-109: 1e-3, 20, 10), exposed so that a test can
+    run both twins to convergence."""
     K, Te, w, Xe, x = map(np.asarray, (K, Te, w, Xe, x))
     m, n = w.shape[1], x.shape[1]
     o = _ref.parse_options(m, n, x, varargin)
@@ -77,8 +80,9 @@ def bundle_euclid_nomex(K, Te, w, Xe, x, *varargin):
     lam, nu = 0.001, 2.0
     it, it2 = 1, 0
     err = []
-    while it < 20 and it2 < 10 and (it < 3 or (err[it - 1] > 1e-20 and
-                                               err[it - 2] - err[it - 1] > 1e-3 * err[it - 2])):
+    while it < max_iter and it2 < max_iter2 and (
+            it < 3 or (err[it - 1] > 1e-20 and
+                       err[it - 2] - err[it - 1] > stop_rel * err[it - 2])):
         ao, bo, Ko = a[:, cam].T, b[:, pt].T, K[:, cam].T
         xh = _project(Ko, ao, bo, nvk)
         A = np.zeros((N, 2, num_a))
