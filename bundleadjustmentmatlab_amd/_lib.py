@@ -139,6 +139,8 @@ def lib():
                              "make -C bundleadjustmentmatlab_amd/csrc")
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("VLGBA_LIB") and not hasattr(L, name):
+                continue   # an older build under A/B timing (tools/ab_run.sh)
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

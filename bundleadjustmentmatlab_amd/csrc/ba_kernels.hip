@@ -57,6 +57,8 @@ extern "C" int vlgba_debug_stamps(unsigned long long *out, int reset)
 #define STAMP(i)
 #endif
 
+typedef double v2d __attribute__((ext_vector_type(2)));   // (for the non-temporal builtins)
+
 // -------------------------------------------------------------------------
 // block reduction of one double per thread -> partial[blockIdx.x]
 // -------------------------------------------------------------------------
@@ -402,8 +404,12 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
             const long long keep = wz[lo] ? 0 : -1;   // forced zeros by a mask, no branch
             const double v0 = 0.0 + (a0.x * bc.x + a0.y * bc.y);
             const double v1 = 0.0 + (a1.x * bc.x + a1.y * bc.y);
-            wdst[q] = make_double2(__builtin_bit_cast(double, __builtin_bit_cast(long long, v0) & keep),
-                                   __builtin_bit_cast(double, __builtin_bit_cast(long long, v1) & keep));
+            // streamed (non-temporal): W is re-read only after the whole 432 MB
+            // (config 3) has been written, so caching it only evicts the
+            // observation / camera / point data of the next workgroups
+            const v2d w2 = {__builtin_bit_cast(double, __builtin_bit_cast(long long, v0) & keep),
+                            __builtin_bit_cast(double, __builtin_bit_cast(long long, v1) & keep)};
+            __builtin_nontemporal_store(w2, reinterpret_cast<v2d *>(wdst) + q);
         }
     } else {
         double *wdst = W + (size_t)3 * NA * obase;
@@ -1052,7 +1058,11 @@ __global__ __launch_bounds__(256, (NA == 6) ? BA_MF_WAVES : 1) void k_schur_mfma
     double *geacc = gacc + gcap * NA * NA;               // [ecap][NA]
     unsigned *rec = (unsigned *)(geacc + ecap * NA);     // the group's chunk records
     __shared__ int gp0[BA_GROUP_CH + 1], gob[BA_GROUP_CH + 1], gbo[BA_GROUP_CH + 1];
-    const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // groups last to first: linearisation wrote W first to last (streamed past
+    // the caches), so the W rows read here last are the first ones, still in
+    // the Infinity Cache when k_point_update_chunk reads W first to last
+    const int g = ngrp - 1 - (int)blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int li = lane & 15, lk = lane >> 4;
     const int c0 = grp_ch[g], nc = grp_ch[g + 1] - c0;
     const int gs0 = grp_gs[g], ngs = grp_gs[g + 1] - gs0;
@@ -1560,7 +1570,7 @@ __global__ __launch_bounds__(256) void k_point_update_chunk(
 #pragma unroll
         for (int u = 0; u < MAXE; u++) {
             const int e = tid + 256 * u;
-            wr[u] = wsrc[e < ne ? e : 0];
+            wr[u] = __builtin_nontemporal_load(wsrc + (e < ne ? e : 0));   // W's last reader
         }
         static_assert(BA_CH_PTS <= 64, "one wave loads the point offsets");
         if (tid < 64)   // wave 0
