@@ -34,6 +34,7 @@
 #include <map>
 #include <new>
 #include <numeric>
+#include <thread>
 #include <vector>
 
 #define VLGBA_VERSION_STR "vlgba 0.1 (gfx950, fp64, MFMA-f64 Cholesky)"
@@ -238,19 +239,54 @@ void build_blocks(int m, const std::vector<int> &pt_ptr_all, const std::vector<i
     if (hb.dense_tab) hb.tab.assign((size_t)m * m, -1);
     else hb.rows.resize(m);
     auto find = [&](int j, int k) -> int { return hb.find(j, k); };
-    if (all_diag)
-        for (int j = 0; j < m; j++) hb.insert(j, j);
-    for (int i = 0; i < n; i++)
-        for (int a = pt_ptr_all[i]; a < pt_ptr_all[i + 1]; a++)
-            for (int b = pt_ptr_all[i]; b < pt_ptr_all[i + 1]; b++) {
-                const int j = cam_all[a], k = cam_all[b];
-                if (lower && j < k) continue;
-                hb.insert(j, k);
-            }
     // canonical block ids, (k, j) ascending: independent of the point order,
     // so ranks that order their own points differently (order_points_by_kind)
     // agree on the packed layout of the all-reduced blocks
-    {
+    if (lower && hb.dense_tab) {
+        // the lower block set as one bit row per column k (bit j: block (j, k),
+        // j >= k), each point's cameras OR-ed in as a word mask over the span
+        // of its track (cameras ascending within a point): O(track x span / 64)
+        // per point instead of one table insert per camera pair, then the ids
+        // handed out row by row = (k, j) ascending
+        const int nw = (m + 63) / 64;
+        std::vector<unsigned long long> rowb((size_t)m * nw, 0ull), mask(nw, 0ull);
+        if (all_diag)
+            for (int j = 0; j < m; j++) rowb[(size_t)j * nw + (j >> 6)] |= 1ull << (j & 63);
+        for (int i = 0; i < n; i++) {
+            const int a0 = pt_ptr_all[i], a1 = pt_ptr_all[i + 1];
+            if (a1 <= a0) continue;
+            const int w0 = cam_all[a0] >> 6, w1 = cam_all[a1 - 1] >> 6;
+            for (int a = a0; a < a1; a++) mask[cam_all[a] >> 6] |= 1ull << (cam_all[a] & 63);
+            for (int a = a0; a < a1; a++) {
+                unsigned long long *row = &rowb[(size_t)cam_all[a] * nw];
+                for (int w = w0; w <= w1; w++) row[w] |= mask[w];
+            }
+            for (int w = w0; w <= w1; w++) mask[w] = 0ull;
+        }
+        for (int k = 0; k < m; k++) {
+            const unsigned long long *row = &rowb[(size_t)k * nw];
+            for (int w = k >> 6; w < nw; w++) {
+                unsigned long long bits = row[w];
+                if (w == (k >> 6)) bits &= ~0ull << (k & 63);   // j >= k only
+                while (bits) {
+                    const int j = 64 * w + __builtin_ctzll(bits);
+                    bits &= bits - 1;
+                    hb.tab[(size_t)j * m + k] = (int)hb.jk.size() / 2;
+                    hb.jk.push_back(j);
+                    hb.jk.push_back(k);
+                }
+            }
+        }
+    } else {
+        if (all_diag)
+            for (int j = 0; j < m; j++) hb.insert(j, j);
+        for (int i = 0; i < n; i++)
+            for (int a = pt_ptr_all[i]; a < pt_ptr_all[i + 1]; a++)
+                for (int b = pt_ptr_all[i]; b < pt_ptr_all[i + 1]; b++) {
+                    const int j = cam_all[a], k = cam_all[b];
+                    if (lower && j < k) continue;
+                    hb.insert(j, k);
+                }
         const int nb0 = (int)hb.jk.size() / 2;
         std::vector<int> ord(nb0);
         std::iota(ord.begin(), ord.end(), 0);
@@ -339,16 +375,105 @@ struct host_plan {
     int mf_max_blob = 0;   // MFMA groups: largest group record block (staged in LDS)
 };
 
-// counting sort of ids by key: ptr[nkey+1], list of ids in ascending id order per key
+static int plan_threads(long long work, long long min_work);
+template <typename F>
+static void parallel_ranges(int n, int nthr, F f, const std::vector<long long> *wpre);
+
+// counting sort of ids by key: ptr[nkey+1], list of ids in ascending id order
+// per key (large inputs: per-thread counts over contiguous id ranges, each
+// thread's ids placed after those of the ranges before it: the same order)
 static void bucket(const std::vector<int> &key, int nkey, std::vector<int> &ptr,
                    std::vector<int> &list)
 {
+    const int n = (int)key.size();
+    const int T = std::min(plan_threads(n, 200000), std::max(1, (int)(4LL * n / (nkey + 1))));
     ptr.assign(nkey + 1, 0);
-    for (int k : key) ptr[k + 1]++;
-    for (int q = 0; q < nkey; q++) ptr[q + 1] += ptr[q];
     list.resize(key.size());
-    std::vector<int> pos(ptr.begin(), ptr.end() - 1);
-    for (size_t s = 0; s < key.size(); s++) list[pos[key[s]]++] = (int)s;
+    if (T <= 1) {
+        for (int k : key) ptr[k + 1]++;
+        for (int q = 0; q < nkey; q++) ptr[q + 1] += ptr[q];
+        std::vector<int> pos(ptr.begin(), ptr.end() - 1);
+        for (int s = 0; s < n; s++) list[pos[key[s]]++] = s;
+        return;
+    }
+    std::vector<std::vector<int>> cnt(T);
+    parallel_ranges(n, T, [&](int t, int s0, int s1) {
+        cnt[t].assign(nkey, 0);
+        for (int s = s0; s < s1; s++) cnt[t][key[s]]++;
+    }, nullptr);
+    for (int k = 0; k < nkey; k++) {   // cnt[t][k] <- start of thread t's ids of key k
+        int at = ptr[k];
+        for (int t = 0; t < T; t++) {
+            const int c = cnt[t][k];
+            cnt[t][k] = at;
+            at += c;
+        }
+        ptr[k + 1] = at;
+    }
+    parallel_ranges(n, T, [&](int t, int s0, int s1) {
+        std::vector<int> &pos = cnt[t];
+        for (int s = s0; s < s1; s++) list[pos[key[s]]++] = s;
+    }, nullptr);
+}
+
+// phase times of build_plan on stderr (tools/bench_plan.sh builds with it)
+#ifdef BA_PLAN_TIMING
+#define PLAN_T0 auto plan_t0_ = std::chrono::steady_clock::now()
+#define PLAN_T(w)                                                                           \
+    do {                                                                                    \
+        const auto t_ = std::chrono::steady_clock::now();                                   \
+        std::fprintf(stderr, "   %-14s %7.2f ms\n", w,                                     \
+                     std::chrono::duration<double, std::milli>(t_ - plan_t0_).count());     \
+        plan_t0_ = t_;                                                                      \
+    } while (0)
+#else
+#define PLAN_T0
+#define PLAN_T(w)
+#endif
+
+// Host threads of a context's plan: VLGBA_HOST_THREADS, else OMP_NUM_THREADS
+// (the GPU box's CPU share), else the hardware's, at most 16; fewer when the
+// work has fewer than min_work items per thread.
+static int plan_threads(long long work, long long min_work)
+{
+    static const int cap = [] {
+        int v = 0;
+        if (const char *e = std::getenv("VLGBA_HOST_THREADS")) v = std::atoi(e);
+        if (v <= 0)
+            if (const char *e = std::getenv("OMP_NUM_THREADS")) v = std::atoi(e);
+        if (v <= 0) v = (int)std::thread::hardware_concurrency();
+        return std::max(1, std::min(v, 16));
+    }();
+    return (int)std::max(1LL, std::min<long long>(cap, work / std::max(1LL, min_work)));
+}
+
+// f(t, lo, hi) on nthr contiguous ranges of [0, n) (thread t takes range t;
+// the calling thread takes range 0), of equal work when wpre (the prefix sums
+// of per-item work, n + 1 entries) is given, else of equal length
+template <typename F>
+static void parallel_ranges(int n, int nthr, F f, const std::vector<long long> *wpre)
+{
+    if (nthr <= 1) {
+        f(0, 0, n);
+        return;
+    }
+    std::vector<int> cut(nthr + 1, n);
+    cut[0] = 0;
+    for (int t = 1; t < nthr; t++) {
+        if (wpre) {
+            const long long target = (*wpre)[n] * t / nthr;
+            cut[t] = (int)(std::lower_bound(wpre->begin(), wpre->begin() + n + 1, target) -
+                           wpre->begin());
+        } else {
+            cut[t] = (int)((long long)n * t / nthr);
+        }
+        cut[t] = std::max(cut[t], cut[t - 1]);
+    }
+    std::vector<std::thread> th;
+    th.reserve(nthr - 1);
+    for (int t = 1; t < nthr; t++) th.emplace_back(f, t, cut[t], cut[t + 1]);
+    f(0, cut[0], cut[1]);
+    for (auto &x : th) x.join();
 }
 
 // MFMA chunks (points below p_split): at most BA_MF_PTS points and cmax
@@ -370,114 +495,173 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
         if (lptr[i + 1] - lptr[i] > BA_CH_OBS || pt_terms(i) > BA_CH_TERMS ||
             (i < p_split && lptr[i + 1] - lptr[i] > cmax))
             return false;
-    std::vector<int> cam_stamp(m, -1);   // chunk camera set (MFMA chunking)
-    P.max_terms = P.max_slots = 0;
-    std::vector<int> slot_of(nb, -1), eslot_of(m, -1), touched, tcam, tcnt, ecnt;
-    P.ch_pt.push_back(0);
-    P.ch_slot.push_back(0);
-    P.ch_eslot.push_back(0);
-    P.slot_tptr.push_back(0);
-    P.eslot_optr.push_back(0);
-    int p = 0;
-    while (p < n) {
-        const bool mf = p < p_split;                // chunk kind
-        const int pend = mf ? p_split : n;
-        const int pts_max = mf ? BA_MF_PTS : BA_CH_PTS;
-        const int obase = lptr[p];
-        int q = p;
-        long long nterm = 0;
-        int ncam = 0;
-        bool uniform = true;   // every point so far sees exactly the first point's cameras
-        auto same_cams = [&](int i1, int i2) {
-            if (lptr[i1 + 1] - lptr[i1] != lptr[i2 + 1] - lptr[i2]) return false;
-            for (int a = 0; a < lptr[i1 + 1] - lptr[i1]; a++)
-                if (lcam[lptr[i1] + a] != lcam[lptr[i2] + a]) return false;
-            return true;
-        };
-        while (q < pend && q - p < pts_max && lptr[q + 1] - obase <= BA_CH_OBS &&
-               nterm + pt_terms(q) <= BA_CH_TERMS) {
-            if (mf) {
-                // a run of points with one camera list (video-like tracks) keeps its
-                // chunks to itself: its MFMA sums stay in registers across chunks
-                const bool same = q == p || same_cams(p, q);
-                if (uniform && !same && q - p >= 4) break;
-                uniform = uniform && same;
-                int add = 0;
-                for (int a = lptr[q]; a < lptr[q + 1]; a++) add += cam_stamp[lcam[a]] != p;
-                if (ncam + add > cmax) break;
-                for (int a = lptr[q]; a < lptr[q + 1]; a++) cam_stamp[lcam[a]] = p;
-                ncam += add;
+    PLAN_T0;
+    // chunk boundaries (sequential: the MFMA chunking follows the camera sets)
+    std::vector<int> cbeg, cend;
+    std::vector<char> cmf;
+    {
+        std::vector<int> cam_stamp(m, -1);   // chunk camera set (MFMA chunking)
+        P.max_terms = 0;
+        int p = 0;
+        while (p < n) {
+            const bool mf = p < p_split;                // chunk kind
+            const int pend = mf ? p_split : n;
+            const int pts_max = mf ? BA_MF_PTS : BA_CH_PTS;
+            const int obase = lptr[p];
+            int q = p;
+            long long nterm = 0;
+            int ncam = 0;
+            bool uniform = true;   // every point so far sees exactly the first point's cameras
+            auto same_cams = [&](int i1, int i2) {
+                if (lptr[i1 + 1] - lptr[i1] != lptr[i2 + 1] - lptr[i2]) return false;
+                for (int a = 0; a < lptr[i1 + 1] - lptr[i1]; a++)
+                    if (lcam[lptr[i1] + a] != lcam[lptr[i2] + a]) return false;
+                return true;
+            };
+            while (q < pend && q - p < pts_max && lptr[q + 1] - obase <= BA_CH_OBS &&
+                   nterm + pt_terms(q) <= BA_CH_TERMS) {
+                if (mf) {
+                    // a run of points with one camera list (video-like tracks) keeps
+                    // its chunks to itself: its MFMA sums stay in registers across
+                    // chunks
+                    const bool same = q == p || same_cams(p, q);
+                    if (uniform && !same && q - p >= 4) break;
+                    uniform = uniform && same;
+                    int add = 0;
+                    for (int a = lptr[q]; a < lptr[q + 1]; a++) add += cam_stamp[lcam[a]] != p;
+                    if (ncam + add > cmax) break;
+                    for (int a = lptr[q]; a < lptr[q + 1]; a++) cam_stamp[lcam[a]] = p;
+                    ncam += add;
+                }
+                nterm += pt_terms(q++);
             }
-            nterm += pt_terms(q++);
+            P.max_terms = std::max(P.max_terms, (int)nterm);
+            P.n_terms += nterm;
+            cbeg.push_back(p);
+            cend.push_back(q);
+            cmf.push_back(mf ? 1 : 0);
+            p = q;
         }
-        P.max_terms = std::max(P.max_terms, (int)nterm);
-        P.n_terms += nterm;
-        // pass 1: the chunk's slots (co-visible blocks, by first touch) and
-        // e-slots (cameras), with their term / observation counts
-        touched.clear();
-        tcam.clear();
-        tcnt.clear();
-        ecnt.clear();
-        for (int i = p; i < q; i++)
-            for (int a = lptr[i]; a < lptr[i + 1]; a++) {
-                const int j = lcam[a];
-                if (eslot_of[j] < 0) {
-                    eslot_of[j] = (int)tcam.size();
-                    tcam.push_back(j);
-                    ecnt.push_back(0);
-                }
-                ecnt[eslot_of[j]]++;
-                for (int b = lptr[i]; b < lptr[i + 1]; b++) {
-                    const int k = lcam[b];
-                    if (j < k) continue;
-                    const int blk = hb.find(j, k);
-                    if (slot_of[blk] < 0) {
-                        slot_of[blk] = (int)touched.size();
-                        touched.push_back(blk);
-                        tcnt.push_back(0);
-                    }
-                    tcnt[slot_of[blk]]++;
-                }
-            }
-        P.max_slots = std::max(P.max_slots, (int)touched.size());
-        // pass 2: the per-term lists (term chunks only: the MFMA records are
-        // dense) and the per-camera observation lists, in the same order
-        const size_t t0 = P.slot_term.size() / 2, u0 = P.eslot_obs.size();
-        for (size_t sl = 0; sl < touched.size(); sl++) {
-            P.slot_blk.push_back(touched[sl]);
-            P.slot_tptr.push_back(P.slot_tptr.back() + (mf ? 0 : tcnt[sl]));
-        }
-        for (size_t e = 0; e < tcam.size(); e++)
-            P.eslot_optr.push_back(P.eslot_optr.back() + ecnt[e]);
-        const int sbase = (int)P.slot_blk.size() - (int)touched.size();
-        const int ebase = (int)P.eslot_optr.size() - 1 - (int)tcam.size();
-        if (!mf) P.slot_term.resize(2 * (size_t)P.slot_tptr.back());
-        P.eslot_obs.resize((size_t)P.eslot_optr.back());
-        for (size_t sl = 0; sl < touched.size(); sl++) tcnt[sl] = P.slot_tptr[sbase + sl] - (int)t0;
-        for (size_t e = 0; e < tcam.size(); e++) ecnt[e] = P.eslot_optr[ebase + e] - (int)u0;
-        for (int i = p; i < q; i++)
-            for (int a = lptr[i]; a < lptr[i + 1]; a++) {
-                const int j = lcam[a];
-                P.eslot_obs[u0 + ecnt[eslot_of[j]]++] = (unsigned short)(a - obase);
-                if (mf) continue;
-                for (int b = lptr[i]; b < lptr[i + 1]; b++) {
-                    const int k = lcam[b];
-                    if (j < k) continue;
-                    const size_t at = t0 + tcnt[slot_of[hb.find(j, k)]]++;
-                    P.slot_term[2 * at] = (unsigned short)(a - obase);
-                    P.slot_term[2 * at + 1] = (unsigned short)(b - obase);
-                }
-            }
-        for (int blk : touched) slot_of[blk] = -1;
-        for (int j : tcam) eslot_of[j] = -1;
-        // cameras of the chunk, for the per-camera reduction below
-        for (size_t s = 0; s < tcam.size(); s++) P.cam_eslots.push_back(tcam[s]);
-        P.ch_pt.push_back(q);
-        P.ch_slot.push_back((int)P.slot_blk.size());
-        P.ch_eslot.push_back((int)P.eslot_optr.size() - 1);
-        if (mf) P.nch_mf++;
-        p = q;
     }
+    PLAN_T("boundaries");
+    // per chunk, in parallel over ranges of chunks (each thread's output is
+    // contiguous in chunk order, so the ranges concatenate to the sequential
+    // plan): pass 1 the chunk's slots (co-visible blocks, by first touch) and
+    // e-slots (cameras) with their term / observation counts; pass 2 the
+    // per-term lists (term chunks only: the MFMA records are dense) and the
+    // per-camera observation lists, grouped by slot / e-slot in that order
+    const int nchk = (int)cbeg.size();
+    struct chunk_out {
+        std::vector<int> blk, tcnt, cam, ecnt, ns, nes;
+        std::vector<unsigned short> term, eobs;
+    };
+    std::vector<long long> cwork(nchk + 1, 0);   // per chunk: its terms and observations
+    for (int c = 0; c < nchk; c++) {
+        long long w = lptr[cend[c]] - lptr[cbeg[c]];
+        for (int i = cbeg[c]; i < cend[c]; i++) w += pt_terms(i);
+        cwork[c + 1] = cwork[c] + w;
+    }
+    const int nthr = plan_threads(cwork[nchk], 20000);
+    std::vector<chunk_out> co(nthr);
+    parallel_ranges(nchk, nthr, [&](int t, int c0, int c1) {
+        chunk_out &o = co[t];
+        std::vector<int> slot_of(nb, -1), eslot_of(m, -1), tpos, epos;
+        for (int c = c0; c < c1; c++) {
+            const int p = cbeg[c], q = cend[c], obase = lptr[p];
+            const bool mf = cmf[c] != 0;
+            const size_t s0 = o.blk.size(), e0 = o.cam.size();
+            for (int i = p; i < q; i++)
+                for (int a = lptr[i]; a < lptr[i + 1]; a++) {
+                    const int j = lcam[a];
+                    if (eslot_of[j] < 0) {
+                        eslot_of[j] = (int)(o.cam.size() - e0);
+                        o.cam.push_back(j);
+                        o.ecnt.push_back(0);
+                    }
+                    o.ecnt[e0 + eslot_of[j]]++;
+                    for (int b = lptr[i]; b < lptr[i + 1]; b++) {
+                        const int k = lcam[b];
+                        if (j < k) continue;
+                        const int blk = hb.find(j, k);
+                        if (slot_of[blk] < 0) {
+                            slot_of[blk] = (int)(o.blk.size() - s0);
+                            o.blk.push_back(blk);
+                            o.tcnt.push_back(0);
+                        }
+                        o.tcnt[s0 + slot_of[blk]]++;
+                    }
+                }
+            const int ns = (int)(o.blk.size() - s0), nes = (int)(o.cam.size() - e0);
+            o.ns.push_back(ns);
+            o.nes.push_back(nes);
+            tpos.assign(ns + 1, 0);
+            epos.assign(nes + 1, 0);
+            for (int sl = 0; sl < ns; sl++) {
+                if (mf) o.tcnt[s0 + sl] = 0;   // the MFMA records are dense: no term lists
+                tpos[sl + 1] = tpos[sl] + o.tcnt[s0 + sl];
+            }
+            for (int e = 0; e < nes; e++) epos[e + 1] = epos[e] + o.ecnt[e0 + e];
+            const size_t tb = o.term.size() / 2, ub = o.eobs.size();
+            o.term.resize(2 * (tb + tpos[ns]));
+            o.eobs.resize(ub + epos[nes]);
+            for (int i = p; i < q; i++)
+                for (int a = lptr[i]; a < lptr[i + 1]; a++) {
+                    const int j = lcam[a];
+                    o.eobs[ub + epos[eslot_of[j]]++] = (unsigned short)(a - obase);
+                    if (mf) continue;
+                    for (int b = lptr[i]; b < lptr[i + 1]; b++) {
+                        const int k = lcam[b];
+                        if (j < k) continue;
+                        const size_t at = tb + tpos[slot_of[hb.find(j, k)]]++;
+                        o.term[2 * at] = (unsigned short)(a - obase);
+                        o.term[2 * at + 1] = (unsigned short)(b - obase);
+                    }
+                }
+            for (size_t sl = s0; sl < o.blk.size(); sl++) slot_of[o.blk[sl]] = -1;
+            for (size_t e = e0; e < o.cam.size(); e++) eslot_of[o.cam[e]] = -1;
+        }
+    }, &cwork);
+    PLAN_T("chunks");
+    // concatenate in chunk order
+    P.max_slots = 0;
+    P.ch_pt.assign(1, 0);
+    P.ch_slot.assign(1, 0);
+    P.ch_eslot.assign(1, 0);
+    P.slot_tptr.assign(1, 0);
+    P.eslot_optr.assign(1, 0);
+    {
+        size_t ns_all = 0, nes_all = 0, nt_all = 0, nu_all = 0;
+        for (const chunk_out &o : co) {
+            ns_all += o.blk.size();
+            nes_all += o.cam.size();
+            nt_all += o.term.size();
+            nu_all += o.eobs.size();
+        }
+        P.slot_blk.reserve(ns_all);
+        P.slot_tptr.reserve(ns_all + 1);
+        P.cam_eslots.reserve(nes_all);
+        P.eslot_optr.reserve(nes_all + 1);
+        P.slot_term.reserve(nt_all);
+        P.eslot_obs.reserve(nu_all);
+    }
+    int c = 0;
+    for (const chunk_out &o : co) {
+        P.slot_blk.insert(P.slot_blk.end(), o.blk.begin(), o.blk.end());
+        for (int v : o.tcnt) P.slot_tptr.push_back(P.slot_tptr.back() + v);
+        P.cam_eslots.insert(P.cam_eslots.end(), o.cam.begin(), o.cam.end());
+        for (int v : o.ecnt) P.eslot_optr.push_back(P.eslot_optr.back() + v);
+        P.slot_term.insert(P.slot_term.end(), o.term.begin(), o.term.end());
+        P.eslot_obs.insert(P.eslot_obs.end(), o.eobs.begin(), o.eobs.end());
+        for (size_t u = 0; u < o.ns.size(); u++, c++) {
+            P.max_slots = std::max(P.max_slots, o.ns[u]);
+            P.ch_pt.push_back(cend[c]);
+            P.ch_slot.push_back(P.ch_slot.back() + o.ns[u]);
+            P.ch_eslot.push_back(P.ch_eslot.back() + o.nes[u]);
+            if (cmf[c]) P.nch_mf++;
+        }
+    }
+    co.clear();
+    PLAN_T("concat");
     // long tracks: segment chunks (one point each, <= BA_CH_OBS observations;
     // every observation its own camera slot: a point sees a camera once)
     P.nch_reg = (int)P.ch_pt.size() - 1;
@@ -522,6 +706,7 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
         std::vector<int> pos(P.cam_eptr.begin(), P.cam_eptr.end() - 1);
         for (int s = 0; s < nes; s++) P.cam_eslots[pos[ecam[s]]++] = s;
     }
+    PLAN_T("blk lists");
     // Schur groups (greedy): at most gs_cap distinct blocks (LDS accumulators),
     // BA_GE_CAP cameras and gmax chunks (>= ~2048 groups keep the chip busy).
     // A chunk with more than gs_cap blocks forms a group of its own whose
@@ -591,18 +776,34 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
         P.grp_ge.push_back((int)P.gecam.size());
         c = d;
     }
+    PLAN_T("groups");
     // long tracks' Schur terms: one group slot per (a, b), a >= b (cameras
     // ascending, so block (cam a, cam b) is a lower block), slot a(a+1)/2 + b
     // of the point; one group e-slot per observation.  After the regular
     // slots: k_schur_reduce subtracts them last.
-    for (size_t l = 0; l < P.long_pt.size(); l++) {
+    const int nlong = (int)P.long_pt.size();
+    std::vector<long long> lwork(nlong + 1, 0);
+    for (int l = 0; l < nlong; l++) {
         const int o0 = P.long_o0[l], k = P.long_o0[l + 1] - o0;
-        P.long_sbase.push_back((int)P.gslot_blk.size());
-        P.long_ebase.push_back((int)P.gecam.size());
-        for (int a = 0; a < k; a++) {
-            P.gecam.push_back(lcam[o0 + a]);
-            for (int b = 0; b <= a; b++) P.gslot_blk.push_back(hb.find(lcam[o0 + a], lcam[o0 + b]));
+        P.long_sbase.push_back((int)(P.gslot_blk.size() + lwork[l]));
+        P.long_ebase.push_back((int)P.gecam.size() + (o0 - P.long_o0[0]));
+        lwork[l + 1] = lwork[l] + (long long)k * (k + 1) / 2;
+    }
+    const size_t gs_long = P.gslot_blk.size(), ge_long = P.gecam.size();
+    P.gslot_blk.resize(gs_long + lwork[nlong]);
+    P.gecam.resize(ge_long + (nlong ? P.long_o0[nlong] - P.long_o0[0] : 0));
+    parallel_ranges(nlong, plan_threads(lwork[nlong], 50000), [&](int, int l0, int l1) {
+        for (int l = l0; l < l1; l++) {
+            const int o0 = P.long_o0[l], k = P.long_o0[l + 1] - o0;
+            int *gs = &P.gslot_blk[P.long_sbase[l]];
+            for (int a = 0; a < k; a++) {
+                P.gecam[P.long_ebase[l] + a] = lcam[o0 + a];
+                for (int b = 0; b <= a; b++) *gs++ = hb.find(lcam[o0 + a], lcam[o0 + b]);
+            }
         }
+    }, &lwork);
+    for (int l = 0; l < nlong; l++) {
+        const int k = P.long_o0[l + 1] - P.long_o0[l];
         const int nt = (k + BA_LONG_TILE - 1) / BA_LONG_TILE;
         for (int ta = 0; ta < nt; ta++)
             for (int tb = 0; tb <= ta; tb++) {
@@ -611,8 +812,10 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
                 P.long_tiles.push_back(tb);
             }
     }
+    PLAN_T("long groups");
     bucket(P.gslot_blk, nb, P.blk_gptr, P.blk_gslots);
     bucket(P.gecam, m, P.cam_gptr, P.cam_gslots);
+    PLAN_T("buckets");
     P.ch_blob.assign(1, 0);
     P.ch_obase.assign(1, lptr[0]);
     if (P.nch_mf > 0) {
@@ -696,31 +899,49 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
             P.mf_max_blob = std::max(P.mf_max_blob,
                                      P.ch_blob[P.grp_ch[g + 1]] - P.ch_blob[P.grp_ch[g]]);
     }
-    for (int c = P.nch_mf; c < nch; c++) {
-        const int p0 = P.ch_pt[c], p1 = P.ch_pt[c + 1];
-        const int nobs = lptr[p1] - lptr[p0];
-        const int s0 = P.ch_slot[c], s1 = P.ch_slot[c + 1];
-        const int e0 = P.ch_eslot[c], e1 = P.ch_eslot[c + 1];
-        const int t0 = P.slot_tptr[s0], t1 = P.slot_tptr[s1];
-        const int u0 = P.eslot_optr[e0], u1 = P.eslot_optr[e1];
-        std::vector<unsigned> &B = P.blob;
-        B.push_back((unsigned)(p1 - p0) | ((unsigned)nobs << 16));
-        B.push_back((unsigned)(s1 - s0) | ((unsigned)(e1 - e0) << 16));
-        B.push_back((unsigned)(t1 - t0));
-        B.push_back((unsigned)(u1 - u0));
-        for (int s = s0; s <= s1; s++) B.push_back((unsigned)(P.slot_tptr[s] - t0));
-        for (int e = e0; e <= e1; e++) B.push_back((unsigned)(P.eslot_optr[e] - u0));
-        for (int s = s0; s < s1; s++) B.push_back(P.cs_g[s]);
-        for (int e = e0; e < e1; e++) B.push_back(P.ce_g[e]);
-        for (int i = p0; i < p1; i++)
-            for (int o = lptr[i]; o < lptr[i + 1]; o++) B.push_back((unsigned)(i - p0));
-        for (int t = t0; t < t1; t++)
-            B.push_back((unsigned)P.slot_term[2 * t] | ((unsigned)P.slot_term[2 * t + 1] << 16));
-        for (int u = u0; u < u1; u++) B.push_back(P.eslot_obs[u]);
-        P.ch_blob.push_back((int)B.size());
-        P.ch_obase.push_back(lptr[p1]);
-        P.max_blob = std::max(P.max_blob, P.ch_blob[c + 1] - P.ch_blob[c]);
+    {   // term-chunk records: sizes first, then filled in parallel at their offsets
+        const int nt = nch - P.nch_mf;
+        std::vector<long long> boff(nt + 1, 0);
+        for (int c = P.nch_mf; c < nch; c++) {
+            const int s0 = P.ch_slot[c], s1 = P.ch_slot[c + 1];
+            const int e0 = P.ch_eslot[c], e1 = P.ch_eslot[c + 1];
+            const long long sz = 4 + (s1 - s0 + 1) + (e1 - e0 + 1) + (s1 - s0) + (e1 - e0) +
+                                 (lptr[P.ch_pt[c + 1]] - lptr[P.ch_pt[c]]) +
+                                 (P.slot_tptr[s1] - P.slot_tptr[s0]) +
+                                 (P.eslot_optr[e1] - P.eslot_optr[e0]);
+            boff[c - P.nch_mf + 1] = boff[c - P.nch_mf] + sz;
+            P.ch_blob.push_back(P.ch_blob.back() + (int)sz);
+            P.ch_obase.push_back(lptr[P.ch_pt[c + 1]]);
+            P.max_blob = std::max(P.max_blob, (int)sz);
+        }
+        const size_t bbase = P.blob.size();
+        P.blob.resize(bbase + boff[nt]);
+        parallel_ranges(nt, plan_threads(boff[nt], 100000), [&](int, int c0, int c1) {
+            for (int c = P.nch_mf + c0; c < P.nch_mf + c1; c++) {
+                const int p0 = P.ch_pt[c], p1 = P.ch_pt[c + 1];
+                const int nobs = lptr[p1] - lptr[p0];
+                const int s0 = P.ch_slot[c], s1 = P.ch_slot[c + 1];
+                const int e0 = P.ch_eslot[c], e1 = P.ch_eslot[c + 1];
+                const int t0 = P.slot_tptr[s0], t1 = P.slot_tptr[s1];
+                const int u0 = P.eslot_optr[e0], u1 = P.eslot_optr[e1];
+                unsigned *B = &P.blob[bbase + boff[c - P.nch_mf]];
+                *B++ = (unsigned)(p1 - p0) | ((unsigned)nobs << 16);
+                *B++ = (unsigned)(s1 - s0) | ((unsigned)(e1 - e0) << 16);
+                *B++ = (unsigned)(t1 - t0);
+                *B++ = (unsigned)(u1 - u0);
+                for (int s = s0; s <= s1; s++) *B++ = (unsigned)(P.slot_tptr[s] - t0);
+                for (int e = e0; e <= e1; e++) *B++ = (unsigned)(P.eslot_optr[e] - u0);
+                for (int s = s0; s < s1; s++) *B++ = P.cs_g[s];
+                for (int e = e0; e < e1; e++) *B++ = P.ce_g[e];
+                for (int i = p0; i < p1; i++)
+                    for (int o = lptr[i]; o < lptr[i + 1]; o++) *B++ = (unsigned)(i - p0);
+                for (int t = t0; t < t1; t++)
+                    *B++ = (unsigned)P.slot_term[2 * t] | ((unsigned)P.slot_term[2 * t + 1] << 16);
+                for (int u = u0; u < u1; u++) *B++ = P.eslot_obs[u];
+            }
+        }, &boff);
     }
+    PLAN_T("blobs");
     for (size_t l = 0; l < P.long_pt.size(); l++)   // segment chunks: no Schur record
         for (int o = P.long_o0[l]; o < P.long_o0[l + 1]; o += BA_CH_OBS) {
             P.ch_blob.push_back(P.ch_blob.back());
@@ -980,6 +1201,50 @@ static void order_points_by_kind(int cmax, host_obs &h, std::vector<int> &pt_ptr
     }
 }
 
+// The host side of a context's plan (ctx_setup; tools/bench_plan.cpp times it
+// on the CPU): the co-visible block set and, on the fast path, the chunk /
+// group plan.  fast is cleared when some track fits no chunk kind (the
+// ordered kernels take the problem; hb then carries their term lists).
+static void plan_host(int m, int na, int n, const std::vector<int> &lptr,
+                      const std::vector<int> &lcam, const std::vector<int> &pt_ptr_all,
+                      const std::vector<int> &cam_all, int p0, int p1, long long o0,
+                      bool lower_blocks, bool all_diag, bool no_mfma, bool &fast, int &p_long,
+                      host_blocks &hb, host_plan &plan)
+{
+    // long tracks (more than a chunk holds) must form the tail [p_long, n) of
+    // the local points (order_points_by_kind) and stay within the caps; else
+    // the sequential kernels take the problem
+    p_long = n;
+    if (fast) {
+        while (p_long > 0 && track_kind(lptr[p_long] - lptr[p_long - 1], BA_MF_CMAX(na)) == 2)
+            p_long--;
+        long long lterms = 0;
+        for (int i = 0; fast && i < n; i++) {
+            const long long k = lptr[i + 1] - lptr[i];
+            const bool lng = track_kind(k, BA_MF_CMAX(na)) == 2;
+            if (lng != (i >= p_long) || k > BA_LONG_OBS) fast = false;
+            if (lng) lterms += k * (k + 1) / 2;
+        }
+        if (lterms > BA_LONG_TERMS) fast = false;
+    }
+    build_blocks(m, pt_ptr_all, cam_all, p0, p1, o0, lower_blocks, all_diag, !fast, hb);
+    ST_MARK("blocks");
+    // MFMA Schur chunks for the leading points whose tracks fit the dense slab
+    // (ctx_create orders the short-track points first), per-term chunks for
+    // the rest; the ordered kernels if some track fits neither
+    if (fast) {
+        int p_split = 0;
+        if (!no_mfma)
+            while (p_split < p_long && lptr[p_split + 1] - lptr[p_split] <= BA_MF_CMAX(na))
+                p_split++;
+        if (!build_plan(m, na, lptr, lcam, hb, plan, BA_MF_CMAX(na), p_split, p_long)) {
+            fast = false;
+            hb = host_blocks();
+            build_blocks(m, pt_ptr_all, cam_all, p0, p1, o0, lower_blocks, all_diag, true, hb);
+        }
+    }
+}
+
 // Device buffers + host-side structure for the observations of points [p0, p1).
 static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
                      const std::vector<int> &pt_ptr_all, bool lower_blocks, bool all_diag,
@@ -1017,45 +1282,13 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         for (int o = 0; o < d.N; o++) cobs[pos[lcam[o]]++] = o;
     }
     bool fast = !d.ordered && !stage_mode;
-    // long tracks (more than a chunk holds) must form the tail [p_long, n) of
-    // the local points (order_points_by_kind) and stay within the caps; else
-    // the sequential kernels take the problem
     int p_long = d.n;
-    if (fast) {
-        while (p_long > 0 && track_kind(lptr[p_long] - lptr[p_long - 1], BA_MF_CMAX(na)) == 2)
-            p_long--;
-        long long lterms = 0;
-        for (int i = 0; fast && i < d.n; i++) {
-            const long long k = lptr[i + 1] - lptr[i];
-            const bool lng = track_kind(k, BA_MF_CMAX(na)) == 2;
-            if (lng != (i >= p_long) || k > BA_LONG_OBS) fast = false;
-            if (lng) lterms += k * (k + 1) / 2;
-        }
-        if (lterms > BA_LONG_TERMS) fast = false;
-    }
     host_blocks hb;
     host_plan plan;
     ST_MARK("lists");
-    build_blocks(p->m, pt_ptr_all, h.cam, c->p0, c->p1, o0, lower_blocks, all_diag, !fast, hb);
-    ST_MARK("blocks");
-    // MFMA Schur chunks for the leading points whose tracks fit the dense slab
-    // (ctx_create orders the short-track points first), per-term chunks for
-    // the rest; the ordered kernels if some track fits neither
-    d.mfma = 0;
-    if (fast) {
-        int p_split = 0;
-        if (!d.no_mfma)
-            while (p_split < p_long && lptr[p_split + 1] - lptr[p_split] <= BA_MF_CMAX(na))
-                p_split++;
-        if (build_plan(p->m, na, lptr, lcam, hb, plan, BA_MF_CMAX(na), p_split, p_long)) {
-            d.mfma = plan.nch_mf > 0;
-        } else {
-            fast = false;
-            hb = host_blocks();
-            build_blocks(p->m, pt_ptr_all, h.cam, c->p0, c->p1, o0, lower_blocks, all_diag, true,
-                         hb);
-        }
-    }
+    plan_host(p->m, na, d.n, lptr, lcam, pt_ptr_all, h.cam, c->p0, c->p1, o0, lower_blocks,
+              all_diag, d.no_mfma != 0, fast, p_long, hb, plan);
+    d.mfma = fast && plan.nch_mf > 0;
     if (!fast) d.ordered = 1;
     ST_MARK("plan");
     d.nb = (int)hb.jk.size() / 2;
