@@ -31,15 +31,16 @@ from .evaluation import align_scene, vl_irodr, vl_rodr
 __all__ = ["incremental_bundle"]
 
 
-def _subset_obs(sc, cams, pts):
-    """Observations of points ``pts`` in cameras ``cams`` re-indexed to the
-    subset (point-major), as x(:, X3d_index, status) / vis(X3d_index, status)
-    select them (incr_reconstruction.m:254-258)."""
+def _subset_obs(sc, cams, pts, cam_on, pt_on):
+    """Observations of points ``pts`` in cameras ``cams`` (``cam_on`` /
+    ``pt_on``: the same sets as masks) re-indexed to the subset (point-major),
+    as x(:, X3d_index, status) / vis(X3d_index, status) select them
+    (incr_reconstruction.m:254-258)."""
+    keep = cam_on[sc.obs_cam] & pt_on[sc.obs_pt]        # one-byte gathers over all obs
     cmap = np.full(sc.m, -1)
     cmap[cams] = np.arange(len(cams))
     pmap = np.full(sc.n, -1)
     pmap[pts] = np.arange(len(pts))
-    keep = (cmap[sc.obs_cam] >= 0) & (pmap[sc.obs_pt] >= 0)
     return pmap[sc.obs_pt[keep]], cmap[sc.obs_cam[keep]], sc.obs_x[keep]
 
 
@@ -71,8 +72,7 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
     X = np.zeros((4, n))
     status = np.zeros(m, dtype=bool)
     status[list(init_cams)] = True
-    nvis = np.zeros(n, dtype=int)
-    np.add.at(nvis, sc.obs_pt, status[sc.obs_cam])
+    nvis = np.bincount(sc.obs_pt, weights=status[sc.obs_cam], minlength=n).astype(int)
     tri = nvis >= 2                                      # two-view triangulation
     X[:3, tri] = sc.X0[:3, tri]
     X[3, tri] = 1.0
@@ -84,7 +84,7 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
         pts = np.nonzero(X[3] == 1)[0]                   # X3d_index (:252)
         if len(pts) == 0 or len(cams) < 2:
             return
-        pt, cam, ox = _subset_obs(sc, cams, pts)
+        pt, cam, ox = _subset_obs(sc, cams, pts, status, X[3] == 1)
         t0 = time.perf_counter()
         world = 1
         if devices:
@@ -143,8 +143,7 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
         T[:, j] = s_ * sc.T0[:, j] - Rc @ t_
         resect(j)                                        # :230, estimate_camera.m:247-253
         ba("before-triangulation", j)                    # :250-267
-        nvis[:] = 0
-        np.add.at(nvis, sc.obs_pt, status[sc.obs_cam])
+        nvis = np.bincount(sc.obs_pt, weights=status[sc.obs_cam], minlength=n).astype(int)
         new = (X[3] == 0) & (nvis >= 2)                  # :281-296 triangulation stand-in
         s_, R_, t_ = _similarity(sc, X)
         X[:3, new] = s_ * R_ @ sc.X0[:3, new] + t_[:, None]
