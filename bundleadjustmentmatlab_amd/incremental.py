@@ -31,11 +31,17 @@ from .evaluation import align_scene, vl_irodr, vl_rodr
 __all__ = ["incremental_bundle"]
 
 
-def _subset_obs(sc, cams, pts, cam_on, pt_on):
+def _subset_obs(sc, cams, pts, cam_on=None, pt_on=None):
     """Observations of points ``pts`` in cameras ``cams`` (``cam_on`` /
-    ``pt_on``: the same sets as masks) re-indexed to the subset (point-major),
-    as x(:, X3d_index, status) / vis(X3d_index, status) select them
-    (incr_reconstruction.m:254-258)."""
+    ``pt_on``: the same sets as masks, if the caller has them) re-indexed to
+    the subset (point-major), as x(:, X3d_index, status) / vis(X3d_index,
+    status) select them (incr_reconstruction.m:254-258)."""
+    if cam_on is None:
+        cam_on = np.zeros(sc.m, dtype=bool)
+        cam_on[cams] = True
+    if pt_on is None:
+        pt_on = np.zeros(sc.n, dtype=bool)
+        pt_on[pts] = True
     keep = cam_on[sc.obs_cam] & pt_on[sc.obs_pt]        # one-byte gathers over all obs
     cmap = np.full(sc.m, -1)
     cmap[cams] = np.arange(len(cams))
