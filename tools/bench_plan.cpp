@@ -102,6 +102,20 @@ int main(int argc, char **argv)
                                        P.nseg, P.max_blob, P.mf_max_blob, (int)P.n_terms,
                                        fast ? 1 : 0, p_long};
         H.add(scal);
+        {   // MFMA chunk records: camera count and flush flag (ba_solver.cpp build_plan)
+            int flush = 0, dense = 0;
+            long long csum = 0;
+            for (int c = 0; c < P.nch_mf; c++) {
+                const unsigned h1 = P.blob[P.ch_blob[c] + 1];
+                csum += h1 & 0xffu;
+                flush += (h1 >> 9) & 1u;
+                dense += (h1 >> 8) & 1u;
+            }
+            if (P.nch_mf)
+                std::printf("  MFMA chunks %d: %.2f cameras each, %d flush (%.1f %%), %d dense\n",
+                            P.nch_mf, csum / (double)P.nch_mf, flush, 100.0 * flush / P.nch_mf,
+                            dense);
+        }
         std::printf("m=%d n=%d N=%d: sort %.2f ms, order %.2f ms, plan_host %.2f ms "
                     "(blocks %d, chunks %zu, groups %zu, blob %zu, fast %d)  hash %016llx\n",
                     m, n, N, t_sort, t_order, t_plan, (int)hb.jk.size() / 2, P.ch_pt.size() - 1,
