@@ -42,8 +42,10 @@ def log(*a):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default 20; 5 for the growing replay cfg5, 1 for cfg5x)")
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed steps first (default 3; 2 for cfg5, 0 for cfg5x)")
     ap.add_argument("--config", default="cfg3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-scene", action="store_true",
@@ -59,6 +61,10 @@ def main():
     ap.add_argument("--spawn-selftest", action="store_true",
                     help="launch only: every rank joins the gloo group and reports (no GPU)")
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = {"cfg5": 5, "cfg5x": 1}.get(args.config, 20)
+    if args.warmup is None:
+        args.warmup = {"cfg5": 2, "cfg5x": 0}.get(args.config, 3)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # not under torch.distributed.run: start one process per GPU ourselves,
         # before this process touches the GPU
