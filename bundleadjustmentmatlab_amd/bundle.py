@@ -192,7 +192,9 @@ class BundleAdjuster:
     observations; K is 4 x m; num_a is 6 (fix_calibration), 7 (fix_principal)
     or 10 (variable K).  Options follow bundle_euclid.m's names.  ``solver``
     picks the reduced-camera solve: "auto" (cyclic reduction when S is
-    tile-tridiagonal, else envelope Cholesky), "envelope" or "dense";
+    tile-tridiagonal, else envelope Cholesky -- on a nested-dissection camera
+    order when that shortens its chain of steps), "envelope", "nd" (the
+    nested-dissection order whenever the cameras split) or "dense";
     ``dense_solve=True`` is the same as solver="dense".  ``schur_kernel``
     picks the fast-path Schur complement kernel: "auto" (dense per-chunk
     products on fp64 MFMA when the tracks fit) or "terms" (per-term sums).
@@ -207,7 +209,7 @@ class BundleAdjuster:
     ``model="projective"`` solves bundle_projective.m instead: num_a = 12
     (a = P(:) per camera), K is None and ``m`` gives the camera count.
     """
-    SOLVERS = {"auto": 0, "dense": 1, "envelope": 2, "sequential": 3}
+    SOLVERS = {"auto": 0, "dense": 1, "envelope": 2, "sequential": 3, "nd": 4}
     SCHUR_KERNELS = {"auto": 0, "terms": 1}
     SEMANTICS = {"mex": 0, "nomex": 1}
     MODELS = {"euclidean": MODEL_EUCLIDEAN, "projective": MODEL_PROJECTIVE}
@@ -395,7 +397,8 @@ class BundleAdjuster:
     PLAN_KEYS = ("obs", "points", "cameras", "num_a", "chunks", "chunk_slots",
                  "chunk_eslots", "groups", "group_slots", "group_eslots", "blocks",
                  "tiles", "cr_levels", "cr_elim", "cr_keep", "ordered", "schur_terms",
-                 "blob_words", "mfma", "cr_rows", "mfma_groups", "reordered", "long_points")
+                 "blob_words", "mfma", "cr_rows", "mfma_groups", "reordered", "long_points",
+                 "nd_arcs", "nd_sep_tiles")
 
     def plan_info(self):
         """Execution-plan sizes of this rank (vlgba_plan_info)."""

@@ -25,6 +25,10 @@
 // then per k descending k_backward: x_k = L_kk^-T z_k, z_j -= L_kj^T x_k.
 #include "ba_internal.h"
 
+#include <algorithm>
+#include <cstdio>
+#include <utility>
+#include <climits>
 #include <cstdlib>
 #include <vector>
 
@@ -459,19 +463,23 @@ __device__ __forceinline__ bool block_potrf_inv(double *As, double *Li, bool zer
 // pan / prev: the envelope rows below k / below k-1 (ascending), T / Tp their
 // counts (Tp = 0 for k = 0).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_factor_step(double *__restrict__ S, long long lds, int k,
-                                                     const int *__restrict__ pan, int T,
-                                                     const int *__restrict__ prev, int Tp,
-                                                     double *__restrict__ linv,
-                                                     double *__restrict__ rhs,
-                                                     double *__restrict__ y,
-                                                     double *__restrict__ status)
+// sep0: the nested dissection's first separator row tile (INT_MAX: none):
+// an arc column leaves the separator's rhs to k_sep_update (two arcs'
+// columns run in the same launch) and its separator x separator trailing
+// pairs, which the host does not launch (they end each pair enumeration).
+__device__ __forceinline__ void factor_step_body(double *__restrict__ S, long long lds, int k,
+                                                 const int *__restrict__ pan, int T,
+                                                 const int *__restrict__ prev, int Tp,
+                                                 double *__restrict__ linv,
+                                                 double *__restrict__ rhs,
+                                                 double *__restrict__ y,
+                                                 double *__restrict__ status, int b, int sep0)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double *As = sm, *Bs = sm + NB * LP, *Cs = sm + 2 * NB * LP;
     __shared__ double yk[NB], rk[NB];
     __shared__ double part[4][NB];
-    const int tid = threadIdx.x, b = blockIdx.x;
+    const int tid = threadIdx.x;
     const bool kin = Tp > 0 && prev[0] == k;   // column k-1 reaches row k
     d4 acc[2][2];
     if (b > T) {
@@ -545,7 +553,137 @@ __global__ __launch_bounds__(256) void k_factor_step(double *__restrict__ S, lon
     store_tile(S, lds, i, k, Cs);
     double ri[1];
     gemv64(Cs, yk, part, nullptr, 1.0, ri);   // (L_ik y_k)[tid] for tid < 64
-    if (tid < NB) rhs[(long long)NB * i + tid] -= ri[0];
+    if (tid < NB && i < sep0) rhs[(long long)NB * i + tid] -= ri[0];
+}
+
+__global__ __launch_bounds__(256) void k_factor_step(double *__restrict__ S, long long lds, int k,
+                                                     const int *__restrict__ pan, int T,
+                                                     const int *__restrict__ prev, int Tp,
+                                                     double *__restrict__ linv,
+                                                     double *__restrict__ rhs,
+                                                     double *__restrict__ y,
+                                                     double *__restrict__ status)
+{
+    factor_step_body(S, lds, k, pan, T, prev, Tp, linv, rhs, y, status, blockIdx.x, INT_MAX);
+}
+
+// one step of every arc of the nested dissection: column k[t] of arc t takes
+// workgroups [b0[t], b0[t+1]) (k_factor_step's roles), pan / prev as offsets
+// into the panel list
+struct nd_step {
+    int np;
+    int k[BA_ND_MAX], T[BA_ND_MAX], Tp[BA_ND_MAX], pofs[BA_ND_MAX], qofs[BA_ND_MAX];
+    int b0[BA_ND_MAX + 1];
+};
+
+__global__ __launch_bounds__(256) void k_factor_multi(double *__restrict__ S, long long lds,
+                                                      const int *__restrict__ pan_list,
+                                                      nd_step P, int sep0,
+                                                      double *__restrict__ linv,
+                                                      double *__restrict__ rhs,
+                                                      double *__restrict__ y,
+                                                      double *__restrict__ status)
+{
+    const int b = blockIdx.x;
+    int t = 0;
+    while (t + 1 < P.np && b >= P.b0[t + 1]) t++;
+    factor_step_body(S, lds, P.k[t], pan_list + P.pofs[t], P.T[t], pan_list + P.qofs[t], P.Tp[t],
+                     linv, rhs, y, status, b - P.b0[t], sep0);
+}
+
+// ---------------------------------------------------------------------------
+// The arcs' contribution to the separator block (nested dissection): record
+// (pair (i, j), arc columns klist[kofs .. kofs+kcnt)) forms
+//     P = sum_k L_ik L_jk^T        (and for i == j:  g = sum_k L_ik y_k)
+// over its columns in ascending order (one MFMA accumulator chain), stored
+// column-major in part[rec][64*64] (+ 64).  Chunks of the arc columns keep
+// every record short enough to fill the chip in one wave.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_sep_update(const double *__restrict__ S, long long lds,
+                                                    const int *__restrict__ pair,
+                                                    const int *__restrict__ rec,
+                                                    const int *__restrict__ klist,
+                                                    const double *__restrict__ y,
+                                                    double *__restrict__ part)
+{
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double *As = sm, *Bs = sm + NB * LP;
+    __shared__ double ys[NB];
+    const int tid = threadIdx.x, r = tid & 63, cq = tid >> 6;
+    const int pr = rec[3 * blockIdx.x], kofs = rec[3 * blockIdx.x + 1], kcnt = rec[3 * blockIdx.x + 2];
+    const int i = pair[2 * pr], j = pair[2 * pr + 1];
+    d4 acc[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int z = 0; z < 2; z++) acc[x][z] = d4{0.0, 0.0, 0.0, 0.0};
+    double g = 0.0;   // thread (r, cq): sum over its quarter of the columns
+    for (int q = 0; q < kcnt; q++) {
+        const int k = klist[kofs + q];
+        __syncthreads();   // previous tiles consumed
+        load_tile(S, lds, i, k, As);
+        if (i != j) load_tile(S, lds, j, k, Bs);
+        if (i == j && tid < NB) ys[tid] = y[(long long)NB * k + tid];
+        __syncthreads();
+        mfma_64x64_acc(As, i == j ? As : Bs, acc);
+        if (i == j) {
+            double s = 0.0;
+#pragma unroll
+            for (int c = 16 * cq; c < 16 * cq + 16; c++) s += As[r * LP + c] * ys[c];
+            g += s;
+        }
+    }
+    __syncthreads();
+    acc_to_lds(acc, As, 1.0, false);
+    __syncthreads();
+    double *out = part + (size_t)blockIdx.x * (NB * NB + NB);
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+        const int c = cq + 4 * u;
+        out[c * NB + r] = As[r * LP + c];
+    }
+    if (i == j) {
+        __shared__ double gp[4][NB];
+        gp[cq][r] = g;
+        __syncthreads();
+        if (tid < NB) out[NB * NB + tid] = ((gp[0][tid] + gp[1][tid]) + gp[2][tid]) + gp[3][tid];
+    }
+}
+
+// A_ij -= sum of the pair's records (in record order); rhs_i -= sum of g
+__global__ __launch_bounds__(256) void k_sep_reduce(double *__restrict__ S, long long lds,
+                                                    const int *__restrict__ pair,
+                                                    const int *__restrict__ pptr,
+                                                    const double *__restrict__ part,
+                                                    double *__restrict__ rhs)
+{
+    const int p = blockIdx.x, tid = threadIdx.x, r = tid & 63, cq = tid >> 6;
+    const int i = pair[2 * p], j = pair[2 * p + 1];
+    const int e0 = pptr[p], e1 = pptr[p + 1];
+    double s[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) s[u] = 0.0;
+    double g = 0.0;
+    for (int e = e0; e < e1; e++) {
+        const double *src = part + (size_t)e * (NB * NB + NB);
+#pragma unroll
+        for (int u = 0; u < 16; u++) s[u] += src[(cq + 4 * u) * NB + r];
+        if (i == j && tid < NB) g += src[NB * NB + tid];
+    }
+    double *base = S + (long long)NB * i + lds * (long long)NB * j;
+#pragma unroll
+    for (int u = 0; u < 16; u++) base[r + lds * (cq + 4 * u)] -= s[u];
+    if (i == j && tid < NB) rhs[(long long)NB * i + tid] -= g;
+}
+
+// da (camera order, ld..lds zero) from the row-ordered solution
+__global__ void k_nd_scatter(const int *__restrict__ prow, const double *__restrict__ x,
+                             double *__restrict__ da, long long lds)
+{
+    const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= lds) return;
+    const int r = prow[c];
+    da[c] = r >= 0 ? x[r] : 0.0;
 }
 
 // ---------------------------------------------------------------------------
@@ -1648,7 +1786,8 @@ __global__ __launch_bounds__(256) void k_assemble_tiles(
     double *__restrict__ S, long long lds, const int *__restrict__ env,
     const int *__restrict__ tb_ptr, const int *__restrict__ tb_blk,
     const int *__restrict__ blk_jk, const double *__restrict__ sblk, int na, long long ld,
-    double *__restrict__ rhs, double *__restrict__ status)
+    double *__restrict__ rhs, double *__restrict__ status, const int *__restrict__ crow,
+    const int *__restrict__ rowsrc, const double *__restrict__ rhs_src)
 {
     __shared__ double T[NB * (NB + 1)];
     const int ti = env[2 * blockIdx.x], tk = env[2 * blockIdx.x + 1], tid = threadIdx.x;
@@ -1665,8 +1804,20 @@ __global__ __launch_bounds__(256) void k_assemble_tiles(
         const int u = q / na2, l = q - na2 * u;
         const int bk = tb_blk[u0 + u];
         const int r = l % na, c = l / na;
-        const long long row = (long long)na * blk_jk[2 * bk] + r;
-        const long long col = (long long)na * blk_jk[2 * bk + 1] + c;
+        const int bj = blk_jk[2 * bk], bc = blk_jk[2 * bk + 1];
+        long long row, col;
+        if (!crow) {
+            row = (long long)na * bj + r;
+            col = (long long)na * bc + c;
+        } else {   // nested-dissection rows: S_kj = S_jk^T where camera k's rows come later
+            row = crow[bj] + r;
+            col = crow[bc] + c;
+            if (row < col && bj != bc) {
+                const long long t = row;
+                row = col;
+                col = t;
+            }
+        }
         if (row < col || row < r0 || row >= r0 + NB || col < c0 || col >= c0 + NB) continue;
         T[(row - r0) * (NB + 1) + (col - c0)] = sblk[(size_t)na2 * bk + l];
     }
@@ -1674,6 +1825,10 @@ __global__ __launch_bounds__(256) void k_assemble_tiles(
     if (ti == tk && tid < NB) {   // pinv semantics for exactly-zero rows, padding rows
         double *d = T + tid * (NB + 1) + tid;
         const long long r = r0 + tid;
+        if (rowsrc) {   // gather the row-ordered rhs (nested dissection)
+            const int src = rowsrc[r];
+            rhs[r] = src >= 0 ? rhs_src[src] : 0.0;
+        }
         if (*d == 0.0) {
             *d = 1.0;
             rhs[r] = 0.0;
@@ -1848,13 +2003,84 @@ static int dev_alloc(T **p, size_t bytes)
     return *p ? 0 : -(int)hipErrorOutOfMemory;
 }
 
+// ---- nested dissection of the envelope (host planner) -------------------
+namespace {
+struct nd_cost_t {
+    int crit, ns, n[BA_ND_MAX];
+};
+
+// arcs [bnd[t], bnd[t+1]) of consecutive cameras; camera j of arc t joins the
+// separator when it is co-visible with a camera of an earlier arc (minK[j] <
+// bnd[t]).  Predicted step chain: the longest arc, the separator's columns,
+// and the two SYRK launches between them.
+nd_cost_t nd_cost(const std::vector<int> &minK, int na, const int *bnd, int K)
+{
+    nd_cost_t e{};
+    int nsep = 0, mx = 0;
+    for (int t = 0; t < K; t++) {
+        int cnt = 0;
+        for (int j = bnd[t]; j < bnd[t + 1]; j++) {
+            if (minK[j] < bnd[t])
+                nsep++;
+            else
+                cnt++;
+        }
+        e.n[t] = (na * cnt + NB - 1) / NB;
+        mx = std::max(mx, e.n[t]);
+    }
+    e.ns = (na * nsep + NB - 1) / NB;
+    e.crit = mx + e.ns + (e.ns > 0 ? 2 : 0);
+    return e;
+}
+
+// K = 2 .. BA_ND_MAX arcs: equal camera counts, then one boundary at a time
+// moved while the predicted chain shortens.  Returns the best K (0: none).
+int nd_choose(const std::vector<int> &minK, int m, int na, int *bnd_out, int &crit_out)
+{
+    int bestK = 0;
+    crit_out = INT_MAX;
+    for (int K = 2; K <= BA_ND_MAX && K <= m; K++) {
+        int bnd[BA_ND_MAX + 1];
+        for (int t = 0; t <= K; t++) bnd[t] = (int)((long long)t * m / K);
+        nd_cost_t cur = nd_cost(minK, na, bnd, K);
+        for (int sweep = 0; sweep < 4; sweep++) {
+            bool moved = false;
+            for (int t = 1; t < K; t++)
+                for (int step = std::max(1, m / (4 * K)); step >= 1; step /= 2)
+                    for (int dir = -1; dir <= 1; dir += 2)
+                        for (;;) {
+                            const int nbd = bnd[t] + dir * step;
+                            if (nbd <= bnd[t - 1] || nbd >= bnd[t + 1]) break;
+                            const int keep = bnd[t];
+                            bnd[t] = nbd;
+                            const nd_cost_t c = nd_cost(minK, na, bnd, K);
+                            if (c.crit < cur.crit) {
+                                cur = c;
+                                moved = true;
+                            } else {
+                                bnd[t] = keep;
+                                break;
+                            }
+                        }
+            if (!moved) break;
+        }
+        if (cur.crit < crit_out) {
+            crit_out = cur.crit;
+            bestK = K;
+            for (int t = 0; t <= K; t++) bnd_out[t] = bnd[t];
+        }
+    }
+    return bestK;
+}
+}   // namespace
+
 int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
 {
-    const int nt = (int)(d->lds / NB);
+    int nt = (int)(d->lds / NB);
     d->nt = nt;
     d->h_tfirst = new int[nt];
     // every lower tile for the measurement mode (1) and the sequential parity
-    // solve (3); the envelope otherwise (0 auto, 2 envelope without CR)
+    // solve (3); the envelope otherwise (0 auto, 2 envelope without CR, 4 ND)
     const bool all_tiles = d->dense_solve == 1 || d->dense_solve == 3;
     for (int i = 0; i < nt; i++) d->h_tfirst[i] = all_tiles ? 0 : i;
     if (!all_tiles)
@@ -1867,47 +2093,6 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
                 if (tk < d->h_tfirst[ti]) d->h_tfirst[ti] = tk;
             }
         }
-    std::vector<int> ptr(nt + 1, 0), list, env;
-    for (int k = 0; k < nt; k++) {
-        for (int i = k + 1; i < nt; i++)
-            if (d->h_tfirst[i] <= k) list.push_back(i);
-        ptr[k + 1] = (int)list.size();
-    }
-    for (int k = 0; k < nt; k++)
-        for (int i = k; i < nt; i++)
-            if (d->h_tfirst[i] <= k) {
-                env.push_back(i);
-                env.push_back(k);
-            }
-    d->n_env = (int)env.size() / 2;
-    {   // per envelope tile: the co-visible blocks (j >= k) overlapping it
-        std::vector<int> tid_of((size_t)nt * nt, -1);
-        for (int e = 0; e < d->n_env; e++) tid_of[(size_t)env[2 * e] * nt + env[2 * e + 1]] = e;
-        std::vector<std::vector<int>> lists(d->n_env);
-        for (int b = 0; b < nb; b++) {
-            const long long r0 = (long long)d->na * blk_jk[2 * b], c0 = (long long)d->na * blk_jk[2 * b + 1];
-            const int t0 = (int)(r0 / NB), t1 = (int)((r0 + d->na - 1) / NB);
-            const int u0 = (int)(c0 / NB), u1 = (int)((c0 + d->na - 1) / NB);
-            for (int t = t0; t <= t1; t++)
-                for (int u = u0; u <= u1 && u <= t; u++) {
-                    const int e = tid_of[(size_t)t * nt + u];
-                    if (e >= 0) lists[e].push_back(b);
-                }
-        }
-        std::vector<int> tptr(d->n_env + 1, 0), tblk;
-        for (int e = 0; e < d->n_env; e++) {
-            tblk.insert(tblk.end(), lists[e].begin(), lists[e].end());
-            tptr[e + 1] = (int)tblk.size();
-        }
-        TRY_RC(dev_alloc(&d->tb_ptr, sizeof(int) * tptr.size()));
-        TRY_RC(dev_alloc(&d->tb_blk, sizeof(int) * (tblk.size() + 1)));
-        VLGBA_CHECK(hipMemcpyAsync(d->tb_ptr, tptr.data(), sizeof(int) * tptr.size(),
-                                   hipMemcpyHostToDevice, d->stream));
-        if (!tblk.empty())
-            VLGBA_CHECK(hipMemcpyAsync(d->tb_blk, tblk.data(), sizeof(int) * tblk.size(),
-                                       hipMemcpyHostToDevice, d->stream));
-        VLGBA_CHECK(hipStreamSynchronize(d->stream));
-    }
     // cyclic reduction when S is tile-tridiagonal (dense_solve 0 = auto):
     // camera-aligned 32-row tiles when the co-visibility band allows them
     // (every block (j, k) within neighbouring groups of floor(32 / NA)
@@ -2025,6 +2210,190 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
             VLGBA_CHECK(hipMemcpyAsync(d->cr_keep, keep.data(), sizeof(int) * keep.size(),
                                        hipMemcpyHostToDevice, d->stream));
     }
+    // nested dissection (not for tridiagonal S, which the cyclic reduction takes)
+    d->nd_np = 0;
+    const int na = d->na, m = d->m;
+    std::vector<int> crow, tpart;   // row of camera j; part of tile (arc t, separator np)
+    if (!tridiag && (d->dense_solve == 0 || d->dense_solve == 4) && m >= 2 && nt > 1) {
+        const char *ev = std::getenv("VLGBA_ND");
+        const bool off = ev && ev[0] == '0';
+        std::vector<int> minK(m);
+        for (int j = 0; j < m; j++) minK[j] = j;
+        for (int b = 0; b < nb; b++) {
+            const int j = blk_jk[2 * b], k = blk_jk[2 * b + 1];
+            if (k < minK[j]) minK[j] = k;
+        }
+        int bnd[BA_ND_MAX + 1], crit = INT_MAX;
+        const int K = off && d->dense_solve == 0 ? 0 : nd_choose(minK, m, na, bnd, crit);
+        const bool take = K > 0 && (d->dense_solve == 4 || (nt >= 8 && 4 * crit <= 3 * nt));
+        if (ev && ev[0] == 'v')
+            std::fprintf(stderr, "[vlgba] nested dissection: natural %d tiles, %d arcs -> chain %d%s\n",
+                         nt, K, crit, take ? "" : " (not taken)");
+        if (take) {
+            crow.assign(m, -1);
+            long long row = 0;
+            for (int t = 0; t < K; t++) {
+                d->nd_a0[t] = (int)(row / NB);
+                for (int j = bnd[t]; j < bnd[t + 1]; j++)
+                    if (minK[j] >= bnd[t]) {
+                        crow[j] = (int)row;
+                        row += na;
+                    }
+                row = (row + NB - 1) / NB * NB;
+            }
+            d->nd_a0[K] = (int)(row / NB);
+            for (int t = 0; t < K; t++)
+                for (int j = bnd[t]; j < bnd[t + 1]; j++)
+                    if (minK[j] < bnd[t]) {
+                        crow[j] = (int)row;
+                        row += na;
+                    }
+            row = (row + NB - 1) / NB * NB;
+            d->nd_np = K;
+            d->slds = row;
+            nt = (int)(row / NB);
+            d->nt = nt;
+            tpart.assign(nt, K);
+            for (int t = 0; t < K; t++)
+                for (int i = d->nd_a0[t]; i < d->nd_a0[t + 1]; i++) tpart[i] = t;
+        }
+    }
+    const bool nd = d->nd_np > 0;
+    const int npart = nd ? d->nd_np + 1 : 1;
+    const int s0 = nd ? d->nd_a0[d->nd_np] : nt;
+    // first[i][P]: the first envelope tile of row i among the columns of part P
+    // (the profile is preserved inside each part: arcs never couple, and the
+    // separator block fills in, so it is taken dense)
+    std::vector<int> first;
+    if (nd) {
+        delete[] d->h_tfirst;
+        d->h_tfirst = new int[nt];
+        first.assign((size_t)nt * npart, INT_MAX);
+        for (int i = 0; i < nt; i++) first[(size_t)i * npart + tpart[i]] = i >= s0 ? s0 : i;
+        for (int b = 0; b < nb; b++) {
+            long long r0 = crow[blk_jk[2 * b]], c0 = crow[blk_jk[2 * b + 1]];
+            if (r0 < c0) std::swap(r0, c0);
+            const int tk = (int)(c0 / NB), P = tpart[tk];
+            for (long long r = r0; r < r0 + na; r++) {
+                int &f = first[(size_t)(r / NB) * npart + P];
+                if (tk < f) f = tk;
+            }
+        }
+        for (int i = 0; i < nt; i++) {
+            int f = i;
+            for (int P = 0; P < npart; P++) f = std::min(f, first[(size_t)i * npart + P]);
+            d->h_tfirst[i] = f;
+        }
+    } else {
+        first.assign(d->h_tfirst, d->h_tfirst + nt);
+    }
+    auto in_env = [&](int i, int k) { return first[(size_t)i * npart + (nd ? tpart[k] : 0)] <= k; };
+    std::vector<int> ptr(nt + 1, 0), list, env;
+    for (int k = 0; k < nt; k++) {
+        for (int i = k + 1; i < nt; i++)
+            if (in_env(i, k)) list.push_back(i);
+        ptr[k + 1] = (int)list.size();
+    }
+    for (int k = 0; k < nt; k++)
+        for (int i = k; i < nt; i++)
+            if (in_env(i, k)) {
+                env.push_back(i);
+                env.push_back(k);
+            }
+    d->n_env = (int)env.size() / 2;
+    {   // per envelope tile: the co-visible blocks (j >= k) overlapping it
+        std::vector<int> tid_of((size_t)nt * nt, -1);
+        for (int e = 0; e < d->n_env; e++) tid_of[(size_t)env[2 * e] * nt + env[2 * e + 1]] = e;
+        std::vector<std::vector<int>> lists(d->n_env);
+        for (int b = 0; b < nb; b++) {
+            long long r0 = (long long)na * blk_jk[2 * b], c0 = (long long)na * blk_jk[2 * b + 1];
+            if (nd) {
+                r0 = crow[blk_jk[2 * b]];
+                c0 = crow[blk_jk[2 * b + 1]];
+                if (r0 < c0) std::swap(r0, c0);
+            }
+            const int t0 = (int)(r0 / NB), t1 = (int)((r0 + na - 1) / NB);
+            const int u0 = (int)(c0 / NB), u1 = (int)((c0 + na - 1) / NB);
+            for (int t = t0; t <= t1; t++)
+                for (int u = u0; u <= u1 && u <= t; u++) {
+                    const int e = tid_of[(size_t)t * nt + u];
+                    if (e >= 0) lists[e].push_back(b);
+                }
+        }
+        std::vector<int> tptr(d->n_env + 1, 0), tblk;
+        for (int e = 0; e < d->n_env; e++) {
+            tblk.insert(tblk.end(), lists[e].begin(), lists[e].end());
+            tptr[e + 1] = (int)tblk.size();
+        }
+        TRY_RC(dev_alloc(&d->tb_ptr, sizeof(int) * tptr.size()));
+        TRY_RC(dev_alloc(&d->tb_blk, sizeof(int) * (tblk.size() + 1)));
+        VLGBA_CHECK(hipMemcpyAsync(d->tb_ptr, tptr.data(), sizeof(int) * tptr.size(),
+                                   hipMemcpyHostToDevice, d->stream));
+        if (!tblk.empty())
+            VLGBA_CHECK(hipMemcpyAsync(d->tb_blk, tblk.data(), sizeof(int) * tblk.size(),
+                                       hipMemcpyHostToDevice, d->stream));
+        VLGBA_CHECK(hipStreamSynchronize(d->stream));
+    }
+    // the factor's storage: S (dense, column major), the diagonal tiles'
+    // inverses, the forward-solve result (+ the 32-row CR's last tile)
+    const long long sdim = nd ? d->slds : d->lds;
+    TRY_RC(dev_alloc(&d->S, sizeof(double) * (size_t)(sdim * sdim)));
+    TRY_RC(dev_alloc(&d->linv, sizeof(double) * (size_t)(sdim / NB) * NB * NB));
+    TRY_RC(dev_alloc(&d->ywork, sizeof(double) * (size_t)(sdim + NB)));
+    if (nd) {
+        std::vector<int> rowsrc(d->slds, -1), prow(d->lds, -1);
+        for (int j = 0; j < m; j++)
+            for (int r = 0; r < na; r++) {
+                rowsrc[crow[j] + r] = na * j + r;
+                prow[(size_t)na * j + r] = crow[j] + r;
+            }
+        // separator pairs (i >= j, ascending) and their arc columns, chunked
+        std::vector<int> pairs, pptr{0}, rec, klist;
+        std::vector<std::vector<int>> kl;
+        long long work = 0;
+        for (int i = s0; i < nt; i++)
+            for (int j = s0; j <= i; j++) {
+                std::vector<int> ks;
+                for (int k = 0; k < s0; k++)
+                    if (in_env(i, k) && in_env(j, k)) ks.push_back(k);
+                if (ks.empty()) continue;
+                work += (long long)ks.size();
+                pairs.push_back(i);
+                pairs.push_back(j);
+                kl.push_back(std::move(ks));
+            }
+        const int kc = (int)std::max<long long>(2, (work + d->ncu - 1) / std::max(1, d->ncu));
+        for (size_t p = 0; p < kl.size(); p++) {
+            for (size_t q = 0; q < kl[p].size(); q += kc) {
+                rec.push_back((int)p);
+                rec.push_back((int)klist.size());
+                const int cnt = (int)std::min<size_t>(kc, kl[p].size() - q);
+                rec.push_back(cnt);
+                klist.insert(klist.end(), kl[p].begin() + q, kl[p].begin() + q + cnt);
+            }
+            pptr.push_back((int)rec.size() / 3);
+        }
+        d->nd_npair = (int)pairs.size() / 2;
+        d->nd_nrec = (int)rec.size() / 3;
+        auto up = [&](int **dst, const std::vector<int> &v) -> int {
+            TRY_RC(dev_alloc(dst, sizeof(int) * (v.size() + 1)));
+            if (!v.empty())
+                VLGBA_CHECK(hipMemcpyAsync(*dst, v.data(), sizeof(int) * v.size(),
+                                           hipMemcpyHostToDevice, d->stream));
+            return 0;
+        };
+        TRY_RC(up(&d->nd_crow, crow));
+        TRY_RC(up(&d->nd_prow, prow));
+        TRY_RC(up(&d->nd_rowsrc, rowsrc));
+        TRY_RC(up(&d->nd_pair, pairs));
+        TRY_RC(up(&d->nd_pptr, pptr));
+        TRY_RC(up(&d->nd_rec, rec));
+        TRY_RC(up(&d->nd_klist, klist));
+        TRY_RC(dev_alloc(&d->nd_rhs, sizeof(double) * (size_t)d->slds));
+        TRY_RC(dev_alloc(&d->nd_x, sizeof(double) * (size_t)d->slds));
+        TRY_RC(dev_alloc(&d->nd_part, sizeof(double) * ((size_t)d->nd_nrec + 1) * (NB * NB + NB)));
+        VLGBA_CHECK(hipStreamSynchronize(d->stream));
+    }
     d->pan_ptr_h = new int[nt + 1];
     for (int k = 0; k <= nt; k++) d->pan_ptr_h[k] = ptr[k];
     d->h_pan_list = new int[list.size() + 1];
@@ -2045,13 +2414,22 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
                                    hipMemcpyHostToDevice, d->stream));
     VLGBA_CHECK(hipMemcpyAsync(d->env_tiles, env.data(), sizeof(int) * env.size(),
                                hipMemcpyHostToDevice, d->stream));
-    VLGBA_CHECK(hipMemsetAsync(d->S, 0, sizeof(double) * d->lds * d->lds, d->stream));
+    VLGBA_CHECK(hipMemsetAsync(d->S, 0, sizeof(double) * sdim * sdim, d->stream));
     VLGBA_CHECK(hipStreamSynchronize(d->stream));
     return 0;
 }
 
 void ba_chol_free(ba_dev *d)
 {
+    for (void *q : {(void *)d->S, (void *)d->linv, (void *)d->ywork, (void *)d->nd_crow,
+                    (void *)d->nd_prow, (void *)d->nd_rowsrc, (void *)d->nd_rhs, (void *)d->nd_x,
+                    (void *)d->nd_pair, (void *)d->nd_pptr, (void *)d->nd_rec, (void *)d->nd_klist,
+                    (void *)d->nd_part})
+        if (q) ba_dfree(q);
+    d->S = d->linv = d->ywork = d->nd_rhs = d->nd_x = d->nd_part = nullptr;
+    d->nd_crow = d->nd_prow = d->nd_rowsrc = d->nd_pair = d->nd_pptr = d->nd_rec = d->nd_klist =
+        nullptr;
+    d->nd_np = 0;
     delete[] d->h_tfirst;
     delete[] d->pan_ptr_h;
     delete[] d->h_pan_list;
@@ -2091,9 +2469,11 @@ void ba_chol_free(ba_dev *d)
 
 int ba_assemble_tiles(ba_dev *d)
 {
-    k_assemble_tiles<<<d->n_env, 256, 0, d->stream>>>(d->S, d->lds, d->env_tiles, d->tb_ptr,
-                                                      d->tb_blk, d->blk_jk, d->sblk, d->na, d->ld,
-                                                      d->rhs, d->scal + 4);
+    const bool nd = d->nd_np > 0;
+    k_assemble_tiles<<<d->n_env, 256, 0, d->stream>>>(
+        d->S, nd ? d->slds : d->lds, d->env_tiles, d->tb_ptr, d->tb_blk, d->blk_jk, d->sblk, d->na,
+        nd ? d->slds : d->ld, nd ? d->nd_rhs : d->rhs, d->scal + 4, nd ? d->nd_crow : nullptr,
+        nd ? d->nd_rowsrc : nullptr, d->rhs);
     return -(int)hipGetLastError();
 }
 
@@ -2106,6 +2486,49 @@ int ba_chol_prepare(ba_dev *d)
 int ba_chol_fix_diag(ba_dev *d)
 {
     k_fix_diag<<<(int)((d->lds + 255) / 256), 256, 0, d->stream>>>(d->S, d->rhs, d->lds);
+    return -(int)hipGetLastError();
+}
+
+// the envelope's tile columns k0 .. k1-1 (k_factor_step), column k0 taking no
+// pending update of column k0-1
+static void envelope_columns(ba_dev *d, int k0, int k1, long long L, double *rhs)
+{
+    const size_t smem3 = sizeof(double) * 3 * NB * LP;
+    for (int k = k0; k < k1; k++) {
+        const int p0 = d->pan_ptr_h[k], T = d->pan_ptr_h[k + 1] - p0;
+        const int q0 = k > k0 ? d->pan_ptr_h[k - 1] : 0, Tp = k > k0 ? p0 - q0 : 0;
+        // column k-1's trailing pairs below row k (see k_factor_step)
+        const int kin = Tp > 0 && d->h_pan_list[q0] == k;
+        const int Tr = Tp - kin;
+        KT_B(d);
+        k_factor_step<<<1 + T + Tr * (Tr + 1) / 2, 256, smem3, d->stream>>>(
+            d->S, L, k, d->pan_list + p0, T, d->pan_list + q0, Tp, d->linv, rhs, d->ywork,
+            d->scal + 4);
+        KT_E(d, KT_FACTOR);
+    }
+}
+
+// x = L^-T y of the envelope factor (ywork holds y; consumed)
+static int envelope_backward(ba_dev *d, long long L, double *x, int nospin)
+{
+    const int nt = d->nt;
+    if (d->xgran64 && !nospin) {   // every column co-resident: the backward solve in one launch
+        if (++d->back_epoch == 0) d->back_epoch = 1;
+        const size_t smem2 = sizeof(double) * 2 * NB * LP;
+        TRY_RC(ba_ensure_dyn_lds((const void *)k_backward_all, smem2));
+        KT_B(d);
+        k_backward_all<<<nt, 256, smem2, d->stream>>>(d->S, L, nt, d->pan_ptr, d->pan_list,
+                                                       d->linv, d->ywork, x, d->xgran64,
+                                                       d->back_epoch, d->scal + 4);
+        KT_E(d, KT_BACKWARD);
+        return -(int)hipGetLastError();
+    }
+    for (int k = nt - 1; k >= 0; k--) {
+        const int j0 = d->h_tfirst[k];
+        KT_B(d);
+        k_backward<<<k - j0 + 1, 256, 0, d->stream>>>(d->S, L, k, j0, d->linv, d->ywork, x);
+        KT_E(d, KT_BACKWARD);
+    }
     return -(int)hipGetLastError();
 }
 
@@ -2219,35 +2642,56 @@ int ba_chol_solve(ba_dev *d, int nospin)
         }
         return -(int)hipGetLastError();
     }
-    for (int k = 0; k < nt; k++) {
-        const int p0 = d->pan_ptr_h[k], T = d->pan_ptr_h[k + 1] - p0;
-        const int q0 = k > 0 ? d->pan_ptr_h[k - 1] : 0, Tp = k > 0 ? p0 - q0 : 0;
-        // column k-1's trailing pairs below row k (see k_factor_step)
-        const int kin = Tp > 0 && d->h_pan_list[q0] == k;
-        const int Tr = Tp - kin;
-        KT_B(d);
-        k_factor_step<<<1 + T + Tr * (Tr + 1) / 2, 256, smem3, d->stream>>>(
-            d->S, d->lds, k, d->pan_list + p0, T, d->pan_list + q0, Tp, d->linv, d->rhs,
-            d->ywork, d->scal + 4);
-        KT_E(d, KT_FACTOR);
-    }
-    if (d->xgran64 && !nospin) {   // every column co-resident: the backward solve in one launch
-        if (++d->back_epoch == 0) d->back_epoch = 1;
-        const size_t smem2 = sizeof(double) * 2 * NB * LP;
-        TRY_RC(ba_ensure_dyn_lds((const void *)k_backward_all, smem2));
-        KT_B(d);
-        k_backward_all<<<nt, 256, smem2, d->stream>>>(d->S, d->lds, nt, d->pan_ptr, d->pan_list,
-                                                       d->linv, d->ywork, d->da, d->xgran64,
-                                                       d->back_epoch, d->scal + 4);
-        KT_E(d, KT_BACKWARD);
+    if (d->nd_np > 0) {   // nested dissection: the arcs side by side, then the separator
+        const int np = d->nd_np, s0 = d->nd_a0[np];
+        const long long L = d->slds;
+        TRY_RC(ba_ensure_dyn_lds((const void *)k_factor_multi, smem3));
+        int nsteps = 0;
+        for (int t = 0; t < np; t++) nsteps = std::max(nsteps, d->nd_a0[t + 1] - d->nd_a0[t]);
+        for (int st = 0; st < nsteps; st++) {
+            nd_step P{};
+            int nbk = 0;
+            for (int t = 0; t < np; t++) {
+                const int k = d->nd_a0[t] + st;
+                if (k >= d->nd_a0[t + 1]) continue;
+                const int p0 = d->pan_ptr_h[k], T = d->pan_ptr_h[k + 1] - p0;
+                const bool cont = k > d->nd_a0[t];   // not the arc's first column
+                const int q0 = cont ? d->pan_ptr_h[k - 1] : 0, Tp = cont ? p0 - q0 : 0;
+                const int kin = Tp > 0 && d->h_pan_list[q0] == k;
+                int nsr = 0;   // separator rows among column k-1's trailing rows
+                for (int q = q0 + kin; q < q0 + Tp; q++) nsr += d->h_pan_list[q] >= s0;
+                const int Tr = Tp - kin, u = P.np++;
+                P.k[u] = k;
+                P.T[u] = T;
+                P.Tp[u] = Tp;
+                P.pofs[u] = p0;
+                P.qofs[u] = q0;
+                P.b0[u] = nbk;
+                nbk += 1 + T + Tr * (Tr + 1) / 2 - nsr * (nsr + 1) / 2;
+            }
+            P.b0[P.np] = nbk;
+            KT_B(d);
+            k_factor_multi<<<nbk, 256, smem3, d->stream>>>(d->S, L, d->pan_list, P, s0, d->linv,
+                                                          d->nd_rhs, d->ywork, d->scal + 4);
+            KT_E(d, KT_FACTOR);
+        }
+        if (d->nd_nrec > 0) {
+            const size_t smem2 = sizeof(double) * 2 * NB * LP;
+            TRY_RC(ba_ensure_dyn_lds((const void *)k_sep_update, smem2));
+            KT_B(d);
+            k_sep_update<<<d->nd_nrec, 256, smem2, d->stream>>>(
+                d->S, L, d->nd_pair, d->nd_rec, d->nd_klist, d->ywork, d->nd_part);
+            k_sep_reduce<<<d->nd_npair, 256, 0, d->stream>>>(d->S, L, d->nd_pair, d->nd_pptr,
+                                                             d->nd_part, d->nd_rhs);
+            KT_E(d, KT_SYRK);
+        }
+        envelope_columns(d, s0, nt, L, d->nd_rhs);
+        TRY_RC(envelope_backward(d, L, d->nd_x, nospin));
+        k_nd_scatter<<<(int)((d->lds + 255) / 256), 256, 0, d->stream>>>(d->nd_prow, d->nd_x,
+                                                                         d->da, d->lds);
         return -(int)hipGetLastError();
     }
-    for (int k = nt - 1; k >= 0; k--) {
-        const int j0 = d->h_tfirst[k];
-        KT_B(d);
-        k_backward<<<k - j0 + 1, 256, 0, d->stream>>>(d->S, d->lds, k, j0, d->linv, d->ywork,
-                                                       d->da);
-        KT_E(d, KT_BACKWARD);
-    }
+    envelope_columns(d, 0, nt, d->lds, d->rhs);
+    TRY_RC(envelope_backward(d, d->lds, d->da, nospin));
     return -(int)hipGetLastError();
 }

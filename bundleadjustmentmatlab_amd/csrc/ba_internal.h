@@ -65,6 +65,10 @@ struct ba_flags {
 #ifndef BA_FUSE_CAMRED
 #define BA_FUSE_CAMRED 1
 #endif
+// nested dissection of the envelope: at most this many camera arcs
+#ifndef BA_ND_MAX
+#define BA_ND_MAX 8
+#endif
 struct ba_camred {
     const int *cam_eptr, *cam_eslots;
     const double *upart;
@@ -114,7 +118,8 @@ struct ba_dev {
     int *tb_ptr, *tb_blk;  // device: per envelope tile, the co-visible blocks overlapping it
     int n_env;
     int dense_solve;   // 0 auto, 1: every lower tile (measurement), 2: envelope, no CR,
-                       // 3: sequential Cholesky (parity mode)
+                       // 3: sequential Cholesky (parity mode), 4: nested dissection
+                       // whenever the cameras split (tests; 0 takes it when it pays)
     // block cyclic reduction (tile-tridiagonal S): per level, eliminated tiles
     // (e, p, q) and kept tiles (k, e-, e+, k2); -1 = none
     int cr_nlev;
@@ -139,6 +144,27 @@ struct ba_dev {
     // per-level launches
     unsigned *crflag;             // [nlev][nt32][4]
     int cr_fused;
+    // one-level nested dissection of the envelope (ba_chol_setup, auto mode
+    // when S is not tridiagonal; dense_solve 4 forces it): the cameras split
+    // into nd_np arcs of consecutive cameras minus the separator (cameras
+    // coupled to an earlier arc).  Rows: arc 0 | arc 1 | ... | separator, each
+    // part padded to whole 64-row tiles.  Arcs never couple to each other, so
+    // step s factors column s of every arc in ONE launch (k_factor_multi);
+    // the arcs' contribution to the separator block is one SYRK
+    // (k_sep_update / k_sep_reduce), then the separator's columns.
+    int nd_np;                    // arcs (0: natural order)
+    int nd_a0[BA_ND_MAX + 1];     // first tile of arc t; nd_a0[nd_np] = first separator tile
+    long long slds;               // rows of the reordered system (nt * 64)
+    int *nd_crow;                 // device [m] first row of camera j
+    int *nd_prow;                 // device [lds] row of camera-space entry c (-1: padding)
+    int *nd_rowsrc;               // device [slds] camera-space entry of row r (-1: padding)
+    double *nd_rhs, *nd_x;        // [slds] the rhs / solution in row order
+    int nd_npair, nd_nrec;        // separator tile pairs, (pair, arc-column chunk) records
+    int *nd_pair;                 // device [npair][2] (i, j), i >= j, ascending
+    int *nd_pptr;                 // device [npair + 1] records of each pair
+    int *nd_rec;                  // device [nrec][3] (pair, kofs, kcnt)
+    int *nd_klist;                // device: the arc columns of the records
+    double *nd_part;              // [nrec][64*64 + 64] per-record L_i L_j^T | L_i y
     // reductions: partial sums per block of the reducing kernels, in fixed order
     double *part;      // [3][PART_MAX]
     double *scal;      // [8] : 0 old_sse, 1 new_sse, 2 dpg cams, 3 dpg pts, 4 non-positive

@@ -1424,10 +1424,7 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
     TRY(ctx_alloc(c, &d.sblk, (size_t)na * na * d.nb + d.lds + 1));
     d.rhs = d.sblk + (size_t)na * na * d.nb;
     if (!stage_mode) {
-        TRY(ctx_alloc(c, &d.S, (size_t)(d.lds * d.lds)));
-        TRY(ctx_alloc(c, &d.linv, (size_t)(d.lds / 64) * 64 * 64));
-        TRY(ctx_alloc(c, &d.ywork, (size_t)d.lds + 64));   // + the 32-row CR's last tile
-        TRY(ctx_alloc(c, &d.da, (size_t)d.lds));
+        TRY(ctx_alloc(c, &d.da, (size_t)d.lds));   // S, linv, ywork: ba_chol_setup
         ST_MARK("allocs");
         TRY(ba_chol_setup(&d, hb.jk.data(), d.nb));
         ST_MARK("chol_setup");
@@ -1570,7 +1567,7 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
             c->d.parity = 1;
             c->d.dense_solve = 3;
         } else if (o->ordered < 0 || o->ordered > 2 || o->dense_solve < 0 ||
-                   o->dense_solve > 3) {
+                   o->dense_solve > 4) {
             rc = VLGBA_E_ARG;
             break;
         }
@@ -2195,7 +2192,8 @@ int vlgba_plan_info(vlgba_ctx *c, long long *info, int len)
                                       d.cr_nlev, ne, nk,    d.ordered,    d.ordered ? d.T : d.nterm_fast,
                                       d.blob_words, d.mfma,
                                       d.cr_nlev ? (d.cr32 ? d.tb32 : 64) : 0,
-                                      d.ngrp_mf, c->pperm.empty() ? 0 : 1, d.nl};
+                                      d.ngrp_mf, c->pperm.empty() ? 0 : 1, d.nl, d.nd_np,
+                                      d.nd_np ? d.nt - d.nd_a0[d.nd_np] : 0};
     for (int k = 0; k < len && k < VLGBA_NPLAN; k++) info[k] = v[k];
     return VLGBA_NPLAN;
 }

@@ -80,7 +80,10 @@ typedef struct {
      * 1: tile Cholesky over every lower tile (measurement);
      * 2: envelope tile Cholesky (tiles outside the envelope are exactly zero,
      *   so 1 and 2 give identical results);
-     * 3: one-workgroup sequential Cholesky (parity mode, small problems).
+     * 3: one-workgroup sequential Cholesky (parity mode, small problems);
+ * 4: the envelope Cholesky on a nested-dissection camera order whenever the
+ *   cameras split into independent arcs + a separator (0 takes that order
+ *   when it shortens the chain of factor steps by a quarter or more).
      * Any of them meeting a non-positive pivot falls back to pinv(S) e_ from
      * a symmetric eigen-decomposition on the GPU (vlgba_step_info.pinv)      */
     int dense_solve;
@@ -224,9 +227,10 @@ const char *vlgba_kernel_name(int k);
  * Schur groups (the leading ones; the rest use per-term sums) [21] points
  * reordered internally (1: short tracks first, input order restored at the
  * API) [22] long tracks (more views than a Schur chunk holds: segment chunks
- * + the long-track kernels).  Writes min(len, VLGBA_NPLAN) entries, returns
- * VLGBA_NPLAN. */
-#define VLGBA_NPLAN 23
+ * + the long-track kernels) [23] nested-dissection arcs of the envelope
+ * Cholesky (0: natural camera order) [24] its separator tiles.  Writes
+ * min(len, VLGBA_NPLAN) entries, returns VLGBA_NPLAN. */
+#define VLGBA_NPLAN 25
 int vlgba_plan_info(vlgba_ctx *ctx, long long *info, int len);
 
 /* ---- stage entries with the reference MEX argument layouts ---------------

@@ -1,0 +1,135 @@
+"""The envelope Cholesky on a nested-dissection camera order (ba_chol.hip:
+ba_chol_setup's planner, k_factor_multi, k_sep_update / k_sep_reduce,
+k_nd_scatter).  The cameras split into arcs of consecutive cameras and a
+separator (cameras co-visible with an earlier arc); the arcs' columns are
+factored side by side, then the separator.  A different elimination order
+than the natural envelope, so the reduced solve agrees with it to rounding
+(not bit for bit); every other quantity of the pass is the same.
+
+The reduced solve is checked against the natural-order envelope Cholesky
+(itself bit-identical to the dense tile Cholesky, test_gpu_parity.py) on the
+same pass: relative error of da within 1e-9 (the systems here have condition
+numbers near 1e4 after the damping), and whole LM runs within the north
+star's 1e-6 relative.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _scene(kind, m, seed):
+    from bundleadjustmentmatlab_amd.scene import make_config
+    if kind == "ladybug":
+        return make_config("ladybug", m=m, n=100 * m, seed=seed)
+    return make_config("cfg2", m=m, n=80 * m, seed=seed)
+
+
+def _params(sc, num_a):
+    a = np.zeros((num_a, sc.m), order="F")
+    a[0:3], a[3:6] = sc.w0, sc.T0
+    if num_a == 7:
+        a[6] = sc.K[0]
+    elif num_a == 10:
+        a[6:10] = sc.K
+    return a, np.asfortranarray(sc.X0[:3])
+
+
+def _pass(gpu, sc, num_a, solver, timing=False):
+    a, b = _params(sc, num_a)
+    with gpu.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, num_a,
+                            solver=solver) as ba:
+        ba.set_params(a, b)
+        ba.set_timing(timing)
+        info = ba.step(relinearize=True, update_lm=False)
+        da, db = ba.last_step()
+        plan = ba.plan_info()
+        km = ba.kernel_ms() if timing else {}
+    return info, da.copy(), db.copy(), plan, km
+
+
+@pytest.mark.parametrize("kind,m,num_a", [("ladybug", 120, 6), ("ladybug", 300, 6),
+                                          ("cfg2", 60, 6), ("ladybug", 90, 7),
+                                          ("ladybug", 80, 10)])
+def test_nd_solve_matches_envelope(gpu, kind, m, num_a):
+    sc = _scene(kind, m, seed=3)
+    env, da0, db0, p0, _ = _pass(gpu, sc, num_a, "envelope")
+    nd, da1, db1, p1, km = _pass(gpu, sc, num_a, "nd", timing=True)
+    assert p0["nd_arcs"] == 0 and p1["nd_arcs"] >= 2, p1
+    assert p1["cr_levels"] == 0
+    assert "k_factor_step" in km          # k_factor_multi and the separator's columns
+    assert env.old_sse == nd.old_sse
+    assert env.chol_failed == 0 and nd.chol_failed == 0
+    scale = np.max(np.abs(da0))
+    assert np.max(np.abs(da1 - da0)) <= 1e-9 * scale, np.max(np.abs(da1 - da0)) / scale
+    assert np.max(np.abs(db1 - db0)) <= 1e-9 * np.max(np.abs(db0))
+    assert abs(nd.new_sse - env.new_sse) <= 1e-9 * env.new_sse
+
+
+def test_nd_separator_update_timed(gpu):
+    """A split with a separator runs the SYRK launches (timed as k_syrk)."""
+    sc = _scene("ladybug", 300, seed=4)
+    _, _, _, plan, km = _pass(gpu, sc, 6, "nd", timing=True)
+    assert plan["nd_arcs"] >= 2 and plan["nd_sep_tiles"] > 0, plan
+    assert "k_syrk" in km, km
+
+
+def test_nd_lm_trajectory(gpu):
+    """Whole LM runs: the nested-dissection order ends where the natural one
+    does.  The first step's cost agrees to 1e-9; later steps start from
+    slightly different points and the slow tail of this scene amplifies the
+    difference (1e-8 relative by iteration 4), so the rest is held to the
+    north star's 1e-6 relative."""
+    sc = _scene("ladybug", 200, seed=9)
+    out = {}
+    for solver in ("envelope", "nd"):
+        a, b = _params(sc, 6)
+        with gpu.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, 6, solver=solver,
+                                stop_rel=1e-9, max_iter=15) as ba:
+            ba.set_params(a, b)
+            err, st = ba.run()
+            out[solver] = (err.copy(), st)
+    e0, e1 = out["envelope"][0], out["nd"][0]
+    assert len(e0) == len(e1)
+    assert np.allclose(e0[:2], e1[:2], rtol=1e-9, atol=0)
+    assert np.allclose(e0, e1, rtol=1e-6, atol=0), (e1 - e0) / e0
+    assert abs(e0[-1] - e1[-1]) <= 1e-7 * e0[-1]
+
+
+def test_nd_auto_takes_it_when_it_pays(gpu):
+    """auto: a long banded sequence with loop closures is not tile-tridiagonal
+    (no cyclic reduction) and the split shortens the step chain by more than
+    a quarter, so the nested-dissection order is used; VLGBA_ND=0 keeps the
+    natural order."""
+    import os
+    sc = _scene("ladybug", 400, seed=5)
+    _, da1, _, p1, _ = _pass(gpu, sc, 6, "auto")
+    os.environ["VLGBA_ND"] = "0"
+    try:
+        _, da0, _, p0, _ = _pass(gpu, sc, 6, "auto")
+    finally:
+        del os.environ["VLGBA_ND"]
+    assert p1["cr_levels"] == 0 and p1["nd_arcs"] >= 2, p1
+    assert p0["nd_arcs"] == 0
+    assert np.max(np.abs(da1 - da0)) <= 1e-9 * np.max(np.abs(da0))
+
+
+def test_nd_spin_timeout_resolves_bit_identically(gpu, monkeypatch):
+    """The one-launch backward solve's hand-off timeout on the
+    nested-dissection order: the re-solve with per-column k_backward gives the
+    same result bit for bit."""
+    sc = _scene("ladybug", 150, seed=7)
+    a, b = _params(sc, 6)
+
+    def run():
+        with gpu.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, 6, solver="nd",
+                                stop_rel=1e-9, max_iter=12) as ba:
+            ba.set_params(a, b)
+            err, st = ba.run()
+            return err.copy(), st, [x.copy() for x in ba.get_params()]
+    e0, s0, p0 = run()
+    monkeypatch.setenv("VLGBA_DEBUG_SPIN_TIMEOUT", "0:3")
+    e1, s1, p1 = run()
+    assert s0.spin_retries == 0 and s1.spin_retries == 3
+    assert np.array_equal(e0, e1)
+    assert np.array_equal(p0[0], p1[0]) and np.array_equal(p0[1], p1[1])
