@@ -463,6 +463,34 @@ __device__ __forceinline__ bool block_potrf_inv(double *As, double *Li, bool zer
 // pan / prev: the envelope rows below k / below k-1 (ascending), T / Tp their
 // counts (Tp = 0 for k = 0).
 // ---------------------------------------------------------------------------
+#ifdef BA_STAMPS
+// per tile column k: [0..3] workgroup 0 entry / factor start / factor end /
+// exit, [4..7] the same for workgroup 1 (first panel tile), [8] the last exit
+#define FS_MAX 4096
+__device__ unsigned long long g_fst[FS_MAX][9];
+extern "C" int vlgba_debug_fstamps(unsigned long long *out, int n)
+{
+    if (n > FS_MAX) n = FS_MAX;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fst), sizeof(unsigned long long) * 9 * n) ==
+                   hipSuccess
+               ? 0
+               : -1;
+}
+#define FS_ST(q)                                                                          \
+    do {                                                                                  \
+        if (threadIdx.x == 0 && b <= 1 && k < FS_MAX)                                     \
+            g_fst[k][4 * b + (q)] = __builtin_amdgcn_s_memrealtime();                     \
+    } while (0)
+#define FS_END()                                                                          \
+    do {                                                                                  \
+        if (threadIdx.x == 0 && k < FS_MAX)                                               \
+            atomicMax(&g_fst[k][8], (unsigned long long)__builtin_amdgcn_s_memrealtime()); \
+    } while (0)
+#else
+#define FS_ST(q)
+#define FS_END()
+#endif
+
 // sep0: the nested dissection's first separator row tile (INT_MAX: none):
 // an arc column leaves the separator's rhs to k_sep_update (two arcs'
 // columns run in the same launch) and its separator x separator trailing
@@ -482,6 +510,7 @@ __device__ __forceinline__ void factor_step_body(double *__restrict__ S, long lo
     const int tid = threadIdx.x;
     const bool kin = Tp > 0 && prev[0] == k;   // column k-1 reaches row k
     d4 acc[2][2];
+    FS_ST(0);
     if (b > T) {
         // trailing pairs of column k-1 below row k (k_syrk's enumeration over
         // prev without k)
@@ -493,50 +522,57 @@ __device__ __forceinline__ void factor_step_body(double *__restrict__ S, long lo
             jj++;
         }
         const int j = pl[jj], i = pl[jj + q];
-        load_tile(S, lds, i, k - 1, As);
-        load_tile(S, lds, j, k - 1, Bs);
+        double va[16], vb[16], vc[16];
+        fetch_tile(S, lds, i, k - 1, va);
+        fetch_tile(S, lds, j, k - 1, vb);
+        fetch_tile(S, lds, i, j, vc);
+        put_tile(As, va, false);
+        put_tile(Bs, vb, false);
+        put_tile(Cs, vc, false);
         __syncthreads();
         mfma_64x64(As, Bs, acc);
+        acc_to_lds(acc, Cs, -1.0, true);
         __syncthreads();
-        load_tile(S, lds, i, j, As);
-        __syncthreads();
-        acc_to_lds(acc, As, -1.0, true);
-        __syncthreads();
-        store_tile(S, lds, i, j, As);
+        store_tile(S, lds, i, j, Cs);
+        FS_END();
         return;
     }
     const int i = b > 0 ? pan[b - 1] : k;
-    bool iin = false;   // column k-1 reaches row i (panel tiles only)
-    if (b > 0 && kin)
-        for (int t = 1; t < Tp && !iin; t++) iin = prev[t] == i;
-    if (b > 0) {   // A_ik and its pending update of column k-1
-        load_tile(S, lds, i, k, Cs);
-        if (iin) {
-            load_tile(S, lds, i, k - 1, As);
-            load_tile(S, lds, k, k - 1, Bs);
-            __syncthreads();
-            mfma_64x64(As, Bs, acc);
-            __syncthreads();
-            acc_to_lds(acc, Cs, -1.0, true);
-        }
-    } else if (kin) {
-        load_tile(S, lds, k, k - 1, Bs);
+    // every tile this workgroup reads, fetched at once (one memory latency
+    // instead of three dependent ones): A_ik, L_k,k-1, A_kk, L_i,k-1
+    double vc[16], va[16], vb[16], vk[16];
+    if (b > 0) fetch_tile(S, lds, i, k, vc);
+    if (kin) fetch_tile(S, lds, k, k - 1, vb);
+    fetch_tile(S, lds, k, k, vk);
+    bool iin = false;   // column k-1 reaches row i (panel tiles only): a wave-wide search
+    if (b > 0 && kin) {
+        const int lane = tid & 63;
+        for (int t0 = 1; t0 < Tp && !iin; t0 += 64)
+            iin = __any(t0 + lane < Tp && prev[t0 + lane] == i);
+    }
+    if (iin) fetch_tile(S, lds, i, k - 1, va);
+    if (tid < NB) rk[tid] = rhs[(long long)NB * k + tid];
+    if (b > 0) put_tile(Cs, vc, false);
+    if (iin) put_tile(As, va, false);
+    if (kin) put_tile(Bs, vb, false);
+    __syncthreads();
+    if (iin) {   // A_ik's pending update of column k-1
+        mfma_64x64(As, Bs, acc);
+        __syncthreads();
+        acc_to_lds(acc, Cs, -1.0, true);
     }
     // A_kk and its pending update
-    if (kin && !iin && b > 0) load_tile(S, lds, k, k - 1, Bs);
+    if (kin) mfma_64x64(Bs, Bs, acc);
     __syncthreads();
-    if (kin) {
-        mfma_64x64(Bs, Bs, acc);
-        __syncthreads();
-    }
-    load_tile(S, lds, k, k, As);
-    if (tid < NB) rk[tid] = rhs[(long long)NB * k + tid];
+    put_tile(As, vk, false);
     __syncthreads();
     if (kin) {
         acc_to_lds(acc, As, -1.0, true);
         __syncthreads();
     }
+    FS_ST(1);
     const bool ok = block_potrf_inv(As, Bs);
+    FS_ST(2);
     gemv64(Bs, rk, part, yk, 1.0);            // y_k = L^-1 r_k
     if (b == 0) {
         store_tile(S, lds, k, k, As);
@@ -544,6 +580,8 @@ __device__ __forceinline__ void factor_step_body(double *__restrict__ S, long lo
         for (int q = tid; q < NB * NB; q += blockDim.x) lo[q] = Bs[(q >> 6) * LP + (q & 63)];
         if (tid < NB) y[(long long)NB * k + tid] = yk[tid];
         if (tid == 0 && !ok) status[0] = 1.0;
+        FS_ST(3);
+        FS_END();
         return;
     }
     mfma_64x64(Cs, Bs, acc);   // L_ik[r][c] = sum_t A_ik[r][t] Li[c][t]
@@ -554,6 +592,8 @@ __device__ __forceinline__ void factor_step_body(double *__restrict__ S, long lo
     double ri[1];
     gemv64(Cs, yk, part, nullptr, 1.0, ri);   // (L_ik y_k)[tid] for tid < 64
     if (tid < NB && i < sep0) rhs[(long long)NB * i + tid] -= ri[0];
+    FS_ST(3);
+    FS_END();
 }
 
 __global__ __launch_bounds__(256) void k_factor_step(double *__restrict__ S, long long lds, int k,

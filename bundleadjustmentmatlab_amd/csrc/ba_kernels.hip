@@ -1952,14 +1952,20 @@ int ba_launch_schur(ba_dev *d, double lambda)
     return -(int)hipGetLastError();
 }
 
+#ifndef BA_SCHUR_TWO_STREAMS
+#define BA_SCHUR_TWO_STREAMS 1
+#endif
 template <int NA>
 static int launch_schur_fast(ba_dev *d, double lambda)
 {
     // MFMA groups [0, ngrp_mf), then the per-term groups [ngrp_mf, ngrp)
+    const bool two = BA_SCHUR_TWO_STREAMS && d->ngrp_mf > 0 && d->ngrp > d->ngrp_mf &&
+                     !d->join_pending && d->side && !(d->kt && d->kt->on);
     if (d->ngrp_mf > 0) {
         KT_B(d);
         k_point_vinv<NA><<<(d->n + 255) / 256, 256, 0, d->stream>>>(d->V, d->n, lambda, d->Vinv);
         KT_E(d, KT_DAMP);
+        if (two) VLGBA_CHECK(hipEventRecord(d->ev_fork, d->stream));   // V*^-1 ready
         const size_t sm2 = sizeof(double) * (d->mf_max_s * NA * NA + d->mf_max_e * NA) +
                            sizeof(unsigned) * (size_t)d->mf_max_blob;
         TRY_RC(ba_ensure_dyn_lds((const void *)k_schur_mfma<NA>, sm2));
@@ -1979,12 +1985,26 @@ static int launch_schur_fast(ba_dev *d, double lambda)
                       sizeof(unsigned) * bcap;
         smem = (smem + 15) & ~(size_t)15;
         TRY_RC(ba_ensure_dyn_lds((const void *)k_schur_group<NA>, smem));
+        // beside the MFMA groups on the side stream (disjoint partial slots;
+        // V*^-1 is ready): the two launches' tails overlap.  Untimed passes
+        // only, and only when the side stream is idle (its camera reduction
+        // ran inside k_schur_mfma); k_schur_reduce joins below.
+        hipStream_t s0 = d->stream;
+        if (two) {
+            VLGBA_CHECK(hipStreamWaitEvent(d->side, d->ev_fork, 0));
+            d->stream = d->side;
+        }
         KT_B(d);
         k_schur_group<NA><<<d->ngrp - d->ngrp_mf, 256, smem, d->stream>>>(
             d->grp_ch + d->ngrp_mf, d->grp_gs + d->ngrp_mf, d->grp_ge + d->ngrp_mf, d->ch_pt,
             d->ch_obase, d->ch_blob, d->blob, d->V, d->eB, d->W, lambda, bcap, gcap, ecap,
             d->Vinv, d->spart, d->epart);
         KT_E(d, KT_SCHUR_CHUNK);
+        if (two) {
+            d->stream = s0;
+            VLGBA_CHECK(hipEventRecord(d->ev_join, d->side));
+            d->join_pending = 1;
+        }
     }
     if (d->nl > 0) {   // long tracks: their V*^-1, then their (obs, obs) tiles
         KT_B(d);
