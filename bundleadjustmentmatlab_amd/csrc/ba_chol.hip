@@ -3,7 +3,7 @@
 //
 // Replaces da = pinv(S) * e_ (toolbox/bundle/bundle_euclid.m:193).  S is
 // symmetric positive definite once its exactly-zero rows (fixed parameters,
-// App. A Q2/Q8) are given a unit diagonal (k_fix_diag), and on that matrix
+// App. A Q2/Q8) are given a unit diagonal (k_assemble_tiles), and on that matrix
 // pinv and the Cholesky solve agree to conditioning-limited rounding.  A
 // non-positive pivot sets status[0]; the host then takes da = pinv(S) e_
 // (rocSOLVER dsyevd, ba_solver.cpp pinv_fallback), as bundle_euclid.m:193 does.
@@ -22,7 +22,15 @@
 //              (MFMA), r_i -= L_ik y_k;
 //   the rest : column k-1's trailing update A_ij -= L_i,k-1 L_j,k-1^T of the
 //              envelope pairs below row k (MFMA)
-// then per k descending k_backward: x_k = L_kk^-T z_k, z_j -= L_kj^T x_k.
+// then the backward solve x_k = L_kk^-T z_k, z_j -= L_kj^T x_k (one launch,
+// k_backward_all, or per column k_backward).
+//
+// Solvers on top of the tiles (ba_chol_setup picks one): block cyclic
+// reduction when S is tile-tridiagonal (k_cr32_fused on camera-aligned 30-row
+// tiles); else the envelope Cholesky, on a nested-dissection camera order
+// (arcs side by side in k_factor_multi, separator SYRK k_sep_update /
+// k_sep_reduce, then the separator) when that shortens the chain of columns;
+// the sequential k_chol_seq in parity mode.
 #include "ba_internal.h"
 
 #include <algorithm>
