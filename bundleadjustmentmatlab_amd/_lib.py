@@ -116,6 +116,7 @@ SIGNATURES = {
     "vlgba_debug_sincos": (c_int, [c_dp, c_dp, c_dp, c_ll]),
     "vlgba_debug_pinv_solve": (c_int, [c_int, c_dp, c_dp, c_dp]),
     "vlgba_debug_force_status": (c_int, [ctypes.c_void_p, c_int, c_int]),
+    "vlgba_debug_nd_plan": (c_int, [c_int, c_int, c_ip, c_int, c_ip, c_ip]),
 }
 
 ERRORS = {-1001: "bad argument",

@@ -2122,6 +2122,27 @@ int nd_choose(const std::vector<int> &minK, int m, int na, int *bnd_out, int &cr
 }
 }   // namespace
 
+static std::vector<int> nd_min_cam(int m, const int *blk_jk, int nb)
+{
+    std::vector<int> minK(m);
+    for (int j = 0; j < m; j++) minK[j] = j;
+    for (int b = 0; b < nb; b++) {
+        const int j = blk_jk[2 * b], k = blk_jk[2 * b + 1];
+        if (k < minK[j]) minK[j] = k;
+    }
+    return minK;
+}
+
+extern "C" int vlgba_debug_nd_plan(int m, int num_a, const int *blk_jk, int nb, int *bnd,
+                                   int *crit)
+{
+    if (m < 2 || num_a < 1 || nb < 0 || (nb > 0 && !blk_jk) || !bnd || !crit) return -1;
+    for (int b = 0; b < nb; b++)
+        if (blk_jk[2 * b] < blk_jk[2 * b + 1] || blk_jk[2 * b + 1] < 0 || blk_jk[2 * b] >= m)
+            return -1;
+    return nd_choose(nd_min_cam(m, blk_jk, nb), m, num_a, bnd, *crit);
+}
+
 int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
 {
     int nt = (int)(d->lds / NB);
@@ -2265,12 +2286,7 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
     if (!tridiag && (d->dense_solve == 0 || d->dense_solve == 4) && m >= 2 && nt > 1) {
         const char *ev = std::getenv("VLGBA_ND");
         const bool off = ev && ev[0] == '0';
-        std::vector<int> minK(m);
-        for (int j = 0; j < m; j++) minK[j] = j;
-        for (int b = 0; b < nb; b++) {
-            const int j = blk_jk[2 * b], k = blk_jk[2 * b + 1];
-            if (k < minK[j]) minK[j] = k;
-        }
+        const std::vector<int> minK = nd_min_cam(m, blk_jk, nb);
         int bnd[BA_ND_MAX + 1], crit = INT_MAX;
         const int K = off && d->dense_solve == 0 ? 0 : nd_choose(minK, m, na, bnd, crit);
         const bool take = K > 0 && (d->dense_solve == 4 || (nt >= 8 && 4 * crit <= 3 * nt));

@@ -326,6 +326,13 @@ int vlgba_debug_pinv_solve(int ld, const double *S, const double *e_, double *da
  * pass is solved again without spins).  VLGBA_DEBUG_SPIN_TIMEOUT="rank:passes"
  * sets word 5 at context creation. */
 int vlgba_debug_force_status(vlgba_ctx *ctx, int word, int passes);
+/* The envelope solve's nested-dissection planner on the host (no GPU): for
+ * m cameras of num_a parameters and the co-visible blocks blk_jk [2 * nb]
+ * (j >= k), the chosen arc count K (0: none), the arc boundaries bnd [K + 1]
+ * (cameras bnd[t] .. bnd[t+1]-1, minus the separator: the cameras co-visible
+ * with an earlier arc) and the predicted chain of factor steps (crit).
+ * bnd must hold 9 ints. */
+int vlgba_debug_nd_plan(int m, int num_a, const int *blk_jk, int nb, int *bnd, int *crit);
 
 /* Library / device info: writes a NUL-terminated string, returns its length. */
 int vlgba_version(char *buf, int len);
