@@ -503,41 +503,28 @@ extern "C" int vlgba_debug_fstamps(unsigned long long *out, int n)
 // an arc column leaves the separator's rhs to k_sep_update (two arcs'
 // columns run in the same launch) and its separator x separator trailing
 // pairs, which the host does not launch (they end each pair enumeration).
-// la: diagonal look-ahead.  Bit 0 (la_in): A_kk was factored by the previous
-// step, so there is no workgroup 0 and the panel tiles read L_kk^-1 / y_k
-// instead of refactoring A_kk.  Bit 1 (la_out): the panel workgroup of row
-// k+1 goes on to apply column k-1's and column k's updates to A_k+1,k+1 (the
-// trailing pair (k+1, k+1) is then not launched), factors it and writes
-// L_k+1,k+1, its inverse and y_k+1 -- the next column's factorisation moves
-// off the next launch's critical path.  Every tile gets the same operations
-// in the same order either way: bit-identical results.
 __device__ __forceinline__ void factor_step_body(double *__restrict__ S, long long lds, int k,
                                                  const int *__restrict__ pan, int T,
                                                  const int *__restrict__ prev, int Tp,
                                                  double *__restrict__ linv,
                                                  double *__restrict__ rhs,
                                                  double *__restrict__ y,
-                                                 double *__restrict__ status, int b, int sep0,
-                                                 int la)
+                                                 double *__restrict__ status, int b, int sep0)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double *As = sm, *Bs = sm + NB * LP, *Cs = sm + 2 * NB * LP;
     __shared__ double yk[NB], rk[NB];
     __shared__ double part[4][NB];
     const int tid = threadIdx.x;
-    const bool la_in = la & 1, la_out = (la & 2) != 0;
-    const bool kprev = Tp > 0 && prev[0] == k;   // column k-1 reaches row k
-    const bool kin = kprev && !la_in;            // ... and A_kk's update is this step's
-    if (la_in) b++;                              // no workgroup 0
+    const bool kin = Tp > 0 && prev[0] == k;   // column k-1 reaches row k
     d4 acc[2][2];
     FS_ST(0);
     if (b > T) {
         // trailing pairs of column k-1 below row k (k_syrk's enumeration over
-        // prev without k), without (k+1, k+1) under la_out
-        const int *pl = prev + (kprev ? 1 : 0);
-        const int Tr = Tp - (kprev ? 1 : 0);
-        const int skip = la_out && Tr > 0 && pl[0] == k + 1;
-        int q = b - T - 1 + skip, jj = 0;
+        // prev without k)
+        const int *pl = prev + (kin ? 1 : 0);
+        const int Tr = Tp - (kin ? 1 : 0);
+        int q = b - T - 1, jj = 0;
         while (q >= Tr - jj) {
             q -= Tr - jj;
             jj++;
@@ -559,64 +546,52 @@ __device__ __forceinline__ void factor_step_body(double *__restrict__ S, long lo
         return;
     }
     const int i = b > 0 ? pan[b - 1] : k;
-    const bool lad = la_out && i == k + 1;   // this workgroup factors the next diagonal
     // every tile this workgroup reads, fetched at once (one memory latency
-    // instead of three dependent ones): A_ik, L_k,k-1, A_kk, L_i,k-1 (+ A_k+1,k+1)
+    // instead of three dependent ones): A_ik, L_k,k-1, A_kk, L_i,k-1
     double vc[16], va[16], vb[16], vk[16];
     if (b > 0) fetch_tile(S, lds, i, k, vc);
-    if (kprev) fetch_tile(S, lds, k, k - 1, vb);
-    if (!la_in) fetch_tile(S, lds, k, k, vk);
+    if (kin) fetch_tile(S, lds, k, k - 1, vb);
+    fetch_tile(S, lds, k, k, vk);
     bool iin = false;   // column k-1 reaches row i (panel tiles only): a wave-wide search
-    if (b > 0 && kprev) {
+    if (b > 0 && kin) {
         const int lane = tid & 63;
         for (int t0 = 1; t0 < Tp && !iin; t0 += 64)
             iin = __any(t0 + lane < Tp && prev[t0 + lane] == i);
     }
     if (iin) fetch_tile(S, lds, i, k - 1, va);
-    if (!la_in && tid < NB) rk[tid] = rhs[(long long)NB * k + tid];
+    if (tid < NB) rk[tid] = rhs[(long long)NB * k + tid];
     if (b > 0) put_tile(Cs, vc, false);
     if (iin) put_tile(As, va, false);
-    if (kprev) put_tile(Bs, vb, false);
+    if (kin) put_tile(Bs, vb, false);
     __syncthreads();
-    d4 acc2[2][2];   // lad: column k-1's update of A_k+1,k+1 (As = L_k+1,k-1)
     if (iin) {   // A_ik's pending update of column k-1
         mfma_64x64(As, Bs, acc);
-        if (lad) mfma_64x64(As, As, acc2);
         __syncthreads();
         acc_to_lds(acc, Cs, -1.0, true);
     }
-    bool ok = true;
-    if (!la_in) {
-        // A_kk and its pending update
-        if (kin) mfma_64x64(Bs, Bs, acc);
-        __syncthreads();
-        put_tile(As, vk, false);
-        __syncthreads();
-        if (kin) {
-            acc_to_lds(acc, As, -1.0, true);
-            __syncthreads();
-        }
-        FS_ST(1);
-        ok = block_potrf_inv(As, Bs);
-        FS_ST(2);
-        gemv64(Bs, rk, part, yk, 1.0);            // y_k = L^-1 r_k
-        if (b == 0) {
-            store_tile(S, lds, k, k, As);
-            double *lo = linv + (long long)NB * NB * k;
-            for (int q = tid; q < NB * NB; q += blockDim.x) lo[q] = Bs[(q >> 6) * LP + (q & 63)];
-            if (tid < NB) y[(long long)NB * k + tid] = yk[tid];
-            if (tid == 0 && !ok) status[0] = 1.0;
-            FS_ST(3);
-            FS_END();
-            return;
-        }
-    } else {   // L_kk^-1 and y_k from the previous step's look-ahead
-        __syncthreads();   // Bs (L_k,k-1) consumed
-        load_rowmajor(linv + (long long)NB * NB * k, Bs);
-        if (tid < NB) yk[tid] = y[(long long)NB * k + tid];
+    // A_kk and its pending update
+    if (kin) mfma_64x64(Bs, Bs, acc);
+    __syncthreads();
+    put_tile(As, vk, false);
+    __syncthreads();
+    if (kin) {
+        acc_to_lds(acc, As, -1.0, true);
         __syncthreads();
     }
-    if (lad) fetch_tile(S, lds, k + 1, k + 1, vk);   // in flight under the panel product
+    FS_ST(1);
+    const bool ok = block_potrf_inv(As, Bs);
+    FS_ST(2);
+    gemv64(Bs, rk, part, yk, 1.0);            // y_k = L^-1 r_k
+    if (b == 0) {
+        store_tile(S, lds, k, k, As);
+        double *lo = linv + (long long)NB * NB * k;
+        for (int q = tid; q < NB * NB; q += blockDim.x) lo[q] = Bs[(q >> 6) * LP + (q & 63)];
+        if (tid < NB) y[(long long)NB * k + tid] = yk[tid];
+        if (tid == 0 && !ok) status[0] = 1.0;
+        FS_ST(3);
+        FS_END();
+        return;
+    }
     mfma_64x64(Cs, Bs, acc);   // L_ik[r][c] = sum_t A_ik[r][t] Li[c][t]
     __syncthreads();
     acc_to_lds(acc, Cs, 1.0, false);
@@ -625,29 +600,6 @@ __device__ __forceinline__ void factor_step_body(double *__restrict__ S, long lo
     double ri[1];
     gemv64(Cs, yk, part, nullptr, 1.0, ri);   // (L_ik y_k)[tid] for tid < 64
     if (tid < NB && i < sep0) rhs[(long long)NB * i + tid] -= ri[0];
-    if (lad) {
-        // A_k+1,k+1 -= L_k+1,k-1 L_k+1,k-1^T (the skipped trailing pair), then
-        // -= L_k+1,k L_k+1,k^T (the next step's kin update), factor, invert
-        if (tid < NB) rk[tid] = rhs[(long long)NB * i + tid];   // this thread's own write above
-        put_tile(As, vk, false);
-        __syncthreads();
-        if (iin) {
-            acc_to_lds(acc2, As, -1.0, true);
-            __syncthreads();
-        }
-        mfma_64x64(Cs, Cs, acc);
-        __syncthreads();
-        acc_to_lds(acc, As, -1.0, true);
-        __syncthreads();
-        const bool ok1 = block_potrf_inv(As, Bs);
-        gemv64(Bs, rk, part, yk, 1.0);   // y_k+1 = L^-1 r_k+1
-        store_tile(S, lds, i, i, As);
-        double *lo = linv + (long long)NB * NB * i;
-        for (int q = tid; q < NB * NB; q += blockDim.x) lo[q] = Bs[(q >> 6) * LP + (q & 63)];
-        if (tid < NB) y[(long long)NB * i + tid] = yk[tid];
-        if (tid == 0 && !ok1) status[0] = 1.0;
-    }
-    if (tid == 0 && !ok) status[0] = 1.0;
     FS_ST(3);
     FS_END();
 }
@@ -658,9 +610,9 @@ __global__ __launch_bounds__(256) void k_factor_step(double *__restrict__ S, lon
                                                      double *__restrict__ linv,
                                                      double *__restrict__ rhs,
                                                      double *__restrict__ y,
-                                                     double *__restrict__ status, int la)
+                                                     double *__restrict__ status)
 {
-    factor_step_body(S, lds, k, pan, T, prev, Tp, linv, rhs, y, status, blockIdx.x, INT_MAX, la);
+    factor_step_body(S, lds, k, pan, T, prev, Tp, linv, rhs, y, status, blockIdx.x, INT_MAX);
 }
 
 // one step of every arc of the nested dissection: column k[t] of arc t takes
@@ -669,7 +621,6 @@ __global__ __launch_bounds__(256) void k_factor_step(double *__restrict__ S, lon
 struct nd_step {
     int np;
     int k[BA_ND_MAX], T[BA_ND_MAX], Tp[BA_ND_MAX], pofs[BA_ND_MAX], qofs[BA_ND_MAX];
-    int la[BA_ND_MAX];
     int b0[BA_ND_MAX + 1];
 };
 
@@ -685,7 +636,7 @@ __global__ __launch_bounds__(256) void k_factor_multi(double *__restrict__ S, lo
     int t = 0;
     while (t + 1 < P.np && b >= P.b0[t + 1]) t++;
     factor_step_body(S, lds, P.k[t], pan_list + P.pofs[t], P.T[t], pan_list + P.qofs[t], P.Tp[t],
-                     linv, rhs, y, status, b - P.b0[t], sep0, P.la[t]);
+                     linv, rhs, y, status, b - P.b0[t], sep0);
 }
 
 // ---------------------------------------------------------------------------
@@ -2604,45 +2555,19 @@ int ba_chol_fix_diag(ba_dev *d)
 
 // the envelope's tile columns k0 .. k1-1 (k_factor_step), column k0 taking no
 // pending update of column k0-1
-#ifndef BA_LOOKAHEAD
-#define BA_LOOKAHEAD 0
-#endif
-// one column's launch shape (k_factor_step's roles): column k of a part whose
-// columns end at kend; la_in = the previous column factored A_kk; nsr = the
-// separator rows among column k-1's trailing rows (pairs not launched)
-struct col_shape {
-    int p0, T, q0, Tp, la, nblk;
-};
-static col_shape column_shape(const ba_dev *d, int k, bool first, int kend, bool la_in, int sep0)
-{
-    col_shape c;
-    c.p0 = d->pan_ptr_h[k];
-    c.T = d->pan_ptr_h[k + 1] - c.p0;
-    c.q0 = first ? 0 : d->pan_ptr_h[k - 1];
-    c.Tp = first ? 0 : c.p0 - c.q0;
-    const int kprev = c.Tp > 0 && d->h_pan_list[c.q0] == k;
-    const int Tr = c.Tp - kprev;
-    int nsr = 0;
-    for (int q = c.q0 + kprev; q < c.q0 + c.Tp; q++) nsr += d->h_pan_list[q] >= sep0;
-    const bool la_out = BA_LOOKAHEAD && k + 1 < kend && c.T > 0 && d->h_pan_list[c.p0] == k + 1;
-    const int skip = la_out && Tr > 0 && d->h_pan_list[c.q0 + kprev] == k + 1;
-    c.la = (la_in ? 1 : 0) | (la_out ? 2 : 0);
-    c.nblk = (la_in ? 0 : 1) + c.T + Tr * (Tr + 1) / 2 - nsr * (nsr + 1) / 2 - skip;
-    return c;
-}
-
 static void envelope_columns(ba_dev *d, int k0, int k1, long long L, double *rhs)
 {
     const size_t smem3 = sizeof(double) * 3 * NB * LP;
-    bool la_in = false;
     for (int k = k0; k < k1; k++) {
-        const col_shape c = column_shape(d, k, k == k0, k1, la_in, INT_MAX);
-        la_in = (c.la & 2) != 0;
-        if (c.nblk == 0) continue;   // a look-ahead diagonal with nothing below it
+        const int p0 = d->pan_ptr_h[k], T = d->pan_ptr_h[k + 1] - p0;
+        const int q0 = k > k0 ? d->pan_ptr_h[k - 1] : 0, Tp = k > k0 ? p0 - q0 : 0;
+        // column k-1's trailing pairs below row k (see k_factor_step)
+        const int kin = Tp > 0 && d->h_pan_list[q0] == k;
+        const int Tr = Tp - kin;
         KT_B(d);
-        k_factor_step<<<c.nblk, 256, smem3, d->stream>>>(
-            d->S, L, k, d->pan_list + c.p0, c.T, d->pan_list + c.q0, c.Tp, d->linv, rhs, d->ywork,
-            d->scal + 4, c.la);
+        k_factor_step<<<1 + T + Tr * (Tr + 1) / 2, 256, smem3, d->stream>>>(
+            d->S, L, k, d->pan_list + p0, T, d->pan_list + q0, Tp, d->linv, rhs, d->ywork,
+            d->scal + 4);
         KT_E(d, KT_FACTOR);
     }
 }
@@ -2787,29 +2712,28 @@ int ba_chol_solve(ba_dev *d, int nospin)
         TRY_RC(ba_ensure_dyn_lds((const void *)k_factor_multi, smem3));
         int nsteps = 0;
         for (int t = 0; t < np; t++) nsteps = std::max(nsteps, d->nd_a0[t + 1] - d->nd_a0[t]);
-        bool la_in[BA_ND_MAX] = {};
         for (int st = 0; st < nsteps; st++) {
             nd_step P{};
             int nbk = 0;
             for (int t = 0; t < np; t++) {
                 const int k = d->nd_a0[t] + st;
                 if (k >= d->nd_a0[t + 1]) continue;
-                const col_shape c =
-                    column_shape(d, k, k == d->nd_a0[t], d->nd_a0[t + 1], la_in[t], s0);
-                la_in[t] = (c.la & 2) != 0;
-                if (c.nblk == 0) continue;
-                const int u = P.np++;
+                const int p0 = d->pan_ptr_h[k], T = d->pan_ptr_h[k + 1] - p0;
+                const bool cont = k > d->nd_a0[t];   // not the arc's first column
+                const int q0 = cont ? d->pan_ptr_h[k - 1] : 0, Tp = cont ? p0 - q0 : 0;
+                const int kin = Tp > 0 && d->h_pan_list[q0] == k;
+                int nsr = 0;   // separator rows among column k-1's trailing rows
+                for (int q = q0 + kin; q < q0 + Tp; q++) nsr += d->h_pan_list[q] >= s0;
+                const int Tr = Tp - kin, u = P.np++;
                 P.k[u] = k;
-                P.T[u] = c.T;
-                P.Tp[u] = c.Tp;
-                P.pofs[u] = c.p0;
-                P.qofs[u] = c.q0;
-                P.la[u] = c.la;
+                P.T[u] = T;
+                P.Tp[u] = Tp;
+                P.pofs[u] = p0;
+                P.qofs[u] = q0;
                 P.b0[u] = nbk;
-                nbk += c.nblk;
+                nbk += 1 + T + Tr * (Tr + 1) / 2 - nsr * (nsr + 1) / 2;
             }
             P.b0[P.np] = nbk;
-            if (nbk == 0) continue;
             KT_B(d);
             k_factor_multi<<<nbk, 256, smem3, d->stream>>>(d->S, L, d->pan_list, P, s0, d->linv,
                                                           d->nd_rhs, d->ywork, d->scal + 4);
