@@ -2006,7 +2006,13 @@ int vlgba_set_params(vlgba_ctx *c, const double *a, const double *b)
     }
     TRY(ba_launch_rotations(&c->d, c->d.a, c->d.rot, 1));
     c->lin_valid = 0;
+    static const bool tm = std::getenv("VLGBA_SETP_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     VLGBA_CHECK(hipStreamSynchronize(c->d.stream));
+    if (tm)
+        std::fprintf(stderr, "[vlgba set_params] m=%d sync %.3f ms\n", c->d.m,
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0)
+                         .count());
     return 0;
 }
 

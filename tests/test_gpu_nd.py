@@ -133,3 +133,27 @@ def test_nd_spin_timeout_resolves_bit_identically(gpu, monkeypatch):
     assert s0.spin_retries == 0 and s1.spin_retries == 3
     assert np.array_equal(e0, e1)
     assert np.array_equal(p0[0], p1[0]) and np.array_equal(p0[1], p1[1])
+
+
+def test_nd_projective(gpu):
+    """The projective camera (num_a = 12: 64-row tiles hold 5 1/3 cameras, so
+    cameras straddle tiles inside every part) on the nested-dissection order:
+    one pass agrees with the natural envelope to rounding."""
+    from bundleadjustmentmatlab_amd.projective import pack_a
+    from bundleadjustmentmatlab_amd.scene import projective_from
+    sc = _scene("ladybug", 160, seed=12)
+    Pp, Xp = projective_from(sc)
+    a, b = pack_a(Pp), np.asfortranarray(Xp[0:3])
+    out = {}
+    for solver in ("envelope", "nd"):
+        with gpu.BundleAdjuster(None, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, 12, m=sc.m,
+                                model="projective", solver=solver) as ba:
+            ba.set_params(a, b)
+            info = ba.step(relinearize=True, update_lm=False)
+            da, db = ba.last_step()
+            out[solver] = (info, da.copy(), db.copy(), ba.plan_info())
+    (e0, da0, db0, p0), (e1, da1, db1, p1) = out["envelope"], out["nd"]
+    assert p0["nd_arcs"] == 0 and p1["nd_arcs"] >= 2
+    assert e0.old_sse == e1.old_sse and e0.chol_failed == 0 and e1.chol_failed == 0
+    assert np.max(np.abs(da1 - da0)) <= 1e-8 * np.max(np.abs(da0))
+    assert np.max(np.abs(db1 - db0)) <= 1e-8 * np.max(np.abs(db0))

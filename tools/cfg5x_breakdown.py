@@ -35,7 +35,18 @@ def run(self):
     return r
 
 
+def timed(name, fn):
+    def w(self, *a, **k):
+        t = time.perf_counter()
+        r = fn(self, *a, **k)
+        cur[name] = cur.get(name, 0.0) + time.perf_counter() - t
+        return r
+    return w
+
+
 bundle.BundleAdjuster.__init__, bundle.BundleAdjuster.run = init, run
+for nm in ("set_params", "get_params", "close"):
+    setattr(bundle.BundleAdjuster, nm, timed(nm, getattr(bundle.BundleAdjuster, nm)))
 cfg = sys.argv[1] if len(sys.argv) > 1 else "cfg5x"
 sc = make_config(cfg)
 rows = []
@@ -44,7 +55,9 @@ rows = []
 def progress(solves):
     s = solves[-1]
     rows.append((s["cameras"], s["observations"], s["passes"], s["seconds"], cur.get("init", 0.0),
-                 cur.get("run", 0.0)))
+                 cur.get("run", 0.0), cur.get("set_params", 0.0), cur.get("get_params", 0.0),
+                 cur.get("close", 0.0)))
+    cur.clear()
 
 
 t0 = time.perf_counter()
@@ -63,4 +76,5 @@ for lo, hi in zip(edges[:-1], edges[1:]):
     print(f"  cams [{lo:4d},{hi:4d}): {sel.sum():5d} solves  {r[:, 3].sum():6.2f} s  "
           f"create {r[:, 4].sum():6.2f} s ({1e3 * r[:, 4].mean():6.2f} ms each)  "
           f"loop {r[:, 5].sum():6.2f} s  passes {int(r[:, 2].sum()):6d} "
-          f"({1e3 * r[:, 5].sum() / max(1, r[:, 2].sum()):.2f} ms/pass)")
+          f"({1e3 * r[:, 5].sum() / max(1, r[:, 2].sum()):.2f} ms/pass)  set {r[:, 6].sum():.2f} "
+          f"get {r[:, 7].sum():.2f} close {r[:, 8].sum():.2f} s")
