@@ -14,6 +14,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # variant, tools/ab_build.sh); the package's own build otherwise
 LIB_PATH = os.environ.get("VLGBA_LIB") or os.path.join(_HERE, "libvlgba.so")
 
+ABI_VERSION = 2   # VLGBA_ABI_VERSION: the struct layouts below
+
 c_int, c_double, c_ll = ctypes.c_int, ctypes.c_double, ctypes.c_longlong
 c_dp = ctypes.POINTER(ctypes.c_double)
 c_ip = ctypes.POINTER(ctypes.c_int)
@@ -111,6 +113,7 @@ SIGNATURES = {
     "vlgba_scene_banded": (c_int, [ctypes.POINTER(VlgbaSceneSpec), c_int,
                                    ctypes.POINTER(VlgbaSceneOut)]),
     "vlgba_version": (c_int, [ctypes.c_char_p, c_int]),
+    "vlgba_abi_check": (c_int, [c_int, c_ll, c_ll, c_ll, c_ll, c_ll]),
     "vlgba_get_unique_id": (c_int, [ctypes.c_void_p]),
     "vlgba_device_count": (c_int, []),
     "vlgba_debug_sincos": (c_int, [c_dp, c_dp, c_dp, c_ll]),
@@ -122,7 +125,8 @@ SIGNATURES = {
 ERRORS = {-1001: "bad argument",
           -1002: "num_a must be 6, 7 or 10 (Euclidean) or 12 (projective)",
           -1003: "duplicate (point, camera) observation", -1004: "out of host memory",
-          -1005: "RCCL communicator failure"}
+          -1005: "RCCL communicator failure",
+          -1006: "library / header ABI mismatch"}
 
 _lib = None
 
@@ -145,6 +149,12 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        if hasattr(L, "vlgba_abi_check") or not os.environ.get("VLGBA_LIB"):
+            rc = L.vlgba_abi_check(ABI_VERSION, *(ctypes.sizeof(s) for s in (
+                VlgbaProblem, VlgbaOptions, VlgbaStats, VlgbaStepInfo, VlgbaResectProblem)))
+            if rc != 0:
+                raise VlgbaError(f"{LIB_PATH} does not match this binding (ABI {ABI_VERSION}): "
+                                 "rebuild it with __graft_entry__.build()")
         _lib = L
     return _lib
 

@@ -37,7 +37,10 @@
 #include <thread>
 #include <vector>
 
-#define VLGBA_VERSION_STR "vlgba 0.1 (gfx950, fp64, MFMA-f64 Cholesky)"
+#define VLGBA_STR2(x) #x
+#define VLGBA_STR(x) VLGBA_STR2(x)
+#define VLGBA_VERSION_STR \
+    "vlgba 0.2 (abi " VLGBA_STR(VLGBA_ABI_VERSION) ", gfx950, fp64, MFMA-f64 Cholesky)"
 
 // ---------------------------------------------------------------------------
 // Device memory: a per-device caching allocator.  A solve's context makes a few
@@ -1576,6 +1579,10 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
             // "R:K": rank R's first K passes report a hand-off timeout (tests)
             int r = -1, k = 0;
             if (std::sscanf(ev, "%d:%d", &r, &k) == 2 && r == c->rank) c->debug_timeouts = k;
+            // a leftover variable would silently force re-solves: say so
+            if (c->debug_timeouts > 0)
+                std::fprintf(stderr, "[vlgba] VLGBA_DEBUG_SPIN_TIMEOUT=%s: rank %d's first %d "
+                             "passes report a hand-off timeout (test hook)\n", ev, r, k);
         }
         c->on_pass = o->on_pass;
         c->on_pass_user = o->on_pass_user;
@@ -1945,6 +1952,18 @@ int vlgba_version(char *buf, int len)
         buf[len - 1] = 0;
     }
     return n;
+}
+
+int vlgba_abi_check(int abi_version, long long sz_problem, long long sz_options,
+                    long long sz_stats, long long sz_step_info, long long sz_resect_problem)
+{
+    const bool ok = abi_version == VLGBA_ABI_VERSION &&
+                    sz_problem == (long long)sizeof(vlgba_problem) &&
+                    sz_options == (long long)sizeof(vlgba_options) &&
+                    sz_stats == (long long)sizeof(vlgba_stats) &&
+                    sz_step_info == (long long)sizeof(vlgba_step_info) &&
+                    sz_resect_problem == (long long)sizeof(vlgba_resect_problem);
+    return ok ? 0 : VLGBA_E_ABI;
 }
 
 int vlgba_get_unique_id(void *id128)

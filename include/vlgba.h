@@ -25,6 +25,15 @@ extern "C" {
 #define VLGBA_E_ORDER (-1003)    /* observation list not point-major / dups  */
 #define VLGBA_E_NOMEM (-1004)    /* host allocation failed                    */
 #define VLGBA_E_COMM (-1005)     /* RCCL failure                              */
+#define VLGBA_E_ABI (-1006)      /* caller built against another vlgba.h      */
+
+/* ABI of this header.  Bumped whenever a public struct, constant or entry
+ * point changes: 1 = the round-1/2 layouts; 2 = vlgba_stats.pinv_passes /
+ * spin_retries, vlgba_step_info.spin_retry, VLGBA_NPLAN 25.  Callers check it
+ * once at load time with VLGBA_ABI_CHECK() (the MEX gateways and the Python
+ * loader do): the library compares the version and the struct sizes the
+ * caller was compiled with against its own and returns 0 or VLGBA_E_ABI. */
+#define VLGBA_ABI_VERSION 2
 
 /* camera models (vlgba_problem.model) */
 #define VLGBA_MODEL_EUCLIDEAN 0   /* bundle_euclid.m: a = [w; T; (K)], num_a 6/7/10     */
@@ -336,6 +345,14 @@ int vlgba_debug_nd_plan(int m, int num_a, const int *blk_jk, int nb, int *bnd, i
 
 /* Library / device info: writes a NUL-terminated string, returns its length. */
 int vlgba_version(char *buf, int len);
+/* 0 when abi_version and the sizes of the public structs the caller was
+ * compiled with are the library's, else VLGBA_E_ABI (see VLGBA_ABI_VERSION). */
+int vlgba_abi_check(int abi_version, long long sz_problem, long long sz_options,
+                    long long sz_stats, long long sz_step_info, long long sz_resect_problem);
+#define VLGBA_ABI_CHECK()                                                                    \
+    vlgba_abi_check(VLGBA_ABI_VERSION, (long long)sizeof(vlgba_problem),                     \
+                    (long long)sizeof(vlgba_options), (long long)sizeof(vlgba_stats),        \
+                    (long long)sizeof(vlgba_step_info), (long long)sizeof(vlgba_resect_problem))
 int vlgba_device_count(void);
 
 /* ---- synthetic scenes on the GPU --------------

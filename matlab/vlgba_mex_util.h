@@ -23,7 +23,14 @@ static void vm_fail(const char *who, const char *what)
 static void vm_check(const char *who, int nrhs, const mxArray *prhs[], int want_in, int nlhs,
                      int max_out)
 {
+    static int abi_ok = 0;   /* libvlgba built from the header this gateway saw */
     int k;
+    if (!abi_ok) {
+        if (VLGBA_ABI_CHECK() != 0)
+            mexErrMsgIdAndTxt("vlgba:abi", "%s: libvlgba does not match vlgba.h (ABI %d)", who,
+                              VLGBA_ABI_VERSION);
+        abi_ok = 1;
+    }
     if (nrhs != want_in)
         mexErrMsgIdAndTxt("vlgba:args", "%s: %d inputs required", who, want_in);
     if (nlhs > max_out)

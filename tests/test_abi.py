@@ -37,6 +37,25 @@ def test_version_and_device_count_without_gpu():
     assert L.vlgba_device_count() >= 0
 
 
+def test_abi_check():
+    """VLGBA_ABI_CHECK: the loader checked the version and the
+    struct sizes; a caller built against another header is refused."""
+    import bundleadjustmentmatlab_amd as pkg
+    from bundleadjustmentmatlab_amd import _lib
+    L = pkg.lib()
+    sizes = [ctypes.sizeof(s) for s in (_lib.VlgbaProblem, _lib.VlgbaOptions, _lib.VlgbaStats,
+                                        _lib.VlgbaStepInfo, _lib.VlgbaResectProblem)]
+    assert L.vlgba_abi_check(_lib.ABI_VERSION, *sizes) == 0
+    assert L.vlgba_abi_check(_lib.ABI_VERSION - 1, *sizes) == -1006
+    old_stats = sizes[:2] + [sizes[2] - 8] + sizes[3:]    # the round-2 vlgba_stats
+    assert L.vlgba_abi_check(_lib.ABI_VERSION, *old_stats) == -1006
+    hdr = open(HDR).read()
+    assert f"#define VLGBA_ABI_VERSION {_lib.ABI_VERSION}" in hdr
+    buf = ctypes.create_string_buffer(128)
+    L.vlgba_version(buf, 128)
+    assert f"abi {_lib.ABI_VERSION}".encode() in buf.value
+
+
 def test_bad_arguments_rejected_before_device_work():
     import bundleadjustmentmatlab_amd as pkg
     from bundleadjustmentmatlab_amd._lib import VlgbaProblem
