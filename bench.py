@@ -226,6 +226,8 @@ def main():
                                   None)},
         "phases_ms": ph,
         "roofline": roof,
+        "whole_pass": whole_pass(plan, ms_step),
+        "solve_roofline": {k: roofs[k] for k in SOLVE_FLOPS if k in roofs},
         "solve_fallbacks": fallbacks,
         "cpu_baseline": cpu,
     }
@@ -408,6 +410,27 @@ def pmc_traffic(config, plan):
     return out, valu
 
 
+# solve timers (vlgba_kernel_name) -> their flop entry of the plan (vlgba_plan_info)
+SOLVE_FLOPS = {"k_factor_step": "solve_flops_factor", "k_cr_factor": "solve_flops_factor",
+               "k_syrk": "solve_flops_syrk", "k_backward": "solve_flops_back",
+               "k_cr_back": "solve_flops_back"}
+
+
+def whole_pass(plan, ms_per_pass):
+    """SURVEY.md 8.d's algorithmic bytes of one whole LM pass (phases (i) + (iv):
+    observations, point / camera gathers and arrays, W written once and read
+    twice, the per-point V / V*^-1 / eB arrays) against the pass time and the
+    HBM peak -- the whole-iteration fraction beside the dominant kernel's."""
+    NA = plan["num_a"]
+    N, n, m = plan["obs"], plan["points"], plan["cameras"]
+    nbytes = (2 * (N * 24 + N * 24 + n * 24 + m * 8 * NA) + N * 8 * 3 * NA * 3 +
+              n * 8 * (9 + 3 + 9) * 2)
+    gbs = nbytes / (ms_per_pass * 1e-3) / 1e9
+    return {"bytes": nbytes, "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": gbs / PEAK_HBM_GBS,
+            "source": "SURVEY.md 8.d algorithmic bytes per iteration / ms_per_step"}
+
+
 def kernel_roofline(name, tot_ms, calls, plan, n_passes):
     """Algorithmic bytes (HBM-bound kernels) or flops (MFMA / VALU kernels) per
     launch divided by the measured average launch duration.
@@ -445,21 +468,15 @@ def kernel_roofline(name, tot_ms, calls, plan, n_passes):
         nbytes = m * 8 * (NA + 45)
     elif name == "k_camera_update":
         nbytes = m * 8 * (3 * NA + 9)
-    elif name in ("k_cr_factor", "k_cr_update", "k_cr_back") and plan["cr_levels"]:
-        T = 64
-        if name == "k_cr_factor":     # potrf + trtri of L_e, two panel products
-            flops = plan["cr_elim"] * (2 * T ** 3 / 3 + 2 * 2 * T ** 3 + 2 * T * T)
-        elif name == "k_cr_update":   # two SYRK-shaped products + the fill product
-            flops = plan["cr_keep"] * (3 * 2 * T ** 3 + 4 * T * T)
-        else:                         # three tile GEMVs
-            flops = plan["cr_elim"] * 3 * 2 * T * T
-        flops /= per_pass
-        nbytes = 0.0
+    elif name in SOLVE_FLOPS:
+        # the reduced solve: the library's own count of its algorithmic flops
+        # per pass (vlgba_plan_info [25..27], ba_chol_setup: tile-dense potrf +
+        # trtri, GEMMs, GEMVs), spread over the pass's launches of that timer
+        flops = plan[SOLVE_FLOPS[name]]
     else:
         nbytes = 0.0
-    if name not in ("k_cr_factor", "k_cr_update", "k_cr_back"):
-        nbytes /= per_pass                  # once-per-pass kernels: bytes per launch
-        flops /= per_pass
+    nbytes /= per_pass                      # per launch (the timers count every launch)
+    flops /= per_pass
     gbs = nbytes / avg_s / 1e9 if nbytes else 0.0
     tfs = flops / avg_s / 1e12 if flops else 0.0
     hbm = dict(bound="hbm", achieved=gbs, peak=PEAK_HBM_GBS, unit="GB/s",
@@ -468,7 +485,7 @@ def kernel_roofline(name, tot_ms, calls, plan, n_passes):
     fl = dict(bound="mfma", achieved=tfs, peak=PEAK_F64_TFLOPS, unit="TFLOP/s",
               frac=tfs / PEAK_F64_TFLOPS, traffic=None, kernel=name,
               per_launch=f"{flops:.4g} flop", avg_launch_us=avg_s * 1e6)
-    if name.startswith("k_cr_"):
+    if name in SOLVE_FLOPS:
         return fl
     # a kernel with both figures is reported against the roof it is closer to
     return hbm if hbm["frac"] >= fl["frac"] else fl

@@ -398,7 +398,8 @@ class BundleAdjuster:
                  "chunk_eslots", "groups", "group_slots", "group_eslots", "blocks",
                  "tiles", "cr_levels", "cr_elim", "cr_keep", "ordered", "schur_terms",
                  "blob_words", "mfma", "cr_rows", "mfma_groups", "reordered", "long_points",
-                 "nd_arcs", "nd_sep_tiles")
+                 "nd_arcs", "nd_sep_tiles", "solve_flops_factor", "solve_flops_syrk",
+                 "solve_flops_back")
 
     def plan_info(self):
         """Execution-plan sizes of this rank (vlgba_plan_info)."""
@@ -418,12 +419,29 @@ class BundleAdjuster:
 # ---------------------------------------------------------------------------
 # drop-in drivers
 # ---------------------------------------------------------------------------
+def euclid_obs_adjuster(K, m, n, obs_pt, obs_cam, obs_x, *varargin, num_vis=0.0, device=0,
+                        rank=0, world_size=1, comm_id=None, semantics="mex", **solver):
+    """The BundleAdjuster that bundle_euclid_obs would create for this problem
+    and these options (its structure only: no parameter values), so a caller
+    can build it ahead of time -- the host plan of vlgba_create runs with the
+    GIL released (ctypes), e.g. on a worker thread while the previous solve
+    runs (incremental.py) -- and hand it to bundle_euclid_obs(adjuster=...)."""
+    o = parse_options(m, n, varargin, nomex=semantics == "nomex")
+    return BundleAdjuster(K, obs_pt, obs_cam, obs_x, n, 6 + o["num_variableK"],
+                          fix_structure=o["fix_structure"], fix_motion=o["fix_motion"],
+                          pivot=o["pivot"] if o["fix_pivot"] else None, verbose=o["verbose"],
+                          num_vis=num_vis, device=device, rank=rank, world_size=world_size,
+                          comm_id=comm_id, semantics=semantics, **solver)
+
+
 def bundle_euclid_obs(K, Te, w, Xe, obs_pt, obs_cam, obs_x, *varargin, num_vis=0.0, device=0,
                       rank=0, world_size=1, comm_id=None, return_stats=False,
-                      semantics="mex", **solver):
+                      semantics="mex", adjuster=None, **solver):
     """bundle_euclid on a COO observation list (0-based point / camera ids).
     ``solver`` keywords go to BundleAdjuster (parity, stop_rel, max_iter,
-    max_iter2, lambda0, solver, ordered, schur_kernel)."""
+    max_iter2, lambda0, solver, ordered, schur_kernel).  ``adjuster``: a handle
+    made beforehand by euclid_obs_adjuster for the same problem and options
+    (or a concurrent.futures.Future of one); it is used and closed here."""
     K, Te, w, Xe = _F(K), _F(Te), _F(w), _F(Xe)
     m, n = w.shape[1], Xe.shape[1]
     nomex = semantics == "nomex"
@@ -432,11 +450,18 @@ def bundle_euclid_obs(K, Te, w, Xe, obs_pt, obs_cam, obs_x, *varargin, num_vis=0
     num_a = 6 + nvk
     a = pack_a(K, Te, w, nvk)
     b = _F(Xe[0:3])
-    with BundleAdjuster(K, obs_pt, obs_cam, obs_x, n, num_a,
-                        fix_structure=o["fix_structure"], fix_motion=o["fix_motion"],
-                        pivot=o["pivot"] if o["fix_pivot"] else None, verbose=o["verbose"],
-                        num_vis=num_vis, device=device, rank=rank, world_size=world_size,
-                        comm_id=comm_id, semantics=semantics, **solver) as ba:
+    if adjuster is not None:
+        if solver:
+            raise ValueError("bundle_euclid_obs: solver options belong to the prebuilt adjuster")
+        ba = adjuster.result() if hasattr(adjuster, "result") else adjuster
+        if (ba.m, ba.n, ba.num_a, ba.num_obs) != (m, n, num_a, len(obs_pt)):
+            ba.close()
+            raise ValueError("bundle_euclid_obs: the prebuilt adjuster is for another problem")
+    else:
+        ba = euclid_obs_adjuster(K, m, n, obs_pt, obs_cam, obs_x, *varargin, num_vis=num_vis,
+                                 device=device, rank=rank, world_size=world_size,
+                                 comm_id=comm_id, semantics=semantics, **solver)
+    with ba:
         ba.set_params(a, b)
         err, st = ba.run()
         a, b = ba.get_params()

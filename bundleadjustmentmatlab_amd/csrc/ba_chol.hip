@@ -2148,6 +2148,7 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
     int nt = (int)(d->lds / NB);
     d->nt = nt;
     d->h_tfirst = new int[nt];
+    d->fl_factor = d->fl_syrk = d->fl_back = 0.0;
     // every lower tile for the measurement mode (1) and the sequential parity
     // solve (3); the envelope otherwise (0 auto, 2 envelope without CR, 4 ND)
     const bool all_tiles = d->dense_solve == 1 || d->dense_solve == 3;
@@ -2213,6 +2214,24 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
             act.swap(next);
         }
         d->cr_nlev = (int)eptr.size() - 1;
+        {   // the CR's algorithmic flops (ba_dev::fl_factor): per elimination
+            // record (e, p, q) the factor + inverse of D_e, y_e and one panel per
+            // neighbour; per kept record (k, e-, e+, k2) the update of D_k and r_k
+            // by its eliminated neighbours and the fill towards k2; the back
+            // substitution's GEMVs
+            const double t = d->cr32 ? T32 : NB;
+            const double potri = 2.0 * t * t * t / 3.0, gemm = 2.0 * t * t * t, gemv = 2.0 * t * t;
+            d->fl_factor = d->fl_syrk = d->fl_back = 0.0;
+            for (size_t i = 0; i < elim.size(); i += 3) {
+                const double nbr = (elim[i + 1] >= 0) + (elim[i + 2] >= 0);
+                d->fl_factor += potri + gemv + nbr * gemm;
+                d->fl_back += (nbr + 1) * gemv;
+            }
+            for (size_t i = 0; i < keep.size(); i += 4) {
+                const double nbe = 1 + (keep[i + 2] >= 0);
+                d->fl_factor += nbe * (gemm + gemv) + (keep[i + 3] >= 0) * gemm;
+            }
+        }
         if (d->cr32) {   // the fused levels' records (see k_cr32_level)
             const int nl = d->cr_nlev;
             std::vector<int> frec, srec, fptr(nl + 1, 0), sptr(nl + 1, 0);
@@ -2437,6 +2456,8 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
             }
             pptr.push_back((int)rec.size() / 3);
         }
+        d->fl_syrk = (double)work * 2.0 * NB * NB * NB +
+                     (double)(pairs.size() / 2) * 2.0 * NB * NB;
         d->nd_npair = (int)pairs.size() / 2;
         d->nd_nrec = (int)rec.size() / 3;
         auto up = [&](int **dst, const std::vector<int> &v) -> int {
@@ -2457,6 +2478,26 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
         TRY_RC(dev_alloc(&d->nd_x, sizeof(double) * (size_t)d->slds));
         TRY_RC(dev_alloc(&d->nd_part, sizeof(double) * ((size_t)d->nd_nrec + 1) * (NB * NB + NB)));
         VLGBA_CHECK(hipStreamSynchronize(d->stream));
+    }
+    {   // the envelope's algorithmic flops (see ba_dev::fl_factor; the CR's: above)
+        const double t = NB;
+        const double potri = 2.0 * t * t * t / 3.0, gemm = 2.0 * t * t * t, gemv = 2.0 * t * t;
+        for (int k = 0; k < nt && !d->cr_nlev && d->dense_solve != 3; k++) {
+            const double T = ptr[k + 1] - ptr[k];
+            // factor + inverse, y_k, T panels and their rhs updates, the trailing
+            // pairs of column k (applied in step k + 1; an arc column's separator
+            // x separator pairs go to the separator SYRK instead)
+            double nsr = 0;
+            if (nd && k < s0)
+                for (int q = ptr[k]; q < ptr[k + 1]; q++) nsr += list[q] >= s0;
+            d->fl_factor += potri + gemv + T * (gemm + gemv) +
+                            (T * (T + 1) / 2 - nsr * (nsr + 1) / 2) * gemm;
+            d->fl_back += (T + 1) * gemv;
+        }
+        if (d->cr_nlev > 0 && d->cr_fused) {   // one CR launch: timed as k_cr_factor
+            d->fl_factor += d->fl_back;
+            d->fl_back = 0.0;
+        }
     }
     d->pan_ptr_h = new int[nt + 1];
     for (int k = 0; k <= nt; k++) d->pan_ptr_h[k] = ptr[k];

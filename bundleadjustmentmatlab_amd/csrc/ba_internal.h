@@ -165,6 +165,14 @@ struct ba_dev {
     int *nd_rec;                  // device [nrec][3] (pair, kofs, kcnt)
     int *nd_klist;                // device: the arc columns of the records
     double *nd_part;              // [nrec][64*64 + 64] per-record L_i L_j^T | L_i y
+    // algorithmic flops of one reduced solve (ba_chol_setup; bench.py's roofline
+    // of the solve kernels): tile-dense potrf + trtri of the diagonal tiles,
+    // panel / trailing / fill / SYRK GEMMs and the triangular GEMVs, each counted
+    // once (the redundant factorisations of the role-split records are not).
+    // fl_factor: the launches timed as k_factor_step / k_cr_factor (with the
+    // one-launch CR its back substitution too); fl_syrk: k_sep_update /
+    // k_sep_reduce; fl_back: k_backward(_all) / the per-level CR back launches
+    double fl_factor, fl_syrk, fl_back;
     // reductions: partial sums per block of the reducing kernels, in fixed order
     double *part;      // [3][PART_MAX]
     double *scal;      // [8] : 0 old_sse, 1 new_sse, 2 dpg cams, 3 dpg pts, 4 non-positive

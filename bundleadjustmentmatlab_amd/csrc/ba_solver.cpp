@@ -2218,7 +2218,9 @@ int vlgba_plan_info(vlgba_ctx *c, long long *info, int len)
                                       d.blob_words, d.mfma,
                                       d.cr_nlev ? (d.cr32 ? d.tb32 : 64) : 0,
                                       d.ngrp_mf, c->pperm.empty() ? 0 : 1, d.nl, d.nd_np,
-                                      d.nd_np ? d.nt - d.nd_a0[d.nd_np] : 0};
+                                      d.nd_np ? d.nt - d.nd_a0[d.nd_np] : 0,
+                                      (long long)d.fl_factor, (long long)d.fl_syrk,
+                                      (long long)d.fl_back};
     for (int k = 0; k < len && k < VLGBA_NPLAN; k++) info[k] = v[k];
     return VLGBA_NPLAN;
 }

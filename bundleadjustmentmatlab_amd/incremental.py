@@ -17,14 +17,23 @@ problem sizes and its visibility subsets are the reference's.
 
 ``incremental_bundle(scene)`` returns the per-solve log and the final
 reconstruction.
+
+The stand-ins make the STRUCTURE of every solve (which cameras, points and
+observations it adjusts) independent of the parameter values, so the replay
+knows solve k+1's problem before solve k ends: a worker thread cuts its
+observation subset and builds its libvlgba context (the host plan of
+vlgba_create, which runs with the GIL released) while solve k runs on the GPU
+("reuse across growing calls").  Only the parameter
+upload and the LM loop stay on the replay's critical path.
 """
 from __future__ import annotations
 
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
-from .bundle import bundle_euclid_obs, bundle_euclid_resect
+from .bundle import bundle_euclid_obs, bundle_euclid_resect, euclid_obs_adjuster
 from .dist import choose_shards, run_sharded
 from .evaluation import align_scene, vl_irodr, vl_rodr
 
@@ -50,9 +59,27 @@ def _subset_obs(sc, cams, pts, cam_on=None, pt_on=None):
     return pmap[sc.obs_pt[keep]], cmap[sc.obs_cam[keep]], sc.obs_x[keep]
 
 
+def _solve_sets(sc, init_cams):
+    """The replay's bundle_euclid calls in order, as (tag, j, camera mask,
+    point mask): incr_reconstruction.m:223-341 with this module's stand-ins --
+    camera j joins the status set, a solve over the points reconstructed so
+    far, the points seen by >= 2 cameras of the set join them, a second solve
+    (the main loop checks every prefetched set against its own state)."""
+    status = np.zeros(sc.m, dtype=bool)
+    status[list(init_cams)] = True
+    tri = np.bincount(sc.obs_pt, weights=status[sc.obs_cam], minlength=sc.n) >= 2
+    for j in range(sc.m):
+        if status[j]:
+            continue
+        status[j] = True
+        yield "before-triangulation", j, status.copy(), tri.copy()
+        tri |= np.bincount(sc.obs_pt, weights=status[sc.obs_cam], minlength=sc.n) >= 2
+        yield "after-triangulation", j, status.copy(), tri.copy()
+
+
 def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, device=0,
                        verbose=False, devices=None, shards=None, obs_per_shard=None,
-                       progress=None):
+                       progress=None, prefetch=True):
     """Replay the incremental reconstruction's BA sequence on scene ``sc``
     (scene.Scene).  Cameras ``init_cams`` form the initial two-view
     reconstruction (VLmvg.m's two_view step); every other camera is added in
@@ -66,11 +93,18 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
     collectives between ranks sharing one); without it every solve runs on
     ``device``.
 
+    ``prefetch`` (fix_calibration, one-rank solves): the next solve's
+    observation subset and context are built on a worker thread while the
+    current solve runs (module docstring); the results are the same as
+    without it (the same contexts, built earlier).
+
     Returns dict(solves=[...], resections=[...], K, T, w, X, status) where each
     solve records the cameras / points / observations it adjusted, its error_
-    trace, LM passes and wall seconds, and each resection the added camera's
-    one-camera refinement (estimate_camera.m:247-253).  ``progress(solves)``,
-    if given, is called after every solve with the solve log so far."""
+    trace, LM passes and wall seconds (``wait_create``: of them, the wait for
+    the prefetched context; ``create``: the worker's time building it), and each
+    resection the added camera's one-camera refinement
+    (estimate_camera.m:247-253).  ``progress(solves)``, if given, is called
+    after every solve with the solve log so far."""
     m, n = sc.m, sc.n
     K = np.array(sc.K, dtype=np.float64)
     T = np.array(sc.T0, dtype=np.float64)
@@ -84,19 +118,55 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
     X[3, tri] = 1.0
     opts = ("fix_calibration",) if fix_calibration else ()
     solves, resections = [], []
+    ndev = len(devices) if devices else 1
+
+    def world_of(nobs):
+        if not devices:
+            return 1
+        return (shards(nobs) if shards else
+                choose_shards(nobs, ndev, **({"obs_per_shard": obs_per_shard}
+                                             if obs_per_shard else {})))
+
+    def build(item):
+        """worker: the solve's subset and (one rank) its context"""
+        tag, j, cam_on, pt_on = item
+        cams, pts = np.nonzero(cam_on)[0], np.nonzero(pt_on)[0]
+        if len(pts) == 0 or len(cams) < 2:
+            return item, None, None, 0.0
+        sub = _subset_obs(sc, cams, pts, cam_on, pt_on)
+        if world_of(len(sub[0])) > 1:
+            return item, sub, None, 0.0
+        t0 = time.perf_counter()
+        ba_ = euclid_obs_adjuster(K[:, cams], len(cams), len(pts), sub[0], sub[1], sub[2], *opts,
+                                  num_vis=float(len(sub[0])),
+                                  device=devices[0] if devices else device)
+        return item, sub, ba_, time.perf_counter() - t0
+
+    use_pf = prefetch and fix_calibration      # K (the context's) is constant then
+    pool = ThreadPoolExecutor(max_workers=1) if use_pf else None
+    seq = _solve_sets(sc, init_cams) if use_pf else None
+    pending = [pool.submit(build, next(seq))] if use_pf else []
 
     def ba(tag, j):
         cams = np.nonzero(status)[0]
         pts = np.nonzero(X[3] == 1)[0]                   # X3d_index (:252)
+        t0 = time.perf_counter()
+        pre = create_s = sub = None
+        if pending:
+            item, sub, pre, create_s = pending.pop().result()
+            nxt = next(seq, None)                        # the next solve's context, built
+            if nxt is not None:                          # while this one runs
+                pending.append(pool.submit(build, nxt))
+            if item[0] != tag or item[1] != j or not (np.array_equal(item[2], status) and
+                                                      np.array_equal(item[3], X[3] == 1)):
+                if pre is not None:
+                    pre.close()
+                raise RuntimeError("incremental_bundle: prefetched solve set out of step")
         if len(pts) == 0 or len(cams) < 2:
             return
-        pt, cam, ox = _subset_obs(sc, cams, pts, status, X[3] == 1)
-        t0 = time.perf_counter()
-        world = 1
-        if devices:
-            world = (shards(len(pt)) if shards else
-                     choose_shards(len(pt), len(devices),
-                                   **({"obs_per_shard": obs_per_shard} if obs_per_shard else {})))
+        wait = time.perf_counter() - t0
+        pt, cam, ox = sub if sub is not None else _subset_obs(sc, cams, pts, status, X[3] == 1)
+        world = world_of(len(pt))
         if world > 1:
             nvk = 0 if fix_calibration else 4
             Kc, Tc, wc, Xc = K[:, cams], T[:, cams], w[:, cams], X[:, pts]
@@ -109,7 +179,7 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
             K_, T_, w_, X_, err, st = bundle_euclid_obs(
                 K[:, cams], T[:, cams], w[:, cams], X[:, pts], pt, cam, ox, *opts,
                 num_vis=float(len(pt)), device=devices[0] if devices else device,
-                return_stats=True)
+                return_stats=True, **({"adjuster": pre} if pre is not None else {}))
         secs = time.perf_counter() - t0
         if align:                                        # :273 align_scene(T_, Omega_, X_ba_)
             T_, w_, X_ = align_scene(T_, w_, X_)
@@ -117,7 +187,9 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
         X[:, pts] = X_
         solves.append(dict(tag=tag, camera=int(j), cameras=len(cams), points=len(pts),
                            observations=len(pt), error=np.asarray(err), passes=st.iterations,
-                           accepted=st.accepted, seconds=secs, shards=world))
+                           accepted=st.accepted, seconds=secs, shards=world,
+                           lm_seconds=float(st.seconds), wait_create=wait,
+                           create=create_s))
         if verbose:
             print(f"[incremental] camera {j} {tag}: {len(cams)} cams {len(pts)} pts "
                   f"{len(pt)} obs  error_ {err[0]:.4g} -> {err[-1]:.4g}  {st.iterations} passes")
@@ -139,22 +211,33 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
         resections.append(dict(camera=int(j), observations=int(sel.sum()),
                                error=errs[0], seconds=time.perf_counter() - t0))
 
-    for j in range(m):                                   # :223
-        if status[j]:
-            continue
-        status[j] = True
-        s_, R_, t_ = _similarity(sc, X)                  # ground truth -> current frame
-        Rc = vl_rodr(sc.w0[:, j]) @ R_.T                 # DLT stand-in: the perturbed
-        w[:, j] = vl_irodr(Rc)                           # pose in the current frame
-        T[:, j] = s_ * sc.T0[:, j] - Rc @ t_
-        resect(j)                                        # :230, estimate_camera.m:247-253
-        ba("before-triangulation", j)                    # :250-267
-        nvis = np.bincount(sc.obs_pt, weights=status[sc.obs_cam], minlength=n).astype(int)
-        new = (X[3] == 0) & (nvis >= 2)                  # :281-296 triangulation stand-in
-        s_, R_, t_ = _similarity(sc, X)
-        X[:3, new] = s_ * R_ @ sc.X0[:3, new] + t_[:, None]
-        X[3, new] = 1.0
-        ba("after-triangulation", j)                     # :300-318
+    try:
+        for j in range(m):                               # :223
+            if status[j]:
+                continue
+            status[j] = True
+            s_, R_, t_ = _similarity(sc, X)              # ground truth -> current frame
+            Rc = vl_rodr(sc.w0[:, j]) @ R_.T             # DLT stand-in: the perturbed
+            w[:, j] = vl_irodr(Rc)                       # pose in the current frame
+            T[:, j] = s_ * sc.T0[:, j] - Rc @ t_
+            resect(j)                                    # :230, estimate_camera.m:247-253
+            ba("before-triangulation", j)                # :250-267
+            nvis = np.bincount(sc.obs_pt, weights=status[sc.obs_cam], minlength=n).astype(int)
+            new = (X[3] == 0) & (nvis >= 2)              # :281-296 triangulation stand-in
+            s_, R_, t_ = _similarity(sc, X)
+            X[:3, new] = s_ * R_ @ sc.X0[:3, new] + t_[:, None]
+            X[3, new] = 1.0
+            ba("after-triangulation", j)                 # :300-318
+    finally:
+        for f in pending:                                # a prefetched context not used
+            try:
+                pre = f.result()[2]
+            except Exception:                            # noqa: BLE001 -- already failing
+                pre = None
+            if pre is not None:
+                pre.close()
+        if pool is not None:
+            pool.shutdown()
     return dict(solves=solves, resections=resections, K=K, T=T, w=w, X=X, status=status)
 
 

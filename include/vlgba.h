@@ -29,7 +29,7 @@ extern "C" {
 
 /* ABI of this header.  Bumped whenever a public struct, constant or entry
  * point changes: 1 = the round-1/2 layouts; 2 = vlgba_stats.pinv_passes /
- * spin_retries, vlgba_step_info.spin_retry, VLGBA_NPLAN 25.  Callers check it
+ * spin_retries, vlgba_step_info.spin_retry, VLGBA_NPLAN 28.  Callers check it
  * once at load time with VLGBA_ABI_CHECK() (the MEX gateways and the Python
  * loader do): the library compares the version and the struct sizes the
  * caller was compiled with against its own and returns 0 or VLGBA_E_ABI. */
@@ -237,9 +237,13 @@ const char *vlgba_kernel_name(int k);
  * reordered internally (1: short tracks first, input order restored at the
  * API) [22] long tracks (more views than a Schur chunk holds: segment chunks
  * + the long-track kernels) [23] nested-dissection arcs of the envelope
- * Cholesky (0: natural camera order) [24] its separator tiles.  Writes
+ * Cholesky (0: natural camera order) [24] its separator tiles [25] the
+ * reduced solve's algorithmic flops in the launches timed as k_factor_step /
+ * k_cr_factor (the one-launch cyclic reduction: all of it) [26] in the
+ * separator SYRK (k_syrk) [27] in the backward solve (k_backward / k_cr_back):
+ * tile-dense potrf + trtri, GEMMs and GEMVs, each counted once.  Writes
  * min(len, VLGBA_NPLAN) entries, returns VLGBA_NPLAN. */
-#define VLGBA_NPLAN 25
+#define VLGBA_NPLAN 28
 int vlgba_plan_info(vlgba_ctx *ctx, long long *info, int len);
 
 /* ---- stage entries with the reference MEX argument layouts ---------------

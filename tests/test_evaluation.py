@@ -73,3 +73,47 @@ def test_incremental_subset_and_similarity():
     X[3] = 1.0
     s, R2, t = _similarity(sc, X)
     assert abs(s - 2.5) < 1e-9 and np.allclose(R2, R, atol=1e-9) and np.allclose(t, [1, 2, 3])
+
+
+@pytest.mark.parametrize("prefetch", [True, False])
+def test_incremental_prefetch_bookkeeping(monkeypatch, prefetch):
+    """The replay's solve sets (incremental._solve_sets, which the prefetching
+    worker builds contexts from) follow the main loop's own status / X3d
+    bookkeeping call by call, and every call gets the context built for its
+    own problem (the GPU solves stubbed: parameters returned unchanged)."""
+    from types import SimpleNamespace
+
+    import bundleadjustmentmatlab_amd.incremental as inc
+    sc = make_config("cfg5", m=12, seed=3)
+    made, calls = [], []
+
+    class FakeAdjuster:
+        def __init__(self, K, m, n, pt, cam, ox, *opts, **kw):
+            self.key = (m, n, len(pt), ox.tobytes())
+            self.closed = False
+            made.append(self)
+
+        def close(self):
+            self.closed = True
+
+    def fake_solve(K, T, w, X, pt, cam, ox, *opts, adjuster=None, return_stats=False, **kw):
+        if prefetch:
+            assert adjuster is not None and adjuster.key == (K.shape[1], X.shape[1], len(pt),
+                                                             ox.tobytes())
+            adjuster.close()
+        else:
+            assert adjuster is None
+        calls.append((K.shape[1], X.shape[1], len(pt)))
+        st = SimpleNamespace(iterations=1, accepted=1, seconds=0.0)
+        return K, T, w, X, np.array([1.0, 0.5]), st
+
+    def fake_resect(K, T, w, Xs, xs, *opts, **kw):
+        return K, T, w, [np.array([1.0])]
+
+    monkeypatch.setattr(inc, "euclid_obs_adjuster", FakeAdjuster)
+    monkeypatch.setattr(inc, "bundle_euclid_obs", fake_solve)
+    monkeypatch.setattr(inc, "bundle_euclid_resect", fake_resect)
+    res = inc.incremental_bundle(sc, prefetch=prefetch)
+    assert len(calls) == len(res["solves"]) == 2 * (sc.m - 2)
+    assert [q["cameras"] for q in res["solves"][::2]] == list(range(3, sc.m + 1))
+    assert len(made) == (len(calls) if prefetch else 0) and all(a.closed for a in made)

@@ -12,11 +12,11 @@
   replay in parity mode is bit-identical to the oracle's solve on the same
   inputs (error_ and outputs); the default fast path matches each solve's
   error_(1) to 1e-12 and, for EVERY solve re-run under a tightened stop rule,
-  its converged cost to 1e-6 relative of the MATLAB-semantics oracle -- or,
-  on a solve whose own FD noise floor is wider, to twice that floor: the
-  spread of three rounding variants of the reference (pinv / pinv, formula
-  V*^-1 + Cholesky, pinv + Cholesky), which the test derives per solve and
-  prints.
+  its converged answer is a converged point of the MATLAB-semantics oracle's
+  LM and the oracle's converged answer one of the GPU's, both to 1e-6
+  relative (the criterion of tests/test_gpu_converged.py: each rounding
+  variant of the reference converges to its own limit point, a few 1e-6
+  apart, so the bar is on the continuations, not on the limit points).
 """
 import numpy as np
 import pytest
@@ -74,7 +74,8 @@ def _replay(gpu, sc, **solver):
 
     inc.bundle_euclid_obs = spy
     try:
-        res = inc.incremental_bundle(sc)
+        # solver options go into each call: no prefetched contexts
+        res = inc.incremental_bundle(sc, prefetch=not solver)
     finally:
         inc.bundle_euclid_obs = orig
     return res, calls
@@ -111,44 +112,38 @@ def test_cfg5_replay_parity_every_solve(gpu, oracle):
 @pytest.mark.timeout(900)
 def test_cfg5_replay_fast_path_per_solve(gpu, oracle):
     """The default path through the replay: each solve's error_(1) equals the
-    oracle's on the same inputs (1e-12) and, re-run with a tightened stop
-    rule, its converged cost matches the MATLAB-semantics oracle to 1e-6 or
-    twice the solve's own noise floor (module docstring)."""
+    oracle's on the same inputs (1e-12); re-run with a tightened stop rule,
+    the MATLAB-semantics oracle (SVD pinv of V*_i and of S) started at the
+    GPU's answer lowers its cost by <= 1e-6 relative, and the GPU started at
+    the oracle's converged answer lowers the oracle's cost by <= 1e-6."""
     from bundleadjustmentmatlab_amd.bundle import bundle_euclid_obs
     from bundleadjustmentmatlab_amd.scene import make_config
     sc = make_config("cfg5")
     res, calls = _replay(gpu, sc)
     kw = dict(stop_rel=1e-9, max_iter=100, max_iter2=30)
-    wide = []
+    worst = [0.0, 0.0]
     for q, c in enumerate(calls):
         x, vis = _dense(c)
         ref = oracle.bundle_euclid_ref(c["K"], c["T"], c["w"], c["X"], x, "visibility", vis,
                                        *c["opts"], form="sparse")
         e = c["out"][4]
         assert abs(e[0] - ref[4][0]) <= 1e-12 * ref[4][0], q
-        tight = bundle_euclid_obs(c["K"], c["T"], c["w"], c["X"], c["pt"], c["cam"], c["ox"],
-                                  *c["opts"], num_vis=float(len(c["pt"])), **kw)
-        def variants(combos):
-            return [oracle.bundle_euclid_ref(c["K"], c["T"], c["w"], c["X"], x, "visibility",
-                                             vis, *c["opts"], form="sparse", vinv=v, solve=s_,
-                                             sums=su, **kw)[4][-1] for v, s_, su in combos]
-
-        # the h = 1e-10 forward differences leave a noise floor at the minimum:
-        # rounding variants of the reference itself stop up to ~1e-5 apart
-        # (a 3-camera solve, 12 variants: 8.6e-6).  Bar: the GPU's converged
-        # cost within 1e-6 relative of the band the variants span -- three
-        # variants first, all twelve (vinv x solve x LM sums) if that is not
-        # enough to decide
-        fin = variants((("pinv", "pinv", "blas"), ("formula", "chol", "blas"),
-                        ("pinv", "chol", "blas")))
-        g = tight[4][-1]
-        out = max(min(fin) - g, g - max(fin), 0.0) / fin[0]
-        if out > 1e-6:
-            import itertools
-            fin += variants(itertools.product(("pinv", "formula"), ("pinv", "chol", "seq"),
-                                              ("blas", "seq")))
-            out = max(min(fin) - g, g - max(fin), 0.0) / fin[0]
-            wide.append((q, len(fin), round((max(fin) - min(fin)) / fin[0], 8)))
-        assert out <= 1e-6, (q, g, sorted(fin))
-    print(f"cfg5: {len(calls)} solves within 1e-6 of the reference band; decided on 15 "
-          f"variants (solve, variants, band width): {wide}")
+        nv = float(len(c["pt"]))
+        g = bundle_euclid_obs(c["K"], c["T"], c["w"], c["X"], c["pt"], c["cam"], c["ox"],
+                              *c["opts"], num_vis=nv, **kw)
+        r = oracle.bundle_euclid_ref(c["K"], c["T"], c["w"], c["X"], x, "visibility", vis,
+                                     *c["opts"], form="sparse", **kw)
+        # the oracle from the GPU's answer, the GPU from the oracle's
+        rg = oracle.bundle_euclid_ref(g[0], g[1], g[2], g[3], x, "visibility", vis, *c["opts"],
+                                      form="sparse", **kw)
+        gr = bundle_euclid_obs(r[0], r[1], r[2], r[3], c["pt"], c["cam"], c["ox"], *c["opts"],
+                               num_vis=nv, **kw)
+        eg = g[4][-1] if len(g[4]) else e[-1]
+        er = r[4][-1] if len(r[4]) else ref[4][-1]
+        assert abs(rg[4][0] - eg) <= 1e-12 * eg if len(rg[4]) else True, q   # one cost
+        d1 = (eg - rg[4][-1]) / eg if len(rg[4]) else 0.0
+        d2 = (er - gr[4][-1]) / er if len(gr[4]) else 0.0
+        worst = [max(worst[0], d1), max(worst[1], d2)]
+        assert d1 <= 1e-6 and d2 <= 1e-6, (q, eg, er, d1, d2)
+    print(f"cfg5: {len(calls)} solves; largest drop of the oracle's LM from the GPU's answer "
+          f"{worst[0]:.2e}, of the GPU's LM from the oracle's answer {worst[1]:.2e}")
