@@ -329,6 +329,7 @@ def bench_incremental(args):
     present (1 -> 8 elastic point sharding: rank threads, RCCL between
     distinct GPUs).  A step is one whole replay; value = BA solves/s."""
     import torch
+    from bundleadjustmentmatlab_amd.dist import OBS_PER_SHARD
     from bundleadjustmentmatlab_amd.incremental import incremental_bundle
     from bundleadjustmentmatlab_amd.scene import make_config
     ndev = max(1, torch.cuda.device_count())
@@ -381,6 +382,28 @@ def bench_incremental(args):
         "time_split_s": {"solves": sum(q["seconds"] for q in sol),
                          "resections": sum(q["seconds"] for q in res["resections"]),
                          "replay": dt / args.steps},
+        # where a replay's solve time goes: the LM loops (vlgba_run: device passes
+        # + the host's per-pass decisions), the wait for the context the worker
+        # thread built ahead (its host plan + uploads; create_worker is the
+        # worker's own time, overlapped with the previous solve), and the rest
+        # of the solve calls on the replay thread (parameter upload / download,
+        # packing); host_glue = the replay's numpy stand-ins around the solves
+        "host_device_split_s": {
+            "lm_loops": sum(q["lm_seconds"] for q in sol),
+            "wait_for_context": sum(q["wait_create"] for q in sol),
+            "create_worker": sum(q["create"] or 0.0 for q in sol),
+            "solve_calls_rest": sum(q["seconds"] - q["lm_seconds"] - q["wait_create"]
+                                    for q in sol),
+            "host_glue": dt / args.steps - sum(q["seconds"] for q in sol) -
+                         sum(q["seconds"] for q in res["resections"])},
+        "elastic": {"obs_per_shard": OBS_PER_SHARD, "max_solve_observations":
+                    max(q["observations"] for q in sol),
+                    "note": "a solve shards only above 2 x obs_per_shard observations "
+                            "(dist.py: the crossover of the sharded kernels' 0.18 us/obs "
+                            "against two all-reduces per pass)" +
+                            ("; every solve of this scene is below it, so the elastic "
+                             "count is 1 throughout" if max(q["observations"] for q in sol)
+                             < 2 * OBS_PER_SHARD else "")},
     }
     print(json.dumps(out), flush=True)
 

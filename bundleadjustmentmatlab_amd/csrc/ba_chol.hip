@@ -2308,10 +2308,23 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
         const std::vector<int> minK = nd_min_cam(m, blk_jk, nb);
         int bnd[BA_ND_MAX + 1], crit = INT_MAX;
         const int K = off && d->dense_solve == 0 ? 0 : nd_choose(minK, m, na, bnd, crit);
-        const bool take = K > 0 && (d->dense_solve == 4 || (nt >= 8 && 4 * crit <= 3 * nt));
+        bool take = K > 0 && (d->dense_solve == 4 || (nt >= 8 && 4 * crit <= 3 * nt));
+        // setup budget: the separator SYRK's host lists cost
+        // O(ns^2 s0) and its partials (pairs + CUs) x 33 KB of device memory --
+        // a graph with a wide separator keeps the natural order instead
+        long long npair_max = 0, setup_ops = 0;
+        if (K > 0) {
+            const nd_cost_t c = nd_cost(minK, na, bnd, K);
+            long long s0t = 0;
+            for (int t = 0; t < K; t++) s0t += c.n[t];
+            npair_max = (long long)c.ns * (c.ns + 1) / 2;
+            setup_ops = npair_max * s0t;
+            if (npair_max > BA_ND_MAX_PAIRS || setup_ops > BA_ND_MAX_SETUP) take = false;
+        }
         if (ev && ev[0] == 'v')
-            std::fprintf(stderr, "[vlgba] nested dissection: natural %d tiles, %d arcs -> chain %d%s\n",
-                         nt, K, crit, take ? "" : " (not taken)");
+            std::fprintf(stderr, "[vlgba] nested dissection: natural %d tiles, %d arcs -> chain %d, "
+                         "<= %lld separator pairs, %lld setup checks%s\n", nt, K, crit, npair_max,
+                         setup_ops, take ? "" : " (not taken)");
         if (take) {
             crow.assign(m, -1);
             long long row = 0;

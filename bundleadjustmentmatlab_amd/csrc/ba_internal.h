@@ -69,6 +69,10 @@ struct ba_flags {
 #ifndef BA_ND_MAX
 #define BA_ND_MAX 8
 #endif
+// ... and at most this many separator tile pairs (their SYRK partials: 33 KB
+// each) / host checks (pairs x arc tiles) in its setup, else the natural order
+#define BA_ND_MAX_PAIRS 16384LL
+#define BA_ND_MAX_SETUP (1LL << 26)
 struct ba_camred {
     const int *cam_eptr, *cam_eslots;
     const double *upart;
@@ -219,11 +223,16 @@ struct ba_dev {
     int ngrp_mf;                      // leading MFMA groups
     // long tracks (points [p_long, n), ba_solver.cpp build_plan): segment
     // chunks [nch_reg, nch), their V / eB partials, Schur tiles, update sums
-    int nch_reg, nl, ntile_long, p_long;
+    int nch_reg, nl, p_long;
     int *seg_pt, *seg_long;           // [nch - nch_reg] point, long index
     int *long_pt, *long_o0, *long_seg0;   // [nl], [nl+1] obs range, [nl+1] segments
-    int *long_sbase, *long_ebase;     // [nl] first group slot / group e-slot
-    int *long_tiles;                  // [ntile_long][3] (long, a tile, b tile)
+    int *long_ebase;                  // [nl] first group e-slot
+    // per camera its long-track observations in track order (k_schur_reduce
+    // merges the lists of a block's two cameras): [m + 1], [nlobs], [nlobs]
+    int *cam_lptr, *cam_lobs, *cam_ltrk;
+    int max_lcam;                     // longest such list
+    int long_o0_h;                    // first long-track observation (host copy)
+    double *ylong;                    // [nlobs][3 NA] Y_a = W_a V*^-1 of each long observation
     double *vseg;                     // [nseg][12] V | eB partials per segment
     double *dpg_long;                 // [nl] point part of dp'(lambda dp + g)
     int mf_max_s, mf_max_e, mf_max_blob;   // MFMA groups' LDS sizes
@@ -280,12 +289,14 @@ struct ba_dev {
 #define BA_MF_GACC 1536    // doubles of LDS block accumulators per MFMA Schur group
 #define BA_MF_GE_CAP 24    // cameras per MFMA Schur group (LDS budget: 2 groups per CU)
 // long tracks (more observations than a chunk holds): segment chunks of
-// BA_CH_OBS observations, Schur tiles of BA_LONG_TILE x BA_LONG_TILE
-// observation pairs; caps (else the ordered kernels): views per track and
-// (obs, obs) terms of all long tracks (one 8 * NA^2-byte partial each)
-#define BA_LONG_TILE 32
+// BA_CH_OBS observations; their Schur terms are added per block by
+// k_schur_reduce (merge of the two cameras' long-observation lists).  Caps
+// (else the ordered kernels): views per track and (obs, obs) terms of all
+// long tracks (the reduce's work)
 #define BA_LONG_OBS 65535
-#define BA_LONG_TERMS (1LL << 23)
+#define BA_LONG_TERMS (1LL << 26)
+// k_schur_reduce stages a camera's long-observation list in LDS up to this length
+#define BA_LCAM_LDS 256
 
 // ---- ba_kernels.hip ----
 int ba_launch_rotations(ba_dev *d, const double *a, double *rot, int all5);

@@ -1280,7 +1280,19 @@ __global__ __launch_bounds__(256, (NA == 6) ? BA_MF_WAVES : 1) void k_schur_mfma
     for (int q = tid; q < nge * NA; q += 256) epart[(size_t)NA * ge0 + q] = geacc[q];
 }
 
-// S blocks and e_ from the chunk partials, in chunk order
+// S blocks and e_ from the chunk partials, in chunk order; then (long tracks)
+// the terms Y_a W_b^T of every long track that sees both cameras of the block,
+// in track order: wave 0 finds them by a binary search of each of camera j's
+// long observations among camera k's (both lists ascending by track, staged
+// in LDS), compacts the matches in order, and every entry's lane subtracts
+// them -- the order and the expression of the former per-pair slots, so the
+// blocks are the same bit for bit.
+struct ba_longs {
+    const int *cam_lptr, *cam_lobs, *cam_ltrk;   // NULL: no long tracks
+    const double *ylong, *W;
+    int L0;                                      // first long observation
+};
+
 template <int NA>
 __global__ void k_schur_reduce(const int *__restrict__ blk_jk, const int *__restrict__ blk_sptr,
                                const int *__restrict__ blk_slots,
@@ -1289,16 +1301,20 @@ __global__ void k_schur_reduce(const int *__restrict__ blk_jk, const int *__rest
                                const double *__restrict__ spart,
                                const double *__restrict__ epart, const double *__restrict__ U,
                                const double *__restrict__ eA, int nb, double lambda, int owner,
-                               double *__restrict__ sblk, double *__restrict__ rhs)
+                               double *__restrict__ sblk, double *__restrict__ rhs, ba_longs lg)
 {
+    constexpr int NN = NA * NA, WS = 3 * NA;
+    __shared__ int la[BA_LCAM_LDS], lt[BA_LCAM_LDS], lb[BA_LCAM_LDS], ltb[BA_LCAM_LDS];
+    __shared__ int mj[BA_LCAM_LDS], mk[BA_LCAM_LDS];
+    __shared__ int nmatch;
     const int bk = blockIdx.x, l = threadIdx.x;
     if (bk >= nb) return;
     const int j = blk_jk[2 * bk], k = blk_jk[2 * bk + 1];
-    if (l < NA * NA) {
+    double acc = 0.0;
+    if (l < NN) {
         const int r = l % NA, c = l / NA;
-        double acc = 0.0;
         if (j == k && owner) {
-            const double u = U[(size_t)NA * NA * j + r + NA * c];
+            const double u = U[(size_t)NN * j + r + NA * c];
             acc = (r == c) ? (1 + lambda) * u : u;
         }
         // 8 independent loads in flight, subtracted in slot order (same result)
@@ -1307,15 +1323,14 @@ __global__ void k_schur_reduce(const int *__restrict__ blk_jk, const int *__rest
         for (; q + 8 <= qe; q += 8) {
             double v[8];
 #pragma unroll
-            for (int t = 0; t < 8; t++) v[t] = spart[(size_t)NA * NA * blk_slots[q + t] + l];
+            for (int t = 0; t < 8; t++) v[t] = spart[(size_t)NN * blk_slots[q + t] + l];
 #pragma unroll
             for (int t = 0; t < 8; t++) acc -= v[t];
         }
-        for (; q < qe; q++) acc -= spart[(size_t)NA * NA * blk_slots[q] + l];
-        sblk[(size_t)NA * NA * bk + l] = acc;
-    } else if (j == k && l < NA * NA + NA) {
-        const int r = l - NA * NA;
-        double acc = owner ? eA[(size_t)NA * j + r] : 0.0;
+        for (; q < qe; q++) acc -= spart[(size_t)NN * blk_slots[q] + l];
+    } else if (j == k && l < NN + NA) {
+        const int r = l - NN;
+        double e = owner ? eA[(size_t)NA * j + r] : 0.0;
         int q = cam_eptr[j];
         const int qe = cam_eptr[j + 1];
         for (; q + 8 <= qe; q += 8) {
@@ -1323,11 +1338,95 @@ __global__ void k_schur_reduce(const int *__restrict__ blk_jk, const int *__rest
 #pragma unroll
             for (int t = 0; t < 8; t++) v[t] = epart[(size_t)NA * cam_eslots[q + t] + r];
 #pragma unroll
-            for (int t = 0; t < 8; t++) acc -= v[t];
+            for (int t = 0; t < 8; t++) e -= v[t];
         }
-        for (; q < qe; q++) acc -= epart[(size_t)NA * cam_eslots[q] + r];
-        rhs[(size_t)NA * j + r] = acc;
+        for (; q < qe; q++) e -= epart[(size_t)NA * cam_eslots[q] + r];
+        rhs[(size_t)NA * j + r] = e;
     }
+    if (lg.cam_lptr) {
+        const int a0 = lg.cam_lptr[j], na_ = lg.cam_lptr[j + 1] - a0;
+        const int b0 = lg.cam_lptr[k], nb_ = lg.cam_lptr[k + 1] - b0;
+        if (na_ > 0 && nb_ > 0) {   // (uniform over the block)
+            const bool lds = na_ <= BA_LCAM_LDS && nb_ <= BA_LCAM_LDS;
+            if (lds) {
+                for (int q = l; q < na_; q += blockDim.x) {
+                    la[q] = lg.cam_lobs[a0 + q];
+                    lt[q] = lg.cam_ltrk[a0 + q];
+                }
+                for (int q = l; q < nb_; q += blockDim.x) {
+                    lb[q] = lg.cam_lobs[b0 + q];
+                    ltb[q] = lg.cam_ltrk[b0 + q];
+                }
+            }
+            __syncthreads();
+            if (lds && l < 64) {   // wave 0: matches of camera j's tracks in camera k's list
+                int cnt = 0;
+                for (int q0 = 0; q0 < na_; q0 += 64) {
+                    const int q = q0 + l;
+                    int pos = -1;
+                    if (q < na_) {
+                        const int t = lt[q];
+                        int lo = 0, hi = nb_;   // first entry with track >= t
+                        while (lo < hi) {
+                            const int mid = (lo + hi) >> 1;
+                            if (ltb[mid] < t) lo = mid + 1;
+                            else hi = mid;
+                        }
+                        if (lo < nb_ && ltb[lo] == t) pos = lo;
+                    }
+                    const unsigned long long m = __ballot(pos >= 0);
+                    if (pos >= 0) {
+                        const int at = cnt + __popcll(m & ((1ull << l) - 1ull));
+                        mj[at] = la[q];
+                        mk[at] = lb[pos];
+                    }
+                    cnt += __popcll(m);
+                }
+                if (l == 0) nmatch = cnt;
+            }
+            __syncthreads();
+            if (l < NN) {
+                const int r = l % NA, c = l / NA;
+                if (lds) {
+                    const int nm = nmatch;
+                    int q = 0;
+                    for (; q + 4 <= nm; q += 4) {   // four terms' loads in flight
+                        double v[4];
+#pragma unroll
+                        for (int t = 0; t < 4; t++) {
+                            const double *y = lg.ylong + (size_t)WS * mj[q + t];
+                            const double *w = lg.W + (size_t)WS * (lg.L0 + mk[q + t]);
+                            v[t] = y[r] * w[c] + y[r + NA] * w[c + NA] + y[r + 2 * NA] * w[c + 2 * NA];
+                        }
+#pragma unroll
+                        for (int t = 0; t < 4; t++) acc -= v[t];
+                    }
+                    for (; q < nm; q++) {
+                        const double *y = lg.ylong + (size_t)WS * mj[q];
+                        const double *w = lg.W + (size_t)WS * (lg.L0 + mk[q]);
+                        acc -= y[r] * w[c] + y[r + NA] * w[c + NA] + y[r + 2 * NA] * w[c + 2 * NA];
+                    }
+                } else {   // a list past the LDS stage: merge in global memory
+                    int p = 0, q = 0;
+                    while (p < na_ && q < nb_) {
+                        const int tp = lg.cam_ltrk[a0 + p], tq = lg.cam_ltrk[b0 + q];
+                        if (tp < tq) {
+                            p++;
+                        } else if (tq < tp) {
+                            q++;
+                        } else {
+                            const double *y = lg.ylong + (size_t)WS * lg.cam_lobs[a0 + p];
+                            const double *w = lg.W + (size_t)WS * (lg.L0 + lg.cam_lobs[b0 + q]);
+                            acc -= y[r] * w[c] + y[r + NA] * w[c + NA] + y[r + 2 * NA] * w[c + 2 * NA];
+                            p++;
+                            q++;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    if (l < NN) sblk[(size_t)NN * bk + l] = acc;
 }
 
 // t_o = Y_o eB_i for given Y (stage-2 entry; k_damp_point forms it otherwise)
@@ -1666,10 +1765,10 @@ __global__ __launch_bounds__(256) void k_point_update_chunk(
 // fast path).  Their observations are linearised by segment chunks of
 // k_linearize_chunk; here:
 //   k_long_vsum  : V_i, eB_i = the sum of the segments' partials (segment order)
-//   k_schur_long : per tile of BA_LONG_TILE^2 (obs a, obs b) pairs, a >= b, the
-//                  block term Y_a W_b^T (mex_bundle_2_Se_.c:80-118, one group
-//                  slot per pair) and, on the diagonal tile column, Y_a eB_i
-//                  (:132-155, one group e-slot per observation)
+//   k_long_y     : Y_a = W_a V*^-1 of every observation of the track (the block
+//                  terms Y_a W_b^T, mex_bundle_2_Se_.c:80-118, are summed by
+//                  k_schur_reduce) and Y_a eB_i (:132-155, one group e-slot
+//                  per observation)
 //   k_long_db    : db_i = V*^-1 (eB_i - sum_o W_o^T da_j) over all the track's
 //                  observations (mex_bundle_3_db_new.c:99-134), b_new, dp'g
 // -------------------------------------------------------------------------
@@ -1687,51 +1786,40 @@ __global__ void k_long_vsum(const int *__restrict__ long_pt, const int *__restri
 }
 
 template <int NA>
-__global__ __launch_bounds__(256) void k_schur_long(
-    const int *__restrict__ tiles, const int *__restrict__ long_pt,
-    const int *__restrict__ long_o0, const int *__restrict__ long_sbase,
-    const int *__restrict__ long_ebase, const double *__restrict__ W,
-    const double *__restrict__ Vinv, const double *__restrict__ eB,
-    double *__restrict__ spart, double *__restrict__ epart)
+__global__ __launch_bounds__(256) void k_long_y(const int *__restrict__ long_pt,
+                                                const int *__restrict__ long_o0,
+                                                const int *__restrict__ long_ebase,
+                                                const double *__restrict__ W,
+                                                const double *__restrict__ Vinv,
+                                                const double *__restrict__ eB,
+                                                double *__restrict__ ylong,
+                                                double *__restrict__ epart)
 {
-    constexpr int WS = 3 * NA, TL = BA_LONG_TILE, NN = NA * NA;
-    __shared__ double Ya[TL * WS], Wb[TL * WS];
-    const int tid = threadIdx.x;
-    const int l = tiles[3 * blockIdx.x], ta = tiles[3 * blockIdx.x + 1],
-              tb = tiles[3 * blockIdx.x + 2];
-    const int i = long_pt[l], o0 = long_o0[l], k = long_o0[l + 1] - o0;
-    const int a0 = TL * ta, na_ = min(TL, k - a0), b0 = TL * tb, nb_ = min(TL, k - b0);
+    constexpr int WS = 3 * NA;
+    const int tid = threadIdx.x, l = blockIdx.x;
+    const int i = long_pt[l], o0 = long_o0[l], k = long_o0[l + 1] - o0, L0 = long_o0[0];
     double vi[9], eb[3];
 #pragma unroll
     for (int q = 0; q < 9; q++) vi[q] = Vinv[9 * (size_t)i + q];
 #pragma unroll
     for (int q = 0; q < 3; q++) eb[q] = eB[3 * (size_t)i + q];
     // Y_a = W_a V*^-1 (bundle_euclid.m:182; each entry summed left to right)
-    for (int q = tid; q < na_ * WS; q += 256) {
+    for (int q = tid; q < k * WS; q += 256) {
         const int lo = q / WS, e = q - WS * lo, r = e % NA, c = e / NA;
-        const double *w = W + (size_t)WS * (o0 + a0 + lo);
-        Ya[q] = w[r] * vi[3 * c] + w[r + NA] * vi[1 + 3 * c] + w[r + 2 * NA] * vi[2 + 3 * c];
+        const double *w = W + (size_t)WS * (o0 + lo);
+        ylong[(size_t)WS * (o0 - L0 + lo) + e] =
+            w[r] * vi[3 * c] + w[r + NA] * vi[1 + 3 * c] + w[r + 2 * NA] * vi[2 + 3 * c];
     }
-    for (int q = tid; q < nb_ * WS; q += 256) Wb[q] = W[(size_t)WS * (o0 + b0) + q];
-    __syncthreads();
-    const long long sb = long_sbase[l];
-    for (int q = tid; q < na_ * nb_ * NN; q += 256) {
-        const int pr = q / NN, e = q - NN * pr, al = pr / nb_, bl = pr - nb_ * al;
-        const int a = a0 + al, b = b0 + bl;
-        if (a < b) continue;
-        const int r = e % NA, c = e / NA;
-        const double *y = Ya + WS * al, *w = Wb + WS * bl;
-        const long long slot = sb + (long long)a * (a + 1) / 2 + b;
-        spart[(size_t)NN * slot + e] = y[r] * w[c] + y[r + NA] * w[c + NA] + y[r + 2 * NA] * w[c + 2 * NA];
-    }
-    if (tb == 0) {
-        const long long eb0 = long_ebase[l];
-        for (int q = tid; q < na_ * NA; q += 256) {
-            const int al = q / NA, r = q - NA * al;
-            const double *y = Ya + WS * al;
-            epart[(size_t)NA * (eb0 + a0 + al) + r] =
-                y[r] * eb[0] + y[r + NA] * eb[1] + y[r + 2 * NA] * eb[2];
-        }
+    // the e_ terms Y_a eB_i (mex_bundle_2_Se_.c:132-155): one group e-slot each
+    const long long eb0 = long_ebase[l];
+    for (int q = tid; q < k * NA; q += 256) {
+        const int al = q / NA, r = q - NA * al;
+        const double *w = W + (size_t)WS * (o0 + al);
+        double y[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++)
+            y[c] = w[r] * vi[3 * c] + w[r + NA] * vi[1 + 3 * c] + w[r + 2 * NA] * vi[2 + 3 * c];
+        epart[(size_t)NA * (eb0 + al) + r] = y[0] * eb[0] + y[1] * eb[1] + y[2] * eb[2];
     }
 }
 
@@ -2012,9 +2100,8 @@ static int launch_schur_fast(ba_dev *d, double lambda)
             k_point_vinv<NA><<<(d->n - d->p_long + 255) / 256, 256, 0, d->stream>>>(
                 d->V + 9 * (size_t)d->p_long, d->n - d->p_long, lambda,
                 d->Vinv + 9 * (size_t)d->p_long);
-        k_schur_long<NA><<<d->ntile_long, 256, 0, d->stream>>>(
-            d->long_tiles, d->long_pt, d->long_o0, d->long_sbase, d->long_ebase, d->W, d->Vinv,
-            d->eB, d->spart, d->epart);
+        k_long_y<NA><<<d->nl, 256, 0, d->stream>>>(d->long_pt, d->long_o0, d->long_ebase, d->W,
+                                                   d->Vinv, d->eB, d->ylong, d->epart);
         KT_E(d, KT_SCHUR_CHUNK);
     }
     const int bs = ((NA * NA + NA) + 63) / 64 * 64;
@@ -2023,9 +2110,18 @@ static int launch_schur_fast(ba_dev *d, double lambda)
         d->join_pending = 0;
     }
     KT_B(d);
+    ba_longs lg{};
+    if (d->nl > 0) {
+        lg.cam_lptr = d->cam_lptr;
+        lg.cam_lobs = d->cam_lobs;
+        lg.cam_ltrk = d->cam_ltrk;
+        lg.ylong = d->ylong;
+        lg.W = d->W;
+        lg.L0 = d->long_o0_h;
+    }
     k_schur_reduce<NA><<<d->nb, bs, 0, d->stream>>>(
         d->blk_jk, d->blk_gptr, d->blk_gslots, d->cam_gptr, d->cam_gslots, d->spart, d->epart,
-        d->U, d->eA, d->nb, lambda, d->schur_owner, d->sblk, d->rhs);
+        d->U, d->eA, d->nb, lambda, d->schur_owner, d->sblk, d->rhs, lg);
     KT_E(d, KT_SCHUR_RED);
     return -(int)hipGetLastError();
 }

@@ -367,8 +367,9 @@ struct host_plan {
     int nch_reg = 0, nseg = 0;
     std::vector<int> seg_pt, seg_long;            // [nseg] point / long index
     std::vector<int> long_pt, long_o0, long_seg0; // [nl], [nl+1], [nl+1]
-    std::vector<int> long_sbase, long_ebase;      // [nl] first group slot / e-slot
-    std::vector<int> long_tiles;                  // [ntile][3] (long, a tile, b tile)
+    std::vector<int> long_ebase;                  // [nl] first group e-slot
+    std::vector<int> cam_lptr, cam_lobs, cam_ltrk; // per camera its long observations
+    int max_lcam = 0;                             // (long-obs index, track), track order
     // per chunk one contiguous metadata record (one coalesced prefetch):
     //   [np | nobs << 16][ns | nes << 16][nterm][neobs] soff[ns+1] eoff[nes+1]
     //   sgl[ns] egl[nes] lpt[nobs] term[nterm] (y | w << 16) eobl[neobs]
@@ -780,42 +781,40 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
         c = d;
     }
     PLAN_T("groups");
-    // long tracks' Schur terms: one group slot per (a, b), a >= b (cameras
-    // ascending, so block (cam a, cam b) is a lower block), slot a(a+1)/2 + b
-    // of the point; one group e-slot per observation.  After the regular
-    // slots: k_schur_reduce subtracts them last.
+    // long tracks' Schur terms (no slots of their own): k_schur_reduce adds,
+    // per block (j, k), the terms Y_a W_b^T of every long track that sees both
+    // cameras, in track order, by merging the two cameras' lists of long-track
+    // observations (cam_lptr / cam_lobs / cam_ltrk: per camera its long-track
+    // observations in ascending order = track order; a point sees a camera at
+    // most once).  One group e-slot per long observation (its Y_a eB_i term,
+    // k_long_y), after the regular ones.
     const int nlong = (int)P.long_pt.size();
-    std::vector<long long> lwork(nlong + 1, 0);
-    for (int l = 0; l < nlong; l++) {
-        const int o0 = P.long_o0[l], k = P.long_o0[l + 1] - o0;
-        P.long_sbase.push_back((int)(P.gslot_blk.size() + lwork[l]));
-        P.long_ebase.push_back((int)P.gecam.size() + (o0 - P.long_o0[0]));
-        lwork[l + 1] = lwork[l] + (long long)k * (k + 1) / 2;
-    }
-    const size_t gs_long = P.gslot_blk.size(), ge_long = P.gecam.size();
-    P.gslot_blk.resize(gs_long + lwork[nlong]);
-    P.gecam.resize(ge_long + (nlong ? P.long_o0[nlong] - P.long_o0[0] : 0));
-    parallel_ranges(nlong, plan_threads(lwork[nlong], 50000), [&](int, int l0, int l1) {
-        for (int l = l0; l < l1; l++) {
-            const int o0 = P.long_o0[l], k = P.long_o0[l + 1] - o0;
-            int *gs = &P.gslot_blk[P.long_sbase[l]];
-            for (int a = 0; a < k; a++) {
-                P.gecam[P.long_ebase[l] + a] = lcam[o0 + a];
-                for (int b = 0; b <= a; b++) *gs++ = hb.find(lcam[o0 + a], lcam[o0 + b]);
+    const int L0 = nlong ? P.long_o0[0] : 0, nlobs = nlong ? P.long_o0[nlong] - L0 : 0;
+    for (int l = 0; l < nlong; l++)
+        P.long_ebase.push_back((int)P.gecam.size() + (P.long_o0[l] - L0));
+    P.gecam.insert(P.gecam.end(), lcam.begin() + L0, lcam.begin() + L0 + nlobs);
+    {
+        P.cam_lptr.assign(m + 1, 0);
+        for (int o = L0; o < L0 + nlobs; o++) P.cam_lptr[lcam[o] + 1]++;
+        for (int j = 0; j < m; j++) P.cam_lptr[j + 1] += P.cam_lptr[j];
+        P.cam_lobs.resize(nlobs);
+        P.cam_ltrk.resize(nlobs);
+        std::vector<int> pos(P.cam_lptr.begin(), P.cam_lptr.end() - 1);
+        for (int l = 0; l < nlong; l++)
+            for (int o = P.long_o0[l]; o < P.long_o0[l + 1]; o++) {
+                const int q = pos[lcam[o]]++;
+                P.cam_lobs[q] = o - L0;
+                P.cam_ltrk[q] = l;
             }
-        }
-    }, &lwork);
-    for (int l = 0; l < nlong; l++) {
-        const int k = P.long_o0[l + 1] - P.long_o0[l];
-        const int nt = (k + BA_LONG_TILE - 1) / BA_LONG_TILE;
-        for (int ta = 0; ta < nt; ta++)
-            for (int tb = 0; tb <= ta; tb++) {
-                P.long_tiles.push_back((int)l);
-                P.long_tiles.push_back(ta);
-                P.long_tiles.push_back(tb);
-            }
+        for (int j = 0; j < m; j++)
+            P.max_lcam = std::max(P.max_lcam, P.cam_lptr[j + 1] - P.cam_lptr[j]);
     }
-    PLAN_T("long groups");
+    PLAN_T("long lists");
+#ifdef BA_PLAN_TIMING
+    std::fprintf(stderr, "   (group slots %zu; group e-slots %zu; long tracks %d, %d observations, "
+                 "at most %d per camera)\n", P.gslot_blk.size(), P.gecam.size(), nlong, nlobs,
+                 P.max_lcam);
+#endif
     bucket(P.gslot_blk, nb, P.blk_gptr, P.blk_gslots);
     bucket(P.gecam, m, P.cam_gptr, P.cam_gslots);
     PLAN_T("buckets");
@@ -1321,7 +1320,8 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         d.nch_reg = plan.nch_reg;
         d.nch = plan.nch_reg + plan.nseg;
         d.nl = (int)plan.long_pt.size();
-        d.ntile_long = (int)plan.long_tiles.size() / 3;
+        d.max_lcam = plan.max_lcam;
+        d.long_o0_h = plan.long_o0.empty() ? 0 : plan.long_o0[0];
         d.p_long = p_long;
         if (d.nl > 0) {
             TRY(ctx_alloc(c, &d.seg_pt, plan.seg_pt.size()));
@@ -1329,9 +1329,11 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
             TRY(ctx_alloc(c, &d.long_pt, plan.long_pt.size()));
             TRY(ctx_alloc(c, &d.long_o0, plan.long_o0.size()));
             TRY(ctx_alloc(c, &d.long_seg0, plan.long_seg0.size()));
-            TRY(ctx_alloc(c, &d.long_sbase, plan.long_sbase.size()));
             TRY(ctx_alloc(c, &d.long_ebase, plan.long_ebase.size()));
-            TRY(ctx_alloc(c, &d.long_tiles, plan.long_tiles.size()));
+            TRY(ctx_alloc(c, &d.cam_lptr, plan.cam_lptr.size()));
+            TRY(ctx_alloc(c, &d.cam_lobs, plan.cam_lobs.size()));
+            TRY(ctx_alloc(c, &d.cam_ltrk, plan.cam_ltrk.size()));
+            TRY(ctx_alloc(c, &d.ylong, (size_t)3 * na * plan.cam_lobs.size()));
             TRY(ctx_alloc(c, &d.vseg, 12 * (size_t)plan.nseg));
             TRY(ctx_alloc(c, &d.dpg_long, (size_t)d.nl));
             TRY(upload(d.seg_pt, plan.seg_pt.data(), plan.seg_pt.size(), s));
@@ -1339,9 +1341,10 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
             TRY(upload(d.long_pt, plan.long_pt.data(), plan.long_pt.size(), s));
             TRY(upload(d.long_o0, plan.long_o0.data(), plan.long_o0.size(), s));
             TRY(upload(d.long_seg0, plan.long_seg0.data(), plan.long_seg0.size(), s));
-            TRY(upload(d.long_sbase, plan.long_sbase.data(), plan.long_sbase.size(), s));
             TRY(upload(d.long_ebase, plan.long_ebase.data(), plan.long_ebase.size(), s));
-            TRY(upload(d.long_tiles, plan.long_tiles.data(), plan.long_tiles.size(), s));
+            TRY(upload(d.cam_lptr, plan.cam_lptr.data(), plan.cam_lptr.size(), s));
+            TRY(upload(d.cam_lobs, plan.cam_lobs.data(), plan.cam_lobs.size(), s));
+            TRY(upload(d.cam_ltrk, plan.cam_ltrk.data(), plan.cam_ltrk.size(), s));
         }
         d.ns = (int)plan.slot_blk.size();
         d.nes = (int)plan.eslot_optr.size() - 1;

@@ -65,7 +65,19 @@ def rank_collective(pg, rank: int, world: int, ndev: int):
 # and the ranks run as threads of one process, one libvlgba context per rank
 # on device rank % ndev, their collectives through host memory.
 # ---------------------------------------------------------------------------
-OBS_PER_SHARD = 250_000   # below this a rank's pass is launch / latency bound
+# The threshold, from measured per-pass times: the sharded
+# kernels (linearisation, V*^-1 + Schur, point update) cost ~0.18 us per
+# observation per pass (540 us for config 3's 3M observations on one MI355X,
+# profiles/r03b_cfg3_kernel_stats.txt); the reduced solve does not shrink with
+# the rank count; sharding adds two all-reduces per pass (~30-60 us by RCCL's
+# per-call latency over xGMI, ~45 us taken).  Going from 1 to 2 ranks saves
+# 0.09 us x N per pass, so it pays only above N ~ 500k observations -- 250k per
+# rank -- and every further doubling needs the same per-rank count.  Config
+# 5's solves stay below it (the 50-camera replay: < 2k observations; the
+# 1000-camera cfg5x: at most 175k), so on these scenes the elastic count is
+# always 1: the 1 -> 8 path is exercised only with a lowered threshold
+# (tests/test_gpu_incremental.py).
+OBS_PER_SHARD = 250_000
 
 
 def choose_shards(num_obs: int, ndev: int, obs_per_shard: int = OBS_PER_SHARD) -> int:

@@ -94,8 +94,9 @@ int main(int argc, char **argv)
         H.add(P.grp_ch); H.add(P.grp_gs); H.add(P.grp_ge); H.add(P.cs_g); H.add(P.ce_g);
         H.add(P.gslot_blk); H.add(P.gecam); H.add(P.blk_gptr); H.add(P.blk_gslots);
         H.add(P.cam_gptr); H.add(P.cam_gslots); H.add(P.seg_pt); H.add(P.seg_long);
-        H.add(P.long_pt); H.add(P.long_o0); H.add(P.long_seg0); H.add(P.long_sbase);
-        H.add(P.long_ebase); H.add(P.long_tiles); H.add(P.blob); H.add(P.ch_blob);
+        H.add(P.long_pt); H.add(P.long_o0); H.add(P.long_seg0);
+        H.add(P.long_ebase); H.add(P.cam_lptr); H.add(P.cam_lobs); H.add(P.cam_ltrk);
+        H.add(P.blob); H.add(P.ch_blob);
         H.add(P.ch_obase);
         const std::vector<int> scal = {P.max_terms, P.max_slots, P.grp_max_s, P.grp_max_e,
                                        P.mf_max_s, P.mf_max_e, P.nch_mf, P.ngrp_mf, P.nch_reg,
