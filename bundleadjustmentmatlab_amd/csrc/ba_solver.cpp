@@ -1065,6 +1065,64 @@ static void aux_release(const ba_aux &a)
     g_aux_pool.push_back(a);
 }
 
+// RCCL communicators outlive their context, keyed by (unique id, rank): a
+// caller that passes the same id again (dist.run_sharded keeps one id per
+// device set for a whole growing replay) takes the idle communicator instead
+// of paying ncclCommInitRank per solve.  One context per (id, rank) at a time;
+// idle communicators of other ids are destroyed once more than
+// BA_COMM_IDLE_MAX are kept.
+#define BA_COMM_IDLE_MAX 32
+static std::mutex g_comm_mu;
+static std::multimap<std::pair<std::string, int>, ncclComm_t> g_comm_idle;
+static std::map<ncclComm_t, std::pair<std::string, int>> g_comm_key;
+
+static ncclResult_t comm_acquire(ncclComm_t *comm, int world, const void *id128, int rank)
+{
+    const std::pair<std::string, int> key(std::string((const char *)id128, 128), rank);
+    {
+        std::lock_guard<std::mutex> lk(g_comm_mu);
+        auto it = g_comm_idle.find(key);
+        if (it != g_comm_idle.end()) {
+            *comm = it->second;
+            g_comm_idle.erase(it);
+            return ncclSuccess;
+        }
+    }
+    ncclUniqueId id;
+    std::memcpy(&id, id128, sizeof id);
+    const ncclResult_t r = ncclCommInitRank(comm, world, id, rank);
+    if (r == ncclSuccess) {
+        std::lock_guard<std::mutex> lk(g_comm_mu);
+        g_comm_key[*comm] = key;
+    }
+    return r;
+}
+
+static void comm_release(ncclComm_t comm)
+{
+    std::vector<ncclComm_t> drop;
+    {
+        std::lock_guard<std::mutex> lk(g_comm_mu);
+        auto it = g_comm_key.find(comm);
+        if (it == g_comm_key.end()) {
+            drop.push_back(comm);
+        } else {
+            g_comm_idle.emplace(it->second, comm);
+            if (g_comm_idle.size() > BA_COMM_IDLE_MAX)
+                for (auto q = g_comm_idle.begin(); q != g_comm_idle.end();) {
+                    if (q->first.first != it->second.first) {
+                        drop.push_back(q->second);
+                        g_comm_key.erase(q->second);
+                        q = g_comm_idle.erase(q);
+                    } else {
+                        ++q;
+                    }
+                }
+        }
+    }
+    for (ncclComm_t x : drop) ncclCommDestroy(x);
+}
+
 static void ctx_free(vlgba_ctx *c)
 {
     if (!c) return;
@@ -1081,7 +1139,7 @@ static void ctx_free(vlgba_ctx *c)
         delete c->d.kt;
     }
     ba_chol_free(&c->d);
-    if (c->comm) ncclCommDestroy(c->comm);
+    if (c->comm) comm_release(c->comm);
     if (c->has_aux) aux_release(c->aux);
     delete c;
 }
@@ -1517,9 +1575,7 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
             c->p0 = c->rank == 0 ? 0 : std::min(bound(c->rank), p->n);
             c->p1 = c->rank == c->world - 1 ? p->n : std::min(bound(c->rank + 1), p->n);
             if (o->comm_id) {
-                ncclUniqueId id;
-                std::memcpy(&id, o->comm_id, sizeof id);
-                if (ncclCommInitRank(&c->comm, c->world, id, c->rank) != ncclSuccess) {
+                if (comm_acquire(&c->comm, c->world, o->comm_id, c->rank) != ncclSuccess) {
                     rc = VLGBA_E_COMM;
                     break;
                 }
@@ -1535,9 +1591,7 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
             c->p1 = p->n;
             if (o->comm_id) {   // a one-rank RCCL communicator: every collective
                                 // of the pass runs through RCCL (identity sums)
-                ncclUniqueId id;
-                std::memcpy(&id, o->comm_id, sizeof id);
-                if (ncclCommInitRank(&c->comm, 1, id, 0) != ncclSuccess) {
+                if (comm_acquire(&c->comm, 1, o->comm_id, 0) != ncclSuccess) {
                     rc = VLGBA_E_COMM;
                     break;
                 }

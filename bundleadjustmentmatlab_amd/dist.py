@@ -116,10 +116,14 @@ class HostGroup:
         return ar
 
 
+_COMM_IDS: dict = {}   # device tuple -> RCCL unique id (libvlgba caches the communicators)
+
+
 def run_sharded(K, obs_pt, obs_cam, obs_x, n, num_a, a, b, world, *, devices=None, **kw):
     """One LM solve (vlgba_run) over `world` rank threads, rank r on device
     devices[r % len(devices)].  Ranks on distinct GPUs share one RCCL
-    communicator (the unique id made here, ncclCommInitRank per thread);
+    communicator (one unique id per device set, ncclCommInitRank per thread
+    on its first use; libvlgba keeps the communicators for the next solve);
     ranks that share a GPU (RCCL refuses two ranks on one device) use the
     host-memory all-reduce (HostGroup).  Returns (a, b, error_, stats) of
     rank 0 (every rank holds the same a, b, error_)."""
@@ -133,7 +137,11 @@ def run_sharded(K, obs_pt, obs_cam, obs_x, n, num_a, a, b, world, *, devices=Non
         return a2, b2, err, st
     devices = devices or [0]
     devs = [devices[r % len(devices)] for r in range(world)]
-    comm = unique_id_bytes() if len(set(devs)) == world else None
+    comm = None
+    if len(set(devs)) == world:   # one RCCL id per device set: the library keeps its
+        comm = _COMM_IDS.get(tuple(devs))   # communicators for the next solve
+        if comm is None:
+            comm = _COMM_IDS[tuple(devs)] = unique_id_bytes()
     grp = None if comm else HostGroup(world)
     out = [None] * world
     errs = []

@@ -6,21 +6,27 @@ The reference adds cameras one at a time.  Per added camera j it estimates
 the pose (estimate_camera.m: DLT + RANSAC, then a one-camera ``bundle_euclid``
 with the structure fixed, :247-253), removes outliers, runs ``bundle_euclid`` over
 the cameras added so far and the points reconstructed so far, aligns the
-scene (align_scene.m), triangulates the points that now have >= 2 views,
-removes outliers again and runs ``bundle_euclid`` a second time.  The BA
-solves are the hot path and run on the GPU here (``bundle_euclid_obs``, and
-``bundle_euclid_resect`` for estimate_camera's one-camera refinement); the DLT /
-RANSAC pose, outlier removal and triangulation are out of scope (SURVEY.md
-sec. 2) and are replaced by the synthetic scene's perturbed initial values
-(the new camera's (w0, T0), the point's X0) -- the BA sequence, its growing
-problem sizes and its visibility subsets are the reference's.
+scene (align_scene.m), triangulates the points that now have >= 2 views
+(triangulation.m: linear DLT on the current cameras, rejected if any view
+sees the point behind it), removes outliers again and runs ``bundle_euclid``
+a second time.  The BA solves are the hot path and run on the GPU here
+(``bundle_euclid_obs``, and ``bundle_euclid_resect`` for estimate_camera's
+one-camera refinement); the triangulation is triangulation.m's (``_triangulate``,
+numpy); the DLT / RANSAC pose and the outlier removal are out of scope
+(SURVEY.md sec. 2): the new camera starts from the synthetic scene's perturbed
+pose (w0, T0) mapped into the current frame, and no observation is dropped --
+the BA sequence, its growing problem sizes and its visibility subsets are the
+reference's.
 
 ``incremental_bundle(scene)`` returns the per-solve log and the final
 reconstruction.
 
-The stand-ins make the STRUCTURE of every solve (which cameras, points and
-observations it adjusts) independent of the parameter values, so the replay
-knows solve k+1's problem before solve k ends: a worker thread cuts its
+The structure of a solve (which cameras, points and observations it
+adjusts) is known before the previous solve ends -- exactly for a
+before-triangulation solve (nothing but the new camera changes it), and up to
+the points whose triangulation fails the depth test for an after-triangulation
+one (predicted: every candidate succeeds; a wrong prediction is detected and
+that solve's context rebuilt) -- so a worker thread cuts solve k+1's
 observation subset and builds its libvlgba context (the host plan of
 vlgba_create, which runs with the GIL released) while solve k runs on the GPU
 ("reuse across growing calls").  Only the parameter
@@ -59,24 +65,6 @@ def _subset_obs(sc, cams, pts, cam_on=None, pt_on=None):
     return pmap[sc.obs_pt[keep]], cmap[sc.obs_cam[keep]], sc.obs_x[keep]
 
 
-def _solve_sets(sc, init_cams):
-    """The replay's bundle_euclid calls in order, as (tag, j, camera mask,
-    point mask): incr_reconstruction.m:223-341 with this module's stand-ins --
-    camera j joins the status set, a solve over the points reconstructed so
-    far, the points seen by >= 2 cameras of the set join them, a second solve
-    (the main loop checks every prefetched set against its own state)."""
-    status = np.zeros(sc.m, dtype=bool)
-    status[list(init_cams)] = True
-    tri = np.bincount(sc.obs_pt, weights=status[sc.obs_cam], minlength=sc.n) >= 2
-    for j in range(sc.m):
-        if status[j]:
-            continue
-        status[j] = True
-        yield "before-triangulation", j, status.copy(), tri.copy()
-        tri |= np.bincount(sc.obs_pt, weights=status[sc.obs_cam], minlength=sc.n) >= 2
-        yield "after-triangulation", j, status.copy(), tri.copy()
-
-
 def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, device=0,
                        verbose=False, devices=None, shards=None, obs_per_shard=None,
                        progress=None, prefetch=True):
@@ -98,10 +86,13 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
     current solve runs (module docstring); the results are the same as
     without it (the same contexts, built earlier).
 
-    Returns dict(solves=[...], resections=[...], K, T, w, X, status) where each
+    Returns dict(solves=[...], resections=[...], K, T, w, X, status, prefetch)
+    (``prefetch``: contexts used as prefetched / rebuilt after a wrong
+    prediction) where each
     solve records the cameras / points / observations it adjusted, its error_
     trace, LM passes and wall seconds (``wait_create``: of them, the wait for
-    the prefetched context; ``create``: the worker's time building it), and each
+    the prefetched context -- or its build, when it was not prefetched;
+    ``create``: the time building it), and each
     resection the added camera's one-camera refinement
     (estimate_camera.m:247-253).  ``progress(solves)``, if given, is called
     after every solve with the solve log so far."""
@@ -128,7 +119,14 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
                                              if obs_per_shard else {})))
 
     def build(item):
-        """worker: the solve's subset and (one rank) its context"""
+        """worker: the solve's subset and (one rank) its context; an
+        after-triangulation set comes with the candidates and a snapshot of the
+        cameras, triangulated here to predict which pass the depth test"""
+        if len(item) == 5:
+            tag, j, cam_on, x3, (Ts, ws, cand) = item
+            pt_on = x3.copy()
+            pt_on[cand] = _triangulate(sc, K, Ts, ws, cand, cam_on)[3] == 1.0
+            item = (tag, j, cam_on, pt_on)
         tag, j, cam_on, pt_on = item
         cams, pts = np.nonzero(cam_on)[0], np.nonzero(pt_on)[0]
         if len(pts) == 0 or len(cams) < 2:
@@ -144,26 +142,53 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
 
     use_pf = prefetch and fix_calibration      # K (the context's) is constant then
     pool = ThreadPoolExecutor(max_workers=1) if use_pf else None
-    seq = _solve_sets(sc, init_cams) if use_pf else None
-    pending = [pool.submit(build, next(seq))] if use_pf else []
+    pending = []
+    stats = {"prefetched": 0, "mispredicted": 0}
+
+    def next_set(tag, j):
+        """the solve after (tag, j), from the current state: after a
+        before-triangulation solve the same cameras and the points that pass
+        the triangulation's depth test on the cameras as they are now (the
+        worker triangulates; the solve in between moves them a little, so a
+        marginal point may still come out the other way); after an
+        after-triangulation solve the next camera joins, points unchanged"""
+        if tag == "before-triangulation":
+            nv = np.bincount(sc.obs_pt, weights=status[sc.obs_cam], minlength=n)
+            cand = np.nonzero((X[3] == 0) & (nv >= 2))[0]
+            return ("after-triangulation", j, status.copy(), X[3] == 1,
+                    (T.copy(), w.copy(), cand))
+        jn = next((q for q in range(j + 1, m) if not status[q]), None)
+        if jn is None:
+            return None
+        st = status.copy()
+        st[jn] = True
+        return "before-triangulation", jn, st, X[3] == 1
 
     def ba(tag, j):
         cams = np.nonzero(status)[0]
         pts = np.nonzero(X[3] == 1)[0]                   # X3d_index (:252)
         t0 = time.perf_counter()
         pre = create_s = sub = None
-        if pending:
-            item, sub, pre, create_s = pending.pop().result()
-            nxt = next(seq, None)                        # the next solve's context, built
+        if use_pf:
+            if pending:
+                item, sub, pre, create_s = pending.pop().result()
+                if item[0] != tag or item[1] != j or not (np.array_equal(item[2], status) and
+                                                          np.array_equal(item[3], X[3] == 1)):
+                    if pre is not None:                  # a triangulation failed the depth
+                        pre.close()                      # test: this context is not the solve's
+                    pre = create_s = sub = None
+                    stats["mispredicted"] += 1
+                else:
+                    stats["prefetched"] += 1
+            nxt = next_set(tag, j)                       # the next solve's context, built
             if nxt is not None:                          # while this one runs
                 pending.append(pool.submit(build, nxt))
-            if item[0] != tag or item[1] != j or not (np.array_equal(item[2], status) and
-                                                      np.array_equal(item[3], X[3] == 1)):
-                if pre is not None:
-                    pre.close()
-                raise RuntimeError("incremental_bundle: prefetched solve set out of step")
         if len(pts) == 0 or len(cams) < 2:
+            if pre is not None:
+                pre.close()
             return
+        if sub is None and use_pf:                       # nothing prefetched (the first
+            _, sub, pre, create_s = build((tag, j, status.copy(), X[3] == 1))   # solve)
         wait = time.perf_counter() - t0
         pt, cam, ox = sub if sub is not None else _subset_obs(sc, cams, pts, status, X[3] == 1)
         world = world_of(len(pt))
@@ -223,10 +248,8 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
             resect(j)                                    # :230, estimate_camera.m:247-253
             ba("before-triangulation", j)                # :250-267
             nvis = np.bincount(sc.obs_pt, weights=status[sc.obs_cam], minlength=n).astype(int)
-            new = (X[3] == 0) & (nvis >= 2)              # :281-296 triangulation stand-in
-            s_, R_, t_ = _similarity(sc, X)
-            X[:3, new] = s_ * R_ @ sc.X0[:3, new] + t_[:, None]
-            X[3, new] = 1.0
+            cand = np.nonzero((X[3] == 0) & (nvis >= 2))[0]   # :281-296
+            X[:, cand] = _triangulate(sc, K, T, w, cand, status)
             ba("after-triangulation", j)                 # :300-318
     finally:
         for f in pending:                                # a prefetched context not used
@@ -238,7 +261,42 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
                 pre.close()
         if pool is not None:
             pool.shutdown()
-    return dict(solves=solves, resections=resections, K=K, T=T, w=w, X=X, status=status)
+    return dict(solves=solves, resections=resections, K=K, T=T, w=w, X=X, status=status,
+                prefetch=stats)
+
+
+def _triangulate(sc, K, T, w, pts, status):
+    """triangulation.m for points ``pts`` from their observations in the
+    cameras of ``status``: the 2k x 4 system of rows u P3 - P1, v P3 - P2
+    (P = calibration_matrix(K) [R(w) T]), X = the right singular vector of the
+    smallest singular value over its 4th entry; (0, 0, 0, 0) if any view has
+    the point at negative depth.  Returns X (4, len(pts))."""
+    out = np.zeros((4, len(pts)))
+    if len(pts) == 0:
+        return out
+    on = np.zeros(sc.n, dtype=bool)
+    on[pts] = True
+    sel = on[sc.obs_pt] & status[sc.obs_cam]             # point-major: rows per point
+    opt, ocam, ox = sc.obs_pt[sel], sc.obs_cam[sel], sc.obs_x[sel]
+    R = vl_rodr(w[:, ocam])                              # (k, 3, 3)
+    Kc = np.zeros((len(ocam), 3, 3))
+    Kc[:, 0, 0], Kc[:, 1, 1] = K[0, ocam], K[1, ocam]
+    Kc[:, 0, 2], Kc[:, 1, 2], Kc[:, 2, 2] = K[2, ocam], K[3, ocam], 1.0
+    P = Kc @ np.concatenate([R, T[:, ocam].T[:, :, None]], axis=2)   # (k, 3, 4)
+    slot = np.searchsorted(pts, opt)                     # pts ascending (np.nonzero)
+    first = np.searchsorted(opt, pts)
+    rank = np.arange(len(opt)) - first[slot]
+    kmax = int(rank.max()) + 1
+    A = np.zeros((len(pts), 2 * kmax, 4))                # zero rows leave V unchanged
+    A[slot, 2 * rank] = ox[:, 0:1] * P[:, 2] - P[:, 0]
+    A[slot, 2 * rank + 1] = ox[:, 1:2] * P[:, 2] - P[:, 1]
+    v = np.linalg.svd(A)[2][:, 3, :]                     # V(:, 4)
+    Xh = v / v[:, 3:4]
+    depth = np.einsum("kj,kj->k", P[:, 2], Xh[slot])
+    bad = np.zeros(len(pts), dtype=bool)
+    np.logical_or.at(bad, slot, depth < 0)
+    out[:, ~bad] = Xh[~bad].T
+    return out
 
 
 def _similarity(sc, X):

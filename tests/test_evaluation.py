@@ -116,4 +116,46 @@ def test_incremental_prefetch_bookkeeping(monkeypatch, prefetch):
     res = inc.incremental_bundle(sc, prefetch=prefetch)
     assert len(calls) == len(res["solves"]) == 2 * (sc.m - 2)
     assert [q["cameras"] for q in res["solves"][::2]] == list(range(3, sc.m + 1))
-    assert len(made) == (len(calls) if prefetch else 0) and all(a.closed for a in made)
+    assert all(a.closed for a in made)
+    pf = res["prefetch"]
+    if prefetch:   # every solve got a context: prefetched, or rebuilt after a wrong guess
+        assert pf["prefetched"] + pf["mispredicted"] + 1 >= len(calls)
+        assert len(made) >= len(calls) and pf["prefetched"] >= len(calls) // 2
+    else:
+        assert not made and pf == {"prefetched": 0, "mispredicted": 0}
+
+
+def test_triangulation_restatement():
+    """incremental._triangulate (triangulation.m): noise-free observations in
+    the true cameras give the true points back; a point behind one of its
+    cameras is rejected (X(4) = 0)."""
+    from bundleadjustmentmatlab_amd import incremental as inc
+    from bundleadjustmentmatlab_amd.scene import project
+    sc = make_config("cfg5", m=12, seed=3)
+    xt, _ = project(sc.K, sc.w, sc.T, sc.X, sc.obs_cam, sc.obs_pt)
+    sc.obs_x = np.ascontiguousarray(xt)
+    status = np.ones(sc.m, dtype=bool)
+    cnt = np.bincount(sc.obs_pt, minlength=sc.n)
+    pts = np.nonzero(cnt >= 2)[0]
+    X = inc._triangulate(sc, sc.K, sc.T, sc.w, pts, status)
+    assert np.all(X[3] == 1.0)
+    assert np.allclose(X[:3], sc.X[:3, pts], rtol=1e-7, atol=1e-7)
+    # move one camera so the first point lies behind it, observations
+    # re-projected in the moved camera (consistent): exactly the points at
+    # negative depth in some view are rejected, the rest come back
+    from bundleadjustmentmatlab_amd.evaluation import vl_rodr
+    i = pts[0]
+    j = sc.obs_cam[sc.obs_pt == i][0]
+    T2 = sc.T.copy()
+    T2[2, j] = -(vl_rodr(sc.w[:, j]) @ sc.X[:3, i])[2] - 5.0
+    xt2, _ = project(sc.K, sc.w, T2, sc.X, sc.obs_cam, sc.obs_pt)
+    sc.obs_x = np.ascontiguousarray(xt2)
+    X2 = inc._triangulate(sc, sc.K, T2, sc.w, pts, status)
+    depth = np.einsum("kij,jk->ki", vl_rodr(sc.w[:, sc.obs_cam]), sc.X[:3, sc.obs_pt])[:, 2] + \
+        T2[2, sc.obs_cam]
+    behind = np.zeros(sc.n, dtype=bool)
+    np.logical_or.at(behind, sc.obs_pt, depth < 0)
+    assert behind[i] and X2[3, 0] == 0.0 and np.all(X2[:, 0] == 0.0)
+    assert np.array_equal(X2[3] == 0.0, behind[pts])
+    ok = X2[3] == 1.0
+    assert np.allclose(X2[:3, ok], sc.X[:3, pts[ok]], rtol=1e-6, atol=1e-6)

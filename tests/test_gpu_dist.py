@@ -108,17 +108,21 @@ def test_rccl_one_rank_communicator():
     a[0:3], a[3:6] = sc.w0, sc.T0
     b = np.asfortranarray(sc.X0[:3])
     out = []
-    for comm in (None, unique_id_bytes()):
+    uid = unique_id_bytes()
+    # the second context with the same id takes the communicator the first
+    # left behind (libvlgba's cache: no second ncclCommInitRank on that id)
+    for comm in (None, uid, uid):
         with pkg.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, 6,
                                 comm_id=comm) as ba:
             ba.set_params(a, b)
             err, st = ba.run()
             a1, b1 = ba.get_params()
             out.append((np.array(err, copy=True), st.iterations, a1.copy(), b1.copy()))
-    (e0, n0, a0, b0), (e1, n1, a1, b1) = out
-    assert n0 == n1 and n0 > 2
-    assert np.array_equal(e0, e1)
-    assert np.array_equal(a0, a1) and np.array_equal(b0, b1)
+    (e0, n0, a0, b0) = out[0]
+    for e1, n1, a1, b1 in out[1:]:
+        assert n0 == n1 and n0 > 2
+        assert np.array_equal(e0, e1)
+        assert np.array_equal(a0, a1) and np.array_equal(b0, b1)
 
 
 @pytest.mark.timeout(600)
