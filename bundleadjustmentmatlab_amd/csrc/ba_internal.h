@@ -233,6 +233,10 @@ struct ba_dev {
     int max_lcam;                     // longest such list
     int long_o0_h;                    // first long-track observation (host copy)
     double *ylong;                    // [nlobs][3 NA] Y_a = W_a V*^-1 of each long observation
+    // per block its long-track terms as (long obs of camera j, of camera k) pairs in
+    // track order, found once at setup (k_long_pairs): [nb + 1], [pairs]
+    int *lpair_ptr;
+    int2 *lpair;
     double *vseg;                     // [nseg][12] V | eB partials per segment
     double *dpg_long;                 // [nl] point part of dp'(lambda dp + g)
     int mf_max_s, mf_max_e, mf_max_blob;   // MFMA groups' LDS sizes
@@ -297,6 +301,7 @@ struct ba_dev {
 #define BA_LONG_TERMS (1LL << 26)
 // k_schur_reduce stages a camera's long-observation list in LDS up to this length
 #define BA_LCAM_LDS 256
+#define BA_LMATCH_BATCH 48   // ... and the matched Y / W rows this many terms at a time
 
 // ---- ba_kernels.hip ----
 int ba_launch_rotations(ba_dev *d, const double *a, double *rot, int all5);
@@ -316,6 +321,9 @@ void *ba_dmalloc(size_t bytes);   // per-device caching allocator (ba_solver.cpp
 int ba_ensure_dyn_lds(const void *fn, size_t bytes);
 void ba_dfree(void *p);
 int ba_launch_schur_fast(ba_dev *d, double lambda);   // fused damp + Vinv + Y + S + e_
+// long tracks: count (fill = 0, into cnt[nb]) / write (fill = 1, at lpair_ptr) the
+// per-block (obs, obs) pairs of k_schur_reduce (context setup)
+int ba_launch_long_pairs(ba_dev *d, int fill, int *cnt);
 int ba_launch_assemble_plain(ba_dev *d, double *S, long long ld, int lower_only);
 // parity mode (ordered = 2): sequential LM scalars in the reference's flat order
 int ba_launch_parity_old_sse(ba_dev *d);

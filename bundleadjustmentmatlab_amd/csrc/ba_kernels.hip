@@ -1288,10 +1288,86 @@ __global__ __launch_bounds__(256, (NA == 6) ? BA_MF_WAVES : 1) void k_schur_mfma
 // them -- the order and the expression of the former per-pair slots, so the
 // blocks are the same bit for bit.
 struct ba_longs {
-    const int *cam_lptr, *cam_lobs, *cam_ltrk;   // NULL: no long tracks
+    const int *pair_ptr;                         // NULL: no long tracks
+    const int2 *pair;                            // per block (j obs, k obs) in track order
     const double *ylong, *W;
     int L0;                                      // first long observation
 };
+
+// Setup (once per context, the structure does not change between passes):
+// per block (j, k), the long tracks that see both cameras, in track order, as
+// (long obs of camera j, long obs of camera k) pairs.  Wave 0 searches each of
+// camera j's long observations in camera k's list (both ascending by track,
+// staged in LDS) and compacts the matches in order.  fill = 0: count them
+// into cnt[bk]; fill = 1: write them at pair[ptr[bk] ...].  Lists longer than
+// the LDS stage are merged in global memory by lane 0.
+__global__ __launch_bounds__(64) void k_long_pairs(const int *__restrict__ blk_jk, int nb,
+                                                   const int *__restrict__ cam_lptr,
+                                                   const int *__restrict__ cam_lobs,
+                                                   const int *__restrict__ cam_ltrk, int fill,
+                                                   int *__restrict__ cnt,
+                                                   const int *__restrict__ ptr,
+                                                   int2 *__restrict__ pair)
+{
+    __shared__ int la[BA_LCAM_LDS], lt[BA_LCAM_LDS], lb[BA_LCAM_LDS], ltb[BA_LCAM_LDS];
+    const int bk = blockIdx.x, l = threadIdx.x;
+    if (bk >= nb) return;
+    const int j = blk_jk[2 * bk], k = blk_jk[2 * bk + 1];
+    const int a0 = cam_lptr[j], na_ = cam_lptr[j + 1] - a0;
+    const int b0 = cam_lptr[k], nb_ = cam_lptr[k + 1] - b0;
+    int at = fill ? ptr[bk] : 0;
+    if (na_ == 0 || nb_ == 0) {
+        if (!fill && l == 0) cnt[bk] = 0;
+        return;
+    }
+    if (na_ > BA_LCAM_LDS || nb_ > BA_LCAM_LDS) {   // rare: sequential merge
+        if (l != 0) return;
+        int p = 0, q = 0, c = 0;
+        while (p < na_ && q < nb_) {
+            const int tp = cam_ltrk[a0 + p], tq = cam_ltrk[b0 + q];
+            if (tp < tq) {
+                p++;
+            } else if (tq < tp) {
+                q++;
+            } else {
+                if (fill) pair[at + c] = int2{cam_lobs[a0 + p], cam_lobs[b0 + q]};
+                c++;
+                p++;
+                q++;
+            }
+        }
+        if (!fill) cnt[bk] = c;
+        return;
+    }
+    for (int q = l; q < na_; q += 64) {
+        la[q] = cam_lobs[a0 + q];
+        lt[q] = cam_ltrk[a0 + q];
+    }
+    for (int q = l; q < nb_; q += 64) {
+        lb[q] = cam_lobs[b0 + q];
+        ltb[q] = cam_ltrk[b0 + q];
+    }
+    __syncthreads();
+    int c = 0;
+    for (int q0 = 0; q0 < na_; q0 += 64) {
+        const int q = q0 + l;
+        int pos = -1;
+        if (q < na_) {
+            const int t = lt[q];
+            int lo = 0, hi = nb_;   // first entry with track >= t
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (ltb[mid] < t) lo = mid + 1;
+                else hi = mid;
+            }
+            if (lo < nb_ && ltb[lo] == t) pos = lo;
+        }
+        const unsigned long long msk = __ballot(pos >= 0);
+        if (fill && pos >= 0) pair[at + c + __popcll(msk & ((1ull << l) - 1ull))] = int2{la[q], lb[pos]};
+        c += __popcll(msk);
+    }
+    if (!fill && l == 0) cnt[bk] = c;
+}
 
 template <int NA>
 __global__ void k_schur_reduce(const int *__restrict__ blk_jk, const int *__restrict__ blk_sptr,
@@ -1304,9 +1380,7 @@ __global__ void k_schur_reduce(const int *__restrict__ blk_jk, const int *__rest
                                double *__restrict__ sblk, double *__restrict__ rhs, ba_longs lg)
 {
     constexpr int NN = NA * NA, WS = 3 * NA;
-    __shared__ int la[BA_LCAM_LDS], lt[BA_LCAM_LDS], lb[BA_LCAM_LDS], ltb[BA_LCAM_LDS];
-    __shared__ int mj[BA_LCAM_LDS], mk[BA_LCAM_LDS];
-    __shared__ int nmatch;
+    __shared__ double ys[BA_LMATCH_BATCH * WS], ws[BA_LMATCH_BATCH * WS];
     const int bk = blockIdx.x, l = threadIdx.x;
     if (bk >= nb) return;
     const int j = blk_jk[2 * bk], k = blk_jk[2 * bk + 1];
@@ -1343,87 +1417,28 @@ __global__ void k_schur_reduce(const int *__restrict__ blk_jk, const int *__rest
         for (; q < qe; q++) e -= epart[(size_t)NA * cam_eslots[q] + r];
         rhs[(size_t)NA * j + r] = e;
     }
-    if (lg.cam_lptr) {
-        const int a0 = lg.cam_lptr[j], na_ = lg.cam_lptr[j + 1] - a0;
-        const int b0 = lg.cam_lptr[k], nb_ = lg.cam_lptr[k + 1] - b0;
-        if (na_ > 0 && nb_ > 0) {   // (uniform over the block)
-            const bool lds = na_ <= BA_LCAM_LDS && nb_ <= BA_LCAM_LDS;
-            if (lds) {
-                for (int q = l; q < na_; q += blockDim.x) {
-                    la[q] = lg.cam_lobs[a0 + q];
-                    lt[q] = lg.cam_ltrk[a0 + q];
-                }
-                for (int q = l; q < nb_; q += blockDim.x) {
-                    lb[q] = lg.cam_lobs[b0 + q];
-                    ltb[q] = lg.cam_ltrk[b0 + q];
-                }
-            }
-            __syncthreads();
-            if (lds && l < 64) {   // wave 0: matches of camera j's tracks in camera k's list
-                int cnt = 0;
-                for (int q0 = 0; q0 < na_; q0 += 64) {
-                    const int q = q0 + l;
-                    int pos = -1;
-                    if (q < na_) {
-                        const int t = lt[q];
-                        int lo = 0, hi = nb_;   // first entry with track >= t
-                        while (lo < hi) {
-                            const int mid = (lo + hi) >> 1;
-                            if (ltb[mid] < t) lo = mid + 1;
-                            else hi = mid;
-                        }
-                        if (lo < nb_ && ltb[lo] == t) pos = lo;
-                    }
-                    const unsigned long long m = __ballot(pos >= 0);
-                    if (pos >= 0) {
-                        const int at = cnt + __popcll(m & ((1ull << l) - 1ull));
-                        mj[at] = la[q];
-                        mk[at] = lb[pos];
-                    }
-                    cnt += __popcll(m);
-                }
-                if (l == 0) nmatch = cnt;
+    if (lg.pair_ptr) {
+        // the block's long-track terms in track order: the pairs' Y / W rows
+        // staged in LDS a batch at a time by every lane (all loads in flight
+        // at once), then each entry's lane subtracts the batch's terms in order
+        const int p0 = lg.pair_ptr[bk], nm = lg.pair_ptr[bk + 1] - p0;
+        for (int q0 = 0; q0 < nm; q0 += BA_LMATCH_BATCH) {
+            const int nbt = min(BA_LMATCH_BATCH, nm - q0);
+            for (int idx = l; idx < nbt * WS; idx += blockDim.x) {
+                const int bt = idx / WS, e = idx - WS * bt;
+                const int2 pr = lg.pair[p0 + q0 + bt];
+                ys[idx] = lg.ylong[(size_t)WS * pr.x + e];
+                ws[idx] = lg.W[(size_t)WS * (lg.L0 + pr.y) + e];
             }
             __syncthreads();
             if (l < NN) {
                 const int r = l % NA, c = l / NA;
-                if (lds) {
-                    const int nm = nmatch;
-                    int q = 0;
-                    for (; q + 4 <= nm; q += 4) {   // four terms' loads in flight
-                        double v[4];
-#pragma unroll
-                        for (int t = 0; t < 4; t++) {
-                            const double *y = lg.ylong + (size_t)WS * mj[q + t];
-                            const double *w = lg.W + (size_t)WS * (lg.L0 + mk[q + t]);
-                            v[t] = y[r] * w[c] + y[r + NA] * w[c + NA] + y[r + 2 * NA] * w[c + 2 * NA];
-                        }
-#pragma unroll
-                        for (int t = 0; t < 4; t++) acc -= v[t];
-                    }
-                    for (; q < nm; q++) {
-                        const double *y = lg.ylong + (size_t)WS * mj[q];
-                        const double *w = lg.W + (size_t)WS * (lg.L0 + mk[q]);
-                        acc -= y[r] * w[c] + y[r + NA] * w[c + NA] + y[r + 2 * NA] * w[c + 2 * NA];
-                    }
-                } else {   // a list past the LDS stage: merge in global memory
-                    int p = 0, q = 0;
-                    while (p < na_ && q < nb_) {
-                        const int tp = lg.cam_ltrk[a0 + p], tq = lg.cam_ltrk[b0 + q];
-                        if (tp < tq) {
-                            p++;
-                        } else if (tq < tp) {
-                            q++;
-                        } else {
-                            const double *y = lg.ylong + (size_t)WS * lg.cam_lobs[a0 + p];
-                            const double *w = lg.W + (size_t)WS * (lg.L0 + lg.cam_lobs[b0 + q]);
-                            acc -= y[r] * w[c] + y[r + NA] * w[c + NA] + y[r + 2 * NA] * w[c + 2 * NA];
-                            p++;
-                            q++;
-                        }
-                    }
+                for (int bt = 0; bt < nbt; bt++) {
+                    const double *y = ys + WS * bt, *w = ws + WS * bt;
+                    acc -= y[r] * w[c] + y[r + NA] * w[c + NA] + y[r + 2 * NA] * w[c + 2 * NA];
                 }
             }
+            __syncthreads();
         }
     }
     if (l < NN) sblk[(size_t)NN * bk + l] = acc;
@@ -2112,9 +2127,8 @@ static int launch_schur_fast(ba_dev *d, double lambda)
     KT_B(d);
     ba_longs lg{};
     if (d->nl > 0) {
-        lg.cam_lptr = d->cam_lptr;
-        lg.cam_lobs = d->cam_lobs;
-        lg.cam_ltrk = d->cam_ltrk;
+        lg.pair_ptr = d->lpair_ptr;
+        lg.pair = d->lpair;
         lg.ylong = d->ylong;
         lg.W = d->W;
         lg.L0 = d->long_o0_h;
@@ -2123,6 +2137,13 @@ static int launch_schur_fast(ba_dev *d, double lambda)
         d->blk_jk, d->blk_gptr, d->blk_gslots, d->cam_gptr, d->cam_gslots, d->spart, d->epart,
         d->U, d->eA, d->nb, lambda, d->schur_owner, d->sblk, d->rhs, lg);
     KT_E(d, KT_SCHUR_RED);
+    return -(int)hipGetLastError();
+}
+
+int ba_launch_long_pairs(ba_dev *d, int fill, int *cnt)
+{
+    k_long_pairs<<<d->nb, 64, 0, d->stream>>>(d->blk_jk, d->nb, d->cam_lptr, d->cam_lobs,
+                                              d->cam_ltrk, fill, cnt, d->lpair_ptr, d->lpair);
     return -(int)hipGetLastError();
 }
 

@@ -974,6 +974,8 @@ struct ba_aux {
     hipStream_t stream, side;
     hipEvent_t ev_fork, ev_join;
     double *hres_host, *hres_dev;
+    double *pin;        // pinned host staging of set_params (grown on demand)
+    size_t pin_cap;     // its capacity in doubles
 };
 
 struct vlgba_ctx {
@@ -1508,6 +1510,28 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         TRY(upload(d.blk_jk, hb.jk.data(), hb.jk.size(), s));
         TRY(upload(d.blk_ptr, hb.ptr.data(), hb.ptr.size(), s));
         TRY(upload(d.term, hb.term.data(), hb.term.size(), s));
+    }
+    ST_MARK("uploads");
+    if (fast && d.nl > 0) {   // the long tracks' per-block pair lists (k_long_pairs)
+        int *cnt = nullptr;
+        TRY(ctx_alloc(c, &cnt, (size_t)d.nb + 1));
+        TRY(ctx_alloc(c, &d.lpair_ptr, (size_t)d.nb + 1));
+        TRY(ba_launch_long_pairs(&d, 0, cnt));
+        std::vector<int> h((size_t)d.nb + 1, 0);
+        TRY(download(h.data(), cnt, (size_t)d.nb, s));
+        VLGBA_CHECK(hipStreamSynchronize(s));
+        long long tot = 0;
+        for (int b = 0; b < d.nb; b++) {
+            const int v = h[b];
+            h[b] = (int)tot;
+            tot += v;
+        }
+        h[d.nb] = (int)tot;
+        if (tot > 0x7fffffffLL) return VLGBA_E_ARG;
+        TRY(ctx_alloc(c, &d.lpair, (size_t)tot + 1));
+        TRY(upload(d.lpair_ptr, h.data(), (size_t)d.nb + 1, s));
+        TRY(ba_launch_long_pairs(&d, 1, nullptr));
+        ST_MARK("long_pairs");
     }
     VLGBA_CHECK(hipMemsetAsync(d.scal, 0, 8 * sizeof(double), s));
     TRY(ctx_alloc(c, &d.pub_cnt, 1));
@@ -2070,15 +2094,37 @@ int vlgba_set_params(vlgba_ctx *c, const double *a, const double *b)
 {
     if (!c || !a || !b) return VLGBA_E_ARG;
     TRY(ctx_enter(c));
-    TRY(upload(c->d.a, a, (size_t)c->d.ld, c->d.stream));
+    static const bool pageable = std::getenv("VLGBA_SETP_PAGEABLE") != nullptr;   // A/B
+    const size_t na = (size_t)c->d.ld, nb = 3 * (size_t)c->d.n;
+    ba_aux &x = c->aux;
+    if (!pageable && x.pin_cap < na + nb) {   // pinned staging: the copies start at once
+        if (x.pin) (void)hipHostFree(x.pin);
+        size_t cap = 1 << 16;
+        while (cap < na + nb) cap <<= 1;
+        x.pin = nullptr;
+        x.pin_cap = 0;
+        if (hipHostMalloc((void **)&x.pin, sizeof(double) * cap, hipHostMallocDefault) ==
+            hipSuccess)
+            x.pin_cap = cap;
+    }
+    double *ha = (!pageable && x.pin) ? x.pin : nullptr, *hb = ha ? ha + na : nullptr;
+    if (ha) std::memcpy(ha, a, sizeof(double) * na);
+    TRY(upload(c->d.a, ha ? ha : a, na, c->d.stream));
     if (!c->pperm.empty()) {   // input point order -> internal order
-        c->hb_tmp.resize(3 * (size_t)c->d.n);
+        double *dst = hb;
+        if (!dst) {
+            c->hb_tmp.resize(nb);
+            dst = c->hb_tmp.data();
+        }
         for (int i = 0; i < c->d.n; i++)
             for (int r = 0; r < 3; r++)
-                c->hb_tmp[3 * (size_t)i + r] = b[3 * ((size_t)c->p0 + c->pperm[i]) + r];
-        TRY(upload(c->d.b, c->hb_tmp.data(), 3 * (size_t)c->d.n, c->d.stream));
+                dst[3 * (size_t)i + r] = b[3 * ((size_t)c->p0 + c->pperm[i]) + r];
+        TRY(upload(c->d.b, dst, nb, c->d.stream));
+    } else if (hb) {
+        std::memcpy(hb, b + 3 * (size_t)c->p0, sizeof(double) * nb);
+        TRY(upload(c->d.b, hb, nb, c->d.stream));
     } else {
-        TRY(upload(c->d.b, b + 3 * (size_t)c->p0, 3 * (size_t)c->d.n, c->d.stream));
+        TRY(upload(c->d.b, b + 3 * (size_t)c->p0, nb, c->d.stream));
     }
     TRY(ba_launch_rotations(&c->d, c->d.a, c->d.rot, 1));
     c->lin_valid = 0;

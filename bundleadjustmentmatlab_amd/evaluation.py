@@ -126,21 +126,29 @@ def align_scene(T, Omega, X, TRef=None, OmegaRef=None, XRef=None, ScaleOption="c
     opt = str(ScaleOption).lower()
     opt = opt if opt in ("centroid", "translation") else "centroid"
     iref = 1                                              # iRef = 2 (1-based)
-    if TRef is None:                                      # :58-62
-        TRef, OmegaRef, XRef = np.zeros((3, m)), np.zeros((3, m)), np.ones((4, n))
-    TRef, OmegaRef, XRef = (np.asarray(v, dtype=np.float64) for v in (TRef, OmegaRef, XRef))
+    default_ref = TRef is None
+    if default_ref:                                       # :58-62
+        TRef, OmegaRef, XRef = np.zeros((3, m)), np.zeros((3, m)), None
+    TRef, OmegaRef = (np.asarray(v, dtype=np.float64) for v in (TRef, OmegaRef))
     Tref1 = TRef[:, 0]
     Rref1 = vl_rodr(OmegaRef[:, 0])
-    Xref1 = (Rref1 @ XRef[0:3] + Tref1[:, None]) * XRef[3]
     if opt == "centroid":
-        Sref = 1.0 / np.linalg.norm(Xref1[:, XRef[3] == 1].mean(1))
+        if default_ref:   # XRef = ones(4, n) in [I | 0]: every point is (1, 1, 1)
+            Sref = 1.0 / np.linalg.norm(np.ones(3))
+        else:
+            XRef = np.asarray(XRef, dtype=np.float64)
+            Xref1 = (Rref1 @ XRef[0:3] + Tref1[:, None]) * XRef[3]
+            Sref = 1.0 / np.linalg.norm(Xref1[:, XRef[3] == 1].mean(1))
     else:
         Sref = 1.0 / np.linalg.norm(Rref1.T @ Tref1 - vl_rodr(OmegaRef[:, iref]).T @ TRef[:, iref])
     R1 = vl_rodr(Omega[:, 0])
     T1 = T[:, 0]
-    X1 = (R1 @ X[0:3] + T1[:, None]) * X[3]
+    on = X[3] == 1                                        # :98-104
+    allon = bool(on.all())
+    Xon = X[0:3] if allon else X[0:3, on]
+    X1 = R1 @ Xon + T1[:, None]                           # the points in camera 1's frame
     if opt == "centroid":
-        S1 = 1.0 / np.linalg.norm(X1[:, X[3] == 1].mean(1))
+        S1 = 1.0 / np.linalg.norm(X1.mean(1))
     else:
         S1 = 1.0 / np.linalg.norm(R1.T @ T1 - vl_rodr(Omega[:, iref]).T @ T[:, iref])
     Rj = vl_rodr(Omega).reshape(m, 3, 3)                 # :90-97, all cameras at once
@@ -148,7 +156,10 @@ def align_scene(T, Omega, X, TRef=None, OmegaRef=None, XRef=None, ScaleOption="c
     Omega_ = vl_irodr(RjR1_ @ Rref1)
     T_ = (RjR1_ @ Tref1).T + S1 / Sref * (-(RjR1_ @ T1).T + T)
     X_ = np.zeros((4, n))
-    on = X[3] == 1                                        # :98-104
-    X_[0:3, on] = Rref1.T @ (S1 / Sref * (R1 @ X[0:3, on] + T1[:, None]) - Tref1[:, None])
+    Xn = Rref1.T @ (S1 / Sref * X1 - Tref1[:, None])
+    if allon:
+        X_[0:3] = Xn
+    else:
+        X_[0:3, on] = Xn
     X_[3, on] = 1.0
     return T_, Omega_, X_

@@ -145,6 +145,12 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
     pending = []
     stats = {"prefetched": 0, "mispredicted": 0}
 
+    # visible counts over the status cameras, kept up to date as cameras join
+    # (a bincount over every observation per solve otherwise)
+    cam_obs_pts = np.split(sc.obs_pt[np.argsort(sc.obs_cam, kind="stable")],
+                           np.cumsum(np.bincount(sc.obs_cam, minlength=m))[:-1])
+    nvis_cur = nvis.copy()
+
     def next_set(tag, j):
         """the solve after (tag, j), from the current state: after a
         before-triangulation solve the same cameras and the points that pass
@@ -153,8 +159,7 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
         marginal point may still come out the other way); after an
         after-triangulation solve the next camera joins, points unchanged"""
         if tag == "before-triangulation":
-            nv = np.bincount(sc.obs_pt, weights=status[sc.obs_cam], minlength=n)
-            cand = np.nonzero((X[3] == 0) & (nv >= 2))[0]
+            cand = np.nonzero((X[3] == 0) & (nvis_cur >= 2))[0]
             return ("after-triangulation", j, status.copy(), X[3] == 1,
                     (T.copy(), w.copy(), cand))
         jn = next((q for q in range(j + 1, m) if not status[q]), None)
@@ -241,14 +246,14 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
             if status[j]:
                 continue
             status[j] = True
+            nvis_cur[cam_obs_pts[j]] += 1
             s_, R_, t_ = _similarity(sc, X)              # ground truth -> current frame
             Rc = vl_rodr(sc.w0[:, j]) @ R_.T             # DLT stand-in: the perturbed
             w[:, j] = vl_irodr(Rc)                       # pose in the current frame
             T[:, j] = s_ * sc.T0[:, j] - Rc @ t_
             resect(j)                                    # :230, estimate_camera.m:247-253
             ba("before-triangulation", j)                # :250-267
-            nvis = np.bincount(sc.obs_pt, weights=status[sc.obs_cam], minlength=n).astype(int)
-            cand = np.nonzero((X[3] == 0) & (nvis >= 2))[0]   # :281-296
+            cand = np.nonzero((X[3] == 0) & (nvis_cur >= 2))[0]   # :281-296
             X[:, cand] = _triangulate(sc, K, T, w, cand, status)
             ba("after-triangulation", j)                 # :300-318
     finally:
