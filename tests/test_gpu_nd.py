@@ -137,10 +137,15 @@ def test_nd_spin_timeout_resolves_bit_identically(gpu, monkeypatch):
 
 def test_nd_projective(gpu):
     """The projective camera (num_a = 12: 64-row tiles hold 5 1/3 cameras, so
-    cameras straddle tiles inside every part) on the nested-dissection order:
-    one pass agrees with the natural envelope to rounding.  lambda0 = 1 keeps
-    the damped S well away from the projective gauge's null space, so both
-    orders factor it (no pinv step) and da is well determined."""
+    cameras straddle tiles inside every part) on the nested-dissection order,
+    at the reference's lambda0 = 1e-3 (bundle_projective.m:86).  The damped S
+    keeps the projective gauge's near-null directions (15 per scene), so its
+    condition number is large (2.3e13 on this scene): each order's da must be
+    a backward-stable solve of the same S (normwise backward error <= 1e-13,
+    numpy's dense S on the host, a bar independent of cond(S)), and the two
+    orders agree to 1e-9 relative as on the well-conditioned scenes (measured
+    2.8e-13: their rounding errors do not line up with the near-null
+    directions).  Neither order meets a non-positive pivot (no pinv step)."""
     from bundleadjustmentmatlab_amd.projective import pack_a
     from bundleadjustmentmatlab_amd.scene import projective_from
     sc = _scene("ladybug", 160, seed=12)
@@ -149,13 +154,24 @@ def test_nd_projective(gpu):
     out = {}
     for solver in ("envelope", "nd"):
         with gpu.BundleAdjuster(None, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, 12, m=sc.m,
-                                model="projective", solver=solver, lambda0=1.0) as ba:
+                                model="projective", solver=solver, lambda0=1e-3) as ba:
             ba.set_params(a, b)
-            info = ba.step(relinearize=True, update_lm=False)
+            S, e = ba.reduced_system(dense=True)
+            info = ba.step(relinearize=False, update_lm=False)
             da, db = ba.last_step()
-            out[solver] = (info, da.copy(), db.copy(), ba.plan_info())
-    (e0, da0, db0, p0), (e1, da1, db1, p1) = out["envelope"], out["nd"]
+            out[solver] = (info, da.reshape(-1, order="F").copy(), db.copy(), ba.plan_info(),
+                           np.tril(S) + np.tril(S, -1).T, e.reshape(-1).copy())
+    (e0, da0, db0, p0, S, rhs), (e1, da1, db1, p1, S1, _) = out["envelope"], out["nd"]
     assert p0["nd_arcs"] == 0 and p1["nd_arcs"] >= 2
+    assert np.array_equal(S, S1)
     assert e0.old_sse == e1.old_sse and e0.chol_failed == 0 and e1.chol_failed == 0
-    assert np.max(np.abs(da1 - da0)) <= 1e-8 * np.max(np.abs(da0))
-    assert np.max(np.abs(db1 - db0)) <= 1e-8 * np.max(np.abs(db0))
+    cond = np.linalg.cond(S)
+    nS = np.linalg.norm(S, 2)
+    for d in (da0, da1):
+        bwd = np.linalg.norm(S @ d - rhs) / (nS * np.linalg.norm(d) + np.linalg.norm(rhs))
+        assert bwd <= 1e-13, bwd
+    bar = 1e-9
+    rel = np.linalg.norm(da1 - da0) / np.linalg.norm(da0)
+    print(f"projective ND: cond(S) {cond:.2e}, da relative difference {rel:.2e} (bar {bar:.1e})")
+    assert rel <= bar, (rel, cond)
+    assert np.linalg.norm(db1 - db0) <= bar * np.linalg.norm(db0)
