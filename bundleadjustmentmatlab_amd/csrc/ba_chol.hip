@@ -1254,37 +1254,171 @@ __device__ __forceinline__ void gemv32(const double *M, const double *v, double 
     __syncthreads();
 }
 
-// the 32 x 32 factor and inverse: two 16-column blocks (schedule of
-// block_potrf_inv).  L -> lower triangle of As (block (0,1) keeps A), L^-1
-// (zero upper) -> Li.
-__device__ __forceinline__ bool potrf32_inv(double *As, double *Li, double *Xs)
+// One wave: wave_factor16's Cholesky of the 16x16 diagonal block at (o, o)
+// of As, and forward substitutions z = L^-1 v of up to 48 more vectors in
+// the same loop.  Every 16-lane row of the wave holds a copy of the factor
+// rows (lane l: row l & 15), so each row's DPP broadcasts see the factor's
+// column and the copies stay bit-identical; lanes 0..15 carry the identity
+// (column r of L^-1 -> Li, if Li), lanes 16 + i (i < 16) vector i of segment
+// lo and lanes 32 + i (i < 32) vector i of segment hi (in == nullptr: none).
+// The substitutions ride on the factor's broadcasts, so a panel A L^-T (rows
+// of A as the vectors) costs no separate stage.  Every lane issues the same
+// 16 unconditional LDS loads for its vector (inactive lanes read As), so the
+// loads are in flight together.  Lanes 0..15 write L (zero upper) to As.
+// Returns false on a non-positive pivot.
+struct vseg {
+    const double *in;   // entry c of vector i: in[i * irs + c * ics]
+    double *out;        // result entry c:      out[i * ors + c * ocs]
+    int irs, ics, ors, ocs;
+    int n;              // vectors (lanes 16 / 32 + i, i < n)
+};
+
+__device__ __forceinline__ bool wave_factor16x(double *As, double *Li, int o, vseg lo, vseg hi)
+{
+    const int lane = threadIdx.x & 63, r = lane & 15;
+    const bool up = lane >= 32;
+    const int idx = up ? lane - 32 : lane - 16;
+    const double *sin = up ? hi.in : lo.in;
+    const bool act = lane >= 16 && sin != nullptr && idx < (up ? hi.n : lo.n);
+    const double *pin = act ? sin + idx * (up ? hi.irs : lo.irs) : As;
+    const int ics = act ? (up ? hi.ics : lo.ics) : 0;
+    double d[16], x[16], v[16];
+#pragma unroll
+    for (int c = 0; c < 16; c++) d[c] = As[(o + r) * LP + o + c];
+#pragma unroll
+    for (int q = 0; q < 16; q++) v[q] = pin[q * ics];
+#pragma unroll
+    for (int q = 0; q < 16; q++) x[q] = lane < 16 ? ((q == r) ? 1.0 : 0.0) : (act ? v[q] : 0.0);
+    auto rsq = [&](double piv) {
+        double y = __builtin_amdgcn_rsq(piv);
+        const double hp = 0.5 * piv;
+        y = y * fma(-hp * y, y, 1.5);
+        y = y * fma(-hp * y, y, 1.5);
+        return y;
+    };
+    double y = rsq(rowbcast_c<0>(d[0]));
+#pragma unroll
+    for (int c = 0; c < 16; c++) {
+        d[c] = d[c] * y;
+        x[c] = x[c] * y;
+        if (c + 1 < 16) {
+            const double b = rowbcast(d[c], c + 1);
+            d[c + 1] = fma(-d[c], b, d[c + 1]);
+            y = rsq(rowbcast(d[c + 1], c + 1));
+            x[c + 1] = fma(-b, x[c], x[c + 1]);
+        }
+#pragma unroll
+        for (int q = c + 2; q < 16; q++) {
+            const double b = rowbcast(d[c], q);
+            d[q] = fma(-d[c], b, d[q]);
+            x[q] = fma(-b, x[c], x[q]);
+        }
+#pragma unroll
+        for (int q = c; q < 16; q++) asm volatile("" : "+v"(x[q]));
+    }
+    double dg = 1.0;
+#pragma unroll
+    for (int c = 0; c < 16; c++)
+        if (r == c) dg = d[c];
+    const bool ok = __all(lane >= 16 || (dg > 0.0 && dg < __builtin_inf()));
+    if (lane < 16) {
+#pragma unroll
+        for (int c = 0; c < 16; c++) As[(o + r) * LP + o + c] = (c <= r) ? d[c] : 0.0;
+        if (Li) {
+#pragma unroll
+            for (int c = 0; c < 16; c++) Li[(o + c) * LP + o + r] = x[c];
+        }
+    } else if (act) {
+        double *po = (up ? hi.out : lo.out) + idx * (up ? hi.ors : lo.ors);
+        const int ocs = up ? hi.ocs : lo.ocs;
+#pragma unroll
+        for (int c = 0; c < 16; c++) po[c * ocs] = x[c];
+    }
+    return ok;
+}
+
+// The 32 x 32 Cholesky of As (lower; block (0, 1) keeps A) and, if Li, L^-1
+// (row-major, zero upper) -> Li, and, if Cm, the panel Cm L^-T in place (32
+// rows), as two wave_factor16x stages with one MFMA stage between them:
+//   F0 (wave 0): L00; L10 = A10 L00^-T (lanes 16..31, in place); P0 = C0
+//      L00^-T (lanes 32..63, in place) -- or, without a panel and with rv,
+//      y0 = L00^-1 r0 (lane 32) -> yv; Li00 (lanes 0..15).  Waves 1..3 run
+//      side(w) meanwhile (work F1 needs but F0 does not, e.g. the rest of a
+//      pending update of A11 or C1).
+//   M: A11 -= L10 L10^T (wave 0); C1 -= P0 L10^T (waves 1, 2) or r1 -= L10
+//      y0 (wave 1, in rv); V = -L10 Li00 (wave 3, for Li10).
+//   F1 (wave 0): L11; P1 = C1 L11^-T (lanes 32..63) or y1 = L11^-1 r1
+//      (lane 32); Li11 (lanes 0..15); Li10 = L11^-1 V (lanes 16..31).
+// The critical path is the two 16-pivot chains plus one MFMA stage: the
+// panel and the inverse's off-diagonal block need no stage of their own.
+// The caller synchronises after filling As / Cm; results visible on return.
+#ifdef BA_STAMPS
+__device__ unsigned long long g_chst[8192][2];
+#define CH_ST(k)                                                                          \
+    do {                                                                                  \
+        if (threadIdx.x == 0 && blockIdx.x < 8192)                                        \
+            g_chst[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();                     \
+    } while (0)
+extern "C" int vlgba_debug_chstamps(unsigned long long *out, int nrec)
+{
+    if (nrec > 8192) nrec = 8192;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chst), sizeof(unsigned long long) * 2 * nrec) ==
+                   hipSuccess
+               ? 0
+               : -1;
+}
+#else
+#define CH_ST(k)
+#endif
+
+template <class Side>
+__device__ __forceinline__ bool cr32_chol(double *As, double *Li, double *Cm, double *Xs,
+                                          double *rv, double *yv, Side side)
 {
     __shared__ int bad32;
     const int tid = threadIdx.x, w = tid >> 6;
-    Li[(tid >> 4) * LP + 16 + (tid & 15)] = 0.0;   // block (0, 1) of L^-1
-    if (tid == 0) bad32 = 0;
-    if (w == 0 && !wave_factor16(As, Li, 0) && tid == 0) bad32 = 1;
-    __syncthreads();
-    if (w == 1) {   // L10 = A10 Dinv00^T
-        d4 acc = {0.0, 0.0, 0.0, 0.0};
-        acc = mfma16_nt(As, 16, 0, Li, 0, 0, acc);
-        put16(As, 16, 0, acc, 1.0, false);
+    if (Li) Li[(tid >> 4) * LP + 16 + (tid & 15)] = 0.0;   // block (0, 1) of L^-1
+    if (w == 0) {
+        const vseg lo{As + 16 * LP, As + 16 * LP, LP, 1, LP, 1, 16};   // A10 rows -> L10
+        const vseg hi = Cm ? vseg{Cm, Cm, LP, 1, LP, 1, 32}            // C0 rows -> P0
+                           : vseg{rv, yv, 0, 1, 0, 1, 1};              // or r0 -> y0
+        const bool ok = wave_factor16x(As, Li, 0, lo, hi);
+        if (tid == 0) bad32 = ok ? 0 : 1;
+    } else {
+        side(w);
     }
     __syncthreads();
-    if (w == 0) {   // A11 -= L10 L10^T, then factor it
+    CH_ST(0);
+    if (w == 0) {   // A11 -= L10 L10^T
         d4 acc = {0.0, 0.0, 0.0, 0.0};
         acc = mfma16_nt(As, 16, 0, As, 16, 0, acc);
         put16(As, 16, 16, acc, -1.0, true);
-        if (!wave_factor16(As, Li, 16) && tid == 0) bad32 = 1;
-    }
-    __syncthreads();
-    if (w == 1) {   // Li10 = -Li11 (L10 Li00)
+    } else if (w <= 2) {   // C1 -= P0 L10^T, rows 16 (w - 1) ..
+        if (Cm) {
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
+            acc = mfma16_nt(Cm, 16 * (w - 1), 0, As, 16, 0, acc);
+            put16(Cm, 16 * (w - 1), 16, acc, -1.0, true);
+        } else if (rv && w == 1 && (tid & 63) < 16) {   // r1' = r1 - L10 y0
+            const int r = tid & 63;
+            double t = 0.0;
+#pragma unroll
+            for (int c = 0; c < 16; c++) t = fma(As[(16 + r) * LP + c], yv[c], t);
+            rv[16 + r] = rv[16 + r] - t;
+        }
+    } else if (Li) {   // V = -L10 Li00
         d4 acc = {0.0, 0.0, 0.0, 0.0};
         acc = mfma16_nn(As, 16, 0, Li, 0, 0, acc);
-        put16(Xs, 0, 0, acc, 1.0, false);
-        d4 acc2 = {0.0, 0.0, 0.0, 0.0};
-        acc2 = mfma16_nn(Li, 16, 16, Xs, 0, 0, acc2);
-        put16(Li, 16, 0, acc2, -1.0, false);
+        put16(Xs, 0, 0, acc, -1.0, false);
+    }
+    __syncthreads();
+    CH_ST(1);
+    if (w == 0) {
+        // V's columns -> Li10's columns; C1 rows -> P1, or r1' -> y1
+        const vseg lo{Li ? Xs : nullptr, Li ? Li + 16 * LP : nullptr, 1, LP, 1, LP, 16};
+        const vseg hi = Cm ? vseg{Cm + 16, Cm + 16, LP, 1, LP, 1, 32}
+                           : vseg{rv ? rv + 16 : nullptr, yv ? yv + 16 : nullptr, 0, 1, 0, 1, 1};
+        const bool ok = wave_factor16x(As, Li, 16, lo, hi);
+        if (tid == 0 && !ok) bad32 = 1;
     }
     __syncthreads();
     return bad32 == 0;
@@ -1310,11 +1444,47 @@ struct cr32_lds {
     const cr32_lds sh{cr_As, cr_Bs, cr_Cs, cr_Ds, cr_Es, cr_Xs, cr_v[0], cr_v[1], cr_v[2], \
                       cr_v[3], cr_v[4], cr_part}
 
+// Diagnostic build only (make stamps): per record of k_cr32_fused, the
+// s_memrealtime (100 MHz) at entry, after its wait, before and after its
+// publish, and inside the record bodies (SC instantiation only): [4] loads
+// in LDS, [5] update applied, [6] factor + panel done, [7] before the panel
+// store; [8] / [9] cr32_chol's first pivot chain / MFMA stage done
+// (tools/cr_timeline.py)
+#ifdef BA_STAMPS
+#define CR_ST_MAX 8192
+__device__ unsigned long long g_crst[CR_ST_MAX][12];
+extern "C" int vlgba_debug_crstamps(unsigned long long *out, int nrec)
+{
+    if (nrec > CR_ST_MAX) nrec = CR_ST_MAX;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_crst), sizeof(unsigned long long) * 12 * nrec) ==
+                   hipSuccess
+               ? 0
+               : -1;
+}
+#define CR_ST(k)                                                                          \
+    do {                                                                                  \
+        if (threadIdx.x == 0 && blockIdx.x < CR_ST_MAX)                                   \
+            g_crst[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();                     \
+    } while (0)
+#define CR_SUB(k)                                                                         \
+    do {                                                                                  \
+        if constexpr (SC)                                                                 \
+            if (threadIdx.x == 0 && blockIdx.x < CR_ST_MAX)                               \
+                g_crst[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();                 \
+    } while (0)
+#else
+#define CR_ST(k)
+#define CR_SUB(k)
+#endif
+
 // factor step (level 0, on the assembled S): role 0 factors D_e, writes L_e^-1
 // (row-major 32 x 32) and y_e = L_e^-1 r_e; role 1 / 2 (split, one workgroup
-// each, redoing the same factorisation) or the same workgroup (role -1: no
-// split) form Lp_e = C(p, e) L_e^-T and Lq_e = C(q, e) L_e^-T into crL;
-// role 4 = roles 0 and 1 in one workgroup.
+// each, redoing the same factorisation) form Lp_e = C(p, e) L_e^-T / Lq_e =
+// C(q, e) L_e^-T into crL (the panel rides on the factor: cr32_chol); role 4
+// = roles 0 and 1 in one workgroup (y by a GEMV with L^-1 there: the panel
+// takes the factor's spare lanes); role -1 (no split) = role 4, then the
+// factorisation again for the q panel (the same operations as role 2, so the
+// split and unsplit launches agree bit for bit).
 template <bool SC>
 __device__ __forceinline__ void cr32_factor_body(const cr32_lds &sh, double *S, long long lds,
                                                  int TB, long long ld, int e, int p, int q,
@@ -1325,41 +1495,40 @@ __device__ __forceinline__ void cr32_factor_body(const cr32_lds &sh, double *S, 
     const int tid = threadIdx.x;
     const long long T2 = (long long)T32 * T32;
     const bool rows = role <= 0 || role == 4;
+    const int side = role == 2 ? 2 : 1;   // the panel of this pass (role 0: none)
+    const bool pan = (role == 1 || role == 4 || role < 0) ? p >= 0 : (role == 2 && q >= 0);
     load32<SC>(S, lds, TB, ld, e, e, As, false, true);
-    if ((role == 1 || role == 4) && p >= 0)
-        load32<SC>(S, lds, TB, ld, e, p, Cs, true, false);   // C(p, e) = tile(e, p)^T
-    if (role == 2) load32<SC>(S, lds, TB, ld, q, e, Cs, false, false);  // C(q, e) = tile(q, e)
+    if (pan && side == 1) load32<SC>(S, lds, TB, ld, e, p, Cs, true, false);   // C(p, e) = tile(e, p)^T
+    if (pan && side == 2) load32<SC>(S, lds, TB, ld, q, e, Cs, false, false);  // C(q, e) = tile(q, e)
     if (rows && tid < T32) {
         const long long g = (long long)TB * e + tid;
         rk[tid] = (tid < TB && g < ld) ? ldg<SC>(rhs + g) : 0.0;
     }
     __syncthreads();
-    const bool ok = potrf32_inv(As, Bs, Xs);
+    CR_SUB(4);
+    CR_SUB(5);
+    // y rides on the factor's spare lanes unless a panel fills them (roles 4, -1)
+    const bool ylanes = rows && !pan;
+    const bool ok = cr32_chol(As, rows ? Bs : nullptr, pan ? Cs : nullptr, Xs,
+                              ylanes ? rk : nullptr, yk, [](int) {});
+    CR_SUB(6);
+    if (pan) {
+        CR_SUB(7);
+        store_rm32<SC>(crL + T2 * (side == 1 ? e : nt + e), Cs);
+    }
     if (rows) {
-        gemv32(Bs, rk, sh.part, yk, false);
+        if (!ylanes) gemv32(Bs, rk, sh.part, yk, false);
         if (tid < TB) stg<SC>(y + (long long)TB * e + tid, yk[tid]);
         store_rm32<SC>(linv + T2 * e, Bs);
         if (tid == 0 && !ok) status[0] = 1.0;
-        if (role == 0) return;   // split: roles 1 and 2 form the panels
     }
-    for (int side = 1; side <= 2; side++) {
-        if (role > 0 && role != side && !(role == 4 && side == 1)) continue;
-        const int nb = side == 1 ? p : q;
-        if (nb < 0) continue;
-        if (role < 0) {
-            __syncthreads();
-            if (side == 1)
-                load32<SC>(S, lds, TB, ld, e, p, Cs, true, false);
-            else
-                load32<SC>(S, lds, TB, ld, q, e, Cs, false, false);
-            __syncthreads();
-        }
-        d4 acc = {0.0, 0.0, 0.0, 0.0};
-        acc = mfma32_nt(Cs, Bs, acc);   // C L^-T: [r][c] = sum_t C[r][t] Li[c][t]
+    if (role < 0 && q >= 0) {   // unsplit: the q panel (role 2's pass)
         __syncthreads();
-        put32(Cs, acc, 1.0, false);
+        load32<SC>(S, lds, TB, ld, e, e, As, false, true);
+        load32<SC>(S, lds, TB, ld, q, e, Cs, false, false);
         __syncthreads();
-        store_rm32<SC>(crL + T2 * (side == 1 ? e : nt + e), Cs);
+        cr32_chol(As, nullptr, Cs, Xs, nullptr, nullptr, [](int) {});
+        store_rm32<SC>(crL + T2 * (nt + e), Cs);
     }
 }
 
@@ -1390,73 +1559,126 @@ __global__ __launch_bounds__(256) void k_cr32_factor(double *__restrict__ S, lon
 // (em / ep: the tiles eliminated at L-1 next to k), and the coupling of two
 // neighbours k < k2 at level L is the fill C(k2, k) = -L(k2, e) L(k, e)^T of
 // the tile e eliminated between them.  Workgroups 3x + role for the tiles
-// eliminated here (role 0: apply the update in LDS, factor, y, L^-1; roles 1 /
-// 2: the same factorisation plus their fill tile C(p, e) / C(q, e), then the
-// panel), then one workgroup per surviving tile (role 3: apply the update,
-// write D_k and r_k back).  Records: fused (e, p, q, em, ep), survivor (k, em, ep).
-template <bool SC>
+// eliminated here (role 0: apply the update, factor, y, L^-1; roles 1 / 2:
+// the same factorisation with their fill tile C(p, e) / C(q, e) as the panel
+// rows of cr32_chol), then one workgroup per surviving tile (role 3: apply
+// the update, write D_k back, mid(), then r_k).  Records: fused (e, p, q,
+// em, ep), survivor (k, em, ep).  The eliminated tiles' update is split by
+// 16 x 16 block: D00 and D10 (and the fill's first 16 columns) before the
+// first pivot chain, D11 and the rest of the fill beside it (cr32_chol's
+// side); role 0's r update runs beside the D00 / D10 blocks.  mid: the
+// survivor's D_k is published before its r_k (k_cr32_fused: the panel roles
+// of the next level need only D_k, and r_k waits for the neighbours' y).
+// r_k -= L(k, em) y_em + L(k, ep) y_ep by one wave: lane r < 32 row r of the
+// first product, lane 32 + r of the second, each a sequential sum over the
+// 32 columns.
+__device__ __forceinline__ void cr32_rupd(const double *Bs, const double *Cs, bool two,
+                                          const double *ym, const double *yp, double *rk,
+                                          double *up)
+{
+    const int lane = threadIdx.x & 63, r = lane & 31;
+    const double *M = lane < 32 ? Bs : Cs;
+    const double *v = lane < 32 ? ym : yp;
+    double t = 0.0;
+#pragma unroll
+    for (int c = 0; c < T32; c++) t = fma(M[r * LP + c], v[c], t);
+    if (lane >= 32) up[r] = two ? t : 0.0;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane < 32) rk[r] = (rk[r] - t) - up[r];
+}
+
+template <bool SC, class Mid>
 __device__ __forceinline__ void cr32_level_body(const cr32_lds &sh, double *S, long long lds,
                                                 int TB, long long ld, int k, int p, int q, int em,
                                                 int ep, int role, int nt, double *linv,
                                                 double *crL, double *rhs, double *y,
-                                                double *status)
+                                                double *status, Mid mid)
 {
     double *As = sh.As, *Bs = sh.Bs, *Cs = sh.Cs, *Ds = sh.Ds, *Es = sh.Es, *Xs = sh.Xs;
     double *rk = sh.rk, *ym = sh.ym, *yp = sh.yp, *um = sh.um, *up = sh.up;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, w = tid >> 6;
     const long long T2 = (long long)T32 * T32;
     const bool surv = role == 3;
+    auto load_r = [&]() {
+        if (tid < T32) {
+            const long long g = (long long)TB * k + tid;
+            rk[tid] = (tid < TB && g < ld) ? ldg<SC>(rhs + g) : 0.0;
+            ym[tid] = tid < TB ? ldg<SC>(y + (long long)TB * em + tid) : 0.0;
+            yp[tid] = (ep >= 0 && tid < TB) ? ldg<SC>(y + (long long)TB * ep + tid) : 0.0;
+        }
+    };
     load32<SC>(S, lds, TB, ld, k, k, As, false, true);
     load_rm32<SC>(crL + T2 * (nt + em), Bs);            // L(k, em)
     if (ep >= 0) load_rm32<SC>(crL + T2 * ep, Cs);      // L(k, ep)
     if (role == 1) load_rm32<SC>(crL + T2 * em, Ds);    // L(p, em)
     if (role == 2) load_rm32<SC>(crL + T2 * (nt + ep), Ds);   // L(q, ep)
-    const bool rows = surv || role == 0;
-    if (rows && tid < T32) {
-        const long long g = (long long)TB * k + tid;
-        rk[tid] = (tid < TB && g < ld) ? ldg<SC>(rhs + g) : 0.0;
-        ym[tid] = tid < TB ? ldg<SC>(y + (long long)TB * em + tid) : 0.0;
-        yp[tid] = (ep >= 0 && tid < TB) ? ldg<SC>(y + (long long)TB * ep + tid) : 0.0;
-    }
+    if (role == 0) load_r();
     __syncthreads();
-    if (role == 1 || role == 2) {   // the fill: C(p, e) = -L(p, em) L(e, em)^T | C(q, e) = -L(q, ep) L(e, ep)^T
-        d4 f = {0.0, 0.0, 0.0, 0.0};
-        f = mfma32_nt(Ds, role == 1 ? Bs : Cs, f);
-        put32(Es, f, -1.0, false);
-    }
-    {
+    CR_SUB(4);
+    if (surv) {
         d4 acc = {0.0, 0.0, 0.0, 0.0};
         acc = mfma32_nt(Bs, Bs, acc);
         if (ep >= 0) acc = mfma32_nt(Cs, Cs, acc);
         put32(As, acc, -1.0, true);   // each thread updates the elements it owns
-    }
-    if (rows) {
-        gemv32(Bs, ym, sh.part, um, false);
-        if (ep >= 0) gemv32(Cs, yp, sh.part, up, false);
-        if (tid < T32) rk[tid] = (rk[tid] - um[tid]) - (ep >= 0 ? up[tid] : 0.0);
-    }
-    __syncthreads();
-    if (surv) {
+        __syncthreads();
         store32<SC>(S, lds, TB, ld, k, k, As);
+        mid();
+        load_r();
+        __syncthreads();
+        if (w == 0) cr32_rupd(Bs, Cs, ep >= 0, ym, yp, rk, up);
+        __syncthreads();
         if (tid < TB) {
             const long long g = (long long)TB * k + tid;
             if (g < ld) stg<SC>(rhs + g, rk[tid]);
         }
         return;
     }
-    const bool ok = potrf32_inv(As, Bs, Xs);   // L^-1 over L(k, em), no longer needed
-    if (role == 0) {
-        gemv32(Bs, rk, sh.part, um, false);
+    const double *G = role == 2 ? Cs : Bs;   // the fill's right factor: L(k, em) | L(k, ep)
+    // block (ri, ci) of D -= Lm Lm^T + Lp Lp^T (K = 32 each)
+    auto dupd = [&](int ri, int ci) {
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        acc = mfma16_nt(Bs, ri, 0, Bs, ci, 0, acc);
+        acc = mfma16_nt(Bs, ri, 16, Bs, ci, 16, acc);
+        if (ep >= 0) {
+            acc = mfma16_nt(Cs, ri, 0, Cs, ci, 0, acc);
+            acc = mfma16_nt(Cs, ri, 16, Cs, ci, 16, acc);
+        }
+        put16(As, ri, ci, acc, -1.0, true);
+    };
+    // block (ri, ci) of the fill: Es = -Ds G^T
+    auto fill = [&](int ri, int ci) {
+        d4 f = {0.0, 0.0, 0.0, 0.0};
+        f = mfma16_nt(Ds, ri, 0, G, ci, 0, f);
+        f = mfma16_nt(Ds, ri, 16, G, ci, 16, f);
+        put16(Es, ri, ci, f, -1.0, false);
+    };
+    const bool pan = role != 0;
+    if (w == 0)
+        dupd(0, 0);
+    else if (w == 1)
+        dupd(16, 0);
+    else if (pan)
+        fill(16 * (w - 2), 0);
+    else if (w == 2)
+        cr32_rupd(Bs, Cs, ep >= 0, ym, yp, rk, up);
+    __syncthreads();
+    CR_SUB(5);
+    const bool ok = cr32_chol(As, pan ? nullptr : Ds, pan ? Es : nullptr, Xs, pan ? nullptr : rk,
+                              um, [&](int ww) {
+                                  if (ww == 1)
+                                      dupd(16, 16);
+                                  else if (pan)
+                                      fill(16 * (ww - 2), 16);
+                              });
+    CR_SUB(6);
+    if (role == 0) {   // L^-1 in Ds (no fill for role 0), y in um
         if (tid < TB) stg<SC>(y + (long long)TB * k + tid, um[tid]);
-        store_rm32<SC>(linv + T2 * k, Bs);
+        store_rm32<SC>(linv + T2 * k, Ds);
         if (tid == 0 && !ok) status[0] = 1.0;
         return;
     }
-    d4 acc = {0.0, 0.0, 0.0, 0.0};
-    acc = mfma32_nt(Es, Bs, acc);   // C L^-T
-    __syncthreads();
-    put32(Es, acc, 1.0, false);
-    __syncthreads();
+    CR_SUB(7);
     store_rm32<SC>(crL + T2 * (role == 1 ? k : nt + k), Es);
 }
 
@@ -1488,10 +1710,66 @@ __global__ __launch_bounds__(256) void k_cr32_level(double *__restrict__ S, long
         if ((role == 1 && p < 0) || (role == 2 && q < 0)) return;
     }
     cr32_level_body<false>(sh, S, lds, TB, ld, k, p, q, em, ep, role, nt, linv, crL, rhs, y,
-                           status);
+                           status, [] {});
 }
 
-// back substitution: x_e = L_e^-T (y_e - Lp_e^T x_p - Lq_e^T x_q)
+// Back substitution of one eliminated tile e (neighbours p, q):
+//     x_e = L_e^-T (y_e - Lp_e^T x_p - Lq_e^T x_q) = z_e - Mp x_p - Mq x_q,
+//     z_e = L_e^-T y_e,  Mp = L_e^-T Lp_e^T,  Mq = L_e^-T Lq_e^T.
+// z, Mp and Mq need only the factor step's outputs, so they are formed
+// before the neighbours' x is fetched (while k_cr32_fused / k_cr32_back_all
+// wait for it); after the fetch a single 32 x 64 matrix-vector product
+// remains.  fetch(xp, xq) puts x_p / x_q (zero where absent) in LDS and ends
+// with a barrier; the caller's loads of the tiles are done and synchronised.
+// Mp / Mq overwrite Lp / Lq.  Returns x_e in u.
+__device__ __forceinline__ d4 mfma32_tn(const double *At, const double *Bt, d4 acc)
+{
+    // acc (one 16 x 16 block per wave) of A B^T over K = 32, A given
+    // transposed (At[t][r]): [r][c] = sum_t At[t][r] Bt[c][t]
+    const int w = threadIdx.x >> 6, ra = 16 * (w >> 1), cb = 16 * (w & 1);
+    const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+#pragma unroll
+    for (int s = 0; s < 8; s++)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(At[(4 * s + lk) * LP + ra + li],
+                                                   Bt[(cb + li) * LP + 4 * s + lk], acc, 0, 0, 0);
+    return acc;
+}
+
+template <class Fetch>
+__device__ __forceinline__ void cr32_back_core(double *Lp, double *Lq, const double *Li,
+                                               const double *t, double *z, double *xp,
+                                               double *xq, double *u, double (*part)[T32],
+                                               bool hp, bool hq, Fetch fetch)
+{
+    const int tid = threadIdx.x;
+    d4 ap = {0.0, 0.0, 0.0, 0.0}, aq = {0.0, 0.0, 0.0, 0.0};
+    if (hp) ap = mfma32_tn(Li, Lp, ap);   // Mp[r][c] = sum_t Li[t][r] Lp[c][t]
+    if (hq) aq = mfma32_tn(Li, Lq, aq);
+    gemv32(Li, t, part, z, true);         // z = L^-T y (ends with a barrier)
+    if (hp) put32(Lp, ap, 1.0, false);
+    if (hq) put32(Lq, aq, 1.0, false);
+    fetch(xp, xq);                        // ends with a barrier
+    // x = z - [Mp | Mq] [x_p; x_q]: thread (row r, part of 8 columns)
+    const int r = tid & 31, pq = tid >> 5;
+    const double *M = pq < 4 ? Lp : Lq;
+    const double *v = pq < 4 ? xp : xq;
+    const bool on = pq < 4 ? hp : hq;
+    const int c0 = 8 * (pq & 3);
+    double acc = 0.0;
+    if (on) {
+#pragma unroll
+        for (int c = c0; c < c0 + 8; c++) acc = fma(M[r * LP + c], v[c], acc);
+    }
+    part[pq][r] = acc;
+    __syncthreads();
+    if (tid < T32)
+        u[tid] = z[tid] - ((((((((part[0][tid] + part[1][tid]) + part[2][tid]) + part[3][tid]) +
+                               part[4][tid]) + part[5][tid]) + part[6][tid]) + part[7][tid]));
+    __syncthreads();
+}
+
+// back substitution, one launch per level (the no-spin re-solve): x_p and x_q
+// come from the previous launches
 __global__ __launch_bounds__(256) void k_cr32_back(const int *__restrict__ elim, int nt, int TB,
                                                    long long ld,
                                                    const double *__restrict__ linv,
@@ -1499,44 +1777,41 @@ __global__ __launch_bounds__(256) void k_cr32_back(const int *__restrict__ elim,
                                                    const double *__restrict__ y,
                                                    double *__restrict__ x)
 {
-    __shared__ __attribute__((aligned(16))) double Ls[T32 * LP];
-    __shared__ double t[T32], u[T32];
+    __shared__ __attribute__((aligned(16))) double Lp[T32 * LP], Lq[T32 * LP], Li[T32 * LP];
+    __shared__ __attribute__((aligned(16))) double t[T32], z[T32], xp[T32], xq[T32], u[T32];
     __shared__ double part[8][T32];
     const int tid = threadIdx.x;
     const int e = elim[3 * blockIdx.x], p = elim[3 * blockIdx.x + 1], q = elim[3 * blockIdx.x + 2];
     const long long T2 = (long long)T32 * T32;
+    if (p >= 0) load_rm32(crL + T2 * e, Lp);
+    if (q >= 0) load_rm32(crL + T2 * (nt + e), Lq);
+    load_rm32(linv + T2 * e, Li);
     if (tid < T32) t[tid] = tid < TB ? y[(long long)TB * e + tid] : 0.0;
-    for (int side = 0; side < 2; side++) {
-        const int nb = side == 0 ? p : q;
-        if (nb < 0) continue;
-        load_rm32(crL + T2 * (side == 0 ? e : nt + e), Ls);
-        if (tid < T32) {
-            const long long g = (long long)TB * nb + tid;
-            u[tid] = (tid < TB && g < ld) ? x[g] : 0.0;
-        }
-        __syncthreads();
-        gemv32(Ls, u, part, u, true);
-        if (tid < T32) t[tid] -= u[tid];
-        __syncthreads();
-    }
-    load_rm32(linv + T2 * e, Ls);
     __syncthreads();
-    gemv32(Ls, t, part, u, true);
+    cr32_back_core(Lp, Lq, Li, t, z, xp, xq, u, part, p >= 0, q >= 0,
+                   [&](double *a, double *b) {
+                       if (tid < 2 * T32) {
+                           const int nb = tid < T32 ? p : q, i = tid & 31;
+                           const long long g = (long long)TB * nb + i;
+                           (tid < T32 ? a : b)[i] = (nb >= 0 && i < TB && g < ld) ? x[g] : 0.0;
+                       }
+                       __syncthreads();
+                   });
     if (tid < TB) {
         const long long g = (long long)TB * e + tid;
         if (g < ld) x[g] = u[tid];
     }
 }
 
-// One record of the one-launch back substitution: it prefetches its three
-// tiles, then waits for x_p and x_q, which the records of the tiles eliminated
-// above it publish as epoch-tagged 8-byte granules {epoch, 32-bit half}
-// (write-through agent-scope stores: the data is the flag, no fences;
-// MI355X_MICROARCH.md / cdna_hip_programming.md Guideline 16, R2).  One wave
-// sweeps one neighbour's 64 granules until every tag matches; a spin that
-// never ends sets the timeout word status[1] (the host then re-solves the pass
-// with the per-level launches, which never spin) instead of
-// hanging.  Same arithmetic as k_cr32_back.
+// One record of the one-launch back substitution: it loads its three tiles,
+// forms z, Mp and Mq (cr32_back_core), then waits for x_p and x_q, which the
+// records of the tiles eliminated above it publish as epoch-tagged 8-byte
+// granules {epoch, 32-bit half} (write-through agent-scope stores: the data
+// is the flag, no fences; MI355X_MICROARCH.md / cdna_hip_programming.md
+// Guideline 16, R2).  One wave sweeps one neighbour's 64 granules until every
+// tag matches; a spin that never ends sets the timeout word status[1] (the
+// host then re-solves the pass with the per-level launches, which never spin)
+// instead of hanging.  Same arithmetic as k_cr32_back.
 template <bool SC>
 __device__ __forceinline__ void cr32_back_body(const cr32_lds &sh, int e, int p, int q, int nt,
                                                int TB, long long ld, const double *linv,
@@ -1545,44 +1820,40 @@ __device__ __forceinline__ void cr32_back_body(const cr32_lds &sh, int e, int p,
                                                double *status)
 {
     double *Lp = sh.As, *Lq = sh.Bs, *Li = sh.Cs;
-    double *t = sh.rk, *xp = sh.ym, *xq = sh.yp, *u = sh.um;
+    double *t = sh.rk, *xp = sh.ym, *xq = sh.yp, *u = sh.um, *z = sh.up;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const long long T2 = (long long)T32 * T32;
-    // the tiles: loads in flight while we wait
     if (p >= 0) load_rm32<SC>(crL + T2 * e, Lp);
     if (q >= 0) load_rm32<SC>(crL + T2 * (nt + e), Lq);
     load_rm32<SC>(linv + T2 * e, Li);
     if (tid < T32) t[tid] = tid < TB ? ldg<SC>(y + (long long)TB * e + tid) : 0.0;
-    if (wv < 2) {
-        const int nb = wv == 0 ? p : q;
-        if (nb >= 0) {
-            const unsigned long long *g = xg + 64 * (size_t)nb + lane;
-            unsigned long long v = 0;
-            for (unsigned spins = 0;; spins++) {
-                v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (__all((unsigned)(v >> 32) == epoch)) break;
-                if (spins >= BA_BACK_SPIN_MAX) {
-                    if (lane == 0) status[1] = 1.0;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-            // lane 2r: low half of x_r, lane 2r + 1: high half
-            reinterpret_cast<unsigned *>(wv == 0 ? xp : xq)[lane] = (unsigned)v;
-        }
-    }
     __syncthreads();
-    if (p >= 0) {
-        gemv32(Lp, xp, sh.part, u, true);
-        if (tid < T32) t[tid] -= u[tid];
-        __syncthreads();
-    }
-    if (q >= 0) {
-        gemv32(Lq, xq, sh.part, u, true);
-        if (tid < T32) t[tid] -= u[tid];
-        __syncthreads();
-    }
-    gemv32(Li, t, sh.part, u, true);   // x_e = L_e^-T t (ends with a barrier)
+    cr32_back_core(Lp, Lq, Li, t, z, xp, xq, u, sh.part, p >= 0, q >= 0,
+                   [&](double *a, double *b) {
+                       if (wv < 2) {
+                           const int nb = wv == 0 ? p : q;
+                           double *dst = wv == 0 ? a : b;
+                           if (nb >= 0) {
+                               const unsigned long long *g = xg + 64 * (size_t)nb + lane;
+                               unsigned long long v = 0;
+                               for (unsigned spins = 0;; spins++) {
+                                   v = __hip_atomic_load(g, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+                                   if (__all((unsigned)(v >> 32) == epoch)) break;
+                                   if (spins >= BA_BACK_SPIN_MAX) {
+                                       if (lane == 0) status[1] = 1.0;
+                                       break;
+                                   }
+                                   __builtin_amdgcn_s_sleep(2);
+                               }
+                               // lane 2r: low half of x_r, lane 2r + 1: high half
+                               reinterpret_cast<unsigned *>(dst)[lane] = (unsigned)v;
+                           } else if (lane < T32) {
+                               dst[lane] = 0.0;
+                           }
+                       }
+                       __syncthreads();
+                   });
     if (wv == 0) {   // publish x_e: 64 granules, one 8-byte write-through store each
         const unsigned h = reinterpret_cast<const unsigned *>(u)[lane];
         __hip_atomic_store(xg + 64 * (size_t)e + lane, ((unsigned long long)epoch << 32) | h,
@@ -1610,9 +1881,9 @@ __global__ __launch_bounds__(256) void k_cr32_back_all(const int *__restrict__ e
                                                        unsigned epoch, double *status)
 {
     __shared__ __attribute__((aligned(16))) double Lp[T32 * LP], Lq[T32 * LP], Li[T32 * LP];
-    __shared__ __attribute__((aligned(16))) double t[T32], xp[T32], xq[T32], u[T32];
+    __shared__ __attribute__((aligned(16))) double t[T32], xp[T32], xq[T32], u[T32], z[T32];
     __shared__ double part[8][T32];
-    const cr32_lds sh{Lp, Lq, Li, nullptr, nullptr, nullptr, t, xp, xq, u, nullptr, part};
+    const cr32_lds sh{Lp, Lq, Li, nullptr, nullptr, nullptr, t, xp, xq, u, z, part};
     const int rec = nrec - 1 - (int)blockIdx.x;
     const int e = elim[3 * rec], p = elim[3 * rec + 1], q = elim[3 * rec + 2];
     cr32_back_body<false>(sh, e, p, q, nt, TB, ld, linv, crL, y, x, xg, epoch, status);
@@ -1627,8 +1898,14 @@ __global__ __launch_bounds__(256) void k_cr32_back_all(const int *__restrict__ e
 // (bit-identical), with the launch boundaries replaced by per-record
 // dependencies: a record waits only for the records whose outputs it reads,
 //   level L >= 1, tile k (neighbours em / ep eliminated at L-1):
-//     roles 0..2 of em and ep at L-1 (L(k, em), L(k, ep), y, the fill panels)
-//     and k's own survivor record at L-1 (D_k, r_k) when L >= 2;
+//     role 0 / survivor: roles 0..2 of em and ep at L-1 (L(k, em), L(k, ep),
+//     y); roles 1 / 2: only the panels they read (L(k, em) = role 2 of em,
+//     L(k, ep) = role 1 of ep, the fill's L(p, em) = role 1 of em or
+//     L(q, ep) = role 2 of ep); all: k's own survivor record at L-1 (D_k,
+//     r_k) when L >= 2 (survivor records publish D_k and r_k separately: the
+//     panel roles wait for D_k only, role 0 for both);
+//   survivor at L: L(k, em), L(k, ep) (and D_k at L-1) for D_k, then the
+//     neighbours' role 0 (y) and its own r_k at L-1 for r_k;
 //   back record of e (eliminated at Le): roles 0..2 of e at Le, then the
 //     x granules of its neighbours (as k_cr32_back_all).
 // Hand-offs: payload stored sc1 (stg<true>), every storing wave's vmcnt(0),
@@ -1684,28 +1961,6 @@ __device__ __forceinline__ void cr32_publish(unsigned *flag, unsigned epoch, int
                            __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Diagnostic build only (make stamps): per record of k_cr32_fused, the
-// s_memrealtime (100 MHz) at entry, after its wait, before and after its
-// publish (tools/cr_timeline.py)
-#ifdef BA_STAMPS
-#define CR_ST_MAX 8192
-__device__ unsigned long long g_crst[CR_ST_MAX][4];
-extern "C" int vlgba_debug_crstamps(unsigned long long *out, int nrec)
-{
-    if (nrec > CR_ST_MAX) nrec = CR_ST_MAX;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_crst), sizeof(unsigned long long) * 4 * nrec) ==
-                   hipSuccess
-               ? 0
-               : -1;
-}
-#define CR_ST(k)                                                                          \
-    do {                                                                                  \
-        if (threadIdx.x == 0 && blockIdx.x < CR_ST_MAX)                                   \
-            g_crst[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();                     \
-    } while (0)
-#else
-#define CR_ST(k)
-#endif
 
 __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, int TB, long long ld,
                                                     const int *__restrict__ elim,
@@ -1721,8 +1976,8 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
     const int b = blockIdx.x;
     int L = 0;
     while (L < P.nl && b >= P.b0[L + 1]) L++;
-    // flag word of (level, tile, role): role 3 = survivor
-    auto fw = [&](int lev, int t, int r) { return 4 * (lev * nt + t) + r; };
+    // flag word of (level, tile, role): 3 = survivor's D_k, 4 = its r_k
+    auto fw = [&](int lev, int t, int r) { return 5 * (lev * nt + t) + r; };
     if (L == 0) {
         // three records per tile, or two (roles 0 + 1 merged) when three would
         // not all fit on the CUs at once (one workgroup per CU)
@@ -1760,17 +2015,42 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
             ep = fr[4];
         }
         int w[8] = {0, 0, 0, 0, 0, 0, 0, 0}, nw = 0;
-        for (int rr = 0; rr < 3; rr++) w[nw++] = fw(L - 1, em, rr);
-        if (ep >= 0)
-            for (int rr = 0; rr < 3; rr++) w[nw++] = fw(L - 1, ep, rr);
-        if (L >= 2) w[nw++] = fw(L - 1, k, 3);
+        if (role == 1 || role == 2) {   // panels only: L(k, em), L(k, ep) and the fill's
+            w[nw++] = fw(L - 1, em, 2);  // L(p, em) | L(q, ep) -- not role 0's y / L^-1
+            if (role == 1) w[nw++] = fw(L - 1, em, 1);
+            if (ep >= 0) {
+                w[nw++] = fw(L - 1, ep, 1);
+                if (role == 2) w[nw++] = fw(L - 1, ep, 2);
+            }
+            if (L >= 2) w[nw++] = fw(L - 1, k, 3);
+        } else if (role == 3) {         // survivor, D_k first: L(k, em), L(k, ep)
+            w[nw++] = fw(L - 1, em, 2);
+            if (ep >= 0) w[nw++] = fw(L - 1, ep, 1);
+            if (L >= 2) w[nw++] = fw(L - 1, k, 3);
+        } else {
+            for (int rr = 0; rr < 3; rr++) w[nw++] = fw(L - 1, em, rr);
+            if (ep >= 0)
+                for (int rr = 0; rr < 3; rr++) w[nw++] = fw(L - 1, ep, rr);
+            if (L >= 2) {
+                w[nw++] = fw(L - 1, k, 3);
+                w[nw++] = fw(L - 1, k, 4);
+            }
+        }
         cr32_wait_flags(flag, nw, w, epoch, status);
         CR_ST(1);
+        // the survivor's r_k: the neighbours' y and its own r_k of level L-1
+        auto mid = [&]() {
+            cr32_publish(flag + fw(L, k, 3), epoch);
+            int w2[8] = {fw(L - 1, em, 0), 0, 0, 0, 0, 0, 0, 0}, n2 = 1;
+            if (ep >= 0) w2[n2++] = fw(L - 1, ep, 0);
+            if (L >= 2) w2[n2++] = fw(L - 1, k, 4);
+            cr32_wait_flags(flag, n2, w2, epoch, status);
+        };
         if (!((role == 1 && p < 0) || (role == 2 && q < 0)))
             cr32_level_body<true>(sh, S, lds, TB, ld, k, p, q, em, ep, role, nt, linv, crL, rhs,
-                                  y, status);
+                                  y, status, mid);
         CR_ST(2);
-        cr32_publish(flag + fw(L, k, role), epoch);
+        cr32_publish(flag + fw(L, k, role == 3 ? 4 : role), epoch);
         CR_ST(3);
         return;
     }
@@ -2270,7 +2550,7 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
                 d->cr_fused = !(ev && ev[0] == '0') && nl <= BA_CR_MAXLEV;
             }
             if (d->cr_fused) {
-                const size_t nfl = (size_t)4 * nl * nt;
+                const size_t nfl = (size_t)5 * nl * nt;
                 TRY_RC(dev_alloc(&d->crflag, sizeof(unsigned) * nfl));
                 VLGBA_CHECK(hipMemsetAsync(d->crflag, 0, sizeof(unsigned) * nfl, d->stream));
             }

@@ -23,9 +23,10 @@ from bundleadjustmentmatlab_amd import BundleAdjuster  # noqa: E402
 from bundleadjustmentmatlab_amd.scene import make_config  # noqa: E402
 
 
-def record_levels(nt, ncu=256):
+def record_levels(nt, ncu=256, roles=None):
     """Block -> (kind, level) of k_cr32_fused, as ba_chol_setup / ba_chol_solve
-    lay the records out."""
+    lay the records out (``roles``, if given, receives each block's role)."""
+    roles = [] if roles is None else roles
     act = list(range(nt))
     levels = []
     while act:
@@ -37,10 +38,13 @@ def record_levels(nt, ncu=256):
     ne0 = levels[0][0]
     per = 2 if 3 * ne0 > ncu else 3
     kinds += [("factor", 0)] * (per * ne0)
+    roles[:] = [(2 if (b & 1) else 4) if per == 2 else b % 3 for b in range(per * ne0)]
     for lv in range(1, len(levels)):
         ne = levels[lv][0]
         kinds += [("fused", lv)] * (3 * ne) + [("survivor", lv)] * levels[lv][1]
+        roles += [b % 3 for b in range(3 * ne)] + [3] * levels[lv][1]
     kinds += [("back", -1)] * nt
+    roles += [-1] * nt
     return kinds
 
 
@@ -62,12 +66,23 @@ def main():
     plan = ba.plan_info()
     rows = plan["cr_rows"]
     nt = -(-6 * sc.m // rows)
-    kinds = record_levels(nt)
+    roles = []
+    kinds = record_levels(nt, roles=roles)
+    roles = np.array(roles)
     nrec = len(kinds)
-    st = (ctypes.c_ulonglong * (4 * nrec))()
+    st = (ctypes.c_ulonglong * (12 * nrec))()
     assert fn(st, nrec) == 0
-    t = np.array(st, dtype=np.float64).reshape(nrec, 4) / 100.0   # us
-    t -= t[:, 0].min()
+    t8 = np.array(st, dtype=np.float64).reshape(nrec, 12)[:, :8] / 100.0   # us
+    fch = lib.vlgba_debug_chstamps
+    fch.restype = ctypes.c_int
+    fch.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    sc2 = (ctypes.c_ulonglong * (2 * nrec))()
+    assert fch(sc2, nrec) == 0
+    tch = np.array(sc2, dtype=np.float64).reshape(nrec, 2) / 100.0
+    t0 = t8[:, 0].min()
+    t8 -= t0
+    tch -= t0
+    t = t8[:, :4]
     print(f"{cfg}: {nt} tiles of {rows} rows, {nrec} records; launch span "
           f"{t[:, 3].max():.1f} us")
     print("   kind     lvl  n   start  waited  computed  published | wait  compute  publish (us)")
@@ -82,6 +97,26 @@ def main():
         d = np.mean(tt[:, 1:] - tt[:, :-1], axis=0)
         print(f"  {k[0]:9s} {k[1]:3d} {len(idx):4d} {med[0]:7.1f} {med[1]:7.1f} {med[2]:9.1f} "
               f"{med[3]:9.1f} | {d[0]:5.1f} {d[1]:7.1f} {d[2]:7.1f}")
+    # inside the level body of the panel roles (1, 2: the next level's inputs)
+    print("   panel records (roles 1/2)  | wait  loads  update  factor+panel  panel  store+publish (us)"
+          "  [F0  M  F1]")
+    for lv in sorted({k[1] for k in kinds if k[0] in ("factor", "fused")}):
+        idx = [i for i, k in enumerate(kinds) if k[1] == lv and k[0] in ("factor", "fused")
+               and roles[i] in (1, 2, 4)]
+        if not idx:
+            continue
+        x = np.concatenate([t8[idx], tch[idx]], axis=1)
+        # records whose role skipped the body (no neighbour on that side) leave
+        # stale sub-stamps: only stamps inside [entry, published] count
+        for c in range(4, 10):
+            bad = (x[:, c] < x[:, 0]) | (x[:, c] > x[:, 3])
+            x[bad, c] = np.nan
+        seq = [x[:, 1] - x[:, 0], x[:, 4] - x[:, 1], x[:, 5] - x[:, 4], x[:, 6] - x[:, 5],
+               x[:, 7] - x[:, 6], x[:, 3] - x[:, 7]]
+        sub = [x[:, 8] - x[:, 5], x[:, 9] - x[:, 8], x[:, 6] - x[:, 9]]
+        print(f"   level {lv:2d} ({len(idx):3d} records)      | " +
+              "  ".join(f"{np.nanmedian(v):5.2f}" for v in seq) + "  [" +
+              "  ".join(f"{np.nanmedian(v):4.2f}" for v in sub) + "]")
     ba.close()
 
 
