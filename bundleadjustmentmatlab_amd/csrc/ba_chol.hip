@@ -1263,8 +1263,8 @@ __device__ __forceinline__ void gemv32(const double *M, const double *v, double 
 // lo and lanes 32 + i (i < 32) vector i of segment hi (in == nullptr: none).
 // The substitutions ride on the factor's broadcasts, so a panel A L^-T (rows
 // of A as the vectors) costs no separate stage.  Every lane issues the same
-// 16 unconditional LDS loads for its vector (inactive lanes read As), so the
-// loads are in flight together.  Lanes 0..15 write L (zero upper) to As.
+// 16 unconditional LDS loads for its start vector (e_r and zeros from a
+// small LDS row), so the loads are in flight together and need no selects.  Lanes 0..15 write L (zero upper) to As.
 // Returns false on a non-positive pivot.
 struct vseg {
     const double *in;   // entry c of vector i: in[i * irs + c * ics]
@@ -1275,20 +1275,24 @@ struct vseg {
 
 __device__ __forceinline__ bool wave_factor16x(double *As, double *Li, int o, vseg lo, vseg hi)
 {
+    // e_r for lanes r < 16 and zeros for idle lanes come from one LDS row
+    // (ident[16] = 1), so every lane's start vector is one strided read
+    __shared__ double ident[33];
     const int lane = threadIdx.x & 63, r = lane & 15;
+    if (lane < 33) ident[lane] = lane == 16 ? 1.0 : 0.0;
     const bool up = lane >= 32;
     const int idx = up ? lane - 32 : lane - 16;
     const double *sin = up ? hi.in : lo.in;
     const bool act = lane >= 16 && sin != nullptr && idx < (up ? hi.n : lo.n);
-    const double *pin = act ? sin + idx * (up ? hi.irs : lo.irs) : As;
-    const int ics = act ? (up ? hi.ics : lo.ics) : 0;
-    double d[16], x[16], v[16];
+    const double *pin =
+        act ? sin + idx * (up ? hi.irs : lo.irs) : (lane < 16 ? ident + 16 - r : ident);
+    const int ics = act ? (up ? hi.ics : lo.ics) : 1;
+    double d[16], x[16];
 #pragma unroll
     for (int c = 0; c < 16; c++) d[c] = As[(o + r) * LP + o + c];
+    __builtin_amdgcn_wave_barrier();   // ident written (same wave: LDS in order)
 #pragma unroll
-    for (int q = 0; q < 16; q++) v[q] = pin[q * ics];
-#pragma unroll
-    for (int q = 0; q < 16; q++) x[q] = lane < 16 ? ((q == r) ? 1.0 : 0.0) : (act ? v[q] : 0.0);
+    for (int q = 0; q < 16; q++) x[q] = pin[q * ics];
     auto rsq = [&](double piv) {
         double y = __builtin_amdgcn_rsq(piv);
         const double hp = 0.5 * piv;
