@@ -363,27 +363,110 @@ __device__ __forceinline__ bool wave_factor16(double *As, double *Bs, int o)
     return ok;
 }
 
+// One wave: wave_factor16's Cholesky of the 16x16 diagonal block at (o, o)
+// of As, and forward substitutions z = L^-1 v of up to 48 more vectors in
+// the same loop.  Every 16-lane row of the wave holds a copy of the factor
+// rows (lane l: row l & 15), so each row's DPP broadcasts see the factor's
+// column and the copies stay bit-identical; lanes 0..15 carry the identity
+// (column r of L^-1 -> Li, if Li), lanes 16 + i (i < 16) vector i of segment
+// lo and lanes 32 + i (i < 32) vector i of segment hi (in == nullptr: none).
+// The substitutions ride on the factor's broadcasts, so a panel A L^-T (rows
+// of A as the vectors) costs no separate stage.  Every lane issues the same
+// 16 unconditional LDS loads for its start vector (e_r and zeros from a
+// small LDS row), so the loads are in flight together and need no selects.  Lanes 0..15 write L (zero upper) to As.
+// Returns false on a non-positive pivot.
+struct vseg {
+    const double *in;   // entry c of vector i: in[i * irs + c * ics]
+    double *out;        // result entry c:      out[i * ors + c * ocs]
+    int irs, ics, ors, ocs;
+    int n;              // vectors (lanes 16 / 32 + i, i < n)
+};
+
+__device__ __forceinline__ bool wave_factor16x(double *As, double *Li, int o, vseg lo, vseg hi)
+{
+    // e_r for lanes r < 16 and zeros for idle lanes come from one LDS row
+    // (ident[16] = 1), so every lane's start vector is one strided read
+    __shared__ double ident[33];
+    const int lane = threadIdx.x & 63, r = lane & 15;
+    if (lane < 33) ident[lane] = lane == 16 ? 1.0 : 0.0;
+    const bool up = lane >= 32;
+    const int idx = up ? lane - 32 : lane - 16;
+    const double *sin = up ? hi.in : lo.in;
+    const bool act = lane >= 16 && sin != nullptr && idx < (up ? hi.n : lo.n);
+    const double *pin =
+        act ? sin + idx * (up ? hi.irs : lo.irs) : (lane < 16 ? ident + 16 - r : ident);
+    const int ics = act ? (up ? hi.ics : lo.ics) : 1;
+    double d[16], x[16];
+#pragma unroll
+    for (int c = 0; c < 16; c++) d[c] = As[(o + r) * LP + o + c];
+    __builtin_amdgcn_wave_barrier();   // ident written (same wave: LDS in order)
+#pragma unroll
+    for (int q = 0; q < 16; q++) x[q] = pin[q * ics];
+    auto rsq = [&](double piv) {
+        double y = __builtin_amdgcn_rsq(piv);
+        const double hp = 0.5 * piv;
+        y = y * fma(-hp * y, y, 1.5);
+        y = y * fma(-hp * y, y, 1.5);
+        return y;
+    };
+    double y = rsq(rowbcast_c<0>(d[0]));
+#pragma unroll
+    for (int c = 0; c < 16; c++) {
+        d[c] = d[c] * y;
+        x[c] = x[c] * y;
+        if (c + 1 < 16) {
+            const double b = rowbcast(d[c], c + 1);
+            d[c + 1] = fma(-d[c], b, d[c + 1]);
+            y = rsq(rowbcast(d[c + 1], c + 1));
+            x[c + 1] = fma(-b, x[c], x[c + 1]);
+        }
+#pragma unroll
+        for (int q = c + 2; q < 16; q++) {
+            const double b = rowbcast(d[c], q);
+            d[q] = fma(-d[c], b, d[q]);
+            x[q] = fma(-b, x[c], x[q]);
+        }
+#pragma unroll
+        for (int q = c; q < 16; q++) asm volatile("" : "+v"(x[q]));
+    }
+    double dg = 1.0;
+#pragma unroll
+    for (int c = 0; c < 16; c++)
+        if (r == c) dg = d[c];
+    const bool ok = __all(lane >= 16 || (dg > 0.0 && dg < __builtin_inf()));
+    if (lane < 16) {
+#pragma unroll
+        for (int c = 0; c < 16; c++) As[(o + r) * LP + o + c] = (c <= r) ? d[c] : 0.0;
+        if (Li) {
+#pragma unroll
+            for (int c = 0; c < 16; c++) Li[(o + c) * LP + o + r] = x[c];
+        }
+    } else if (act) {
+        double *po = (up ? hi.out : lo.out) + idx * (up ? hi.ors : lo.ors);
+        const int ocs = up ? hi.ocs : lo.ocs;
+#pragma unroll
+        for (int c = 0; c < 16; c++) po[c * ocs] = x[c];
+    }
+    return ok;
+}
+
 // The 256-thread workgroup factors the 64x64 SPD tile in As (row-major, lower
-// used) and inverts the factor, blocked by 16 (blocks 0..3).  Per block column
-// k one wave factors the diagonal block (wave_factor16: L_kk and its inverse),
-// the panel blocks L_ik = A_ik Dinv_kk^T follow on the matrix pipe, then the
-// trailing blocks A_ij -= L_ik L_jk^T.  Look-ahead schedule: wave 0 updates
-// the next diagonal block first and factors it at once, while the other waves
-// finish the trailing blocks and form the off-diagonal blocks of L^-1,
-//     Li_ij = -Li_ii sum_{t=j}^{i-1} L_it Li_tj,
-// as soon as their inputs exist -- the critical path is the four diagonal
-// factorisations plus three panel steps.  Every block is formed by exactly
-// the operations of the plain right-looking order, so the result is the
-// same bit for bit.  Writes L to the lower triangle of As (the upper
-// triangle is zeroed only if zero_upper: the 16x16 blocks above the diagonal
-// keep A otherwise) and L^-1 (zero upper) to Li.  Returns false on a
-// non-positive pivot.  The caller synchronises after filling As; the result
-// is visible after return.
+// used) and inverts the factor, blocked by 16: four wave_factor16x chains on
+// wave 0, each carrying on its spare lanes the rows of A below its block (->
+// the panel L_ib) and the columns of V_b = -L_b,0:b Li_0:b,0:b (-> the
+// inverse's blocks Li_b,c = L_bb^-1 V_b), so no separate panel or inverse
+// stage remains; between chains b and b+1 one MFMA stage (one task per wave:
+// the trailing blocks of column b+1 and V_b+1's blocks); the other trailing
+// blocks run on waves 1..3 beside the next chain.  Lanes per chain: 16
+// identity + 48 A rows | 16 V + 32 A rows | 16 A rows + 32 V | 48 V.  Writes L
+// to the lower triangle of As (the upper triangle is zeroed only if
+// zero_upper: the 16x16 blocks above the diagonal keep A otherwise) and L^-1
+// (zero upper) to Li.  Returns false on a non-positive pivot.  The caller
+// synchronises after filling As; the result is visible after return.
 __device__ __forceinline__ bool block_potrf_inv(double *As, double *Li, bool zero_upper = true)
 {
-    __shared__ double Xs[4][16 * LP];
-    __shared__ __attribute__((aligned(16))) int bad;   // keeps the static LDS a
-                                                       // multiple of 16 B (G17)
+    __shared__ __attribute__((aligned(16))) double Vs[16 * LP];   // V_b: 16 x 16 b
+    __shared__ __attribute__((aligned(16))) int bad;
     const int tid = threadIdx.x, w = tid >> 6;
     // one trailing block (i, j) of block column k: A_ij -= L_ik L_jk^T
     auto trail = [&](int i, int j, int k) {
@@ -391,59 +474,58 @@ __device__ __forceinline__ bool block_potrf_inv(double *As, double *Li, bool zer
         acc = mfma16_nt(As, 16 * i, 16 * k, As, 16 * j, 16 * k, acc);
         put16(As, 16 * i, 16 * j, acc, -1.0, true);
     };
-    // one panel block: L_ik = A_ik Dinv_kk^T
-    auto panel = [&](int i, int k) {
+    // block c of V_b = -sum_{t=c}^{b-1} L_bt Li_tc
+    auto vblk = [&](int b, int c) {
         d4 acc = {0.0, 0.0, 0.0, 0.0};
-        acc = mfma16_nt(As, 16 * i, 16 * k, Li, 16 * k, 16 * k, acc);
-        put16(As, 16 * i, 16 * k, acc, 1.0, false);
-    };
-    // one off-diagonal block of the inverse, Li_ij (i > j), by wave w (> 0)
-    auto inv = [&](int i, int j) {
-        d4 acc = {0.0, 0.0, 0.0, 0.0};
-        for (int t = j; t < i; t++) acc = mfma16_nn(As, 16 * i, 16 * t, Li, 16 * t, 16 * j, acc);
-        put16(Xs[w], 0, 0, acc, 1.0, false);
-        d4 acc2 = {0.0, 0.0, 0.0, 0.0};
-        acc2 = mfma16_nn(Li, 16 * i, 16 * i, Xs[w], 0, 0, acc2);
-        put16(Li, 16 * i, 16 * j, acc2, -1.0, false);
-    };
-    auto f16 = [&](int k) {
-        if (!wave_factor16(As, Li, 16 * k) && (tid & 63) == 0) bad = 1;
+        for (int t = c; t < b; t++) acc = mfma16_nn(As, 16 * b, 16 * t, Li, 16 * t, 16 * c, acc);
+        put16(Vs, 0, 16 * c, acc, -1.0, false);
     };
     // the six 16x16 blocks above the diagonal of L^-1 (everything else is
-    // written below); ordered before their readers by the step barriers
+    // written below); ordered before their readers by the stage barriers
     for (int q = tid; q < 6 * 256; q += blockDim.x) {
         const int b = q >> 8, e = q & 255;
         const int bi = b < 3 ? 0 : (b < 5 ? 1 : 2), bj = b < 3 ? b + 1 : (b < 5 ? b - 1 : 3);
         Li[(16 * bi + (e >> 4)) * LP + 16 * bj + (e & 15)] = 0.0;
     }
-    if (tid == 0) bad = 0;   // same wave as the writer below: program order
 #pragma unroll 1
-    for (int k = 0; k < 4; k++) {
-        // A(k): wave 0 updates diagonal block k by column k-1 and factors it;
-        // waves 1-3 apply column k-1 to the other trailing blocks
+    for (int b = 0; b < 4; b++) {
+        const int o = 16 * b, na = 48 - o;   // A rows below the block
         if (w == 0) {
-            if (k > 0) trail(k, k, k - 1);
-            f16(k);
-        } else if (k > 0) {
-            int p = 0;
-            for (int j = k; j < 4; j++)
-                for (int i = j; i < 4; i++) {
-                    if (i == k && j == k) continue;
-                    if (1 + p % 3 == w) trail(i, j, k - 1);
-                    p++;
-                }
+            vseg lo, hi;
+            double *ar = As + (o + 16) * LP + o;   // A rows below, block column b
+            if (b == 0) {
+                lo = vseg{ar, ar, LP, 1, LP, 1, 16};
+                hi = vseg{ar + 16 * LP, ar + 16 * LP, LP, 1, LP, 1, 32};
+            } else if (b == 1) {
+                lo = vseg{Vs, Li + o * LP, 1, LP, 1, LP, 16};
+                hi = vseg{ar, ar, LP, 1, LP, 1, 32};
+            } else if (b == 2) {
+                lo = vseg{ar, ar, LP, 1, LP, 1, 16};
+                hi = vseg{Vs, Li + o * LP, 1, LP, 1, LP, 32};
+            } else {
+                lo = vseg{Vs, Li + o * LP, 1, LP, 1, LP, 16};
+                hi = vseg{Vs + 16, Li + o * LP + 16, 1, LP, 1, LP, 32};
+            }
+            (void)na;
+            const bool ok = wave_factor16x(As, Li, o, lo, hi);
+            if (tid == 0) bad = (b > 0 ? bad : 0) | (ok ? 0 : 1);
+        } else if (b == 1) {   // column 0's trailing blocks right of column 1
+            if (w == 1) trail(2, 2, 0);
+            else if (w == 2) trail(3, 2, 0);
+            else trail(3, 3, 0);
+        } else if (b == 2) {   // column 1's
+            if (w == 1) trail(3, 3, 1);
         }
         __syncthreads();
-        // B(k): three tasks for waves 1-3 -- the panels of column k, then the
-        // inverse blocks of block row k
-        if (w >= 1) {
-            const int t = w - 1;
-            if (t < 3 - k)
-                panel(k + 1 + t, k);
+        if (b < 3) {
+            // column b+1 of the trailing blocks, and V_b+1: one task per wave
+            const int nt = 3 - b;   // blocks (b+1 .. 3, b+1)
+            if (w < nt)
+                trail(b + 1 + w, b + 1, b);
             else
-                inv(k, t - (3 - k));
+                vblk(b + 1, w - nt);
+            __syncthreads();
         }
-        __syncthreads();
     }
     if (zero_upper) {
         for (int q = tid; q < NB * NB; q += blockDim.x) {   // zero the upper triangle of L
@@ -1252,93 +1334,6 @@ __device__ __forceinline__ void gemv32(const double *M, const double *v, double 
         out[tid] = ((((((part[0][tid] + part[1][tid]) + part[2][tid]) + part[3][tid]) +
                      part[4][tid]) + part[5][tid]) + part[6][tid]) + part[7][tid];
     __syncthreads();
-}
-
-// One wave: wave_factor16's Cholesky of the 16x16 diagonal block at (o, o)
-// of As, and forward substitutions z = L^-1 v of up to 48 more vectors in
-// the same loop.  Every 16-lane row of the wave holds a copy of the factor
-// rows (lane l: row l & 15), so each row's DPP broadcasts see the factor's
-// column and the copies stay bit-identical; lanes 0..15 carry the identity
-// (column r of L^-1 -> Li, if Li), lanes 16 + i (i < 16) vector i of segment
-// lo and lanes 32 + i (i < 32) vector i of segment hi (in == nullptr: none).
-// The substitutions ride on the factor's broadcasts, so a panel A L^-T (rows
-// of A as the vectors) costs no separate stage.  Every lane issues the same
-// 16 unconditional LDS loads for its start vector (e_r and zeros from a
-// small LDS row), so the loads are in flight together and need no selects.  Lanes 0..15 write L (zero upper) to As.
-// Returns false on a non-positive pivot.
-struct vseg {
-    const double *in;   // entry c of vector i: in[i * irs + c * ics]
-    double *out;        // result entry c:      out[i * ors + c * ocs]
-    int irs, ics, ors, ocs;
-    int n;              // vectors (lanes 16 / 32 + i, i < n)
-};
-
-__device__ __forceinline__ bool wave_factor16x(double *As, double *Li, int o, vseg lo, vseg hi)
-{
-    // e_r for lanes r < 16 and zeros for idle lanes come from one LDS row
-    // (ident[16] = 1), so every lane's start vector is one strided read
-    __shared__ double ident[33];
-    const int lane = threadIdx.x & 63, r = lane & 15;
-    if (lane < 33) ident[lane] = lane == 16 ? 1.0 : 0.0;
-    const bool up = lane >= 32;
-    const int idx = up ? lane - 32 : lane - 16;
-    const double *sin = up ? hi.in : lo.in;
-    const bool act = lane >= 16 && sin != nullptr && idx < (up ? hi.n : lo.n);
-    const double *pin =
-        act ? sin + idx * (up ? hi.irs : lo.irs) : (lane < 16 ? ident + 16 - r : ident);
-    const int ics = act ? (up ? hi.ics : lo.ics) : 1;
-    double d[16], x[16];
-#pragma unroll
-    for (int c = 0; c < 16; c++) d[c] = As[(o + r) * LP + o + c];
-    __builtin_amdgcn_wave_barrier();   // ident written (same wave: LDS in order)
-#pragma unroll
-    for (int q = 0; q < 16; q++) x[q] = pin[q * ics];
-    auto rsq = [&](double piv) {
-        double y = __builtin_amdgcn_rsq(piv);
-        const double hp = 0.5 * piv;
-        y = y * fma(-hp * y, y, 1.5);
-        y = y * fma(-hp * y, y, 1.5);
-        return y;
-    };
-    double y = rsq(rowbcast_c<0>(d[0]));
-#pragma unroll
-    for (int c = 0; c < 16; c++) {
-        d[c] = d[c] * y;
-        x[c] = x[c] * y;
-        if (c + 1 < 16) {
-            const double b = rowbcast(d[c], c + 1);
-            d[c + 1] = fma(-d[c], b, d[c + 1]);
-            y = rsq(rowbcast(d[c + 1], c + 1));
-            x[c + 1] = fma(-b, x[c], x[c + 1]);
-        }
-#pragma unroll
-        for (int q = c + 2; q < 16; q++) {
-            const double b = rowbcast(d[c], q);
-            d[q] = fma(-d[c], b, d[q]);
-            x[q] = fma(-b, x[c], x[q]);
-        }
-#pragma unroll
-        for (int q = c; q < 16; q++) asm volatile("" : "+v"(x[q]));
-    }
-    double dg = 1.0;
-#pragma unroll
-    for (int c = 0; c < 16; c++)
-        if (r == c) dg = d[c];
-    const bool ok = __all(lane >= 16 || (dg > 0.0 && dg < __builtin_inf()));
-    if (lane < 16) {
-#pragma unroll
-        for (int c = 0; c < 16; c++) As[(o + r) * LP + o + c] = (c <= r) ? d[c] : 0.0;
-        if (Li) {
-#pragma unroll
-            for (int c = 0; c < 16; c++) Li[(o + c) * LP + o + r] = x[c];
-        }
-    } else if (act) {
-        double *po = (up ? hi.out : lo.out) + idx * (up ? hi.ors : lo.ors);
-        const int ocs = up ? hi.ocs : lo.ocs;
-#pragma unroll
-        for (int c = 0; c < 16; c++) po[c * ocs] = x[c];
-    }
-    return ok;
 }
 
 // The 32 x 32 Cholesky of As (lower; block (0, 1) keeps A) and, if Li, L^-1

@@ -20,6 +20,7 @@
 #include <rocsolver/rocsolver.h>   // types only: the library is dlopen'ed on first use
 
 #include <dlfcn.h>
+#include <unistd.h>
 #include <cstdlib>
 #include <string>
 
@@ -27,6 +28,8 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <functional>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -451,6 +454,76 @@ static int plan_threads(long long work, long long min_work)
     return (int)std::max(1LL, std::min<long long>(cap, work / std::max(1LL, min_work)));
 }
 
+// The host planner's worker threads: created once and kept (a context is
+// created per growing-replay solve, and spawning 15 threads per plan phase
+// cost more than some phases).  One job at a time; a caller that finds the
+// pool busy (contexts created concurrently by rank threads), or a forked
+// child (the pool's threads stayed in the parent), runs its job on threads
+// of its own instead.
+class plan_pool {
+  public:
+    static plan_pool &get()
+    {
+        static plan_pool *pp = new plan_pool();   // never destroyed: no join at exit
+        return *pp;
+    }
+    // f(t) for t in [0, nthr): t = 0 on the calling thread
+    void run(int nthr, const std::function<void(int)> &f)
+    {
+        std::unique_lock<std::mutex> busy(job_mu_, std::defer_lock);
+        if (getpid() != pid_ || nthr - 1 > kMax || !busy.try_lock()) {   // threads of our own
+            std::vector<std::thread> th;
+            for (int t = 1; t < nthr; t++) th.emplace_back(f, t);
+            f(0);
+            for (auto &x : th) x.join();
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            while ((int)th_.size() < nthr - 1) {
+                const int id = (int)th_.size() + 1;
+                th_.emplace_back([this, id] { loop(id); });
+            }
+            job_ = &f;
+            njob_ = nthr;
+            pending_ = nthr - 1;
+            gen_++;
+        }
+        cv_.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [this] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+
+  private:
+    static constexpr int kMax = 15;
+    void loop(int id)
+    {
+        unsigned long long seen = 0;
+        for (;;) {
+            const std::function<void(int)> *f = nullptr;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (id < njob_) f = job_;
+            }
+            if (!f) continue;
+            (*f)(id);
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    const pid_t pid_ = getpid();
+    std::mutex job_mu_, mu_;
+    std::condition_variable cv_, done_;
+    std::vector<std::thread> th_;
+    const std::function<void(int)> *job_ = nullptr;
+    int njob_ = 0, pending_ = 0;
+    unsigned long long gen_ = 0;
+};
+
 // f(t, lo, hi) on nthr contiguous ranges of [0, n) (thread t takes range t;
 // the calling thread takes range 0), of equal work when wpre (the prefix sums
 // of per-item work, n + 1 entries) is given, else of equal length
@@ -473,11 +546,7 @@ static void parallel_ranges(int n, int nthr, F f, const std::vector<long long> *
         }
         cut[t] = std::max(cut[t], cut[t - 1]);
     }
-    std::vector<std::thread> th;
-    th.reserve(nthr - 1);
-    for (int t = 1; t < nthr; t++) th.emplace_back(f, t, cut[t], cut[t + 1]);
-    f(0, cut[0], cut[1]);
-    for (auto &x : th) x.join();
+    plan_pool::get().run(nthr, [&](int t) { f(t, cut[t], cut[t + 1]); });
 }
 
 // MFMA chunks (points below p_split): at most BA_MF_PTS points and cmax
