@@ -57,12 +57,15 @@ def _subset_obs(sc, cams, pts, cam_on=None, pt_on=None):
     if pt_on is None:
         pt_on = np.zeros(sc.n, dtype=bool)
         pt_on[pts] = True
-    keep = cam_on[sc.obs_cam] & pt_on[sc.obs_pt]        # one-byte gathers over all obs
+    keep = np.take(cam_on, sc.obs_cam)               # one-byte gathers over all obs
+    keep &= np.take(pt_on, sc.obs_pt)
+    idx = np.flatnonzero(keep)                        # index takes: ~6x a boolean mask
     cmap = np.full(sc.m, -1)
     cmap[cams] = np.arange(len(cams))
     pmap = np.full(sc.n, -1)
     pmap[pts] = np.arange(len(pts))
-    return pmap[sc.obs_pt[keep]], cmap[sc.obs_cam[keep]], sc.obs_x[keep]
+    return (np.take(pmap, np.take(sc.obs_pt, idx)), np.take(cmap, np.take(sc.obs_cam, idx)),
+            np.take(sc.obs_x, idx, axis=0))
 
 
 def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, device=0,
@@ -147,8 +150,11 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
 
     # visible counts over the status cameras, kept up to date as cameras join
     # (a bincount over every observation per solve otherwise)
-    cam_obs_pts = np.split(sc.obs_pt[np.argsort(sc.obs_cam, kind="stable")],
+    # (camera-major observation ids, ascending within a camera: the resection's
+    # selection in observation order without a pass over every observation)
+    cam_obs_ids = np.split(np.argsort(sc.obs_cam, kind="stable"),
                            np.cumsum(np.bincount(sc.obs_cam, minlength=m))[:-1])
+    cam_obs_pts = [sc.obs_pt[ids] for ids in cam_obs_ids]
     nvis_cur = nvis.copy()
 
     def next_set(tag, j):
@@ -229,8 +235,9 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
     def resect(j):
         """estimate_camera.m:247-253: the new camera refined against the points
         reconstructed so far that it sees (structure fixed), on the GPU."""
-        sel = (sc.obs_cam == j) & (X[3, sc.obs_pt] == 1)
-        if sel.sum() < 6:
+        oj = cam_obs_ids[j]
+        sel = oj[X[3, cam_obs_pts[j]] == 1]              # camera j's obs of reconstructed points
+        if len(sel) < 6:
             return
         ids = sc.obs_pt[sel]
         t0 = time.perf_counter()
@@ -238,7 +245,7 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
                                                 [X[:, ids]], [sc.obs_x[sel].T], *opts,
                                                 device=device)
         K[:, j], T[:, j], w[:, j] = K_[:, 0], T_[:, 0], w_[:, 0]
-        resections.append(dict(camera=int(j), observations=int(sel.sum()),
+        resections.append(dict(camera=int(j), observations=int(len(sel)),
                                error=errs[0], seconds=time.perf_counter() - t0))
 
     try:
@@ -281,8 +288,10 @@ def _triangulate(sc, K, T, w, pts, status):
         return out
     on = np.zeros(sc.n, dtype=bool)
     on[pts] = True
-    sel = on[sc.obs_pt] & status[sc.obs_cam]             # point-major: rows per point
-    opt, ocam, ox = sc.obs_pt[sel], sc.obs_cam[sel], sc.obs_x[sel]
+    sel = np.take(on, sc.obs_pt)                         # point-major: rows per point
+    sel &= np.take(status, sc.obs_cam)
+    sel = np.flatnonzero(sel)
+    opt, ocam, ox = sc.obs_pt[sel], sc.obs_cam[sel], np.take(sc.obs_x, sel, axis=0)
     R = vl_rodr(w[:, ocam])                              # (k, 3, 3)
     Kc = np.zeros((len(ocam), 3, 3))
     Kc[:, 0, 0], Kc[:, 1, 1] = K[0, ocam], K[1, ocam]
