@@ -25,12 +25,13 @@ The structure of a solve (which cameras, points and observations it
 adjusts) is known before the previous solve ends -- exactly for a
 before-triangulation solve (nothing but the new camera changes it), and up to
 the points whose triangulation fails the depth test for an after-triangulation
-one (predicted: every candidate succeeds; a wrong prediction is detected and
-that solve's context rebuilt) -- so a worker thread cuts solve k+1's
-observation subset and builds its libvlgba context (the host plan of
-vlgba_create, which runs with the GIL released) while solve k runs on the GPU
-("reuse across growing calls").  Only the parameter
-upload and the LM loop stay on the replay's critical path.
+one (predicted by triangulating on the cameras as they are; a wrong prediction
+is detected and that solve's context rebuilt) -- so two worker threads cut
+the next two solves' observation subsets and build their libvlgba contexts
+(the host plan of vlgba_create, which runs with the GIL released) while the
+current solve runs on the GPU ("reuse across
+growing calls").  Only the parameter upload and the LM loop stay on the
+replay's critical path.
 """
 from __future__ import annotations
 
@@ -122,13 +123,17 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
                                              if obs_per_shard else {})))
 
     def build(item):
-        """worker: the solve's subset and (one rank) its context; an
-        after-triangulation set comes with the candidates and a snapshot of the
-        cameras, triangulated here to predict which pass the depth test"""
-        if len(item) == 5:
-            tag, j, cam_on, x3, (Ts, ws, cand) = item
+        """worker: the solve's subset and (one rank) its context.  An item
+        predicted across a triangulation comes with the candidates and a
+        snapshot of the cameras, triangulated here (on the cameras before the
+        added one) to predict which points pass the depth test"""
+        if len(item) == 6:
+            tag, j, cam_on, x3, (Ts, ws, cand), add = item
             pt_on = x3.copy()
             pt_on[cand] = _triangulate(sc, K, Ts, ws, cand, cam_on)[3] == 1.0
+            if add is not None:
+                cam_on = cam_on.copy()
+                cam_on[add] = True
             item = (tag, j, cam_on, pt_on)
         tag, j, cam_on, pt_on = item
         cams, pts = np.nonzero(cam_on)[0], np.nonzero(pt_on)[0]
@@ -144,8 +149,13 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
         return item, sub, ba_, time.perf_counter() - t0
 
     use_pf = prefetch and fix_calibration      # K (the context's) is constant then
-    pool = ThreadPoolExecutor(max_workers=1) if use_pf else None
-    pending = []
+    # two workers: at a before-triangulation solve of camera j both following
+    # solves are predicted -- camera j's after-triangulation solve and camera
+    # j+1's before-triangulation solve (the same points, one camera more) --
+    # and their contexts built side by side, so each has two LM loops to hide
+    # behind instead of one
+    pool = ThreadPoolExecutor(max_workers=2) if use_pf else None
+    pending = {}
     stats = {"prefetched": 0, "mispredicted": 0}
 
     # visible counts over the status cameras, kept up to date as cameras join
@@ -157,23 +167,29 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
     cam_obs_pts = [sc.obs_pt[ids] for ids in cam_obs_ids]
     nvis_cur = nvis.copy()
 
-    def next_set(tag, j):
-        """the solve after (tag, j), from the current state: after a
-        before-triangulation solve the same cameras and the points that pass
-        the triangulation's depth test on the cameras as they are now (the
-        worker triangulates; the solve in between moves them a little, so a
-        marginal point may still come out the other way); after an
-        after-triangulation solve the next camera joins, points unchanged"""
-        if tag == "before-triangulation":
-            cand = np.nonzero((X[3] == 0) & (nvis_cur >= 2))[0]
-            return ("after-triangulation", j, status.copy(), X[3] == 1,
-                    (T.copy(), w.copy(), cand))
+    def next_sets(tag, j):
+        """the solves predicted at (tag, j), from the current state: at a
+        before-triangulation solve, the after-triangulation solve (the same
+        cameras and the points that pass the triangulation's depth test on the
+        cameras as they are now -- the worker triangulates; the solve in
+        between moves them a little, so a marginal point may still come out
+        the other way) and the next camera's before-triangulation solve (those
+        points, the camera added); nothing at an after-triangulation solve
+        (its successor was predicted with it).  The first solve of a replay
+        that starts after a triangulation predicts the next camera's."""
+        cand = np.nonzero((X[3] == 0) & (nvis_cur >= 2))[0]
         jn = next((q for q in range(j + 1, m) if not status[q]), None)
-        if jn is None:
-            return None
-        st = status.copy()
-        st[jn] = True
-        return "before-triangulation", jn, st, X[3] == 1
+        snap = (T.copy(), w.copy(), cand)
+        out = []
+        if tag == "before-triangulation":
+            out.append(("after-triangulation", j, status.copy(), X[3] == 1, snap, None))
+            if jn is not None:
+                out.append(("before-triangulation", jn, status.copy(), X[3] == 1, snap, jn))
+        elif jn is not None and ("before-triangulation", jn) not in pending:
+            st = status.copy()
+            st[jn] = True
+            out.append(("before-triangulation", jn, st, X[3] == 1))
+        return out
 
     def ba(tag, j):
         cams = np.nonzero(status)[0]
@@ -181,19 +197,18 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
         t0 = time.perf_counter()
         pre = create_s = sub = None
         if use_pf:
-            if pending:
-                item, sub, pre, create_s = pending.pop().result()
-                if item[0] != tag or item[1] != j or not (np.array_equal(item[2], status) and
-                                                          np.array_equal(item[3], X[3] == 1)):
+            fut = pending.pop((tag, j), None)
+            if fut is not None:
+                item, sub, pre, create_s = fut.result()
+                if not (np.array_equal(item[2], status) and np.array_equal(item[3], X[3] == 1)):
                     if pre is not None:                  # a triangulation failed the depth
                         pre.close()                      # test: this context is not the solve's
                     pre = create_s = sub = None
                     stats["mispredicted"] += 1
                 else:
                     stats["prefetched"] += 1
-            nxt = next_set(tag, j)                       # the next solve's context, built
-            if nxt is not None:                          # while this one runs
-                pending.append(pool.submit(build, nxt))
+            for nxt in next_sets(tag, j):                # the next solves' contexts, built
+                pending[(nxt[0], nxt[1])] = pool.submit(build, nxt)   # while this one runs
         if len(pts) == 0 or len(cams) < 2:
             if pre is not None:
                 pre.close()
@@ -264,7 +279,7 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
             X[:, cand] = _triangulate(sc, K, T, w, cand, status)
             ba("after-triangulation", j)                 # :300-318
     finally:
-        for f in pending:                                # a prefetched context not used
+        for f in pending.values():                       # a prefetched context not used
             try:
                 pre = f.result()[2]
             except Exception:                            # noqa: BLE001 -- already failing
