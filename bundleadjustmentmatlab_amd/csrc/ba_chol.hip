@@ -450,6 +450,14 @@ __device__ __forceinline__ bool wave_factor16x(double *As, double *Li, int o, vs
     return ok;
 }
 
+// Two builds of the 64x64 diagonal factor: BA_ENV_FACTOR_X = 1 runs the
+// panels and the inverse's blocks on the pivot chains' spare lanes
+// (wave_factor16x); 0 (the default until measured on the box) the
+// look-ahead schedule of rounds 2-3.
+#ifndef BA_ENV_FACTOR_X
+#define BA_ENV_FACTOR_X 0
+#endif
+#if BA_ENV_FACTOR_X
 // The 256-thread workgroup factors the 64x64 SPD tile in As (row-major, lower
 // used) and inverts the factor, blocked by 16: four wave_factor16x chains on
 // wave 0, each carrying on its spare lanes the rows of A below its block (->
@@ -536,6 +544,101 @@ __device__ __forceinline__ bool block_potrf_inv(double *As, double *Li, bool zer
     }
     return bad == 0;
 }
+
+#else
+// The 256-thread workgroup factors the 64x64 SPD tile in As (row-major, lower
+// used) and inverts the factor, blocked by 16 (blocks 0..3).  Per block column
+// k one wave factors the diagonal block (wave_factor16: L_kk and its inverse),
+// the panel blocks L_ik = A_ik Dinv_kk^T follow on the matrix pipe, then the
+// trailing blocks A_ij -= L_ik L_jk^T.  Look-ahead schedule: wave 0 updates
+// the next diagonal block first and factors it at once, while the other waves
+// finish the trailing blocks and form the off-diagonal blocks of L^-1,
+//     Li_ij = -Li_ii sum_{t=j}^{i-1} L_it Li_tj,
+// as soon as their inputs exist -- the critical path is the four diagonal
+// factorisations plus three panel steps.  Every block is formed by exactly
+// the operations of the plain right-looking order, so the result is the
+// same bit for bit.  Writes L to the lower triangle of As (the upper
+// triangle is zeroed only if zero_upper: the 16x16 blocks above the diagonal
+// keep A otherwise) and L^-1 (zero upper) to Li.  Returns false on a
+// non-positive pivot.  The caller synchronises after filling As; the result
+// is visible after return.
+__device__ __forceinline__ bool block_potrf_inv(double *As, double *Li, bool zero_upper = true)
+{
+    __shared__ double Xs[4][16 * LP];
+    __shared__ __attribute__((aligned(16))) int bad;   // keeps the static LDS a
+                                                       // multiple of 16 B (G17)
+    const int tid = threadIdx.x, w = tid >> 6;
+    // one trailing block (i, j) of block column k: A_ij -= L_ik L_jk^T
+    auto trail = [&](int i, int j, int k) {
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        acc = mfma16_nt(As, 16 * i, 16 * k, As, 16 * j, 16 * k, acc);
+        put16(As, 16 * i, 16 * j, acc, -1.0, true);
+    };
+    // one panel block: L_ik = A_ik Dinv_kk^T
+    auto panel = [&](int i, int k) {
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        acc = mfma16_nt(As, 16 * i, 16 * k, Li, 16 * k, 16 * k, acc);
+        put16(As, 16 * i, 16 * k, acc, 1.0, false);
+    };
+    // one off-diagonal block of the inverse, Li_ij (i > j), by wave w (> 0)
+    auto inv = [&](int i, int j) {
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        for (int t = j; t < i; t++) acc = mfma16_nn(As, 16 * i, 16 * t, Li, 16 * t, 16 * j, acc);
+        put16(Xs[w], 0, 0, acc, 1.0, false);
+        d4 acc2 = {0.0, 0.0, 0.0, 0.0};
+        acc2 = mfma16_nn(Li, 16 * i, 16 * i, Xs[w], 0, 0, acc2);
+        put16(Li, 16 * i, 16 * j, acc2, -1.0, false);
+    };
+    auto f16 = [&](int k) {
+        if (!wave_factor16(As, Li, 16 * k) && (tid & 63) == 0) bad = 1;
+    };
+    // the six 16x16 blocks above the diagonal of L^-1 (everything else is
+    // written below); ordered before their readers by the step barriers
+    for (int q = tid; q < 6 * 256; q += blockDim.x) {
+        const int b = q >> 8, e = q & 255;
+        const int bi = b < 3 ? 0 : (b < 5 ? 1 : 2), bj = b < 3 ? b + 1 : (b < 5 ? b - 1 : 3);
+        Li[(16 * bi + (e >> 4)) * LP + 16 * bj + (e & 15)] = 0.0;
+    }
+    if (tid == 0) bad = 0;   // same wave as the writer below: program order
+#pragma unroll 1
+    for (int k = 0; k < 4; k++) {
+        // A(k): wave 0 updates diagonal block k by column k-1 and factors it;
+        // waves 1-3 apply column k-1 to the other trailing blocks
+        if (w == 0) {
+            if (k > 0) trail(k, k, k - 1);
+            f16(k);
+        } else if (k > 0) {
+            int p = 0;
+            for (int j = k; j < 4; j++)
+                for (int i = j; i < 4; i++) {
+                    if (i == k && j == k) continue;
+                    if (1 + p % 3 == w) trail(i, j, k - 1);
+                    p++;
+                }
+        }
+        __syncthreads();
+        // B(k): three tasks for waves 1-3 -- the panels of column k, then the
+        // inverse blocks of block row k
+        if (w >= 1) {
+            const int t = w - 1;
+            if (t < 3 - k)
+                panel(k + 1 + t, k);
+            else
+                inv(k, t - (3 - k));
+        }
+        __syncthreads();
+    }
+    if (zero_upper) {
+        for (int q = tid; q < NB * NB; q += blockDim.x) {   // zero the upper triangle of L
+            const int r = q >> 6, c = q & 63;
+            if (c > r) As[r * LP + c] = 0.0;
+        }
+        __syncthreads();
+    }
+    return bad == 0;
+}
+
+#endif
 
 // ---------------------------------------------------------------------------
 // One tile column k of the envelope Cholesky, with the trailing update of

@@ -17,11 +17,22 @@ from bundleadjustmentmatlab_amd.scene import make_config  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "ladybug"
 solver = sys.argv[2] if len(sys.argv) > 2 else "auto"
-sc = make_config(cfg)
-a = np.vstack([sc.w0, sc.T0])
-b = np.asfortranarray(sc.X0[:3])
+if cfg.startswith("cfg5x:"):   # the first M cameras of cfg5x (tools/prof_cfg5x_solve.py)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from prof_cfg5x_solve import sub_problem
+    M = int(cfg.split(":")[1])
+    full = make_config("cfg5x")
+    used, pt, cam, x = sub_problem(full, M)
+    K, n = full.K[:, :M], len(used)
+    a = np.vstack([full.w0[:, :M], full.T0[:, :M]])
+    b = np.asfortranarray(full.X0[:3, used])
+else:
+    sc = make_config(cfg)
+    K, n, pt, cam, x = sc.K, sc.n, sc.obs_pt, sc.obs_cam, sc.obs_x
+    a = np.vstack([sc.w0, sc.T0])
+    b = np.asfortranarray(sc.X0[:3])
 L = ctypes.CDLL(os.environ["VLGBA_LIB"])
-with gpu.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, 6, solver=solver) as ba:
+with gpu.BundleAdjuster(K, pt, cam, x, n, 6, solver=solver) as ba:
     ba.set_params(a, b)
     for _ in range(3):
         ba.step(relinearize=True, update_lm=False)
