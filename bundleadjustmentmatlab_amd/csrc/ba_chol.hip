@@ -1579,6 +1579,81 @@ extern "C" int vlgba_debug_crstamps(unsigned long long *out, int nrec)
 #define CR_SUB(k)
 #endif
 
+// Panel tiles of the one-launch CR.  In a BA_CR_GRAN build k_cr32_fused
+// hands the panels over as epoch-tagged granules {epoch, 32-bit half} (two
+// 8-byte write-through agent-scope stores per value, the pattern of the back
+// substitution's x granules): a consumer polls the tile's own granules until
+// every tag matches, so the producer needs no vmcnt(0) + barrier + flag
+// before the data is usable and the consumer no flag round trip before its
+// loads.  gr.g == nullptr (per-level kernels, default builds): plain crL.
+#ifndef BA_CR_GRAN
+#define BA_CR_GRAN 0
+#endif
+struct cr32_gran {
+    unsigned long long *g;
+    unsigned epoch;
+    double *status;
+};
+
+template <bool SC>
+__device__ __forceinline__ void store_panel(double *crL, const cr32_gran &gr, long long idx,
+                                            const double *T)
+{
+    const long long T2 = (long long)T32 * T32;
+    if (SC && gr.g) {
+        const int c = threadIdx.x & 31, r0 = threadIdx.x >> 5;
+        unsigned long long *g = gr.g + 2 * T2 * idx;
+        const unsigned long long tag = (unsigned long long)gr.epoch << 32;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int r = r0 + 8 * u;
+            const unsigned long long v = __builtin_bit_cast(unsigned long long, T[r * LP + c]);
+            __hip_atomic_store(g + 2 * (r * T32 + c), tag | (v & 0xffffffffULL), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(g + 2 * (r * T32 + c) + 1, tag | (v >> 32), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+    } else {
+        store_rm32<SC>(crL + T2 * idx, T);
+    }
+}
+
+template <bool SC>
+__device__ __forceinline__ void load_panel(const double *crL, const cr32_gran &gr, long long idx,
+                                           double *T)
+{
+    const long long T2 = (long long)T32 * T32;
+    if (SC && gr.g) {
+        const int c = threadIdx.x & 31, r0 = threadIdx.x >> 5;
+        const unsigned long long *g = gr.g + 2 * T2 * idx;
+        unsigned long long v[8];
+        for (unsigned spins = 0;; spins++) {
+            bool ok = true;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int q = 2 * ((r0 + 8 * u) * T32 + c);
+                v[2 * u] = __hip_atomic_load(g + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                v[2 * u + 1] =
+                    __hip_atomic_load(g + q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = ok && (unsigned)(v[2 * u] >> 32) == gr.epoch &&
+                     (unsigned)(v[2 * u + 1] >> 32) == gr.epoch;
+            }
+            if (__all(ok)) break;
+            if (spins >= BA_BACK_SPIN_MAX) {
+                if ((threadIdx.x & 63) == 0) gr.status[1] = 1.0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            T[(r0 + 8 * u) * LP + c] = __builtin_bit_cast(
+                double, (v[2 * u] & 0xffffffffULL) | (v[2 * u + 1] << 32));
+    } else {
+        load_rm32<SC>(crL + T2 * idx, T);
+    }
+}
+
 // factor step (level 0, on the assembled S): role 0 factors D_e, writes L_e^-1
 // (row-major 32 x 32) and y_e = L_e^-1 r_e; role 1 / 2 (split, one workgroup
 // each, redoing the same factorisation) form Lp_e = C(p, e) L_e^-T / Lq_e =
@@ -1591,7 +1666,8 @@ template <bool SC>
 __device__ __forceinline__ void cr32_factor_body(const cr32_lds &sh, double *S, long long lds,
                                                  int TB, long long ld, int e, int p, int q,
                                                  int role, int nt, double *linv, double *crL,
-                                                 const double *rhs, double *y, double *status)
+                                                 const double *rhs, double *y, double *status,
+                                                 cr32_gran gr = {nullptr, 0, nullptr})
 {
     double *As = sh.As, *Bs = sh.Bs, *Cs = sh.Cs, *Xs = sh.Xs, *rk = sh.rk, *yk = sh.ym;
     const int tid = threadIdx.x;
@@ -1616,7 +1692,7 @@ __device__ __forceinline__ void cr32_factor_body(const cr32_lds &sh, double *S, 
     CR_SUB(6);
     if (pan) {
         CR_SUB(7);
-        store_rm32<SC>(crL + T2 * (side == 1 ? e : nt + e), Cs);
+        store_panel<SC>(crL, gr, side == 1 ? e : nt + e, Cs);
     }
     if (rows) {
         if (!ylanes) gemv32(Bs, rk, sh.part, yk, false);
@@ -1630,7 +1706,7 @@ __device__ __forceinline__ void cr32_factor_body(const cr32_lds &sh, double *S, 
         load32<SC>(S, lds, TB, ld, q, e, Cs, false, false);
         __syncthreads();
         cr32_chol(As, nullptr, Cs, Xs, nullptr, nullptr, [](int) {});
-        store_rm32<SC>(crL + T2 * (nt + e), Cs);
+        store_panel<SC>(crL, gr, nt + e, Cs);
     }
 }
 
@@ -1695,7 +1771,8 @@ __device__ __forceinline__ void cr32_level_body(const cr32_lds &sh, double *S, l
                                                 int TB, long long ld, int k, int p, int q, int em,
                                                 int ep, int role, int nt, double *linv,
                                                 double *crL, double *rhs, double *y,
-                                                double *status, Mid mid)
+                                                double *status, Mid mid,
+                                                cr32_gran gr = {nullptr, 0, nullptr})
 {
     double *As = sh.As, *Bs = sh.Bs, *Cs = sh.Cs, *Ds = sh.Ds, *Es = sh.Es, *Xs = sh.Xs;
     double *rk = sh.rk, *ym = sh.ym, *yp = sh.yp, *um = sh.um, *up = sh.up;
@@ -1711,10 +1788,10 @@ __device__ __forceinline__ void cr32_level_body(const cr32_lds &sh, double *S, l
         }
     };
     load32<SC>(S, lds, TB, ld, k, k, As, false, true);
-    load_rm32<SC>(crL + T2 * (nt + em), Bs);            // L(k, em)
-    if (ep >= 0) load_rm32<SC>(crL + T2 * ep, Cs);      // L(k, ep)
-    if (role == 1) load_rm32<SC>(crL + T2 * em, Ds);    // L(p, em)
-    if (role == 2) load_rm32<SC>(crL + T2 * (nt + ep), Ds);   // L(q, ep)
+    load_panel<SC>(crL, gr, nt + em, Bs);               // L(k, em)
+    if (ep >= 0) load_panel<SC>(crL, gr, ep, Cs);       // L(k, ep)
+    if (role == 1) load_panel<SC>(crL, gr, em, Ds);     // L(p, em)
+    if (role == 2) load_panel<SC>(crL, gr, nt + ep, Ds);   // L(q, ep)
     if (role == 0) load_r();
     __syncthreads();
     CR_SUB(4);
@@ -1781,7 +1858,7 @@ __device__ __forceinline__ void cr32_level_body(const cr32_lds &sh, double *S, l
         return;
     }
     CR_SUB(7);
-    store_rm32<SC>(crL + T2 * (role == 1 ? k : nt + k), Es);
+    store_panel<SC>(crL, gr, role == 1 ? k : nt + k, Es);
 }
 
 __global__ __launch_bounds__(256) void k_cr32_level(double *__restrict__ S, long long lds, int TB,
@@ -1919,14 +1996,15 @@ __device__ __forceinline__ void cr32_back_body(const cr32_lds &sh, int e, int p,
                                                int TB, long long ld, const double *linv,
                                                const double *crL, const double *y, double *x,
                                                unsigned long long *xg, unsigned epoch,
-                                               double *status)
+                                               double *status,
+                                               cr32_gran gr = {nullptr, 0, nullptr})
 {
     double *Lp = sh.As, *Lq = sh.Bs, *Li = sh.Cs;
     double *t = sh.rk, *xp = sh.ym, *xq = sh.yp, *u = sh.um, *z = sh.up;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const long long T2 = (long long)T32 * T32;
-    if (p >= 0) load_rm32<SC>(crL + T2 * e, Lp);
-    if (q >= 0) load_rm32<SC>(crL + T2 * (nt + e), Lq);
+    if (p >= 0) load_panel<SC>(crL, gr, e, Lp);
+    if (q >= 0) load_panel<SC>(crL, gr, nt + e, Lq);
     load_rm32<SC>(linv + T2 * e, Li);
     if (tid < T32) t[tid] = tid < TB ? ldg<SC>(y + (long long)TB * e + tid) : 0.0;
     __syncthreads();
@@ -2070,11 +2148,13 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
                                                     const int *__restrict__ srec, int nt,
                                                     double *linv, double *crL, double *rhs,
                                                     double *y, double *x, unsigned *flag,
-                                                    unsigned long long *xg, unsigned epoch,
+                                                    unsigned long long *xg,
+                                                    unsigned long long *crg, unsigned epoch,
                                                     double *status, cr32_fplan P)
 {
     CR32_LDS_DECL;
     CR_ST(0);
+    const cr32_gran gr{crg, epoch, status};   // crg: panels as granules (BA_CR_GRAN)
     const int b = blockIdx.x;
     int L = 0;
     while (L < P.nl && b >= P.b0[L + 1]) L++;
@@ -2089,7 +2169,7 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
         CR_ST(1);
         if (!((role == 1 && p < 0) || (role == 2 && q < 0)))
             cr32_factor_body<true>(sh, S, lds, TB, ld, e, p, q, role, nt, linv, crL, rhs, y,
-                                   status);
+                                   status, gr);
         CR_ST(2);
         if (role == 4)
             cr32_publish(flag + fw(0, e, 0), epoch, 2);
@@ -2117,7 +2197,14 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
             ep = fr[4];
         }
         int w[8] = {0, 0, 0, 0, 0, 0, 0, 0}, nw = 0;
-        if (role == 1 || role == 2) {   // panels only: L(k, em), L(k, ep) and the fill's
+        if (crg) {   // panels polled as granules: flags only for D_k, r_k and y
+            if (role == 0) {
+                w[nw++] = fw(L - 1, em, 0);
+                if (ep >= 0) w[nw++] = fw(L - 1, ep, 0);
+                if (L >= 2) w[nw++] = fw(L - 1, k, 4);
+            }
+            if (L >= 2) w[nw++] = fw(L - 1, k, 3);
+        } else if (role == 1 || role == 2) {   // panels only: L(k, em), L(k, ep) and the fill's
             w[nw++] = fw(L - 1, em, 2);  // L(p, em) | L(q, ep) -- not role 0's y / L^-1
             if (role == 1) w[nw++] = fw(L - 1, em, 1);
             if (ep >= 0) {
@@ -2150,7 +2237,7 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
         };
         if (!((role == 1 && p < 0) || (role == 2 && q < 0)))
             cr32_level_body<true>(sh, S, lds, TB, ld, k, p, q, em, ep, role, nt, linv, crL, rhs,
-                                  y, status, mid);
+                                  y, status, mid, gr);
         CR_ST(2);
         cr32_publish(flag + fw(L, k, role == 3 ? 4 : role), epoch);
         CR_ST(3);
@@ -2162,9 +2249,9 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
     while (Le + 1 < P.nl && rec >= P.eofs[Le + 1]) Le++;
     const int e = elim[3 * rec], p = elim[3 * rec + 1], q = elim[3 * rec + 2];
     const int w[8] = {fw(Le, e, 0), fw(Le, e, 1), fw(Le, e, 2), 0, 0, 0, 0, 0};
-    cr32_wait_flags(flag, 3, w, epoch, status);
+    cr32_wait_flags(flag, crg ? 1 : 3, w, epoch, status);   // granules: L^-1 and y only
     CR_ST(1);
-    cr32_back_body<true>(sh, e, p, q, nt, TB, ld, linv, crL, y, x, xg, epoch, status);
+    cr32_back_body<true>(sh, e, p, q, nt, TB, ld, linv, crL, y, x, xg, epoch, status, gr);
     CR_ST(2);
     CR_ST(3);
 }
@@ -2655,6 +2742,12 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
                 const size_t nfl = (size_t)5 * nl * nt;
                 TRY_RC(dev_alloc(&d->crflag, sizeof(unsigned) * nfl));
                 VLGBA_CHECK(hipMemsetAsync(d->crflag, 0, sizeof(unsigned) * nfl, d->stream));
+                if (BA_CR_GRAN) {   // [2][nt][32 * 32] values, two granules each
+                    const size_t ng = (size_t)2 * nt * T32 * T32 * 2;
+                    TRY_RC(dev_alloc(&d->crgran, sizeof(unsigned long long) * ng));
+                    VLGBA_CHECK(hipMemsetAsync(d->crgran, 0, sizeof(unsigned long long) * ng,
+                                               d->stream));
+                }
             }
             TRY_RC(dev_alloc(&d->crf, sizeof(int) * (frec.size() + 1)));
             TRY_RC(dev_alloc(&d->crs, sizeof(int) * (srec.size() + 1)));
@@ -2941,6 +3034,8 @@ void ba_chol_free(ba_dev *d)
     d->xgran = nullptr;
     if (d->crflag) ba_dfree(d->crflag);
     d->crflag = nullptr;
+    if (d->crgran) ba_dfree(d->crgran);
+    d->crgran = nullptr;
     d->cr_fused = 0;
     if (d->crf) ba_dfree(d->crf);
     if (d->crs) ba_dfree(d->crs);
@@ -3067,7 +3162,8 @@ int ba_chol_solve(ba_dev *d, int nospin)
         KT_B(d);
         k_cr32_fused<<<P.b0[nl] + nrec, 256, 0, d->stream>>>(
             d->S, d->lds, d->tb32, d->ld, d->cr_elim, d->crf, d->crs, d->nt32, d->linv, d->crL,
-            d->rhs, d->ywork, d->da, d->crflag, d->xgran, d->back_epoch, d->scal + 4, P);
+            d->rhs, d->ywork, d->da, d->crflag, d->xgran, d->crgran, d->back_epoch, d->scal + 4,
+            P);
         KT_E(d, KT_CR_FACTOR);
         return -(int)hipGetLastError();
     }

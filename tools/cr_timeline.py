@@ -18,7 +18,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import bundleadjustmentmatlab_amd._lib as L  # noqa: E402
 
-L.LIB_PATH = os.path.join(ROOT, "bundleadjustmentmatlab_amd", "libvlgba_stamps.so")
+L.LIB_PATH = os.environ.get("VLGBA_LIB") or os.path.join(ROOT, "bundleadjustmentmatlab_amd",
+                                                       "libvlgba_stamps.so")
 from bundleadjustmentmatlab_amd import BundleAdjuster  # noqa: E402
 from bundleadjustmentmatlab_amd.scene import make_config  # noqa: E402
 

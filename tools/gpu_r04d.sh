@@ -34,6 +34,18 @@ timeout -k 10 300 python -u bench.py --config ladybug > gpurun_out/bench_ladybug
   2> gpurun_out/bench_ladybug.log &&
 VLGBA_LIB=$X timeout -k 10 300 python -u bench.py --config ladybug > gpurun_out/bench_ladybug_x.json \
   2> gpurun_out/bench_ladybug_x.log || exit 1
+echo "== cr granules $(date +%T)"
+G=tools/build/ab/gran/libvlgba.so
+VLGBA_LIB=$G timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+  tests/test_gpu_parity.py -k "cr or cyclic" tests/test_gpu_solve_status.py \
+  > gpurun_out/grantests.log 2>&1 || { tail -30 gpurun_out/grantests.log; exit 1; }
+tail -2 gpurun_out/grantests.log
+VLGBA_LIB=tools/build/ab/granst/libvlgba.so timeout -k 10 200 python -u tools/cr_timeline.py cfg3 \
+  > gpurun_out/cr_timeline_gran.txt 2>&1 &&
+timeout -k 10 200 python -u tools/cr_timeline.py cfg3 > gpurun_out/cr_timeline_base.txt 2>&1 &&
+timeout -k 10 300 python -u bench.py > gpurun_out/bench_cfg3.json 2> gpurun_out/bench_cfg3.log &&
+VLGBA_LIB=$G timeout -k 10 300 python -u bench.py > gpurun_out/bench_cfg3_gran.json \
+  2> gpurun_out/bench_cfg3_gran.log || exit 1
 echo "== setup $(date +%T)"
 timeout -k 10 300 python -u tools/prof_cfg5x_setup.py 300 600 900 1000 > gpurun_out/setup_trace.log 2>&1 || exit 1
 echo "== cfg5x $(date +%T)"
