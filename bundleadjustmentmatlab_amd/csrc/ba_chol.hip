@@ -363,189 +363,6 @@ __device__ __forceinline__ bool wave_factor16(double *As, double *Bs, int o)
     return ok;
 }
 
-// One wave: wave_factor16's Cholesky of the 16x16 diagonal block at (o, o)
-// of As, and forward substitutions z = L^-1 v of up to 48 more vectors in
-// the same loop.  Every 16-lane row of the wave holds a copy of the factor
-// rows (lane l: row l & 15), so each row's DPP broadcasts see the factor's
-// column and the copies stay bit-identical; lanes 0..15 carry the identity
-// (column r of L^-1 -> Li, if Li), lanes 16 + i (i < 16) vector i of segment
-// lo and lanes 32 + i (i < 32) vector i of segment hi (in == nullptr: none).
-// The substitutions ride on the factor's broadcasts, so a panel A L^-T (rows
-// of A as the vectors) costs no separate stage.  Every lane issues the same
-// 16 unconditional LDS loads for its start vector (e_r and zeros from a
-// small LDS row), so the loads are in flight together and need no selects.  Lanes 0..15 write L (zero upper) to As.
-// Returns false on a non-positive pivot.
-struct vseg {
-    const double *in;   // entry c of vector i: in[i * irs + c * ics]
-    double *out;        // result entry c:      out[i * ors + c * ocs]
-    int irs, ics, ors, ocs;
-    int n;              // vectors (lanes 16 / 32 + i, i < n)
-};
-
-__device__ __forceinline__ bool wave_factor16x(double *As, double *Li, int o, vseg lo, vseg hi)
-{
-    // e_r for lanes r < 16 and zeros for idle lanes come from one LDS row
-    // (ident[16] = 1), so every lane's start vector is one strided read
-    __shared__ double ident[33];
-    const int lane = threadIdx.x & 63, r = lane & 15;
-    if (lane < 33) ident[lane] = lane == 16 ? 1.0 : 0.0;
-    const bool up = lane >= 32;
-    const int idx = up ? lane - 32 : lane - 16;
-    const double *sin = up ? hi.in : lo.in;
-    const bool act = lane >= 16 && sin != nullptr && idx < (up ? hi.n : lo.n);
-    const double *pin =
-        act ? sin + idx * (up ? hi.irs : lo.irs) : (lane < 16 ? ident + 16 - r : ident);
-    const int ics = act ? (up ? hi.ics : lo.ics) : 1;
-    double d[16], x[16];
-#pragma unroll
-    for (int c = 0; c < 16; c++) d[c] = As[(o + r) * LP + o + c];
-    __builtin_amdgcn_wave_barrier();   // ident written (same wave: LDS in order)
-#pragma unroll
-    for (int q = 0; q < 16; q++) x[q] = pin[q * ics];
-    auto rsq = [&](double piv) {
-        double y = __builtin_amdgcn_rsq(piv);
-        const double hp = 0.5 * piv;
-        y = y * fma(-hp * y, y, 1.5);
-        y = y * fma(-hp * y, y, 1.5);
-        return y;
-    };
-    double y = rsq(rowbcast_c<0>(d[0]));
-#pragma unroll
-    for (int c = 0; c < 16; c++) {
-        d[c] = d[c] * y;
-        x[c] = x[c] * y;
-        if (c + 1 < 16) {
-            const double b = rowbcast(d[c], c + 1);
-            d[c + 1] = fma(-d[c], b, d[c + 1]);
-            y = rsq(rowbcast(d[c + 1], c + 1));
-            x[c + 1] = fma(-b, x[c], x[c + 1]);
-        }
-#pragma unroll
-        for (int q = c + 2; q < 16; q++) {
-            const double b = rowbcast(d[c], q);
-            d[q] = fma(-d[c], b, d[q]);
-            x[q] = fma(-b, x[c], x[q]);
-        }
-#pragma unroll
-        for (int q = c; q < 16; q++) asm volatile("" : "+v"(x[q]));
-    }
-    double dg = 1.0;
-#pragma unroll
-    for (int c = 0; c < 16; c++)
-        if (r == c) dg = d[c];
-    const bool ok = __all(lane >= 16 || (dg > 0.0 && dg < __builtin_inf()));
-    if (lane < 16) {
-#pragma unroll
-        for (int c = 0; c < 16; c++) As[(o + r) * LP + o + c] = (c <= r) ? d[c] : 0.0;
-        if (Li) {
-#pragma unroll
-            for (int c = 0; c < 16; c++) Li[(o + c) * LP + o + r] = x[c];
-        }
-    } else if (act) {
-        double *po = (up ? hi.out : lo.out) + idx * (up ? hi.ors : lo.ors);
-        const int ocs = up ? hi.ocs : lo.ocs;
-#pragma unroll
-        for (int c = 0; c < 16; c++) po[c * ocs] = x[c];
-    }
-    return ok;
-}
-
-// Two builds of the 64x64 diagonal factor: BA_ENV_FACTOR_X = 1 runs the
-// panels and the inverse's blocks on the pivot chains' spare lanes
-// (wave_factor16x); 0 (the default until measured on the box) the
-// look-ahead schedule of rounds 2-3.
-#ifndef BA_ENV_FACTOR_X
-#define BA_ENV_FACTOR_X 0
-#endif
-#if BA_ENV_FACTOR_X
-// The 256-thread workgroup factors the 64x64 SPD tile in As (row-major, lower
-// used) and inverts the factor, blocked by 16: four wave_factor16x chains on
-// wave 0, each carrying on its spare lanes the rows of A below its block (->
-// the panel L_ib) and the columns of V_b = -L_b,0:b Li_0:b,0:b (-> the
-// inverse's blocks Li_b,c = L_bb^-1 V_b), so no separate panel or inverse
-// stage remains; between chains b and b+1 one MFMA stage (one task per wave:
-// the trailing blocks of column b+1 and V_b+1's blocks); the other trailing
-// blocks run on waves 1..3 beside the next chain.  Lanes per chain: 16
-// identity + 48 A rows | 16 V + 32 A rows | 16 A rows + 32 V | 48 V.  Writes L
-// to the lower triangle of As (the upper triangle is zeroed only if
-// zero_upper: the 16x16 blocks above the diagonal keep A otherwise) and L^-1
-// (zero upper) to Li.  Returns false on a non-positive pivot.  The caller
-// synchronises after filling As; the result is visible after return.
-__device__ __forceinline__ bool block_potrf_inv(double *As, double *Li, bool zero_upper = true)
-{
-    __shared__ __attribute__((aligned(16))) double Vs[16 * LP];   // V_b: 16 x 16 b
-    __shared__ __attribute__((aligned(16))) int bad;
-    const int tid = threadIdx.x, w = tid >> 6;
-    // one trailing block (i, j) of block column k: A_ij -= L_ik L_jk^T
-    auto trail = [&](int i, int j, int k) {
-        d4 acc = {0.0, 0.0, 0.0, 0.0};
-        acc = mfma16_nt(As, 16 * i, 16 * k, As, 16 * j, 16 * k, acc);
-        put16(As, 16 * i, 16 * j, acc, -1.0, true);
-    };
-    // block c of V_b = -sum_{t=c}^{b-1} L_bt Li_tc
-    auto vblk = [&](int b, int c) {
-        d4 acc = {0.0, 0.0, 0.0, 0.0};
-        for (int t = c; t < b; t++) acc = mfma16_nn(As, 16 * b, 16 * t, Li, 16 * t, 16 * c, acc);
-        put16(Vs, 0, 16 * c, acc, -1.0, false);
-    };
-    // the six 16x16 blocks above the diagonal of L^-1 (everything else is
-    // written below); ordered before their readers by the stage barriers
-    for (int q = tid; q < 6 * 256; q += blockDim.x) {
-        const int b = q >> 8, e = q & 255;
-        const int bi = b < 3 ? 0 : (b < 5 ? 1 : 2), bj = b < 3 ? b + 1 : (b < 5 ? b - 1 : 3);
-        Li[(16 * bi + (e >> 4)) * LP + 16 * bj + (e & 15)] = 0.0;
-    }
-#pragma unroll 1
-    for (int b = 0; b < 4; b++) {
-        const int o = 16 * b, na = 48 - o;   // A rows below the block
-        if (w == 0) {
-            vseg lo, hi;
-            double *ar = As + (o + 16) * LP + o;   // A rows below, block column b
-            if (b == 0) {
-                lo = vseg{ar, ar, LP, 1, LP, 1, 16};
-                hi = vseg{ar + 16 * LP, ar + 16 * LP, LP, 1, LP, 1, 32};
-            } else if (b == 1) {
-                lo = vseg{Vs, Li + o * LP, 1, LP, 1, LP, 16};
-                hi = vseg{ar, ar, LP, 1, LP, 1, 32};
-            } else if (b == 2) {
-                lo = vseg{ar, ar, LP, 1, LP, 1, 16};
-                hi = vseg{Vs, Li + o * LP, 1, LP, 1, LP, 32};
-            } else {
-                lo = vseg{Vs, Li + o * LP, 1, LP, 1, LP, 16};
-                hi = vseg{Vs + 16, Li + o * LP + 16, 1, LP, 1, LP, 32};
-            }
-            (void)na;
-            const bool ok = wave_factor16x(As, Li, o, lo, hi);
-            if (tid == 0) bad = (b > 0 ? bad : 0) | (ok ? 0 : 1);
-        } else if (b == 1) {   // column 0's trailing blocks right of column 1
-            if (w == 1) trail(2, 2, 0);
-            else if (w == 2) trail(3, 2, 0);
-            else trail(3, 3, 0);
-        } else if (b == 2) {   // column 1's
-            if (w == 1) trail(3, 3, 1);
-        }
-        __syncthreads();
-        if (b < 3) {
-            // column b+1 of the trailing blocks, and V_b+1: one task per wave
-            const int nt = 3 - b;   // blocks (b+1 .. 3, b+1)
-            if (w < nt)
-                trail(b + 1 + w, b + 1, b);
-            else
-                vblk(b + 1, w - nt);
-            __syncthreads();
-        }
-    }
-    if (zero_upper) {
-        for (int q = tid; q < NB * NB; q += blockDim.x) {   // zero the upper triangle of L
-            const int r = q >> 6, c = q & 63;
-            if (c > r) As[r * LP + c] = 0.0;
-        }
-        __syncthreads();
-    }
-    return bad == 0;
-}
-
-#else
 // The 256-thread workgroup factors the 64x64 SPD tile in As (row-major, lower
 // used) and inverts the factor, blocked by 16 (blocks 0..3).  Per block column
 // k one wave factors the diagonal block (wave_factor16: L_kk and its inverse),
@@ -637,8 +454,6 @@ __device__ __forceinline__ bool block_potrf_inv(double *As, double *Li, bool zer
     }
     return bad == 0;
 }
-
-#endif
 
 // ---------------------------------------------------------------------------
 // One tile column k of the envelope Cholesky, with the trailing update of
@@ -1439,6 +1254,93 @@ __device__ __forceinline__ void gemv32(const double *M, const double *v, double 
     __syncthreads();
 }
 
+// One wave: wave_factor16's Cholesky of the 16x16 diagonal block at (o, o)
+// of As, and forward substitutions z = L^-1 v of up to 48 more vectors in
+// the same loop.  Every 16-lane row of the wave holds a copy of the factor
+// rows (lane l: row l & 15), so each row's DPP broadcasts see the factor's
+// column and the copies stay bit-identical; lanes 0..15 carry the identity
+// (column r of L^-1 -> Li, if Li), lanes 16 + i (i < 16) vector i of segment
+// lo and lanes 32 + i (i < 32) vector i of segment hi (in == nullptr: none).
+// The substitutions ride on the factor's broadcasts, so a panel A L^-T (rows
+// of A as the vectors) costs no separate stage.  Every lane issues the same
+// 16 unconditional LDS loads for its start vector (e_r and zeros from a
+// small LDS row), so the loads are in flight together and need no selects.  Lanes 0..15 write L (zero upper) to As.
+// Returns false on a non-positive pivot.
+struct vseg {
+    const double *in;   // entry c of vector i: in[i * irs + c * ics]
+    double *out;        // result entry c:      out[i * ors + c * ocs]
+    int irs, ics, ors, ocs;
+    int n;              // vectors (lanes 16 / 32 + i, i < n)
+};
+
+__device__ __forceinline__ bool wave_factor16x(double *As, double *Li, int o, vseg lo, vseg hi)
+{
+    // e_r for lanes r < 16 and zeros for idle lanes come from one LDS row
+    // (ident[16] = 1), so every lane's start vector is one strided read
+    __shared__ double ident[33];
+    const int lane = threadIdx.x & 63, r = lane & 15;
+    if (lane < 33) ident[lane] = lane == 16 ? 1.0 : 0.0;
+    const bool up = lane >= 32;
+    const int idx = up ? lane - 32 : lane - 16;
+    const double *sin = up ? hi.in : lo.in;
+    const bool act = lane >= 16 && sin != nullptr && idx < (up ? hi.n : lo.n);
+    const double *pin =
+        act ? sin + idx * (up ? hi.irs : lo.irs) : (lane < 16 ? ident + 16 - r : ident);
+    const int ics = act ? (up ? hi.ics : lo.ics) : 1;
+    double d[16], x[16];
+#pragma unroll
+    for (int c = 0; c < 16; c++) d[c] = As[(o + r) * LP + o + c];
+    __builtin_amdgcn_wave_barrier();   // ident written (same wave: LDS in order)
+#pragma unroll
+    for (int q = 0; q < 16; q++) x[q] = pin[q * ics];
+    auto rsq = [&](double piv) {
+        double y = __builtin_amdgcn_rsq(piv);
+        const double hp = 0.5 * piv;
+        y = y * fma(-hp * y, y, 1.5);
+        y = y * fma(-hp * y, y, 1.5);
+        return y;
+    };
+    double y = rsq(rowbcast_c<0>(d[0]));
+#pragma unroll
+    for (int c = 0; c < 16; c++) {
+        d[c] = d[c] * y;
+        x[c] = x[c] * y;
+        if (c + 1 < 16) {
+            const double b = rowbcast(d[c], c + 1);
+            d[c + 1] = fma(-d[c], b, d[c + 1]);
+            y = rsq(rowbcast(d[c + 1], c + 1));
+            x[c + 1] = fma(-b, x[c], x[c + 1]);
+        }
+#pragma unroll
+        for (int q = c + 2; q < 16; q++) {
+            const double b = rowbcast(d[c], q);
+            d[q] = fma(-d[c], b, d[q]);
+            x[q] = fma(-b, x[c], x[q]);
+        }
+#pragma unroll
+        for (int q = c; q < 16; q++) asm volatile("" : "+v"(x[q]));
+    }
+    double dg = 1.0;
+#pragma unroll
+    for (int c = 0; c < 16; c++)
+        if (r == c) dg = d[c];
+    const bool ok = __all(lane >= 16 || (dg > 0.0 && dg < __builtin_inf()));
+    if (lane < 16) {
+#pragma unroll
+        for (int c = 0; c < 16; c++) As[(o + r) * LP + o + c] = (c <= r) ? d[c] : 0.0;
+        if (Li) {
+#pragma unroll
+            for (int c = 0; c < 16; c++) Li[(o + c) * LP + o + r] = x[c];
+        }
+    } else if (act) {
+        double *po = (up ? hi.out : lo.out) + idx * (up ? hi.ors : lo.ors);
+        const int ocs = up ? hi.ocs : lo.ocs;
+#pragma unroll
+        for (int c = 0; c < 16; c++) po[c * ocs] = x[c];
+    }
+    return ok;
+}
+
 // The 32 x 32 Cholesky of As (lower; block (0, 1) keeps A) and, if Li, L^-1
 // (row-major, zero upper) -> Li, and, if Cm, the panel Cm L^-T in place (32
 // rows), as two wave_factor16x stages with one MFMA stage between them:
@@ -1579,81 +1481,6 @@ extern "C" int vlgba_debug_crstamps(unsigned long long *out, int nrec)
 #define CR_SUB(k)
 #endif
 
-// Panel tiles of the one-launch CR.  In a BA_CR_GRAN build k_cr32_fused
-// hands the panels over as epoch-tagged granules {epoch, 32-bit half} (two
-// 8-byte write-through agent-scope stores per value, the pattern of the back
-// substitution's x granules): a consumer polls the tile's own granules until
-// every tag matches, so the producer needs no vmcnt(0) + barrier + flag
-// before the data is usable and the consumer no flag round trip before its
-// loads.  gr.g == nullptr (per-level kernels, default builds): plain crL.
-#ifndef BA_CR_GRAN
-#define BA_CR_GRAN 0
-#endif
-struct cr32_gran {
-    unsigned long long *g;
-    unsigned epoch;
-    double *status;
-};
-
-template <bool SC>
-__device__ __forceinline__ void store_panel(double *crL, const cr32_gran &gr, long long idx,
-                                            const double *T)
-{
-    const long long T2 = (long long)T32 * T32;
-    if (SC && gr.g) {
-        const int c = threadIdx.x & 31, r0 = threadIdx.x >> 5;
-        unsigned long long *g = gr.g + 2 * T2 * idx;
-        const unsigned long long tag = (unsigned long long)gr.epoch << 32;
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int r = r0 + 8 * u;
-            const unsigned long long v = __builtin_bit_cast(unsigned long long, T[r * LP + c]);
-            __hip_atomic_store(g + 2 * (r * T32 + c), tag | (v & 0xffffffffULL), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(g + 2 * (r * T32 + c) + 1, tag | (v >> 32), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
-    } else {
-        store_rm32<SC>(crL + T2 * idx, T);
-    }
-}
-
-template <bool SC>
-__device__ __forceinline__ void load_panel(const double *crL, const cr32_gran &gr, long long idx,
-                                           double *T)
-{
-    const long long T2 = (long long)T32 * T32;
-    if (SC && gr.g) {
-        const int c = threadIdx.x & 31, r0 = threadIdx.x >> 5;
-        const unsigned long long *g = gr.g + 2 * T2 * idx;
-        unsigned long long v[8];
-        for (unsigned spins = 0;; spins++) {
-            bool ok = true;
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int q = 2 * ((r0 + 8 * u) * T32 + c);
-                v[2 * u] = __hip_atomic_load(g + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                v[2 * u + 1] =
-                    __hip_atomic_load(g + q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok = ok && (unsigned)(v[2 * u] >> 32) == gr.epoch &&
-                     (unsigned)(v[2 * u + 1] >> 32) == gr.epoch;
-            }
-            if (__all(ok)) break;
-            if (spins >= BA_BACK_SPIN_MAX) {
-                if ((threadIdx.x & 63) == 0) gr.status[1] = 1.0;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-            T[(r0 + 8 * u) * LP + c] = __builtin_bit_cast(
-                double, (v[2 * u] & 0xffffffffULL) | (v[2 * u + 1] << 32));
-    } else {
-        load_rm32<SC>(crL + T2 * idx, T);
-    }
-}
-
 // factor step (level 0, on the assembled S): role 0 factors D_e, writes L_e^-1
 // (row-major 32 x 32) and y_e = L_e^-1 r_e; role 1 / 2 (split, one workgroup
 // each, redoing the same factorisation) form Lp_e = C(p, e) L_e^-T / Lq_e =
@@ -1666,8 +1493,7 @@ template <bool SC>
 __device__ __forceinline__ void cr32_factor_body(const cr32_lds &sh, double *S, long long lds,
                                                  int TB, long long ld, int e, int p, int q,
                                                  int role, int nt, double *linv, double *crL,
-                                                 const double *rhs, double *y, double *status,
-                                                 cr32_gran gr = {nullptr, 0, nullptr})
+                                                 const double *rhs, double *y, double *status)
 {
     double *As = sh.As, *Bs = sh.Bs, *Cs = sh.Cs, *Xs = sh.Xs, *rk = sh.rk, *yk = sh.ym;
     const int tid = threadIdx.x;
@@ -1692,7 +1518,7 @@ __device__ __forceinline__ void cr32_factor_body(const cr32_lds &sh, double *S, 
     CR_SUB(6);
     if (pan) {
         CR_SUB(7);
-        store_panel<SC>(crL, gr, side == 1 ? e : nt + e, Cs);
+        store_rm32<SC>(crL + T2 * (side == 1 ? e : nt + e), Cs);
     }
     if (rows) {
         if (!ylanes) gemv32(Bs, rk, sh.part, yk, false);
@@ -1706,7 +1532,7 @@ __device__ __forceinline__ void cr32_factor_body(const cr32_lds &sh, double *S, 
         load32<SC>(S, lds, TB, ld, q, e, Cs, false, false);
         __syncthreads();
         cr32_chol(As, nullptr, Cs, Xs, nullptr, nullptr, [](int) {});
-        store_panel<SC>(crL, gr, nt + e, Cs);
+        store_rm32<SC>(crL + T2 * (nt + e), Cs);
     }
 }
 
@@ -1771,8 +1597,7 @@ __device__ __forceinline__ void cr32_level_body(const cr32_lds &sh, double *S, l
                                                 int TB, long long ld, int k, int p, int q, int em,
                                                 int ep, int role, int nt, double *linv,
                                                 double *crL, double *rhs, double *y,
-                                                double *status, Mid mid,
-                                                cr32_gran gr = {nullptr, 0, nullptr})
+                                                double *status, Mid mid)
 {
     double *As = sh.As, *Bs = sh.Bs, *Cs = sh.Cs, *Ds = sh.Ds, *Es = sh.Es, *Xs = sh.Xs;
     double *rk = sh.rk, *ym = sh.ym, *yp = sh.yp, *um = sh.um, *up = sh.up;
@@ -1788,10 +1613,10 @@ __device__ __forceinline__ void cr32_level_body(const cr32_lds &sh, double *S, l
         }
     };
     load32<SC>(S, lds, TB, ld, k, k, As, false, true);
-    load_panel<SC>(crL, gr, nt + em, Bs);               // L(k, em)
-    if (ep >= 0) load_panel<SC>(crL, gr, ep, Cs);       // L(k, ep)
-    if (role == 1) load_panel<SC>(crL, gr, em, Ds);     // L(p, em)
-    if (role == 2) load_panel<SC>(crL, gr, nt + ep, Ds);   // L(q, ep)
+    load_rm32<SC>(crL + T2 * (nt + em), Bs);            // L(k, em)
+    if (ep >= 0) load_rm32<SC>(crL + T2 * ep, Cs);      // L(k, ep)
+    if (role == 1) load_rm32<SC>(crL + T2 * em, Ds);    // L(p, em)
+    if (role == 2) load_rm32<SC>(crL + T2 * (nt + ep), Ds);   // L(q, ep)
     if (role == 0) load_r();
     __syncthreads();
     CR_SUB(4);
@@ -1858,7 +1683,7 @@ __device__ __forceinline__ void cr32_level_body(const cr32_lds &sh, double *S, l
         return;
     }
     CR_SUB(7);
-    store_panel<SC>(crL, gr, role == 1 ? k : nt + k, Es);
+    store_rm32<SC>(crL + T2 * (role == 1 ? k : nt + k), Es);
 }
 
 __global__ __launch_bounds__(256) void k_cr32_level(double *__restrict__ S, long long lds, int TB,
@@ -1996,15 +1821,14 @@ __device__ __forceinline__ void cr32_back_body(const cr32_lds &sh, int e, int p,
                                                int TB, long long ld, const double *linv,
                                                const double *crL, const double *y, double *x,
                                                unsigned long long *xg, unsigned epoch,
-                                               double *status,
-                                               cr32_gran gr = {nullptr, 0, nullptr})
+                                               double *status)
 {
     double *Lp = sh.As, *Lq = sh.Bs, *Li = sh.Cs;
     double *t = sh.rk, *xp = sh.ym, *xq = sh.yp, *u = sh.um, *z = sh.up;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const long long T2 = (long long)T32 * T32;
-    if (p >= 0) load_panel<SC>(crL, gr, e, Lp);
-    if (q >= 0) load_panel<SC>(crL, gr, nt + e, Lq);
+    if (p >= 0) load_rm32<SC>(crL + T2 * e, Lp);
+    if (q >= 0) load_rm32<SC>(crL + T2 * (nt + e), Lq);
     load_rm32<SC>(linv + T2 * e, Li);
     if (tid < T32) t[tid] = tid < TB ? ldg<SC>(y + (long long)TB * e + tid) : 0.0;
     __syncthreads();
@@ -2148,13 +1972,11 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
                                                     const int *__restrict__ srec, int nt,
                                                     double *linv, double *crL, double *rhs,
                                                     double *y, double *x, unsigned *flag,
-                                                    unsigned long long *xg,
-                                                    unsigned long long *crg, unsigned epoch,
+                                                    unsigned long long *xg, unsigned epoch,
                                                     double *status, cr32_fplan P)
 {
     CR32_LDS_DECL;
     CR_ST(0);
-    const cr32_gran gr{crg, epoch, status};   // crg: panels as granules (BA_CR_GRAN)
     const int b = blockIdx.x;
     int L = 0;
     while (L < P.nl && b >= P.b0[L + 1]) L++;
@@ -2169,7 +1991,7 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
         CR_ST(1);
         if (!((role == 1 && p < 0) || (role == 2 && q < 0)))
             cr32_factor_body<true>(sh, S, lds, TB, ld, e, p, q, role, nt, linv, crL, rhs, y,
-                                   status, gr);
+                                   status);
         CR_ST(2);
         if (role == 4)
             cr32_publish(flag + fw(0, e, 0), epoch, 2);
@@ -2197,14 +2019,7 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
             ep = fr[4];
         }
         int w[8] = {0, 0, 0, 0, 0, 0, 0, 0}, nw = 0;
-        if (crg) {   // panels polled as granules: flags only for D_k, r_k and y
-            if (role == 0) {
-                w[nw++] = fw(L - 1, em, 0);
-                if (ep >= 0) w[nw++] = fw(L - 1, ep, 0);
-                if (L >= 2) w[nw++] = fw(L - 1, k, 4);
-            }
-            if (L >= 2) w[nw++] = fw(L - 1, k, 3);
-        } else if (role == 1 || role == 2) {   // panels only: L(k, em), L(k, ep) and the fill's
+        if (role == 1 || role == 2) {   // panels only: L(k, em), L(k, ep) and the fill's
             w[nw++] = fw(L - 1, em, 2);  // L(p, em) | L(q, ep) -- not role 0's y / L^-1
             if (role == 1) w[nw++] = fw(L - 1, em, 1);
             if (ep >= 0) {
@@ -2237,7 +2052,7 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
         };
         if (!((role == 1 && p < 0) || (role == 2 && q < 0)))
             cr32_level_body<true>(sh, S, lds, TB, ld, k, p, q, em, ep, role, nt, linv, crL, rhs,
-                                  y, status, mid, gr);
+                                  y, status, mid);
         CR_ST(2);
         cr32_publish(flag + fw(L, k, role == 3 ? 4 : role), epoch);
         CR_ST(3);
@@ -2249,9 +2064,9 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
     while (Le + 1 < P.nl && rec >= P.eofs[Le + 1]) Le++;
     const int e = elim[3 * rec], p = elim[3 * rec + 1], q = elim[3 * rec + 2];
     const int w[8] = {fw(Le, e, 0), fw(Le, e, 1), fw(Le, e, 2), 0, 0, 0, 0, 0};
-    cr32_wait_flags(flag, crg ? 1 : 3, w, epoch, status);   // granules: L^-1 and y only
+    cr32_wait_flags(flag, 3, w, epoch, status);
     CR_ST(1);
-    cr32_back_body<true>(sh, e, p, q, nt, TB, ld, linv, crL, y, x, xg, epoch, status, gr);
+    cr32_back_body<true>(sh, e, p, q, nt, TB, ld, linv, crL, y, x, xg, epoch, status);
     CR_ST(2);
     CR_ST(3);
 }
@@ -2742,12 +2557,6 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
                 const size_t nfl = (size_t)5 * nl * nt;
                 TRY_RC(dev_alloc(&d->crflag, sizeof(unsigned) * nfl));
                 VLGBA_CHECK(hipMemsetAsync(d->crflag, 0, sizeof(unsigned) * nfl, d->stream));
-                if (BA_CR_GRAN) {   // [2][nt][32 * 32] values, two granules each
-                    const size_t ng = (size_t)2 * nt * T32 * T32 * 2;
-                    TRY_RC(dev_alloc(&d->crgran, sizeof(unsigned long long) * ng));
-                    VLGBA_CHECK(hipMemsetAsync(d->crgran, 0, sizeof(unsigned long long) * ng,
-                                               d->stream));
-                }
             }
             TRY_RC(dev_alloc(&d->crf, sizeof(int) * (frec.size() + 1)));
             TRY_RC(dev_alloc(&d->crs, sizeof(int) * (srec.size() + 1)));
@@ -3034,8 +2843,6 @@ void ba_chol_free(ba_dev *d)
     d->xgran = nullptr;
     if (d->crflag) ba_dfree(d->crflag);
     d->crflag = nullptr;
-    if (d->crgran) ba_dfree(d->crgran);
-    d->crgran = nullptr;
     d->cr_fused = 0;
     if (d->crf) ba_dfree(d->crf);
     if (d->crs) ba_dfree(d->crs);
@@ -3162,8 +2969,7 @@ int ba_chol_solve(ba_dev *d, int nospin)
         KT_B(d);
         k_cr32_fused<<<P.b0[nl] + nrec, 256, 0, d->stream>>>(
             d->S, d->lds, d->tb32, d->ld, d->cr_elim, d->crf, d->crs, d->nt32, d->linv, d->crL,
-            d->rhs, d->ywork, d->da, d->crflag, d->xgran, d->crgran, d->back_epoch, d->scal + 4,
-            P);
+            d->rhs, d->ywork, d->da, d->crflag, d->xgran, d->back_epoch, d->scal + 4, P);
         KT_E(d, KT_CR_FACTOR);
         return -(int)hipGetLastError();
     }

@@ -147,9 +147,6 @@ struct ba_dev {
     // role 0..2 | survivor); cr_fused = 0 (VLGBA_CR_FUSED=0) keeps the
     // per-level launches
     unsigned *crflag;             // [nlev][nt32][5]
-    // BA_CR_GRAN builds: the panels of k_cr32_fused as epoch-tagged 32-bit
-    // halves (the data is the flag: the panel records poll them, no flag wait)
-    unsigned long long *crgran;   // [2][nt32][32 * 32][2]
     int cr_fused;
     // one-level nested dissection of the envelope (ba_chol_setup, auto mode
     // when S is not tridiagonal; dense_solve 4 forces it): the cameras split
