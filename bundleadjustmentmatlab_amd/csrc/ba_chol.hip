@@ -2885,6 +2885,14 @@ int ba_chol_prepare(ba_dev *d)
     return -(int)hipGetLastError();
 }
 
+// the same rule on a dense ld x ld S (the natural-order retry of a
+// nested-dissection pivot, ba_solver.cpp) and the camera-order rhs
+int ba_fix_diag_plain(ba_dev *d, double *S, long long ld)
+{
+    k_fix_diag<<<(int)((ld + 255) / 256), 256, 0, d->stream>>>(S, d->rhs, ld);
+    return -(int)hipGetLastError();
+}
+
 int ba_chol_fix_diag(ba_dev *d)
 {
     k_fix_diag<<<(int)((d->lds + 255) / 256), 256, 0, d->stream>>>(d->S, d->rhs, d->lds);

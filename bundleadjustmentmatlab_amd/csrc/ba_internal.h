@@ -333,6 +333,7 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk_host, int nb);
 void ba_chol_free(ba_dev *d);
 int ba_chol_prepare(ba_dev *d);
 int ba_assemble_tiles(ba_dev *d);   // envelope tiles of S + pinv rule + status, one launch
+int ba_fix_diag_plain(ba_dev *d, double *S, long long ld);
 int ba_chol_fix_diag(ba_dev *d);
 // nospin = 1: only launches that never wait on other workgroups (the
 // per-level / per-column paths) -- the re-solve after a hand-off timeout

@@ -1082,6 +1082,7 @@ struct vlgba_ctx {
     double *pinv_S = nullptr, *pinv_ev = nullptr, *pinv_e = nullptr, *pinv_w = nullptr;
     int *pinv_info = nullptr;
     int pinv_used = 0;            // passes that took the pinv fallback
+    int nd_retries = 0;           // nested-dissection pivots solved in the natural order
     int spin_retries = 0;         // passes re-solved after a hand-off timeout
     int debug_timeouts = 0;       // test hooks: passes whose timeout word / pivot word
     int debug_pivots = 0;         // is forced (vlgba_debug_force_status)
@@ -1865,6 +1866,11 @@ struct rs_api {
     rocblas_status (*syevd)(rocblas_handle, const rocblas_evect, const rocblas_fill,
                             const rocblas_int, double *, const rocblas_int, double *, double *,
                             rocblas_int *);
+    rocblas_status (*potrf)(rocblas_handle, const rocblas_fill, const rocblas_int, double *,
+                            const rocblas_int, rocblas_int *);
+    rocblas_status (*potrs)(rocblas_handle, const rocblas_fill, const rocblas_int,
+                            const rocblas_int, double *, const rocblas_int, double *,
+                            const rocblas_int);
     bool ok = false;
 };
 rs_api *rs_load()
@@ -1878,6 +1884,8 @@ rs_api *rs_load()
         api.create = (decltype(api.create))dlsym(h, "rocblas_create_handle");
         api.set_stream = (decltype(api.set_stream))dlsym(h, "rocblas_set_stream");
         api.syevd = (decltype(api.syevd))dlsym(h, "rocsolver_dsyevd");
+        api.potrf = (decltype(api.potrf))dlsym(h, "rocsolver_dpotrf");
+        api.potrs = (decltype(api.potrs))dlsym(h, "rocsolver_dpotrs");
         api.ok = api.create && api.set_stream && api.syevd;
     });
     return api.ok ? &api : nullptr;
@@ -1891,10 +1899,10 @@ std::map<int, rocblas_handle> g_rs_handle;   // per device
 // in place), the lower triangle of S assembled densely, rocSOLVER dsyevd,
 // then V diag(1/ev, |ev| > tol) V^T e_ (ba_pinv_apply), and the update with
 // that da.  Every rank runs it on the identical all-reduced system.
-static int pinv_fallback(vlgba_ctx *c, double lam, double hs[6])
+// rocSOLVER, the dense scratch of the fallbacks and this device's handle
+static int rs_prepare(vlgba_ctx *c, rs_api **rs_out, rocblas_handle *hdl_out)
 {
     ba_dev &d = c->d;
-    const auto t0 = std::chrono::steady_clock::now();
     rs_api *rs = rs_load();
     if (!rs) return VLGBA_E_ARG;
     const long long ld = d.ld;
@@ -1917,6 +1925,70 @@ static int pinv_fallback(vlgba_ctx *c, double lam, double hs[6])
             hdl = it->second;
         }
     }
+    *rs_out = rs;
+    *hdl_out = hdl;
+    return 0;
+}
+
+// A pass whose nested-dissection Cholesky met a non-positive pivot: the same
+// S (the Cholesky took it in place) is assembled densely in the natural
+// camera order and factored by rocSOLVER dpotrf before the pinv fallback is
+// considered -- the pivot may be an artefact of the elimination order on a
+// system whose gauge directions only the damping lifts (cond(S) up to 1e17 on
+// the growing replays), and the natural order is the one bundle_euclid.m's
+// pinv is then compared with.  Returns 1 if dpotrf fails
+// too (the caller takes the pinv step), 0 with the pass finished.
+static int nd_natural_retry(vlgba_ctx *c, double lam, double hs[6])
+{
+    ba_dev &d = c->d;
+    rs_api *rs = nullptr;
+    rocblas_handle hdl = nullptr;
+    TRY(rs_prepare(c, &rs, &hdl));
+    if (!rs->potrf || !rs->potrs) return 1;
+    const long long ld = d.ld;
+    TRY(schur_phase(c, lam));
+    TRY(ba_launch_assemble_plain(&d, c->pinv_S, ld, 1));
+    TRY(ba_fix_diag_plain(&d, c->pinv_S, ld));   // exactly-zero rows: unit diagonal, rhs 0
+    VLGBA_CHECK(hipMemcpyAsync(c->pinv_e, d.rhs, sizeof(double) * ld, hipMemcpyDeviceToDevice,
+                               d.stream));
+    VLGBA_CHECK(hipStreamSynchronize(d.stream));
+    int info = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_rs_mu);
+        if (rs->set_stream(hdl, d.stream) != rocblas_status_success ||
+            rs->potrf(hdl, rocblas_fill_lower, (rocblas_int)ld, c->pinv_S, (rocblas_int)ld,
+                      c->pinv_info) != rocblas_status_success)
+            return VLGBA_E_ARG;
+        VLGBA_CHECK(hipMemcpyAsync(&info, c->pinv_info, sizeof info, hipMemcpyDeviceToHost,
+                                   d.stream));
+        VLGBA_CHECK(hipStreamSynchronize(d.stream));
+        if (info != 0) return 1;
+        if (rs->potrs(hdl, rocblas_fill_lower, (rocblas_int)ld, 1, c->pinv_S, (rocblas_int)ld,
+                      c->pinv_e, (rocblas_int)ld) != rocblas_status_success)
+            return VLGBA_E_ARG;
+    }
+    VLGBA_CHECK(hipMemcpyAsync(d.da, c->pinv_e, sizeof(double) * ld, hipMemcpyDeviceToDevice,
+                               d.stream));
+    d.publish_req = 0;
+    d.published = 0;
+    TRY(ba_launch_update(&d, lam));
+    if (d.parity) TRY(ba_launch_parity_new_sums(&d, lam));
+    TRY(collect_scalars(c, false, hs));
+    c->nd_retries++;
+    if (c->rank == 0 && !std::getenv("VLGBA_QUIET"))
+        std::fprintf(stderr, "[vlgba] non-positive pivot in the nested-dissection order: the "
+                             "natural-order Cholesky (dpotrf) took the pass\n");
+    return 0;
+}
+
+static int pinv_fallback(vlgba_ctx *c, double lam, double hs[6])
+{
+    ba_dev &d = c->d;
+    const auto t0 = std::chrono::steady_clock::now();
+    rs_api *rs = nullptr;
+    rocblas_handle hdl = nullptr;
+    TRY(rs_prepare(c, &rs, &hdl));
+    const long long ld = d.ld;
     TRY(schur_phase(c, lam));
     TRY(ba_launch_assemble_plain(&d, c->pinv_S, ld, 1));
     // the library stream is non-blocking: make S complete before rocSOLVER
@@ -2024,6 +2096,11 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
     if (hs[5] != 0.0) {   // the solve did not finish: again, without spins
         TRY(resolve_nospin(c, lam, hs));
         info->spin_retry = 1;
+    }
+    if (hs[4] != 0.0 && d.nd_np > 0) {   // the nested-dissection order's pivot: the
+        const int rc = nd_natural_retry(c, lam, hs);   // natural order first
+        if (rc < 0) return rc;
+        if (rc == 0) hs[4] = 0.0;
     }
     if (hs[4] != 0.0) {
         // non-positive pivot: bundle_euclid.m:193 takes pinv(S)*e_ whatever S is
