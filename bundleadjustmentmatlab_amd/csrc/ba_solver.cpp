@@ -67,6 +67,19 @@ size_t mem_bucket(size_t bytes)
 }
 }   // namespace
 
+// VLGBA_POISON=1 (debugging): every block handed out is filled with 0xff
+// bytes (NaN doubles, -1 ints), so a kernel that reads memory it never wrote
+// shows up as NaN instead of as a stale value of a previous context
+static void *poisoned(void *p, size_t b)
+{
+    static const bool on = std::getenv("VLGBA_POISON") != nullptr;
+    if (on && p) {   // null-stream memset: not ordered with non-blocking streams
+        (void)hipMemset(p, 0xff, b);
+        (void)hipDeviceSynchronize();
+    }
+    return p;
+}
+
 void *ba_dmalloc(size_t bytes)
 {
     int dev = 0;
@@ -79,7 +92,7 @@ void *ba_dmalloc(size_t bytes)
             void *p = it->second;
             g_mem_free.erase(it);
             g_mem_live[p] = {dev, b};
-            return p;
+            return poisoned(p, b);
         }
     }
     void *p = nullptr;
@@ -96,7 +109,7 @@ void *ba_dmalloc(size_t bytes)
     }
     std::lock_guard<std::mutex> lk(g_mem_mu);
     g_mem_live[p] = {dev, b};
-    return p;
+    return poisoned(p, b);
 }
 
 void ba_dfree(void *p)

@@ -69,6 +69,9 @@ def _subset_obs(sc, cams, pts, cam_on=None, pt_on=None):
             np.take(sc.obs_x, idx, axis=0))
 
 
+PREFETCH_WORKERS = 2   # incremental_bundle's context builders (see below)
+
+
 def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, device=0,
                        verbose=False, devices=None, shards=None, obs_per_shard=None,
                        progress=None, prefetch=True):
@@ -154,7 +157,7 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
     # j+1's before-triangulation solve (the same points, one camera more) --
     # and their contexts built side by side, so each has two LM loops to hide
     # behind instead of one
-    pool = ThreadPoolExecutor(max_workers=2) if use_pf else None
+    pool = ThreadPoolExecutor(max_workers=PREFETCH_WORKERS) if use_pf else None
     pending = {}
     stats = {"prefetched": 0, "mispredicted": 0}
 
