@@ -583,7 +583,11 @@ __device__ __forceinline__ void factor_step_body(double *__restrict__ S, long lo
     FS_ST(2);
     gemv64(Bs, rk, part, yk, 1.0);            // y_k = L^-1 r_k
     if (b == 0) {
-        store_tile(S, lds, k, k, As);
+        // L_kk is NOT stored back to S(k, k): the panel workgroups of this
+        // launch read A_kk from there, and one that starts after this store
+        // (a busy GPU: not every workgroup is resident at once) would factor
+        // L_kk instead of A_kk.  Nothing reads L_kk later (the backward solve
+        // takes L_kk^-1 from linv, the next columns only off-diagonal tiles).
         double *lo = linv + (long long)NB * NB * k;
         for (int q = tid; q < NB * NB; q += blockDim.x) lo[q] = Bs[(q >> 6) * LP + (q & 63)];
         if (tid < NB) y[(long long)NB * k + tid] = yk[tid];

@@ -4,6 +4,8 @@ prefetch on (2 or 1 workers) or off: the first solve whose final error differs
 from the first run's, and the pinv passes.
 
 usage: python tools/replay_determinism.py [M] [--runs pf2,pf2,none] [--fresh]
+  a run spec ending in "@spin" (with --fresh) reports a hand-off timeout on
+  every pass (VLGBA_DEBUG_SPIN_TIMEOUT): every pass re-solved without spins
 """
 import json
 import os
@@ -18,14 +20,16 @@ def run(M, spec):
     import bundleadjustmentmatlab_amd.incremental as inc
     from bundleadjustmentmatlab_amd.scene import make_config
     sc = make_config("cfg5x", m=M)
-    pinv = []
+    pinv, spin = [], []
     orig = inc.bundle_euclid_obs
 
     def spy(*a, **kw):
         r = orig(*a, **kw)
         pinv.append(int(r[-1].pinv_passes))
+        spin.append(int(r[-1].spin_retries))
         return r
     inc.bundle_euclid_obs = spy
+    spec = spec.split("@")[0]
     if spec.startswith("pf"):
         inc.PREFETCH_WORKERS = int(spec[2:] or 2)
     try:
@@ -35,7 +39,7 @@ def run(M, spec):
     e = [float(q["error"][-1]) if len(q["error"]) else float("nan") for q in res["solves"]]
     info = [(q["tag"], q["camera"], int(q["passes"]), float(q["error"][0]) if len(q["error"]) else 0.0)
             for q in res["solves"]]
-    return e, pinv, res["prefetch"], info
+    return e, pinv, dict(res["prefetch"], spin_retries=sum(spin)), info
 
 
 def main():
@@ -48,8 +52,11 @@ def main():
     out = []
     for spec in specs:
         if "--fresh" in args:
+            env = dict(os.environ)
+            if spec.endswith("@spin"):
+                env["VLGBA_DEBUG_SPIN_TIMEOUT"] = "0:1000000"
             p = subprocess.run([sys.executable, "-u", __file__, str(M), "--runs", spec, "--child"],
-                               capture_output=True, text=True, timeout=1000)
+                               capture_output=True, text=True, timeout=1000, env=env)
             line = [ln for ln in p.stdout.splitlines() if ln.startswith("JSON")]
             if p.returncode != 0 or not line:
                 print(spec, "failed", p.returncode, p.stderr[-2000:])
