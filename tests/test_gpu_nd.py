@@ -175,3 +175,49 @@ def test_nd_projective(gpu):
     print(f"projective ND: cond(S) {cond:.2e}, da relative difference {rel:.2e} (bar {bar:.1e})")
     assert rel <= bar, (rel, cond)
     assert np.linalg.norm(db1 - db0) <= bar * np.linalg.norm(db0)
+
+
+@pytest.mark.parametrize("solver", ["envelope", "nd"])
+def test_envelope_factor_bit_identical_under_load(gpu, solver):
+    """The envelope factor's workgroups of one tile column must not depend on
+    being resident together: with another stream keeping the GPU busy, the
+    column's workgroups start at different times.  Workgroup 0 used to store
+    L_kk over A_kk, which a late panel workgroup then factored again (a
+    non-positive pivot or a wrong panel: run-to-run differences and pinv steps
+    of the growing replay, tools/solve_stress.py).  Every pass under load
+    equals the idle pass bit for bit."""
+    import threading
+
+    import torch
+    sc = _scene("ladybug", 300, seed=3)
+    a, b = _params(sc, 6)
+    with gpu.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, 6,
+                            solver=solver) as ba:
+        ba.set_params(a, b)
+        info0 = ba.step(relinearize=True, update_lm=False)
+        da0 = ba.last_step()[0].copy()
+        assert not info0.chol_failed and not info0.pinv
+        stop = threading.Event()
+
+        def burn():
+            s = torch.cuda.Stream()
+            x = torch.randn(4096, 4096, device="cuda")
+            with torch.cuda.stream(s):
+                while not stop.is_set():
+                    for _ in range(10):
+                        x = torch.tanh(x @ x * 1e-4)
+                    s.synchronize()
+        th = threading.Thread(target=burn)
+        th.start()
+        try:
+            bad = []
+            for rep in range(40):
+                info = ba.step(relinearize=True, update_lm=False)
+                da = ba.last_step()[0]
+                if info.chol_failed or info.pinv or not np.array_equal(da, da0):
+                    bad.append((rep, bool(info.chol_failed), bool(info.pinv),
+                                float(np.abs(da - da0).max())))
+        finally:
+            stop.set()
+            th.join()
+    assert not bad, bad
