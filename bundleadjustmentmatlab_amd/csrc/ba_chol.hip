@@ -96,6 +96,27 @@ __device__ __forceinline__ void put_tile(double *T, const double v[16], bool tra
     }
 }
 
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+typedef __attribute__((address_space(1))) unsigned gu32_t;
+
+template <bool SC> __device__ __forceinline__ double ldg(const double *p)
+{
+    if constexpr (SC)
+        return __builtin_bit_cast(
+            double, __hip_atomic_load((gu64_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    else
+        return *p;
+}
+
+template <bool SC> __device__ __forceinline__ void stg(double *p, double v)
+{
+    if constexpr (SC)
+        __hip_atomic_store((gu64_t *)p, __builtin_bit_cast(unsigned long long, v),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        *p = v;
+}
+
 // LDS T[r][c] -> row-major 64x64 dst[r*64 + c]
 __device__ __forceinline__ void store_rowmajor(double *__restrict__ dst, const double *T)
 {
@@ -503,13 +524,29 @@ extern "C" int vlgba_debug_fstamps(unsigned long long *out, int n)
 // an arc column leaves the separator's rhs to k_sep_update (two arcs'
 // columns run in the same launch) and its separator x separator trailing
 // pairs, which the host does not launch (they end each pair enumeration).
+// the 64 x 64 diagonal factor + inverse as two 32 x 32 factors (defined below)
+__device__ __forceinline__ bool potrf64_via32(double *As, double *Bs, double *Xs);
+
+// bounded spins of the in-launch hand-offs (then status[1]: re-solve without them)
+#ifndef BA_BACK_SPIN_MAX
+#define BA_BACK_SPIN_MAX 400000u
+#endif
+// kflag (one-launch hand-off, may be null): workgroup 0 publishes L_kk^-1 and
+// y_k (write-through stores, then flag k = epoch) and the panel workgroups
+// take them from there instead of updating and factoring A_kk themselves --
+// the same bits (workgroup 0's factor is the one they would recompute), with
+// the panel's own pending update overlapping workgroup 0's factor.  A panel
+// workgroup only waits on workgroup 0 of its column, which has a lower index
+// (dispatched first); a spin that gives up sets status[1] and the host
+// re-solves with kflag = null.
 __device__ __forceinline__ void factor_step_body(double *__restrict__ S, long long lds, int k,
                                                  const int *__restrict__ pan, int T,
                                                  const int *__restrict__ prev, int Tp,
                                                  double *__restrict__ linv,
                                                  double *__restrict__ rhs,
                                                  double *__restrict__ y,
-                                                 double *__restrict__ status, int b, int sep0)
+                                                 double *__restrict__ status, int b, int sep0,
+                                                 unsigned *__restrict__ kflag, unsigned epoch)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double *As = sm, *Bs = sm + NB * LP, *Cs = sm + 2 * NB * LP;
@@ -546,12 +583,13 @@ __device__ __forceinline__ void factor_step_body(double *__restrict__ S, long lo
         return;
     }
     const int i = b > 0 ? pan[b - 1] : k;
+    const bool hand = kflag != nullptr && b > 0;   // a panel taking L_kk^-1 / y_k from workgroup 0
     // every tile this workgroup reads, fetched at once (one memory latency
     // instead of three dependent ones): A_ik, L_k,k-1, A_kk, L_i,k-1
     double vc[16], va[16], vb[16], vk[16];
     if (b > 0) fetch_tile(S, lds, i, k, vc);
     if (kin) fetch_tile(S, lds, k, k - 1, vb);
-    fetch_tile(S, lds, k, k, vk);
+    if (!hand) fetch_tile(S, lds, k, k, vk);
     bool iin = false;   // column k-1 reaches row i (panel tiles only): a wave-wide search
     if (b > 0 && kin) {
         const int lane = tid & 63;
@@ -559,7 +597,7 @@ __device__ __forceinline__ void factor_step_body(double *__restrict__ S, long lo
             iin = __any(t0 + lane < Tp && prev[t0 + lane] == i);
     }
     if (iin) fetch_tile(S, lds, i, k - 1, va);
-    if (tid < NB) rk[tid] = rhs[(long long)NB * k + tid];
+    if (!hand && tid < NB) rk[tid] = rhs[(long long)NB * k + tid];
     if (b > 0) put_tile(Cs, vc, false);
     if (iin) put_tile(As, va, false);
     if (kin) put_tile(Bs, vb, false);
@@ -569,6 +607,34 @@ __device__ __forceinline__ void factor_step_body(double *__restrict__ S, long lo
         __syncthreads();
         acc_to_lds(acc, Cs, -1.0, true);
     }
+    if (hand) {
+        if (tid < 64) {   // wave 0 waits for workgroup 0's flag
+            for (unsigned spins = 0;; spins++) {
+                const unsigned f = __hip_atomic_load((const gu32_t *)(kflag + k), __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                if (f == epoch) break;
+                if (spins >= BA_BACK_SPIN_MAX) {
+                    if (tid == 0) status[1] = 1.0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        __syncthreads();
+        {   // L_kk^-1 (row-major, write-through) -> Bs, y_k -> yk (agent-scope loads)
+            const double *lo = linv + (long long)NB * NB * k;
+            const int c = tid & 63, r0 = tid >> 6;
+            double v[16];
+#pragma unroll
+            for (int u = 0; u < 16; u++) v[u] = ldg<true>(lo + (r0 + 4 * u) * NB + c);
+#pragma unroll
+            for (int u = 0; u < 16; u++) Bs[(r0 + 4 * u) * LP + c] = v[u];
+            if (tid < NB) yk[tid] = ldg<true>(y + (long long)NB * k + tid);
+        }
+        __syncthreads();
+        FS_ST(1);
+        FS_ST(2);
+    } else {
     // A_kk and its pending update
     if (kin) mfma_64x64(Bs, Bs, acc);
     __syncthreads();
@@ -579,9 +645,25 @@ __device__ __forceinline__ void factor_step_body(double *__restrict__ S, long lo
         __syncthreads();
     }
     FS_ST(1);
-    const bool ok = block_potrf_inv(As, Bs);
+    __shared__ __attribute__((aligned(16))) double fXs[16 * LP];
+    const bool ok = potrf64_via32(As, Bs, fXs);
     FS_ST(2);
     gemv64(Bs, rk, part, yk, 1.0);            // y_k = L^-1 r_k
+    if (b == 0 && kflag) {   // published for the column's panel workgroups
+        double *lo = linv + (long long)NB * NB * k;
+        for (int q = tid; q < NB * NB; q += blockDim.x)
+            stg<true>(lo + q, Bs[(q >> 6) * LP + (q & 63)]);
+        if (tid < NB) stg<true>(y + (long long)NB * k + tid, yk[tid]);
+        if (tid == 0 && !ok) status[0] = 1.0;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave
+        __syncthreads();
+        if (tid == 0)
+            __hip_atomic_store((gu32_t *)(kflag + k), epoch, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        FS_ST(3);
+        FS_END();
+        return;
+    }
     if (b == 0) {
         // L_kk is NOT stored back to S(k, k): the panel workgroups of this
         // launch read A_kk from there, and one that starts after this store
@@ -596,6 +678,7 @@ __device__ __forceinline__ void factor_step_body(double *__restrict__ S, long lo
         FS_END();
         return;
     }
+    }   // (!hand)
     mfma_64x64(Cs, Bs, acc);   // L_ik[r][c] = sum_t A_ik[r][t] Li[c][t]
     __syncthreads();
     acc_to_lds(acc, Cs, 1.0, false);
@@ -614,9 +697,11 @@ __global__ __launch_bounds__(256) void k_factor_step(double *__restrict__ S, lon
                                                      double *__restrict__ linv,
                                                      double *__restrict__ rhs,
                                                      double *__restrict__ y,
-                                                     double *__restrict__ status)
+                                                     double *__restrict__ status,
+                                                     unsigned *__restrict__ kflag, unsigned epoch)
 {
-    factor_step_body(S, lds, k, pan, T, prev, Tp, linv, rhs, y, status, blockIdx.x, INT_MAX);
+    factor_step_body(S, lds, k, pan, T, prev, Tp, linv, rhs, y, status, blockIdx.x, INT_MAX,
+                     kflag, epoch);
 }
 
 // one step of every arc of the nested dissection: column k[t] of arc t takes
@@ -634,13 +719,15 @@ __global__ __launch_bounds__(256) void k_factor_multi(double *__restrict__ S, lo
                                                       double *__restrict__ linv,
                                                       double *__restrict__ rhs,
                                                       double *__restrict__ y,
-                                                      double *__restrict__ status)
+                                                      double *__restrict__ status,
+                                                      unsigned *__restrict__ kflag,
+                                                      unsigned epoch)
 {
     const int b = blockIdx.x;
     int t = 0;
     while (t + 1 < P.np && b >= P.b0[t + 1]) t++;
     factor_step_body(S, lds, P.k[t], pan_list + P.pofs[t], P.T[t], pan_list + P.qofs[t], P.Tp[t],
-                     linv, rhs, y, status, b - P.b0[t], sep0);
+                     linv, rhs, y, status, b - P.b0[t], sep0, kflag, epoch);
 }
 
 // ---------------------------------------------------------------------------
@@ -781,9 +868,6 @@ __global__ __launch_bounds__(256) void k_backward(const double *__restrict__ S, 
         z[(long long)NB * j + tid] -= ((part[0][tid] + part[1][tid]) + part[2][tid]) + part[3][tid];
 }
 
-#ifndef BA_BACK_SPIN_MAX
-#define BA_BACK_SPIN_MAX 400000u
-#endif
 // ---------------------------------------------------------------------------
 // The envelope's backward solve in ONE launch (the per-column k_backward
 // launches sat at the launch floor).  Workgroup w takes tile column
@@ -1145,27 +1229,6 @@ __global__ __launch_bounds__(256) void k_cr_update(double *__restrict__ S, long 
 // first row of MI355X_MICROARCH.md's hand-off table (no acquire fence).
 // SC = false: plain accesses (the per-level kernels, whose hand-offs cross a
 // launch boundary).
-typedef __attribute__((address_space(1))) unsigned long long gu64_t;
-typedef __attribute__((address_space(1))) unsigned gu32_t;
-
-template <bool SC> __device__ __forceinline__ double ldg(const double *p)
-{
-    if constexpr (SC)
-        return __builtin_bit_cast(
-            double, __hip_atomic_load((gu64_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    else
-        return *p;
-}
-
-template <bool SC> __device__ __forceinline__ void stg(double *p, double v)
-{
-    if constexpr (SC)
-        __hip_atomic_store((gu64_t *)p, __builtin_bit_cast(unsigned long long, v),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-        *p = v;
-}
-
 template <bool SC = false>
 __device__ __forceinline__ void load32(const double *__restrict__ S, long long lds, int TB,
                                        long long ld, int ti, int tj, double *T, bool transposed,
@@ -1430,6 +1493,61 @@ __device__ __forceinline__ bool cr32_chol(double *As, double *Li, double *Cm, do
     }
     __syncthreads();
     return bad32 == 0;
+}
+
+// The envelope's 64 x 64 diagonal factor and L^-1 (row-major, zero upper, in
+// Bs) as two cr32_chol factors: F(A00) -> L00, Li00 and the panel L10 = A10
+// L00^-T on the same pivot chains; then A11 -= L10 L10^T (waves 0-2, its
+// three lower 16-blocks) beside T = L10 Li00 (into Bs's block (1, 0)); F(A11)
+// -> L11, Li11; Li10 = -Li11 T.  Two 32-row factors (~8.2k cycles each,
+// profiles/r04c_ubench_cr32.txt) instead of four dependent 16-row stages with
+// their updates in between (block_potrf_inv, ~29.5k cycles).  Xs: 16 x LP
+// scratch.  Ends with a barrier.
+__device__ __forceinline__ bool potrf64_via32(double *As, double *Bs, double *Xs)
+{
+    const int tid = threadIdx.x, w = tid >> 6;
+    for (int q = tid; q < 32 * 32; q += blockDim.x) Bs[(q >> 5) * LP + 32 + (q & 31)] = 0.0;
+    bool ok = cr32_chol(As, Bs, As + 32 * LP, Xs, nullptr, nullptr, [](int) {});
+    {
+        // A11 -= L10 L10^T: blocks (32, 32), (48, 32), (48, 48) by waves 0..2;
+        // T = L10 Li00 blocks (32 + 16 (u >> 1), 16 (u & 1)), u = w and w + 4 - 1 ...
+        const int ri = w == 0 ? 32 : 48, ci = w == 2 ? 48 : 32;
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        if (w < 3) {
+            acc = mfma16_nt(As, ri, 0, As, ci, 0, acc);
+            acc = mfma16_nt(As, ri, 16, As, ci, 16, acc);
+        }
+        // T blocks: wave 3 takes (32, 0) and (32, 16), waves 0 / 1 take (48, 0) / (48, 16)
+        d4 t0 = {0.0, 0.0, 0.0, 0.0}, t1 = {0.0, 0.0, 0.0, 0.0};
+        if (w == 3) {
+            t0 = mfma16_nn(As, 32, 0, Bs, 0, 0, t0);
+            t0 = mfma16_nn(As, 32, 16, Bs, 16, 0, t0);
+            t1 = mfma16_nn(As, 32, 16, Bs, 16, 16, t1);   // Li00 block (0, 1) is zero
+        } else if (w < 2) {
+            t0 = mfma16_nn(As, 48, 0, Bs, 0, 16 * w, t0);
+            t0 = mfma16_nn(As, 48, 16, Bs, 16, 16 * w, t0);
+        }
+        if (w < 3) put16(As, ri, ci, acc, -1.0, true);
+        if (w == 3) {
+            put16(Bs, 32, 0, t0, 1.0, false);
+            put16(Bs, 32, 16, t1, 1.0, false);
+        } else if (w < 2) {
+            put16(Bs, 48, 16 * w, t0, 1.0, false);
+        }
+    }
+    __syncthreads();
+    ok = cr32_chol(As + 32 * LP + 32, Bs + 32 * LP + 32, nullptr, Xs, nullptr, nullptr,
+                   [](int) {}) && ok;
+    {   // Li10 = -Li11 T, block (32 + 16 (w >> 1), 16 (w & 1)) by wave w
+        const int ri = 32 + 16 * (w >> 1), cj = 16 * (w & 1);
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        acc = mfma16_nn(Bs, ri, 32, Bs, 32, cj, acc);
+        acc = mfma16_nn(Bs, ri, 48, Bs, 48, cj, acc);
+        __syncthreads();
+        put16(Bs, ri, cj, acc, -1.0, false);
+    }
+    __syncthreads();
+    return ok;
 }
 
 // LDS of one cyclic-reduction record: five 32-row tiles, the 16-row scratch
@@ -2814,6 +2932,11 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
                                    d->stream));
         d->back_epoch = 0;
     }
+    if (!d->cr_nlev && d->dense_solve != 3) {   // the factor's in-launch hand-off
+        TRY_RC(dev_alloc(&d->kflag, sizeof(unsigned) * (size_t)nt));
+        VLGBA_CHECK(hipMemsetAsync(d->kflag, 0, sizeof(unsigned) * (size_t)nt, d->stream));
+        d->fac_epoch = 0;
+    }
     TRY_RC(dev_alloc(&d->env_tiles, sizeof(int) * (env.size() + 1)));
     if (!list.empty())
         VLGBA_CHECK(hipMemcpyAsync(d->pan_list, list.data(), sizeof(int) * list.size(),
@@ -2866,8 +2989,10 @@ void ba_chol_free(ba_dev *d)
     if (d->pan_list) ba_dfree(d->pan_list);
     if (d->pan_ptr) ba_dfree(d->pan_ptr);
     if (d->xgran64) ba_dfree(d->xgran64);
+    if (d->kflag) ba_dfree(d->kflag);
     d->pan_ptr = nullptr;
     d->xgran64 = nullptr;
+    d->kflag = nullptr;
     if (d->env_tiles) ba_dfree(d->env_tiles);
     d->h_tfirst = d->pan_ptr_h = nullptr;
     d->pan_list = d->env_tiles = nullptr;
@@ -2905,7 +3030,8 @@ int ba_chol_fix_diag(ba_dev *d)
 
 // the envelope's tile columns k0 .. k1-1 (k_factor_step), column k0 taking no
 // pending update of column k0-1
-static void envelope_columns(ba_dev *d, int k0, int k1, long long L, double *rhs)
+static void envelope_columns(ba_dev *d, int k0, int k1, long long L, double *rhs,
+                             unsigned *kflag)
 {
     const size_t smem3 = sizeof(double) * 3 * NB * LP;
     for (int k = k0; k < k1; k++) {
@@ -2917,7 +3043,7 @@ static void envelope_columns(ba_dev *d, int k0, int k1, long long L, double *rhs
         KT_B(d);
         k_factor_step<<<1 + T + Tr * (Tr + 1) / 2, 256, smem3, d->stream>>>(
             d->S, L, k, d->pan_list + p0, T, d->pan_list + q0, Tp, d->linv, rhs, d->ywork,
-            d->scal + 4);
+            d->scal + 4, kflag, d->fac_epoch);
         KT_E(d, KT_FACTOR);
     }
 }
@@ -3056,6 +3182,9 @@ int ba_chol_solve(ba_dev *d, int nospin)
         }
         return -(int)hipGetLastError();
     }
+    // the envelope factor's in-launch hand-off (not in a re-solve)
+    unsigned *kflag = nospin ? nullptr : d->kflag;
+    if (kflag && ++d->fac_epoch == 0) d->fac_epoch = 1;
     if (d->nd_np > 0) {   // nested dissection: the arcs side by side, then the separator
         const int np = d->nd_np, s0 = d->nd_a0[np];
         const long long L = d->slds;
@@ -3086,7 +3215,8 @@ int ba_chol_solve(ba_dev *d, int nospin)
             P.b0[P.np] = nbk;
             KT_B(d);
             k_factor_multi<<<nbk, 256, smem3, d->stream>>>(d->S, L, d->pan_list, P, s0, d->linv,
-                                                          d->nd_rhs, d->ywork, d->scal + 4);
+                                                          d->nd_rhs, d->ywork, d->scal + 4, kflag,
+                                                          d->fac_epoch);
             KT_E(d, KT_FACTOR);
         }
         if (d->nd_nrec > 0) {
@@ -3099,13 +3229,13 @@ int ba_chol_solve(ba_dev *d, int nospin)
                                                              d->nd_part, d->nd_rhs);
             KT_E(d, KT_SYRK);
         }
-        envelope_columns(d, s0, nt, L, d->nd_rhs);
+        envelope_columns(d, s0, nt, L, d->nd_rhs, kflag);
         TRY_RC(envelope_backward(d, L, d->nd_x, nospin));
         k_nd_scatter<<<(int)((d->lds + 255) / 256), 256, 0, d->stream>>>(d->nd_prow, d->nd_x,
                                                                          d->da, d->lds);
         return -(int)hipGetLastError();
     }
-    envelope_columns(d, 0, nt, d->lds, d->rhs);
+    envelope_columns(d, 0, nt, d->lds, d->rhs, kflag);
     TRY_RC(envelope_backward(d, d->lds, d->da, nospin));
     return -(int)hipGetLastError();
 }

@@ -118,6 +118,8 @@ struct ba_dev {
     int *pan_list;     // device: tile rows i > k with tfirst[i] <= k, per k
     int *pan_ptr;      // device copy of pan_ptr_h (k_backward_all)
     unsigned long long *xgran64;  // [nt][128] x_k granules of the one-launch backward
+    unsigned *kflag;   // [nt] envelope factor: L_kk^-1 / y_k published (epoch fac_epoch)
+    unsigned fac_epoch;
     int *env_tiles;    // device [n_env][2] (i, k) tiles inside the envelope
     int *tb_ptr, *tb_blk;  // device: per envelope tile, the co-visible blocks overlapping it
     int n_env;
