@@ -183,6 +183,43 @@ __device__ __forceinline__ void mfma_64x64(const double *As, const double *Bs, d
     mfma_64x64_acc(As, Bs, acc);
 }
 
+// acc = A B^T over K = 64 for A = S tile (ia, kc), B = S tile (jb, kc), the
+// operands read straight from S (column-major, L2) in the 16x16x4 operand
+// layout instead of from LDS: the same MFMA chain as mfma_64x64 on the
+// loaded tiles, bit for bit, without their 64 KB of LDS.
+__device__ __forceinline__ void mfma_64x64_glb(const double *__restrict__ S, long long lds,
+                                               int ia, int jb, int kc, d4 acc[2][2])
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r0 = 32 * (w >> 1), c0 = 32 * (w & 1);
+    const int li = lane & 15, lk = lane >> 4;
+    const double *A = S + (long long)NB * ia + lds * (long long)NB * kc;
+    const double *B = S + (long long)NB * jb + lds * (long long)NB * kc;
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) acc[x][y] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int h = 0; h < 2; h++) {   // K in two halves of operand loads
+        double a0[8], a1[8], b0[8], b1[8];
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            const long long kk = lds * (4 * (8 * h + s) + lk);
+            a0[s] = A[r0 + li + kk];
+            a1[s] = A[r0 + 16 + li + kk];
+            b0[s] = B[c0 + li + kk];
+            b1[s] = B[c0 + 16 + li + kk];
+        }
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[s], b0[s], acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[s], b1[s], acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[s], b0[s], acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[s], b1[s], acc[1][1], 0, 0, 0);
+        }
+    }
+}
+
 // write acc (scale * acc + (add ? T : 0)) into LDS tile T in MFMA layout
 __device__ __forceinline__ void acc_to_lds(const d4 acc[2][2], double *T, double scale, bool add)
 {
@@ -645,8 +682,7 @@ __device__ __forceinline__ void factor_step_body(double *__restrict__ S, long lo
         __syncthreads();
     }
     FS_ST(1);
-    __shared__ __attribute__((aligned(16))) double fXs[16 * LP];
-    const bool ok = potrf64_via32(As, Bs, fXs);
+    const bool ok = potrf64_via32(As, Bs, As + 32);   // scratch: A's upper-right block
     FS_ST(2);
     gemv64(Bs, rk, part, yk, 1.0);            // y_k = L^-1 r_k
     if (b == 0 && kflag) {   // published for the column's panel workgroups
@@ -691,6 +727,129 @@ __device__ __forceinline__ void factor_step_body(double *__restrict__ S, long lo
     FS_END();
 }
 
+// factor_step_body with the in-launch hand-off on two LDS tiles instead of
+// three (two workgroups per CU): the pending updates' operands come straight
+// from S (mfma_64x64_glb), workgroup 0 factors in As -> Bs, a panel keeps
+// A_ik in As and L_kk^-1 in Bs, a trailing pair its C tile in As.  The same
+// operations in the same order: bit-identical to factor_step_body.
+__device__ __forceinline__ void factor_step_two(double *__restrict__ S, long long lds, int k,
+                                                const int *__restrict__ pan, int T,
+                                                const int *__restrict__ prev, int Tp,
+                                                double *__restrict__ linv,
+                                                double *__restrict__ rhs,
+                                                double *__restrict__ y,
+                                                double *__restrict__ status, int b, int sep0,
+                                                unsigned *__restrict__ kflag, unsigned epoch)
+{
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double *As = sm, *Bs = sm + NB * LP;
+    __shared__ double yk[NB], rk[NB];
+    __shared__ double part[4][NB];
+    const int tid = threadIdx.x;
+    const bool kin = Tp > 0 && prev[0] == k;   // column k-1 reaches row k
+    d4 acc[2][2];
+    FS_ST(0);
+    if (b > T) {   // a trailing pair of column k-1 below row k
+        const int *pl = prev + (kin ? 1 : 0);
+        const int Tr = Tp - (kin ? 1 : 0);
+        int q = b - T - 1, jj = 0;
+        while (q >= Tr - jj) {
+            q -= Tr - jj;
+            jj++;
+        }
+        const int j = pl[jj], i = pl[jj + q];
+        double vc[16];
+        fetch_tile(S, lds, i, j, vc);
+        mfma_64x64_glb(S, lds, i, j, k - 1, acc);
+        put_tile(As, vc, false);
+        __syncthreads();
+        acc_to_lds(acc, As, -1.0, true);
+        __syncthreads();
+        store_tile(S, lds, i, j, As);
+        FS_END();
+        return;
+    }
+    if (b == 0) {   // A_kk's pending update, factor, L_kk^-1, y_k; published
+        double vk[16];
+        fetch_tile(S, lds, k, k, vk);
+        if (tid < NB) rk[tid] = rhs[(long long)NB * k + tid];
+        if (kin) mfma_64x64_glb(S, lds, k, k, k - 1, acc);
+        put_tile(As, vk, false);
+        __syncthreads();
+        if (kin) {
+            acc_to_lds(acc, As, -1.0, true);
+            __syncthreads();
+        }
+        FS_ST(1);
+        const bool ok = potrf64_via32(As, Bs, As + 32);
+        FS_ST(2);
+        gemv64(Bs, rk, part, yk, 1.0);   // y_k = L^-1 r_k
+        double *lo = linv + (long long)NB * NB * k;
+        for (int q = tid; q < NB * NB; q += blockDim.x)
+            stg<true>(lo + q, Bs[(q >> 6) * LP + (q & 63)]);
+        if (tid < NB) stg<true>(y + (long long)NB * k + tid, yk[tid]);
+        if (tid == 0 && !ok) status[0] = 1.0;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave
+        __syncthreads();
+        if (tid == 0)
+            __hip_atomic_store((gu32_t *)(kflag + k), epoch, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        FS_ST(3);
+        FS_END();
+        return;
+    }
+    // a panel tile: A_ik and its pending update, then L_ik = A_ik L_kk^-T
+    const int i = pan[b - 1];
+    double vc[16];
+    fetch_tile(S, lds, i, k, vc);
+    bool iin = false;   // column k-1 reaches row i: a wave-wide search
+    if (kin) {
+        const int lane = tid & 63;
+        for (int t0 = 1; t0 < Tp && !iin; t0 += 64)
+            iin = __any(t0 + lane < Tp && prev[t0 + lane] == i);
+    }
+    if (iin) mfma_64x64_glb(S, lds, i, k, k - 1, acc);
+    put_tile(As, vc, false);
+    __syncthreads();
+    if (iin) acc_to_lds(acc, As, -1.0, true);
+    if (tid < 64) {   // wave 0 waits for workgroup 0's flag
+        for (unsigned spins = 0;; spins++) {
+            const unsigned f = __hip_atomic_load((const gu32_t *)(kflag + k), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            if (f == epoch) break;
+            if (spins >= BA_BACK_SPIN_MAX) {
+                if (tid == 0) status[1] = 1.0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+    {   // L_kk^-1 (row-major, write-through) -> Bs, y_k -> yk (agent-scope loads)
+        const double *lo = linv + (long long)NB * NB * k;
+        const int c = tid & 63, r0 = tid >> 6;
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) v[u] = ldg<true>(lo + (r0 + 4 * u) * NB + c);
+#pragma unroll
+        for (int u = 0; u < 16; u++) Bs[(r0 + 4 * u) * LP + c] = v[u];
+        if (tid < NB) yk[tid] = ldg<true>(y + (long long)NB * k + tid);
+    }
+    __syncthreads();
+    FS_ST(1);
+    FS_ST(2);
+    mfma_64x64(As, Bs, acc);   // L_ik[r][c] = sum_t A_ik[r][t] Li[c][t]
+    __syncthreads();
+    acc_to_lds(acc, As, 1.0, false);
+    __syncthreads();
+    store_tile(S, lds, i, k, As);
+    double ri[1];
+    gemv64(As, yk, part, nullptr, 1.0, ri);   // (L_ik y_k)[tid] for tid < 64
+    if (tid < NB && i < sep0) rhs[(long long)NB * i + tid] -= ri[0];
+    FS_ST(3);
+    FS_END();
+}
+
 __global__ __launch_bounds__(256) void k_factor_step(double *__restrict__ S, long long lds, int k,
                                                      const int *__restrict__ pan, int T,
                                                      const int *__restrict__ prev, int Tp,
@@ -700,8 +859,12 @@ __global__ __launch_bounds__(256) void k_factor_step(double *__restrict__ S, lon
                                                      double *__restrict__ status,
                                                      unsigned *__restrict__ kflag, unsigned epoch)
 {
-    factor_step_body(S, lds, k, pan, T, prev, Tp, linv, rhs, y, status, blockIdx.x, INT_MAX,
-                     kflag, epoch);
+    if (kflag)
+        factor_step_two(S, lds, k, pan, T, prev, Tp, linv, rhs, y, status, blockIdx.x, INT_MAX,
+                        kflag, epoch);
+    else
+        factor_step_body(S, lds, k, pan, T, prev, Tp, linv, rhs, y, status, blockIdx.x, INT_MAX,
+                         nullptr, 0);
 }
 
 // one step of every arc of the nested dissection: column k[t] of arc t takes
@@ -726,8 +889,12 @@ __global__ __launch_bounds__(256) void k_factor_multi(double *__restrict__ S, lo
     const int b = blockIdx.x;
     int t = 0;
     while (t + 1 < P.np && b >= P.b0[t + 1]) t++;
-    factor_step_body(S, lds, P.k[t], pan_list + P.pofs[t], P.T[t], pan_list + P.qofs[t], P.Tp[t],
-                     linv, rhs, y, status, b - P.b0[t], sep0, kflag, epoch);
+    if (kflag)
+        factor_step_two(S, lds, P.k[t], pan_list + P.pofs[t], P.T[t], pan_list + P.qofs[t],
+                        P.Tp[t], linv, rhs, y, status, b - P.b0[t], sep0, kflag, epoch);
+    else
+        factor_step_body(S, lds, P.k[t], pan_list + P.pofs[t], P.T[t], pan_list + P.qofs[t],
+                         P.Tp[t], linv, rhs, y, status, b - P.b0[t], sep0, nullptr, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -3033,7 +3200,8 @@ int ba_chol_fix_diag(ba_dev *d)
 static void envelope_columns(ba_dev *d, int k0, int k1, long long L, double *rhs,
                              unsigned *kflag)
 {
-    const size_t smem3 = sizeof(double) * 3 * NB * LP;
+    // two LDS tiles with the hand-off (two workgroups per CU), three without
+    const size_t smem3 = sizeof(double) * 3 * NB * LP, smem2 = sizeof(double) * 2 * NB * LP;
     for (int k = k0; k < k1; k++) {
         const int p0 = d->pan_ptr_h[k], T = d->pan_ptr_h[k + 1] - p0;
         const int q0 = k > k0 ? d->pan_ptr_h[k - 1] : 0, Tp = k > k0 ? p0 - q0 : 0;
@@ -3041,7 +3209,7 @@ static void envelope_columns(ba_dev *d, int k0, int k1, long long L, double *rhs
         const int kin = Tp > 0 && d->h_pan_list[q0] == k;
         const int Tr = Tp - kin;
         KT_B(d);
-        k_factor_step<<<1 + T + Tr * (Tr + 1) / 2, 256, smem3, d->stream>>>(
+        k_factor_step<<<1 + T + Tr * (Tr + 1) / 2, 256, kflag ? smem2 : smem3, d->stream>>>(
             d->S, L, k, d->pan_list + p0, T, d->pan_list + q0, Tp, d->linv, rhs, d->ywork,
             d->scal + 4, kflag, d->fac_epoch);
         KT_E(d, KT_FACTOR);
@@ -3214,7 +3382,8 @@ int ba_chol_solve(ba_dev *d, int nospin)
             }
             P.b0[P.np] = nbk;
             KT_B(d);
-            k_factor_multi<<<nbk, 256, smem3, d->stream>>>(d->S, L, d->pan_list, P, s0, d->linv,
+            k_factor_multi<<<nbk, 256, kflag ? sizeof(double) * 2 * NB * LP : smem3, d->stream>>>(
+                d->S, L, d->pan_list, P, s0, d->linv,
                                                           d->nd_rhs, d->ywork, d->scal + 4, kflag,
                                                           d->fac_epoch);
             KT_E(d, KT_FACTOR);
