@@ -469,28 +469,19 @@ static int plan_threads(long long work, long long min_work)
 
 // The host planner's worker threads: created once and kept (a context is
 // created per growing-replay solve, and spawning 15 threads per plan phase
-// cost more than some phases).  One job at a time; a caller that finds the
-// pool busy (contexts created concurrently by rank threads), or a forked
-// child (the pool's threads stayed in the parent), runs its job on threads
-// of its own instead.
+// cost more than some phases).  Two pools, one job each at a time: the
+// replay builds two contexts side by side (its two prefetch workers); a
+// caller that finds both busy (more concurrent creations, e.g. rank
+// threads), or a forked child (the pools' threads stayed in the parent), runs
+// its job on threads of its own instead.
 class plan_pool {
   public:
-    static plan_pool &get()
-    {
-        static plan_pool *pp = new plan_pool();   // never destroyed: no join at exit
-        return *pp;
-    }
-    // f(t) for t in [0, nthr): t = 0 on the calling thread
-    void run(int nthr, const std::function<void(int)> &f)
+    // f(t) for t in [0, nthr): t = 0 on the calling thread; false (nothing
+    // run) if this pool is busy or unusable here
+    bool try_run(int nthr, const std::function<void(int)> &f)
     {
         std::unique_lock<std::mutex> busy(job_mu_, std::defer_lock);
-        if (getpid() != pid_ || nthr - 1 > kMax || !busy.try_lock()) {   // threads of our own
-            std::vector<std::thread> th;
-            for (int t = 1; t < nthr; t++) th.emplace_back(f, t);
-            f(0);
-            for (auto &x : th) x.join();
-            return;
-        }
+        if (getpid() != pid_ || nthr - 1 > kMax || !busy.try_lock()) return false;
         {
             std::lock_guard<std::mutex> lk(mu_);
             while ((int)th_.size() < nthr - 1) {
@@ -507,6 +498,7 @@ class plan_pool {
         std::unique_lock<std::mutex> lk(mu_);
         done_.wait(lk, [this] { return pending_ == 0; });
         job_ = nullptr;
+        return true;
     }
 
   private:
@@ -537,6 +529,17 @@ class plan_pool {
     unsigned long long gen_ = 0;
 };
 
+static void plan_run(int nthr, const std::function<void(int)> &f)
+{
+    static plan_pool *pools = new plan_pool[2];   // never destroyed: no join at exit
+    for (int q = 0; q < 2; q++)
+        if (pools[q].try_run(nthr, f)) return;
+    std::vector<std::thread> th;   // threads of our own
+    for (int t = 1; t < nthr; t++) th.emplace_back(f, t);
+    f(0);
+    for (auto &x : th) x.join();
+}
+
 // f(t, lo, hi) on nthr contiguous ranges of [0, n) (thread t takes range t;
 // the calling thread takes range 0), of equal work when wpre (the prefix sums
 // of per-item work, n + 1 entries) is given, else of equal length
@@ -559,7 +562,7 @@ static void parallel_ranges(int n, int nthr, F f, const std::vector<long long> *
         }
         cut[t] = std::max(cut[t], cut[t - 1]);
     }
-    plan_pool::get().run(nthr, [&](int t) { f(t, cut[t], cut[t + 1]); });
+    plan_run(nthr, [&](int t) { f(t, cut[t], cut[t + 1]); });
 }
 
 // MFMA chunks (points below p_split): at most BA_MF_PTS points and cmax

@@ -47,6 +47,30 @@ from .evaluation import align_scene, vl_irodr, vl_rodr
 __all__ = ["incremental_bundle"]
 
 
+def _obs_of(sc, pts):
+    """Observation ids of points ``pts`` (ascending), ascending -- from the
+    per-point observation ranges of a point-major scene (built once per
+    scene) instead of a pass over every observation; None if the scene's
+    observations are not point-major or ``pts`` is not ascending."""
+    ptr = getattr(sc, "_vlg_pt_ptr", None)
+    if ptr is None:
+        op = np.asarray(sc.obs_pt)
+        ptr = (np.searchsorted(op, np.arange(sc.n + 1)) if np.all(op[1:] >= op[:-1])
+               else False)
+        try:
+            sc._vlg_pt_ptr = ptr
+        except AttributeError:
+            pass
+    pts = np.asarray(pts)
+    if ptr is False or (len(pts) > 1 and np.any(pts[1:] <= pts[:-1])):
+        return None
+    lo = ptr[pts]
+    cnt = ptr[pts + 1] - lo
+    tot = int(cnt.sum())
+    start = np.cumsum(cnt) - cnt                     # position of each point's first obs
+    return np.repeat(lo - start, cnt) + np.arange(tot)
+
+
 def _subset_obs(sc, cams, pts, cam_on=None, pt_on=None):
     """Observations of points ``pts`` in cameras ``cams`` (``cam_on`` /
     ``pt_on``: the same sets as masks, if the caller has them) re-indexed to
@@ -58,9 +82,13 @@ def _subset_obs(sc, cams, pts, cam_on=None, pt_on=None):
     if pt_on is None:
         pt_on = np.zeros(sc.n, dtype=bool)
         pt_on[pts] = True
-    keep = np.take(cam_on, sc.obs_cam)               # one-byte gathers over all obs
-    keep &= np.take(pt_on, sc.obs_pt)
-    idx = np.flatnonzero(keep)                        # index takes: ~6x a boolean mask
+    ids = _obs_of(sc, pts)                            # the points' observations only
+    if ids is not None:
+        idx = ids[np.take(cam_on, np.take(sc.obs_cam, ids))]
+    else:
+        keep = np.take(cam_on, sc.obs_cam)           # one-byte gathers over all obs
+        keep &= np.take(pt_on, sc.obs_pt)
+        idx = np.flatnonzero(keep)                    # index takes: ~6x a boolean mask
     cmap = np.full(sc.m, -1)
     cmap[cams] = np.arange(len(cams))
     pmap = np.full(sc.n, -1)
@@ -304,11 +332,15 @@ def _triangulate(sc, K, T, w, pts, status):
     out = np.zeros((4, len(pts)))
     if len(pts) == 0:
         return out
-    on = np.zeros(sc.n, dtype=bool)
-    on[pts] = True
-    sel = np.take(on, sc.obs_pt)                         # point-major: rows per point
-    sel &= np.take(status, sc.obs_cam)
-    sel = np.flatnonzero(sel)
+    ids = _obs_of(sc, pts)                               # point-major: rows per point
+    if ids is not None:
+        sel = ids[np.take(status, np.take(sc.obs_cam, ids))]
+    else:
+        on = np.zeros(sc.n, dtype=bool)
+        on[pts] = True
+        sel = np.take(on, sc.obs_pt)
+        sel &= np.take(status, sc.obs_cam)
+        sel = np.flatnonzero(sel)
     opt, ocam, ox = sc.obs_pt[sel], sc.obs_cam[sel], np.take(sc.obs_x, sel, axis=0)
     R = vl_rodr(w[:, ocam])                              # (k, 3, 3)
     Kc = np.zeros((len(ocam), 3, 3))
