@@ -75,6 +75,38 @@ def test_incremental_subset_and_similarity():
     assert abs(s - 2.5) < 1e-9 and np.allclose(R2, R, atol=1e-9) and np.allclose(t, [1, 2, 3])
 
 
+def test_incremental_obs_ranges_match_the_full_pass():
+    """The replay's observation subsets and triangulation rows come from the
+    per-point observation ranges (incremental._obs_of) instead of a pass over
+    every observation: the same ids in the same order as the boolean-mask
+    selection, on random camera / point sets; an unsorted point list and a
+    scene whose observations are not point-major take the full pass."""
+    import types
+
+    from bundleadjustmentmatlab_amd import incremental as inc
+    sc = make_config("cfg5x", m=60)
+    rng = np.random.default_rng(11)
+    for _ in range(10):
+        cam_on = rng.random(sc.m) < 0.6
+        pt_on = rng.random(sc.n) < 0.5
+        cams, pts = np.nonzero(cam_on)[0], np.nonzero(pt_on)[0]
+        got = inc._subset_obs(sc, cams, pts, cam_on, pt_on)
+        idx = np.flatnonzero(cam_on[sc.obs_cam] & pt_on[sc.obs_pt])
+        cmap = np.full(sc.m, -1)
+        cmap[cams] = np.arange(len(cams))
+        pmap = np.full(sc.n, -1)
+        pmap[pts] = np.arange(len(pts))
+        want = (pmap[sc.obs_pt[idx]], cmap[sc.obs_cam[idx]], sc.obs_x[idx])
+        assert all(np.array_equal(g, w) for g, w in zip(got, want))
+        ids = inc._obs_of(sc, pts)
+        assert np.array_equal(ids, np.flatnonzero(pt_on[sc.obs_pt]))
+    assert inc._obs_of(sc, np.array([5, 3])) is None
+    perm = rng.permutation(sc.num_obs)
+    shuffled = types.SimpleNamespace(n=sc.n, m=sc.m, obs_pt=sc.obs_pt[perm],
+                                     obs_cam=sc.obs_cam[perm], obs_x=sc.obs_x[perm])
+    assert inc._obs_of(shuffled, np.arange(4)) is None
+
+
 @pytest.mark.parametrize("prefetch", [True, False])
 def test_incremental_prefetch_bookkeeping(monkeypatch, prefetch):
     """The replay's solve sets (incremental._solve_sets, which the prefetching
