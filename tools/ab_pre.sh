@@ -4,7 +4,7 @@
 # da_compare), untimed pass times of both builds, then the solver tests.
 set -o pipefail
 export TMPDIR=/tmp
-for sc in ladybug long "cfg5x 600" "cfg5x 900"; do
+for sc in ${AB_SCENES:-ladybug long "cfg5x 600" "cfg5x 900"}; do
   tag=${sc// /_}
   VLGBA_LIB=tools/build/ab/pre/libvlgba.so timeout -k 10 300 python -u tools/da_dump.py gpurun_out/abp_base_$tag.npz $sc > gpurun_out/abp_$tag.log 2>&1 &&
   timeout -k 10 300 python -u tools/da_dump.py gpurun_out/abp_new_$tag.npz $sc >> gpurun_out/abp_$tag.log 2>&1 &&
