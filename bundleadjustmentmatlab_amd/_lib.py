@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # variant, tools/ab_build.sh); the package's own build otherwise
 LIB_PATH = os.environ.get("VLGBA_LIB") or os.path.join(_HERE, "libvlgba.so")
 
-ABI_VERSION = 2   # VLGBA_ABI_VERSION: the struct layouts below
+ABI_VERSION = 3   # VLGBA_ABI_VERSION: the struct layouts below
 
 c_int, c_double, c_ll = ctypes.c_int, ctypes.c_double, ctypes.c_longlong
 c_dp = ctypes.POINTER(ctypes.c_double)
@@ -56,13 +56,14 @@ class VlgbaResectProblem(ctypes.Structure):
 class VlgbaStats(ctypes.Structure):
     _fields_ = [("iterations", c_int), ("accepted", c_int), ("num_error", c_int),
                 ("lambda_", c_double), ("seconds", c_double), ("pinv_passes", c_int),
-                ("spin_retries", c_int)]
+                ("spin_retries", c_int), ("nd_retries", c_int)]
 
 
 class VlgbaStepInfo(ctypes.Structure):
     _fields_ = [("old_sse", c_double), ("new_sse", c_double), ("dpg", c_double),
                 ("rho", c_double), ("lambda_", c_double), ("accepted", c_int),
-                ("chol_failed", c_int), ("pinv", c_int), ("spin_retry", c_int)]
+                ("chol_failed", c_int), ("pinv", c_int), ("spin_retry", c_int),
+                ("nd_retry", c_int)]
 
 
 class VlgbaSceneSpec(ctypes.Structure):
@@ -115,6 +116,7 @@ SIGNATURES = {
     "vlgba_version": (c_int, [ctypes.c_char_p, c_int]),
     "vlgba_abi_check": (c_int, [c_int, c_ll, c_ll, c_ll, c_ll, c_ll]),
     "vlgba_get_unique_id": (c_int, [ctypes.c_void_p]),
+    "vlgba_comm_release": (c_int, [ctypes.c_void_p]),
     "vlgba_device_count": (c_int, []),
     "vlgba_debug_sincos": (c_int, [c_dp, c_dp, c_dp, c_ll]),
     "vlgba_debug_pinv_solve": (c_int, [c_int, c_dp, c_dp, c_dp]),

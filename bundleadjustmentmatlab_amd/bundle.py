@@ -427,11 +427,32 @@ def euclid_obs_adjuster(K, m, n, obs_pt, obs_cam, obs_x, *varargin, num_vis=0.0,
     GIL released (ctypes), e.g. on a worker thread while the previous solve
     runs (incremental.py) -- and hand it to bundle_euclid_obs(adjuster=...)."""
     o = parse_options(m, n, varargin, nomex=semantics == "nomex")
-    return BundleAdjuster(K, obs_pt, obs_cam, obs_x, n, 6 + o["num_variableK"],
-                          fix_structure=o["fix_structure"], fix_motion=o["fix_motion"],
-                          pivot=o["pivot"] if o["fix_pivot"] else None, verbose=o["verbose"],
-                          num_vis=num_vis, device=device, rank=rank, world_size=world_size,
-                          comm_id=comm_id, semantics=semantics, **solver)
+    ba = BundleAdjuster(K, obs_pt, obs_cam, obs_x, n, 6 + o["num_variableK"],
+                        fix_structure=o["fix_structure"], fix_motion=o["fix_motion"],
+                        pivot=o["pivot"] if o["fix_pivot"] else None, verbose=o["verbose"],
+                        num_vis=num_vis, device=device, rank=rank, world_size=world_size,
+                        comm_id=comm_id, semantics=semantics, **solver)
+    ba.fingerprint = _adjuster_fingerprint(K, m, n, obs_pt, obs_cam, obs_x, o, num_vis,
+                                           semantics, rank, world_size)
+    return ba
+
+
+def _adjuster_fingerprint(K, m, n, obs_pt, obs_cam, obs_x, o, num_vis, semantics, rank,
+                          world_size):
+    """What a prebuilt adjuster was made for: sizes, the parsed
+    options, K and a hash of the observation list -- a context built for
+    another subset or other options with the same counts must not be used."""
+    import hashlib
+    h = hashlib.blake2b(digest_size=16)
+    for arr, dt in ((obs_pt, np.int32), (obs_cam, np.int32), (obs_x, np.float64),
+                    (K, np.float64)):
+        h.update(np.ascontiguousarray(arr, dtype=dt).tobytes())
+    piv = o["pivot"] if o["fix_pivot"] else None
+    if piv is not None:
+        h.update(np.asarray(piv, dtype=bool).tobytes())
+    return (int(m), int(n), int(o["num_variableK"]), bool(o["fix_structure"]),
+            bool(o["fix_motion"]), bool(o["fix_pivot"]), bool(o["verbose"]), float(num_vis),
+            semantics, int(rank), int(world_size), h.hexdigest())
 
 
 def bundle_euclid_obs(K, Te, w, Xe, obs_pt, obs_cam, obs_x, *varargin, num_vis=0.0, device=0,
@@ -454,9 +475,12 @@ def bundle_euclid_obs(K, Te, w, Xe, obs_pt, obs_cam, obs_x, *varargin, num_vis=0
         if solver:
             raise ValueError("bundle_euclid_obs: solver options belong to the prebuilt adjuster")
         ba = adjuster.result() if hasattr(adjuster, "result") else adjuster
-        if (ba.m, ba.n, ba.num_a, ba.num_obs) != (m, n, num_a, len(obs_pt)):
+        want = _adjuster_fingerprint(K, m, n, obs_pt, obs_cam, obs_x, o, num_vis, semantics,
+                                     rank, world_size)
+        if getattr(ba, "fingerprint", None) != want:
             ba.close()
-            raise ValueError("bundle_euclid_obs: the prebuilt adjuster is for another problem")
+            raise ValueError("bundle_euclid_obs: the prebuilt adjuster is for another problem "
+                             "or other options (make it with euclid_obs_adjuster)")
     else:
         ba = euclid_obs_adjuster(K, m, n, obs_pt, obs_cam, obs_x, *varargin, num_vis=num_vis,
                                  device=device, rank=rank, world_size=world_size,

@@ -483,6 +483,7 @@ extern "C" int vlgba_resect(const vlgba_resect_problem *pr, const vlgba_options 
         stats->accepted = total_acc;
         stats->num_error = 0;
         stats->lambda = np ? lam[0] : 0.0;
+        stats->pinv_passes = stats->spin_retries = stats->nd_retries = 0;
         stats->seconds =
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     }

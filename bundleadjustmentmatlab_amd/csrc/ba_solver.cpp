@@ -1153,20 +1153,31 @@ static void aux_release(const ba_aux &a)
     g_aux_pool.push_back(a);
 }
 
-// RCCL communicators outlive their context, keyed by (unique id, rank): a
-// caller that passes the same id again (dist.run_sharded keeps one id per
-// device set for a whole growing replay) takes the idle communicator instead
-// of paying ncclCommInitRank per solve.  One context per (id, rank) at a time;
-// idle communicators of other ids are destroyed once more than
-// BA_COMM_IDLE_MAX are kept.
-#define BA_COMM_IDLE_MAX 32
+// RCCL communicators outlive their context, keyed by (unique id, world size,
+// rank): a caller that passes the same id again (dist.run_sharded keeps one
+// id per device set for a whole growing replay) takes the idle communicator
+// instead of paying ncclCommInitRank per solve.  One context per key at a
+// time.  An idle communicator is destroyed only when its caller says the id
+// is done (vlgba_comm_release): a unique id serves ONE bootstrap, so evicting
+// the communicator of an id the caller may pass again would send that next
+// context into an ncclCommInitRank that waits forever.
+struct comm_key {
+    std::string id;
+    int world, rank;
+    bool operator<(const comm_key &o) const
+    {
+        if (id != o.id) return id < o.id;
+        if (world != o.world) return world < o.world;
+        return rank < o.rank;
+    }
+};
 static std::mutex g_comm_mu;
-static std::multimap<std::pair<std::string, int>, ncclComm_t> g_comm_idle;
-static std::map<ncclComm_t, std::pair<std::string, int>> g_comm_key;
+static std::multimap<comm_key, ncclComm_t> g_comm_idle;
+static std::map<ncclComm_t, comm_key> g_comm_key;
 
 static ncclResult_t comm_acquire(ncclComm_t *comm, int world, const void *id128, int rank)
 {
-    const std::pair<std::string, int> key(std::string((const char *)id128, 128), rank);
+    const comm_key key{std::string((const char *)id128, 128), world, rank};
     {
         std::lock_guard<std::mutex> lk(g_comm_mu);
         auto it = g_comm_idle.find(key);
@@ -1188,27 +1199,15 @@ static ncclResult_t comm_acquire(ncclComm_t *comm, int world, const void *id128,
 
 static void comm_release(ncclComm_t comm)
 {
-    std::vector<ncclComm_t> drop;
     {
         std::lock_guard<std::mutex> lk(g_comm_mu);
         auto it = g_comm_key.find(comm);
-        if (it == g_comm_key.end()) {
-            drop.push_back(comm);
-        } else {
+        if (it != g_comm_key.end()) {
             g_comm_idle.emplace(it->second, comm);
-            if (g_comm_idle.size() > BA_COMM_IDLE_MAX)
-                for (auto q = g_comm_idle.begin(); q != g_comm_idle.end();) {
-                    if (q->first.first != it->second.first) {
-                        drop.push_back(q->second);
-                        g_comm_key.erase(q->second);
-                        q = g_comm_idle.erase(q);
-                    } else {
-                        ++q;
-                    }
-                }
+            return;
         }
     }
-    for (ncclComm_t x : drop) ncclCommDestroy(x);
+    ncclCommDestroy(comm);   // its id was released while this context held it
 }
 
 static void ctx_free(vlgba_ctx *c)
@@ -2109,6 +2108,7 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
     TRY(collect_scalars(c, spin, hs));
     info->pinv = 0;
     info->spin_retry = 0;
+    info->nd_retry = 0;
     if (hs[5] != 0.0) {   // the solve did not finish: again, without spins
         TRY(resolve_nospin(c, lam, hs));
         info->spin_retry = 1;
@@ -2116,6 +2116,7 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
     if (hs[4] != 0.0 && d.nd_np > 0) {   // the nested-dissection order's pivot: the
         const int rc = nd_natural_retry(c, lam, hs);   // natural order first
         if (rc < 0) return rc;
+        info->nd_retry = 1;
         if (rc == 0) hs[4] = 0.0;
     }
     if (hs[4] != 0.0) {
@@ -2217,6 +2218,32 @@ int vlgba_get_unique_id(void *id128)
     static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
     std::memcpy(id128, &id, sizeof id);
     return 0;
+}
+
+// the caller forgets a unique id: destroy the idle communicators made from it
+// (contexts still holding one keep it until vlgba_destroy, which then
+// destroys it as an unkeyed communicator).  Returns the number destroyed.
+int vlgba_comm_release(const void *id128)
+{
+    if (!id128) return VLGBA_E_ARG;
+    const std::string id((const char *)id128, 128);
+    std::vector<ncclComm_t> drop;
+    {
+        std::lock_guard<std::mutex> lk(g_comm_mu);
+        for (auto q = g_comm_idle.begin(); q != g_comm_idle.end();) {
+            if (q->first.id == id) {
+                drop.push_back(q->second);
+                g_comm_key.erase(q->second);
+                q = g_comm_idle.erase(q);
+            } else {
+                ++q;
+            }
+        }
+        for (auto q = g_comm_key.begin(); q != g_comm_key.end();)   // in use: unkeyed,
+            q = q->second.id == id ? g_comm_key.erase(q) : std::next(q);   // destroyed on release
+    }
+    for (ncclComm_t x : drop) ncclCommDestroy(x);
+    return (int)drop.size();
 }
 
 int vlgba_device_count(void)
@@ -2538,7 +2565,7 @@ int vlgba_run(vlgba_ctx *c, double *error_out, int error_cap, vlgba_stats *stats
     c->lin_valid = 0;
     std::vector<double> err;   // error_, 1-based in the reference
     int iter = 1, iter2 = 0, passes = 0, acc = 0;
-    const int pinv0 = c->pinv_used, retry0 = c->spin_retries;
+    const int pinv0 = c->pinv_used, retry0 = c->spin_retries, nd0 = c->nd_retries;
     for (;;) {
         if (!(iter < c->max_iter && iter2 < c->max_iter2)) break;
         if (iter >= 3) {
@@ -2577,6 +2604,7 @@ int vlgba_run(vlgba_ctx *c, double *error_out, int error_cap, vlgba_stats *stats
         stats->lambda = c->lambda;
         stats->pinv_passes = c->pinv_used - pinv0;
         stats->spin_retries = c->spin_retries - retry0;
+        stats->nd_retries = c->nd_retries - nd0;
         stats->seconds =
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     }

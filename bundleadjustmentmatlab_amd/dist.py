@@ -119,6 +119,18 @@ class HostGroup:
 _COMM_IDS: dict = {}   # device tuple -> RCCL unique id (libvlgba caches the communicators)
 
 
+def release_comms() -> int:
+    """Forget every RCCL id run_sharded made: libvlgba destroys the idle
+    communicators bootstrapped from them (vlgba_comm_release).  An id is never
+    passed again after this, so no later context waits in ncclCommInitRank on
+    a spent id.  Returns the number of communicators destroyed."""
+    L = lib()
+    n = 0
+    for key in list(_COMM_IDS):
+        n += max(0, int(L.vlgba_comm_release(_COMM_IDS.pop(key))))
+    return n
+
+
 def run_sharded(K, obs_pt, obs_cam, obs_x, n, num_a, a, b, world, *, devices=None, **kw):
     """One LM solve (vlgba_run) over `world` rank threads, rank r on device
     devices[r % len(devices)].  Ranks on distinct GPUs share one RCCL

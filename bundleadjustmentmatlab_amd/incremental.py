@@ -341,6 +341,9 @@ def _triangulate(sc, K, T, w, pts, status):
         sel = np.take(on, sc.obs_pt)
         sel &= np.take(status, sc.obs_cam)
         sel = np.flatnonzero(sel)
+        # observation order: group the rows by point (stable, so each point's
+        # views keep their order) -- the slot / rank arithmetic below needs it
+        sel = sel[np.argsort(sc.obs_pt[sel], kind="stable")]
     opt, ocam, ox = sc.obs_pt[sel], sc.obs_cam[sel], np.take(sc.obs_x, sel, axis=0)
     R = vl_rodr(w[:, ocam])                              # (k, 3, 3)
     Kc = np.zeros((len(ocam), 3, 3))

@@ -29,11 +29,12 @@ extern "C" {
 
 /* ABI of this header.  Bumped whenever a public struct, constant or entry
  * point changes: 1 = the round-1/2 layouts; 2 = vlgba_stats.pinv_passes /
- * spin_retries, vlgba_step_info.spin_retry, VLGBA_NPLAN 28.  Callers check it
+ * spin_retries, vlgba_step_info.spin_retry, VLGBA_NPLAN 28; 3 =
+ * vlgba_stats.nd_retries, vlgba_step_info.nd_retry, vlgba_comm_release.  Callers check it
  * once at load time with VLGBA_ABI_CHECK() (the MEX gateways and the Python
  * loader do): the library compares the version and the struct sizes the
  * caller was compiled with against its own and returns 0 or VLGBA_E_ABI. */
-#define VLGBA_ABI_VERSION 2
+#define VLGBA_ABI_VERSION 3
 
 /* camera models (vlgba_problem.model) */
 #define VLGBA_MODEL_EUCLIDEAN 0   /* bundle_euclid.m: a = [w; T; (K)], num_a 6/7/10     */
@@ -142,6 +143,9 @@ typedef struct {
     double seconds;        /* wall time of the solve (setup excluded)         */
     int pinv_passes;       /* passes whose step came from the pinv fallback   */
     int spin_retries;      /* passes re-solved after a hand-off spin timeout  */
+    int nd_retries;        /* passes whose nested-dissection Cholesky met a
+                              non-positive pivot and the natural-order Cholesky
+                              (rocSOLVER dpotrf) took the step instead        */
 } vlgba_stats;
 
 /* One LM pass, for benchmarking / custom drivers. */
@@ -164,6 +168,9 @@ typedef struct vlgba_step_info {
                               again with the per-level launches (every rank
                               takes the same decision: the status words are
                               all-reduced with the pass scalars)              */
+    int nd_retry;          /* the nested-dissection order met a non-positive
+                              pivot; the natural-order dpotrf solved the pass
+                              (pinv = 0) or failed too (pinv = 1)             */
 } vlgba_step_info;
 
 typedef struct vlgba_ctx vlgba_ctx;
@@ -324,6 +331,11 @@ int vlgba_resect(const vlgba_resect_problem *prob, const vlgba_options *opt, dou
 /* Multi-GPU: rank 0 creates the 128-byte RCCL unique id, the caller
  * broadcasts it (e.g. torch.distributed) and passes it as opt->comm_id. */
 int vlgba_get_unique_id(void *id128);
+/* The library keeps RCCL communicators for the next context created with the
+ * same (id, world size, rank).  A caller that will not pass an id again
+ * releases it: the idle communicators made from it are destroyed (ones still
+ * held by a context are destroyed with it).  Returns the number destroyed. */
+int vlgba_comm_release(const void *id128);
 
 /* Diagnostics: the device sin / cos the rotation tables use (glibc's
  * algorithm, vlg_libm.h) for n host arguments -- the parity tests compare them

@@ -191,3 +191,24 @@ def test_triangulation_restatement():
     assert np.array_equal(X2[3] == 0.0, behind[pts])
     ok = X2[3] == 1.0
     assert np.allclose(X2[:3, ok], sc.X[:3, pts[ok]], rtol=1e-6, atol=1e-6)
+
+
+def test_triangulation_observation_order_fallback():
+    """a scene whose observations are not point-major takes
+    _triangulate's fallback selection; its rows are grouped by point there, so
+    the result equals the point-major scene's."""
+    import types
+
+    from bundleadjustmentmatlab_amd import incremental as inc
+    sc = make_config("cfg5", m=12, seed=3)
+    status = np.ones(sc.m, dtype=bool)
+    status[5] = False
+    pts = np.nonzero(np.bincount(sc.obs_pt, minlength=sc.n) >= 2)[0]
+    want = inc._triangulate(sc, sc.K, sc.T0, sc.w0, pts, status)
+    perm = np.random.default_rng(7).permutation(sc.num_obs)
+    shuffled = types.SimpleNamespace(n=sc.n, m=sc.m, obs_pt=sc.obs_pt[perm],
+                                     obs_cam=sc.obs_cam[perm], obs_x=sc.obs_x[perm])
+    assert inc._obs_of(shuffled, pts) is None          # the fallback path
+    got = inc._triangulate(shuffled, sc.K, sc.T0, sc.w0, pts, status)
+    assert np.array_equal(got[3], want[3])
+    assert np.allclose(got, want, rtol=1e-9, atol=1e-9)

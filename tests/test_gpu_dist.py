@@ -118,6 +118,18 @@ def test_rccl_one_rank_communicator():
             err, st = ba.run()
             a1, b1 = ba.get_params()
             out.append((np.array(err, copy=True), st.iterations, a1.copy(), b1.copy()))
+    # the caller forgets the id: its idle communicator is destroyed
+    # (one), a second release finds none, and a fresh id bootstraps again
+    L = pkg.lib()
+    assert L.vlgba_comm_release(uid) == 1
+    assert L.vlgba_comm_release(uid) == 0
+    uid2 = unique_id_bytes()
+    with pkg.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, 6, comm_id=uid2) as ba:
+        ba.set_params(a, b)
+        err, st = ba.run()
+        a1, b1 = ba.get_params()
+        out.append((np.array(err, copy=True), st.iterations, a1.copy(), b1.copy()))
+    assert L.vlgba_comm_release(uid2) == 1
     (e0, n0, a0, b0) = out[0]
     for e1, n1, a1, b1 in out[1:]:
         assert n0 == n1 and n0 > 2
