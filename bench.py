@@ -2,10 +2,14 @@
 """Benchmark: Euclidean LM iterations/s on the BASELINE.json workload.
 
 A "step" is one full Levenberg-Marquardt pass of bundle_euclid.m:120-249 on
-the GPU: rotations + linearisation (10 projections / observation, FD
-Jacobians) + U/V/W/eA/eB + damping / V*^-1 / Y + Schur complement + dense fp64
-MFMA Cholesky solve + back-substitution / update / new cost.  Every timed
-step relinearises (the accepted-step cost, the most expensive pass).
+the GPU: linearisation (10 projections / observation, FD Jacobians) +
+U/V/W/eA/eB + damping / V*^-1 / Y + Schur complement + fp64 MFMA reduced
+solve + back-substitution / update / new cost.  Every timed step linearises
+once (the accepted-step cost, the most expensive pass): on the default fast
+path the update kernel linearises at the new point in the same pass over the
+observations (k_update_linearize), so a step is camera
+reduction + Schur + solve + that fused update -- exactly the work of an
+accepted pass, whose linearisation the next pass starts from.
 
 Workload at N=1: config 3, 1000 cameras x 500k points x 3M observations
 (synthetic, seeded; BASELINE.json configs[2]).  With --gpus N the same scene
@@ -226,7 +230,10 @@ def main():
                  "csrc/ba_scene.hip)" if not args.host_scene and args.config in ("cfg2", "cfg3")
                  else "synthetic (seeded scene, SURVEY.md 8.d, numpy)"),
         "config": {"workload": f"{args.config}: {sc.m} cams x {sc.n} pts x {N} obs, "
-                               "fix_calibration (num_a=6), full LM pass per step",
+                               "fix_calibration (num_a=6), full LM pass per step, one "
+                               "linearisation per step" + (
+                                   " (fused into the update: k_update_linearize)"
+                                   if "k_update_linearize" in kms else ""),
                    "cameras": sc.m, "points": sc.n, "observations": N,
                    "parallelism": f"point-shard x{world}",
                    "collective": "rccl" if comm_id is not None else
@@ -416,8 +423,10 @@ def bench_incremental(args):
     print(json.dumps(out), flush=True)
 
 
-# timer name (vlgba_kernel_name) -> device kernel base name in rocprofv3 output
-PMC_ALIAS = {"k_linearize": "k_linearize_chunk", "k_camera_reduce": "k_camera_reduce_chunks"}
+# timer name (vlgba_kernel_name) -> device kernel name in the rocprofv3 output
+# (tools/kstats.py / pmc_traffic.py key the linearisation by its template flag)
+PMC_ALIAS = {"k_linearize": "k_linearize_chunk", "k_camera_reduce": "k_camera_reduce_chunks",
+             "k_update_linearize": "k_update_linearize"}
 
 
 def pmc_traffic(config, plan):
@@ -480,6 +489,14 @@ def kernel_roofline(name, tot_ms, calls, plan, n_passes):
                   plan["chunk_eslots"] * (8 * (NU + NA) + 4) + plan["chunks"] * 20)
         # 1 + NA + 3 projections per observation (~53 flop each) + 2(NA+3) FD divides
         flops = N * ((1 + NA + 3) * 53 + 2 * (NA + 3) * 2 + 3 * NA * 3)
+    elif name == "k_update_linearize":
+        # the point update (W rows of the pass read once, da rows, eB / V*^-1 / b
+        # in, db / b_new out) + the linearisation at (a_new, b_new) as above
+        # (b_new read back; the SSE partials are the pass's new SSE)
+        nbytes = (N * (4 + 16 + 2 + WS + WS) + n * (4 + 24 + 72 + 24) +
+                  n * (24 + 72 + 24 + 24 + 24) + m * 8 * NA +
+                  plan["chunk_eslots"] * (8 * (NU + NA) + 4) + plan["chunks"] * 28)
+        flops = N * ((1 + NA + 3) * 53 + 2 * (NA + 3) * 2 + 3 * NA * 3 + 3 * 6 * 2) + n * 30
     elif name == "k_camera_reduce":
         nbytes = plan["chunk_eslots"] * (8 * (NU + NA) + 4) + m * 8 * (NA * NA + NA)
     elif name in ("k_schur_group", "k_schur_mfma"):

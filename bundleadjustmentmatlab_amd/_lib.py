@@ -42,7 +42,7 @@ class VlgbaOptions(ctypes.Structure):
                 ("on_pass", ctypes.c_void_p), ("on_pass_user", ctypes.c_void_p)]
 
 
-NKERNELS = 17   # VLGBA_NKERNELS
+NKERNELS = 18   # VLGBA_NKERNELS
 
 # int (*allreduce)(double *buf, long long count, void *user)
 ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, c_dp, c_ll, ctypes.c_void_p)

@@ -35,7 +35,7 @@
 enum {
     KT_ROT, KT_LIN, KT_CAMRED, KT_DAMP, KT_SCHUR, KT_SCHUR_CHUNK, KT_SCHUR_RED,
     KT_ASSEMBLE, KT_FACTOR, KT_SYRK, KT_BACKWARD, KT_CAMUPD, KT_PTUPD, KT_CR_FACTOR,
-    KT_CR_UPDATE, KT_CR_BACK, KT_SCHUR_MF, KT_N
+    KT_CR_UPDATE, KT_CR_BACK, KT_SCHUR_MF, KT_LIN_UPD, KT_N
 };
 #define KT_MAX_EV 8192
 struct ba_ktimer {
@@ -210,6 +210,10 @@ struct ba_dev {
     double *epart;     // [nge][NA] per group e-slot
     double *upart;     // [nes][NA(NA+1)/2 + NA] per-chunk U_j (lower) | eA_j partials
     double *chsse;     // [3][nch] per-chunk partials: linearisation SSE, new SSE, point dpg
+    // fused update (fast path, ba_launch_update -> k_update_linearize): the
+    // next linearisation's buffers, swapped in by an accepted step
+    int fused;
+    double *W2, *V2, *eB2, *upart2, *chsse2;
     int ns, nes;
     int ch_max_terms, ch_max_slots;   // per-chunk maxima: LDS staging of the term lists
     long long nterm_fast;             // (obs, obs) Schur terms of the chunk plan
@@ -314,7 +318,7 @@ int ba_launch_camera_reduce(ba_dev *d, ba_flags f, int fuse = 0);
 int ba_launch_damp_point(ba_dev *d, double lambda);
 int ba_launch_schur(ba_dev *d, double lambda);
 int ba_launch_assemble(ba_dev *d);
-int ba_launch_update(ba_dev *d, double lambda);
+int ba_launch_update(ba_dev *d, double lambda, ba_flags f);
 int ba_launch_yeb(ba_dev *d);
 int ba_launch_publish(ba_dev *d);   // scal[0..5] + ++seq -> hres (host-mapped)
 void *ba_dmalloc(size_t bytes);   // per-device caching allocator (ba_solver.cpp)

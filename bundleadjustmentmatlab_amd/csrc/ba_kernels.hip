@@ -287,8 +287,26 @@ __global__ __launch_bounds__(256) void k_linearize(
 #define BA_LIN_W2_ON 1
 #endif
 
-template <int NA>
-__global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
+// UPD = true (k_update_linearize): the point update of the pass that just
+// solved (mex_bundle_3_db_new.c:99-146: db_i, b_new, the point part of
+// dp'(lambda dp + g)) runs first in the same workgroup, from the pass's W / eB
+// / V*^-1 (double-buffered: they stay valid for a rejected step), and the
+// chunk is then linearised at (a_new, b_new) into the other buffers -- whose
+// base projection IS the update's new projection (:149-166), so its SSE is
+// the pass's new SSE and, if the step is accepted, the next pass's old SSE
+// (bundle_euclid.m:139 of the next iteration recomputes exactly that, App. A
+// Q12).  One pass over the observations instead of two.
+struct ba_upd {
+    const double *W_old, *da, *eB_old, *Vinv, *b_old;
+    int ndb;
+    double lambda;
+    double *db, *b_new, *part_dpg;
+    const int *seg_long, *long_o0;
+    const double *dpg_long;
+};
+
+template <int NA, bool UPD>
+__device__ __forceinline__ void linearize_chunk_body(
     const int *__restrict__ ch_pt, const int *__restrict__ ch_obase,
     const int *__restrict__ ch_eslot, const int *__restrict__ eslot_optr,
     const unsigned short *__restrict__ eslot_obs, const int *__restrict__ pt_ptr,
@@ -298,13 +316,18 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
     const double *__restrict__ b, ba_flags f, const unsigned char *__restrict__ pivot,
     double *__restrict__ W, double *__restrict__ V, double *__restrict__ eB,
     double *__restrict__ upart, double *__restrict__ part_sse, int nch_reg,
-    const int *__restrict__ seg_pt, double *__restrict__ vseg)
+    const int *__restrict__ seg_pt, double *__restrict__ vseg, ba_upd u)
 {
     constexpr int NC0 = (NA + 4) / 2;       // lane 0: base + FD columns [0, NC0)
     constexpr int RS = 2 * NA + 8;          // LDS row: A (2 NA), B (6), e (2)
     constexpr int NU = NA * (NA + 1) / 2;
     static_assert(BA_CH_OBS + 1 <= 256 && BA_CH_PTS + 1 <= 256, "one metadata word per lane");
-    __shared__ __attribute__((aligned(16))) double rows[BA_CH_OBS * RS];
+    // UPD: the rows hold the chunk's old W rows, then t_o, before they take
+    // A, B, e (NA = 6: the same 20 KB, so 7 workgroups per CU still fit)
+    constexpr int LW = BA_CH_OBS * 3 * NA;
+    constexpr int NROWS = (UPD && LW > BA_CH_OBS * RS) ? LW : BA_CH_OBS * RS;
+    static_assert(NA != 6 || NROWS == BA_CH_OBS * RS, "fused update must not grow NA = 6 LDS");
+    __shared__ __attribute__((aligned(16))) double rows[NROWS];
     // pt_ptr[p0 + t] (t <= np) and eslot_optr[e0 + t] (t <= nes) as they are
     // in memory, written by LDS-DMA (no registers, no wait until the barrier)
     // from the waves whose lanes cover them
@@ -312,6 +335,11 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
     __shared__ int eoff_raw[64 * (BA_CH_OBS / 64 + 1)];
     __shared__ unsigned short eobl[BA_CH_OBS];
     __shared__ unsigned char wz[BA_CH_OBS]; // W_ij forced to zero (fix masks, :140-154)
+    // UPD: the point lanes' dp'(lambda dp + g) terms (wave 0), summed by
+    // thread 0 after the projections (a shuffle reduction here would keep its
+    // lane addresses live through the projections: spills)
+    __shared__ double dpl[UPD ? BA_CH_PTS : 1];
+    static_assert(BA_CH_PTS <= 64, "the point lanes are wave 0");
     const int ch = blockIdx.x, tid = threadIdx.x;
     // a segment chunk (ch >= nch_reg) holds part of one long track: its V / eB
     // sums are partials (vseg), added up per track by k_long_vsum
@@ -340,6 +368,96 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
     }
     int m_eobl = 0;
     STAMP(16);
+    if constexpr (UPD) {
+        // ---- the update (k_point_update_chunk's arithmetic, same order) ----
+        if (seg) {   // a long track's segment: db / b_new / dp'g by k_long_db
+            if (tid == 0)
+                dpl[0] = obase == u.long_o0[u.seg_long[ch - nch_reg]]
+                             ? __hip_atomic_load(u.dpg_long + u.seg_long[ch - nch_reg],
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : 0.0;
+        } else {
+            const int ne = nobs * 3 * NA;
+            const double *wsrc = u.W_old + (size_t)3 * NA * obase;
+            double dl[NA];
+            if (nobs > 0) {
+                if constexpr (NA == 6) {
+                    // the chunk's old W rows (one contiguous range, 144 B per
+                    // observation: 16-byte aligned) straight into LDS by LDS-DMA,
+                    // 1 KiB per wave-instruction, non-temporal (W's last reader):
+                    // no registers, in flight until the barrier below
+                    // (the 16-byte form exists for gfx950 only: the host pass of
+                    // the compiler would drop the kernel's launch stub over it)
+#if defined(__HIP_DEVICE_COMPILE__)
+                    const int nbytes = 8 * ne, ninst = (nbytes + 1023) >> 10;
+                    const char *src = reinterpret_cast<const char *>(wsrc);
+                    for (int q = tid >> 6; q < ninst; q += 4)
+                        __builtin_amdgcn_global_load_lds(
+                            src + min(q * 1024 + 16 * (tid & 63), nbytes - 16), &rows[128 * q],
+                            16, 0, 2);
+#endif
+                } else {
+                    constexpr int MAXE = (LW + 255) / 256;
+#pragma unroll
+                    for (int q = 0; q < MAXE; q++) {
+                        const int e = tid + 256 * q;
+                        if (e < ne) rows[e] = __builtin_nontemporal_load(wsrc + e);
+                    }
+                }
+                const double *dd = u.da + (size_t)NA * obs_cam[obase + min(tid, nobs - 1)];
+#pragma unroll
+                for (int k = 0; k < NA; k++) dl[k] = dd[k];
+#pragma unroll
+                for (int k = 0; k < NA; k++)
+                    if (k >= u.ndb) dl[k] = 0.0;
+            }
+            __syncthreads();
+            // t_o[r] = W_o(:, r)' da_j (mex_bundle_3_db_new.c:113-120), into the
+            // row's first slot (only this lane reads the row)
+            if (tid < nobs) {
+                double *wo = rows + 3 * NA * tid;
+#pragma unroll
+                for (int r = 0; r < 3; r++) {
+                    double *w = wo + NA * r;
+                    double t = w[0] * dl[0] + w[1] * dl[1] + w[2] * dl[2] + w[3] * dl[3] +
+                               w[4] * dl[4] + w[5] * dl[5];
+#pragma unroll
+                    for (int k = 6; k < NA; k++)   // nomex semantics only (ndb = NA)
+                        if (k < u.ndb) t = t + w[k] * dl[k];
+                    w[0] = t;
+                }
+            }
+            __syncthreads();
+            // rhs = eB_i - t_o1 - t_o2 - ... (cameras ascending), db_i = V*_i^-1 rhs,
+            // b_new, dp'(lambda dp + g) (:99-146, bundle_euclid.m:213-217); a
+            // point without observations gets db = V*^-1 eB (= 0) all the same
+            if (tid < np) {
+                const int i = p0 + tid;
+                double rhs[3] = {u.eB_old[3 * (size_t)i], u.eB_old[3 * (size_t)i + 1],
+                                 u.eB_old[3 * (size_t)i + 2]};
+                const int lo1 = lptr_raw[tid + 1] - obase;
+                for (int lo = lptr_raw[tid] - obase; lo < lo1; lo++) {
+#pragma unroll
+                    for (int r = 0; r < 3; r++) rhs[r] -= rows[3 * NA * lo + NA * r];
+                }
+                const double *vi = u.Vinv + 9 * (size_t)i;
+                double dpg = 0.0;
+#pragma unroll
+                for (int r = 0; r < 3; r++) {
+                    const double dbr = vi[r] * rhs[0] + vi[r + 3] * rhs[1] + vi[r + 6] * rhs[2];
+                    const double bnr = u.b_old[3 * (size_t)i + r] + dbr;
+                    u.db[3 * (size_t)i + r] = dbr;
+                    u.b_new[3 * (size_t)i + r] = bnr;
+                    dpg += dbr * (u.lambda * dbr + u.eB_old[3 * (size_t)i + r]);
+                }
+                dpl[tid] = dpg;
+            }
+        }
+        // (workgroup-scope release / acquire) the point lanes' b_new stores are
+        // visible to the projection lanes, which read b_new through u.b_new
+        // (not the __restrict__ b: the loads must stay after the barrier)
+        __syncthreads();
+    }
     double sse = 0.0;
     if (nobs > 0) {   // (nu > 0 too)
         m_eobl = __hip_atomic_load(eslot_obs + u0 + min(tid, nu - 1), __ATOMIC_RELAXED,
@@ -353,8 +471,9 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
         {
             const int o = obase + min(lo, nobs - 1);
             const int j = obs_cam[o], i = p0 + obs_lpt[o];
-            const double bi[3] = {b[3 * (size_t)i], b[3 * (size_t)i + 1],
-                                  b[3 * (size_t)i + 2]};
+            const double *bsrc = UPD ? u.b_new : b;
+            const double bi[3] = {bsrc[3 * (size_t)i], bsrc[3 * (size_t)i + 1],
+                                  bsrc[3 * (size_t)i + 2]};
             cam_view<NA> cv(a, K4, rot, j);
             double xh[2];
             cv.project(bi, xh);
@@ -389,6 +508,14 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
     if (tid < nu) eobl[tid] = (unsigned short)m_eobl;
     __syncthreads();
     STAMP(17);
+    if constexpr (UPD) {   // the chunk's point part of dp'(lambda dp + g), points in order
+        if (tid == 0) {
+            double acc = 0.0;
+            const int k1 = seg ? 1 : np;
+            for (int k = 0; k < k1; k++) acc += dpl[k];
+            u.part_dpg[ch] = acc;
+        }
+    }
     // W_ij = A^T B onto a zeroed output (:305-314): the chunk's W rows are one
     // contiguous HBM range, written lane by lane (coalesced), two entries
     // (rows r, r + 1 of one column) per lane
@@ -482,6 +609,39 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(
 #ifdef BA_STAMPS
     if (tid == 0) atomicAdd(&g_stamp[22], 1ull);
 #endif
+}
+
+#define BA_LIN_ARGS                                                                        \
+    const int *__restrict__ ch_pt, const int *__restrict__ ch_obase,                       \
+        const int *__restrict__ ch_eslot, const int *__restrict__ eslot_optr,              \
+        const unsigned short *__restrict__ eslot_obs, const int *__restrict__ pt_ptr,      \
+        const int *__restrict__ obs_cam, const unsigned char *__restrict__ obs_lpt,        \
+        const double *__restrict__ obs_x, const double *__restrict__ K4,                   \
+        const double *__restrict__ a, const double *__restrict__ rot,                      \
+        const double *__restrict__ b, ba_flags f, const unsigned char *__restrict__ pivot, \
+        double *__restrict__ W, double *__restrict__ V, double *__restrict__ eB,           \
+        double *__restrict__ upart, double *__restrict__ part_sse, int nch_reg,            \
+        const int *__restrict__ seg_pt, double *__restrict__ vseg
+#define BA_LIN_PASS                                                                        \
+    ch_pt, ch_obase, ch_eslot, eslot_optr, eslot_obs, pt_ptr, obs_cam, obs_lpt, obs_x, K4, a, \
+        rot, b, f, pivot, W, V, eB, upart, part_sse, nch_reg, seg_pt, vseg
+
+// the linearisation at the current parameters (after set_params, the ordered
+// and stage paths' fast twin)
+template <int NA>
+__global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(BA_LIN_ARGS)
+{
+    linearize_chunk_body<NA, false>(BA_LIN_PASS, ba_upd{});
+}
+
+// the fused update: the point update of the pass, then the linearisation at
+// (a_new, b_new) (a, rot, b = a_new, rot_new, b_new; W .. part_sse = the
+// second buffers)
+template <int NA>
+__global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_update_linearize(BA_LIN_ARGS,
+                                                                             ba_upd u)
+{
+    linearize_chunk_body<NA, true>(BA_LIN_PASS, u);
 }
 
 // U_j, eA_j from the per-chunk partials (fast path).  One 256-lane workgroup
@@ -2194,8 +2354,58 @@ int ba_launch_assemble(ba_dev *d)
     return 0;
 }
 
-int ba_launch_update(ba_dev *d, double lambda)
+// The fused update (d->fused, fast path): k_camera_update, the long tracks'
+// db, then ONE pass over the observations -- the point update and the
+// linearisation at (a_new, b_new) into the second buffers (k_linearize_chunk
+// with UPD: W2, V2, eB2, upart2, chsse2) -- and the pass's final sums: the new
+// SSE is the sum of the new linearisation's per-chunk SSE partials.  lm_apply
+// swaps the buffers when the step is accepted; a rejected step keeps the
+// pass's own linearisation (App. A Q12).
+static int launch_update_fused(ba_dev *d, double lambda, ba_flags f)
 {
+    const int gc = (d->m + 63) / 64;
+    KT_B(d);
+    const double lam_dpg = d->dpg_lambda ? lambda : 0.0;
+    BA_DISPATCH(d->na, (k_camera_update<NA><<<gc, 320, 0, d->stream>>>(
+                           d->a, d->da, d->eA, d->m, lam_dpg, d->a_new, d->rot_new,
+                           d->part)));
+    KT_E(d, KT_CAMUPD);
+    KT_B(d);
+    if (d->nl > 0)   // long tracks: db, b_new, dp'g over all their observations
+        BA_DISPATCH(d->na, (k_long_db<NA><<<d->nl, 256, 0, d->stream>>>(
+                               d->long_pt, d->long_o0, d->obs_cam, d->W, d->da, d->eB,
+                               d->Vinv, d->b, d->ndb, lambda, d->db, d->b_new,
+                               d->dpg_long)));
+    const ba_upd u{d->W, d->da, d->eB, d->Vinv, d->b, d->ndb, lambda, d->db, d->b_new,
+                   d->chsse2 + 2 * (size_t)d->nch, d->seg_long, d->long_o0, d->dpg_long};
+    BA_DISPATCH(d->na, (k_update_linearize<NA><<<d->nch, 256, 0, d->stream>>>(
+                           d->ch_pt, d->ch_obase, d->ch_eslot, d->eslot_optr, d->eslot_obs,
+                           d->pt_ptr, d->obs_cam, d->obs_lpt, d->obs_x, d->K4, d->a_new,
+                           d->rot_new, d->b_new, f, d->pivot, d->W2, d->V2, d->eB2, d->upart2,
+                           d->chsse2, d->nch_reg, d->seg_pt, d->vseg, u)));
+    if (d->nl > 0)   // long tracks: V2 / eB2 = sum of their segments' partials
+        k_long_vsum<<<d->nl, 64, 0, d->stream>>>(d->long_pt, d->long_seg0, d->vseg, d->V2,
+                                                 d->eB2);
+    KT_E(d, KT_LIN_UPD);
+    // new SSE (= the new linearisation's SSE), point dpg, camera dpg: one launch
+    ba_sum3 s3 = {{d->chsse2, d->chsse2 + 2 * (size_t)d->nch, d->part},
+                  {d->nch, d->nch, gc},
+                  {d->scal + 1, d->scal + 3, d->scal + 2},
+                  d->scal, nullptr, 0.0, d->pub_cnt};
+    if (d->publish_req) {
+        d->seq++;
+        s3.hres = d->hres_dev;
+        s3.seq = (double)d->seq;
+        d->publish_req = 0;
+        d->published = 1;
+    }
+    k_sum_parts3<<<3, 1024, 0, d->stream>>>(s3);
+    return -(int)hipGetLastError();
+}
+
+int ba_launch_update(ba_dev *d, double lambda, ba_flags f)
+{
+    if (d->fused) return launch_update_fused(d, lambda, f);
     const int gc = (d->m + 63) / 64;
     KT_B(d);
     // lambda dp'dp once over the ranks (each adds da' eA of its partial eA)

@@ -1078,6 +1078,8 @@ struct vlgba_ctx {
     double lambda = 1e-3, lambda0 = 1e-3, nu = 2.0;
     int model = VLGBA_MODEL_EUCLIDEAN;
     int lin_valid = 0;
+    int camred_due = 0;           // fused update: the linearisation swapped in by an
+                                  // accepted step still needs its camera reduction
     int timing = 0;
     hipEvent_t ev[8] = {};
     double phase_ms[7] = {};
@@ -1568,6 +1570,20 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
     VLGBA_CHECK(hipMemsetAsync(d.eB + 3 * (size_t)d.n, 0, sizeof(double) * 3, s));
     VLGBA_CHECK(hipMemsetAsync(d.Vinv + 9 * (size_t)d.n, 0, sizeof(double) * 9, s));
     TRY(ctx_alloc(c, &d.db, 3 * (size_t)d.n));
+    // fused update (fast path): the next linearisation's buffers (VLGBA_FUSED=0
+    // keeps the separate update and linearisation launches: A/B)
+    const char *fused_env = std::getenv("VLGBA_FUSED");   // read per context (tests)
+    const bool fused_on = !(fused_env && fused_env[0] == '0');
+    if (fast && d.nch > 0 && fused_on) {
+        TRY(ctx_alloc(c, &d.W2, (size_t)3 * na * (d.N + 1)));
+        VLGBA_CHECK(hipMemsetAsync(d.W2 + (size_t)3 * na * d.N, 0, sizeof(double) * 3 * na, s));
+        TRY(ctx_alloc(c, &d.V2, 9 * (size_t)d.n));
+        TRY(ctx_alloc(c, &d.eB2, 3 * (size_t)(d.n + 1)));
+        VLGBA_CHECK(hipMemsetAsync(d.eB2 + 3 * (size_t)d.n, 0, sizeof(double) * 3, s));
+        TRY(ctx_alloc(c, &d.upart2, (size_t)(na * (na + 1) / 2 + na) * d.nes));
+        TRY(ctx_alloc(c, &d.chsse2, 3 * (size_t)d.nch));
+        d.fused = 1;
+    }
     TRY(ctx_alloc(c, &d.blk_jk, 2 * (size_t)d.nb));
     TRY(ctx_alloc(c, &d.blk_ptr, (size_t)d.nb + 1));
     TRY(ctx_alloc(c, &d.term, 2 * (size_t)d.T));
@@ -1865,7 +1881,7 @@ static int resolve_nospin(vlgba_ctx *c, double lam, double hs[6])
     TRY(ba_chol_solve(&d, 1));
     d.publish_req = 0;
     d.published = 0;
-    TRY(ba_launch_update(&d, lam));
+    TRY(ba_launch_update(&d, lam, c->flags));
     if (d.parity) TRY(ba_launch_parity_new_sums(&d, lam));
     TRY(collect_scalars(c, false, hs));
     c->spin_retries++;
@@ -1986,7 +2002,7 @@ static int nd_natural_retry(vlgba_ctx *c, double lam, double hs[6])
                                d.stream));
     d.publish_req = 0;
     d.published = 0;
-    TRY(ba_launch_update(&d, lam));
+    TRY(ba_launch_update(&d, lam, c->flags));
     if (d.parity) TRY(ba_launch_parity_new_sums(&d, lam));
     TRY(collect_scalars(c, false, hs));
     c->nd_retries++;
@@ -2026,7 +2042,7 @@ static int pinv_fallback(vlgba_ctx *c, double lam, double hs[6])
     TRY(ba_pinv_apply(&d, c->pinv_S, c->pinv_ev, ld, d.rhs, c->pinv_w, d.da));
     d.publish_req = 0;
     d.published = 0;
-    TRY(ba_launch_update(&d, lam));
+    TRY(ba_launch_update(&d, lam, c->flags));
     if (d.parity) TRY(ba_launch_parity_new_sums(&d, lam));
     TRY(collect_scalars(c, false, hs));
     c->pinv_used++;
@@ -2044,10 +2060,16 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
     ba_dev &d = c->d;
     const double lam = c->lambda;
     mark(c, 0);
-    if (relinearize || !c->lin_valid) {
+    // fused update: every pass's update linearises at the new point (into the
+    // second buffers, swapped in on accept), so a pass linearises here only
+    // after set_params; relinearize then means the camera reduction of the
+    // current linearisation (the rest of stage 1), the work an accepted pass
+    // does
+    const bool full = !c->lin_valid || (relinearize && !d.fused);
+    if (full || (d.fused && (relinearize || c->camred_due))) {
         // the rotation table of d.a is current: set_params builds it and an
         // accepted step swaps in the one k_camera_update built for a_new
-        TRY(ba_launch_linearize(&d, c->flags));
+        if (full) TRY(ba_launch_linearize(&d, c->flags));
         mark(c, 1);
         if (!d.ordered && d.fuse_camred && d.ngrp_mf > 0) {
             // U / eA / old SSE: workgroups of this pass's MFMA Schur launch
@@ -2075,6 +2097,7 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
             VLGBA_CHECK(hipMemcpyAsync(d.eA + d.ld, d.scal + 0, sizeof(double),
                                        hipMemcpyDeviceToDevice, d.stream));
         c->lin_valid = 1;
+        c->camred_due = 0;
     } else {
         mark(c, 1);
     }
@@ -2098,7 +2121,7 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
     const bool spin = (c->world == 1 || c->comm) && !c->timing;
     d.publish_req = spin && !c->comm;   // the fast update's final-sums launch publishes
     d.published = 0;
-    TRY(ba_launch_update(&d, lam));
+    TRY(ba_launch_update(&d, lam, c->flags));
     d.publish_req = 0;
     if (d.parity) TRY(ba_launch_parity_new_sums(&d, lam));
     mark(c, 7);
@@ -2162,12 +2185,20 @@ static void lm_apply(vlgba_ctx *c, const vlgba_step_info *info)
         std::swap(d.a, d.a_new);
         std::swap(d.b, d.b_new);
         std::swap(d.rot, d.rot_new);   // rotation table of the new a
+        if (d.fused) {   // the update linearised at the new point: take it
+            std::swap(d.W, d.W2);
+            std::swap(d.V, d.V2);
+            std::swap(d.eB, d.eB2);
+            std::swap(d.upart, d.upart2);
+            std::swap(d.chsse, d.chsse2);
+        }
         if (proj)
             c->lambda = c->lambda / 10;
         else
             c->lambda = c->lambda * std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * info->rho - 1.0, 3));
         c->nu = 2.0;
-        c->lin_valid = 0;
+        c->lin_valid = d.fused ? 1 : 0;
+        c->camred_due = d.fused ? 1 : 0;
     } else if (proj) {
         c->lambda = c->lambda * 10;
     } else {
@@ -2369,13 +2400,21 @@ int vlgba_get_linearization(vlgba_ctx *c, double *U, double *eA, double *V, doub
     if (!c) return VLGBA_E_ARG;
     TRY(ctx_enter(c));
     ba_dev &d = c->d;
-    TRY(ba_launch_rotations(&d, d.a, d.rot, 1));
-    TRY(ba_launch_linearize(&d, c->flags));
-    TRY(ba_launch_camera_reduce(&d, c->flags));
-    if (d.ordered)
-        VLGBA_CHECK(hipMemcpyAsync(d.eA + d.ld, d.scal + 0, sizeof(double),
-                                   hipMemcpyDeviceToDevice, d.stream));
+    // the linearisation the context holds for the current parameters (a
+    // rejected step's, or the one the fused update made at an accepted step's
+    // new point), else a new one
+    if (!c->lin_valid) {
+        TRY(ba_launch_rotations(&d, d.a, d.rot, 1));
+        TRY(ba_launch_linearize(&d, c->flags));
+    }
+    if (!c->lin_valid || c->camred_due) {
+        TRY(ba_launch_camera_reduce(&d, c->flags));
+        if (d.ordered)
+            VLGBA_CHECK(hipMemcpyAsync(d.eA + d.ld, d.scal + 0, sizeof(double),
+                                       hipMemcpyDeviceToDevice, d.stream));
+    }
     c->lin_valid = 1;
+    c->camred_due = 0;
     // U / eA stay per-rank partials on the device (schur_owner); the caller
     // gets their sum over ranks
     const size_t nue = (size_t)d.na * d.na * d.m + d.ld + 1;
@@ -2421,9 +2460,10 @@ int vlgba_get_reduced_system(vlgba_ctx *c, int *blk_jk, double *blocks, double *
     if (!c) return VLGBA_E_ARG;
     TRY(ctx_enter(c));
     ba_dev &d = c->d;
-    if (!c->lin_valid) {   // stage 1 at the current parameters (as a pass would)
-        TRY(ba_launch_linearize(&d, c->flags));
+    if (!c->lin_valid || c->camred_due) {   // stage 1 at the current parameters (as a
+        if (!c->lin_valid) TRY(ba_launch_linearize(&d, c->flags));   // pass would)
         TRY(ba_launch_camera_reduce(&d, c->flags));
+        c->camred_due = 0;
         if (d.ordered)
             VLGBA_CHECK(hipMemcpyAsync(d.eA + d.ld, d.scal + 0, sizeof(double),
                                        hipMemcpyDeviceToDevice, d.stream));
@@ -2494,7 +2534,7 @@ const char *vlgba_kernel_name(int k)
         "k_rotations", "k_linearize", "k_camera_reduce", "k_damp_point", "k_schur",
         "k_schur_group", "k_schur_reduce", "k_assemble", "k_factor_step", "k_syrk",
         "k_backward", "k_camera_update", "k_point_update", "k_cr_factor", "k_cr_update",
-        "k_cr_back", "k_schur_mfma"};
+        "k_cr_back", "k_schur_mfma", "k_update_linearize"};
     return (k >= 0 && k < KT_N) ? names[k] : "";
 }
 
@@ -2803,7 +2843,7 @@ static int mex3_impl(int model, int m, int n, int num_a, const double *W, const 
         if ((rc = upload(d.a, a, (size_t)d.ld, d.stream))) break;
         if ((rc = upload(d.b, b, 3 * (size_t)n, d.stream))) break;
         VLGBA_CHECK(hipMemsetAsync(d.eA, 0, sizeof(double) * d.ld, d.stream));
-        if ((rc = ba_launch_update(&d, 0.0))) break;
+        if ((rc = ba_launch_update(&d, 0.0, ba_flags{}))) break;
         if ((rc = download(db, d.db, 3 * (size_t)n, d.stream))) break;
         if ((rc = download(a_new, d.a_new, (size_t)d.ld, d.stream))) break;
         if ((rc = download(b_new, d.b_new, 3 * (size_t)n, d.stream))) break;

@@ -30,7 +30,8 @@ extern "C" {
 /* ABI of this header.  Bumped whenever a public struct, constant or entry
  * point changes: 1 = the round-1/2 layouts; 2 = vlgba_stats.pinv_passes /
  * spin_retries, vlgba_step_info.spin_retry, VLGBA_NPLAN 28; 3 =
- * vlgba_stats.nd_retries, vlgba_step_info.nd_retry, vlgba_comm_release.  Callers check it
+ * vlgba_stats.nd_retries, vlgba_step_info.nd_retry, vlgba_comm_release,
+ * VLGBA_NKERNELS 18 (k_update_linearize).  Callers check it
  * once at load time with VLGBA_ABI_CHECK() (the MEX gateways and the Python
  * loader do): the library compares the version and the struct sizes the
  * caller was compiled with against its own and returns 0 or VLGBA_E_ABI. */
@@ -193,7 +194,9 @@ int vlgba_get_params(vlgba_ctx *ctx, double *a, double *b);
  * update_lm != 0 applies the accept/reject rule (:218-241) to the context. */
 int vlgba_step(vlgba_ctx *ctx, int relinearize, int update_lm, vlgba_step_info *info);
 /* stage 1 at the current parameters (mex_bundle_1_XABeUVWeAeB.c outputs, the
- * reduced forms of bundle_euclid.m:139-154): U (num_a x num_a x m), eA
+ * reduced forms of bundle_euclid.m:139-154) -- the one the context holds when
+ * it is current (after a rejected step, or the fast path's fused update after
+ * an accepted one), else computed: U (num_a x num_a x m), eA
  * (num_a x m) summed over all ranks; V (3 x 3 x n_local), eB (3 x n_local) and
  * W (num_a x 3 per observation, observations point-major: points ascending,
  * cameras ascending within a point) for this rank's points.  Any pointer may
@@ -228,7 +231,7 @@ int vlgba_phase_ms(vlgba_ctx *ctx, double *ms7);
 /* per-kernel device time accumulated over the passes run with timing on
  * (HIP events around every launch): ms[k], calls[k] for k < VLGBA_NKERNELS,
  * named by vlgba_kernel_name(k); reset = 1 clears the accumulators. */
-#define VLGBA_NKERNELS 17
+#define VLGBA_NKERNELS 18
 int vlgba_kernel_ms(vlgba_ctx *ctx, double *ms, long long *calls, int reset);
 const char *vlgba_kernel_name(int k);
 /* execution-plan sizes of this rank (roofline accounting in bench.py):
