@@ -361,11 +361,35 @@ def bench_incremental(args):
                 f"(solve time so far {sum(s['seconds'] for s in solves):.1f} s)")
     for _ in range(args.warmup):
         incremental_bundle(sc, devices=devices, progress=progress)
+    # the CPU baseline's sample: every k-th BA call of the last timed replay
+    # (its inputs by reference -- the replay builds them fresh per call -- and
+    # the wall time of the GPU call), re-solved on the host afterwards
+    import bundleadjustmentmatlab_amd.incremental as inc
+    ncalls = 2 * (sc.m - 2)
+    k_every = max(1, -(-ncalls // 48))
+    sample, spy_on = [], [False]
+    orig = inc.bundle_euclid_obs
+
+    def spy(K, T, w, X, pt, cam, ox, *opts, **kw):
+        t1 = time.perf_counter()
+        out = orig(K, T, w, X, pt, cam, ox, *opts, **kw)
+        if spy_on[0] and spy.count % k_every == 0:
+            sample.append(dict(K=K, T=T, w=w, X=X, pt=pt, cam=cam, ox=ox, opts=opts,
+                               gpu_s=time.perf_counter() - t1, passes=out[-1].iterations))
+        spy.count += 1
+        return out
+    spy.count = 0
+    inc.bundle_euclid_obs = spy
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     res = None
-    for _ in range(args.steps):
-        res = incremental_bundle(sc, devices=devices, progress=progress)
+    try:
+        for q in range(args.steps):
+            spy_on[0] = q == args.steps - 1
+            spy.count = 0
+            res = incremental_bundle(sc, devices=devices, progress=progress)
+    finally:
+        inc.bundle_euclid_obs = orig
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     sol = res["solves"]
@@ -419,8 +443,110 @@ def bench_incremental(args):
                             ("; every solve of this scene is below it, so the elastic "
                              "count is 1 throughout" if max(q["observations"] for q in sol)
                              < 2 * OBS_PER_SHARD else "")},
+        "cpu_baseline": None if args.no_cpu_baseline else replay_cpu_baseline(sample, k_every,
+                                                                              ncalls),
     }
+    out["roofline"] = replay_roofline(sc, devices, dt / args.steps)
     print(json.dumps(out), flush=True)
+
+
+def replay_roofline(sc, devices, replay_s):
+    """Where the device time of a growing replay goes: one more replay (after
+    the timed ones) with every context timing its kernels (VLGBA_KTIME_ALL=1:
+    HIP events around each launch, summed over the destroyed contexts by
+    vlgba_kernel_ms(NULL)); device_busy_frac = the summed kernel time over the
+    timed replay's wall time; the dominant kernel against its roof -- a solve
+    kernel against the fp64 matrix peak with the library's own count of the
+    solve's algorithmic flops (vlgba_kernel_flops), the others as busy time
+    only (their bytes vary per solve)."""
+    import ctypes
+    from bundleadjustmentmatlab_amd._lib import NKERNELS, lib
+    from bundleadjustmentmatlab_amd.incremental import incremental_bundle
+    L = lib()
+    ms = np.zeros(NKERNELS)
+    calls = (ctypes.c_longlong * NKERNELS)()
+    fl = np.zeros(NKERNELS)
+    dp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))   # noqa: E731
+    L.vlgba_kernel_ms(None, dp(ms), calls, 1)
+    os.environ["VLGBA_KTIME_ALL"] = "1"
+    try:
+        t0 = time.perf_counter()
+        incremental_bundle(sc, devices=devices)
+        t_timed = time.perf_counter() - t0
+    finally:
+        del os.environ["VLGBA_KTIME_ALL"]
+    L.vlgba_kernel_ms(None, dp(ms), calls, 0)
+    L.vlgba_kernel_flops(None, dp(fl))
+    names = [L.vlgba_kernel_name(k).decode() for k in range(NKERNELS)]
+    busy = float(ms.sum()) * 1e-3
+    dom = int(np.argmax(ms))
+    per = {names[k]: {"ms": float(ms[k]), "launches": int(calls[k])}
+           for k in np.argsort(-ms) if calls[k] > 0}
+    out = {"device_busy_s": busy, "replay_s": replay_s,
+           "device_busy_frac": busy / replay_s,
+           "timing_replay_s": t_timed, "kernel": names[dom], "kernels": per}
+    if fl[dom] > 0:
+        tfs = fl[dom] / (ms[dom] * 1e-3) / 1e12
+        out.update(bound="mfma", achieved=tfs, peak=PEAK_F64_TFLOPS, unit="TFLOP/s",
+                   frac=tfs / PEAK_F64_TFLOPS, traffic=None,
+                   per_launch=f"{fl[dom] / max(1, calls[dom]):.4g} flop")
+    # every solve kernel's rate (the replay's reduced solves are its MFMA work)
+    out["solve_kernels"] = {names[k]: {"achieved_tflops": fl[k] / (ms[k] * 1e-3) / 1e12,
+                                       "frac": fl[k] / (ms[k] * 1e-3) / 1e12 / PEAK_F64_TFLOPS}
+                            for k in range(NKERNELS) if fl[k] > 0 and ms[k] > 0}
+    log(f"[bench] replay device time {busy:.2f} s of {replay_s:.2f} s "
+        f"({100 * busy / replay_s:.0f} %), dominant {names[dom]} {ms[dom] * 1e-3:.2f} s")
+    return out
+
+
+def replay_cpu_baseline(sample, k_every, ncalls):
+    """The growing replay's BA solves on the host (SURVEY.md 8.d ref_sparse_mt;
+    the reference's own timing point is test_incremental.m:42-44's tic / toc
+    around the growing reconstruction): every k-th call of the timed replay
+    re-solved from its own inputs by oracle/cpu_port.py SparsePort.lm -- the
+    OpenMP C port of the MEX stages with the reference's MATLAB semantics
+    (pinv V*_i, pinv(S) e_ as LAPACK's banded Cholesky), the same LM rule and
+    stop -- against the GPU's wall time for the same calls (context wait,
+    upload, LM loop, download).  Bounded: the sample is at most 48 calls."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cpu_port
+    if not sample:
+        return None
+    cpu_port.band_cholesky_solve(np.eye(12) * 2.0, np.ones(12))   # first-call costs
+    t_cpu, passes, worst = 0.0, 0, 0.0
+    # in a fixed shuffled order until ~30 s of CPU work (a spread subset of the
+    # sample when the large solves are slow); the GPU side is summed over the
+    # same calls
+    order = np.random.default_rng(0).permutation(len(sample))
+    done = []
+    for q in order:
+        if t_cpu > 30.0:
+            break
+        c = sample[q]
+        done.append(c)
+        assert c["opts"] == ("fix_calibration",), c["opts"]
+        t1 = time.perf_counter()
+        port = cpu_port.SparsePort(c["K"].shape[1], c["X"].shape[1], c["pt"], c["cam"], c["ox"],
+                                   c["K"])
+        e, _, _, info = port.lm(np.vstack([c["w"], c["T"]]), np.asfortranarray(c["X"][:3]),
+                                vinv="pinv", solve="band", check_pinv=0)
+        t_cpu += time.perf_counter() - t1
+        passes += info["passes"]
+        worst = max(worst, 6 * c["K"].shape[1])
+    t_gpu = sum(c["gpu_s"] for c in done)
+    info = cpu_port.host_info()
+    n = len(done)
+    log(f"[bench] cpu replay sample: {n} solves, CPU {t_cpu:.2f} s, GPU {t_gpu:.3f} s "
+        f"(x{t_cpu / t_gpu:.1f}) {info}")
+    return {"value": n / t_cpu, "unit": "BA solves/s", "cores": info["omp_threads"],
+            "kind": "port",
+            "sample": f"{n} of every-{k_every}th of the replay's {ncalls} BA calls ({n} solves, "
+                      f"{passes} LM passes, reduced systems up to {worst} rows) re-solved "
+                      f"from their own inputs: OpenMP C port of the MEX stages "
+                      f"({info['omp_threads']} threads), pinv V*_i, LAPACK banded Cholesky "
+                      f"of S; port construction included",
+            "seconds": t_cpu, "gpu_same_calls_s": t_gpu, "gpu_same_calls_solves_per_s": n / t_gpu,
+            "host": info}
 
 
 # timer name (vlgba_kernel_name) -> device kernel name in the rocprofv3 output

@@ -102,6 +102,7 @@ SIGNATURES = {
     "vlgba_phase_ms": (c_int, [ctypes.c_void_p, c_dp]),
     "vlgba_kernel_ms": (c_int, [ctypes.c_void_p, c_dp, ctypes.POINTER(c_ll), c_int]),
     "vlgba_kernel_name": (ctypes.c_char_p, [c_int]),
+    "vlgba_kernel_flops": (c_int, [ctypes.c_void_p, c_dp]),
     "vlgba_plan_info": (c_int, [ctypes.c_void_p, ctypes.POINTER(c_ll), c_int]),
     "vlgba_mex_bundle_1": (c_int, [c_int, c_int, c_int] + [c_dp] * 14),
     "vlgba_mex_bundle_2": (c_int, [c_int, c_int, c_int] + [c_dp] * 7),

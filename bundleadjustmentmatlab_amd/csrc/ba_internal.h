@@ -41,10 +41,13 @@ enum {
 struct ba_ktimer {
     int on;
     int nev;
+    int ncreated;      // events created so far (on first use: a context that times
+                       // few launches creates few)
     hipEvent_t ev[KT_MAX_EV];
     int kid[KT_MAX_EV / 2];
     double ms[KT_N];
     long long calls[KT_N];
+    double flops[KT_N];   // the reduced solve's algorithmic flops of the timed passes
 };
 void kt_begin(struct ba_ktimer *t, hipStream_t s);
 void kt_end(struct ba_ktimer *t, hipStream_t s, int kid);

@@ -322,10 +322,12 @@ __device__ __forceinline__ void linearize_chunk_body(
     constexpr int RS = 2 * NA + 8;          // LDS row: A (2 NA), B (6), e (2)
     constexpr int NU = NA * (NA + 1) / 2;
     static_assert(BA_CH_OBS + 1 <= 256 && BA_CH_PTS + 1 <= 256, "one metadata word per lane");
-    // UPD: the rows hold the chunk's old W rows, then t_o, before they take
-    // A, B, e (NA = 6: the same 20 KB, so 7 workgroups per CU still fit)
+    // UPD: the rows hold the chunk's old W rows, then t_o, with the new points
+    // b_new after them (LW), before they take A, B, e (NA = 6: the same 20 KB,
+    // so 7 workgroups per CU still fit)
     constexpr int LW = BA_CH_OBS * 3 * NA;
-    constexpr int NROWS = (UPD && LW > BA_CH_OBS * RS) ? LW : BA_CH_OBS * RS;
+    constexpr int NROWS = (UPD && LW + 3 * BA_CH_PTS > BA_CH_OBS * RS) ? LW + 3 * BA_CH_PTS
+                                                                        : BA_CH_OBS * RS;
     static_assert(NA != 6 || NROWS == BA_CH_OBS * RS, "fused update must not grow NA = 6 LDS");
     __shared__ __attribute__((aligned(16))) double rows[NROWS];
     // pt_ptr[p0 + t] (t <= np) and eslot_optr[e0 + t] (t <= nes) as they are
@@ -368,6 +370,7 @@ __device__ __forceinline__ void linearize_chunk_body(
     }
     int m_eobl = 0;
     STAMP(16);
+    double bu[3] = {0.0, 0.0, 0.0};   // UPD: this lane's point at b_new
     if constexpr (UPD) {
         // ---- the update (k_point_update_chunk's arithmetic, same order) ----
         if (seg) {   // a long track's segment: db / b_new / dp'g by k_long_db
@@ -380,6 +383,15 @@ __device__ __forceinline__ void linearize_chunk_body(
             const int ne = nobs * 3 * NA;
             const double *wsrc = u.W_old + (size_t)3 * NA * obase;
             double dl[NA];
+            // the point lanes' operands (eB, V*^-1, b): in flight with the W rows
+            const int ip = np > 0 ? p0 + min(tid, np - 1) : 0;
+            double pe[3], pv[9], pb[3];
+#pragma unroll
+            for (int r = 0; r < 3; r++) pe[r] = u.eB_old[3 * (size_t)ip + r];
+#pragma unroll
+            for (int r = 0; r < 9; r++) pv[r] = u.Vinv[9 * (size_t)ip + r];
+#pragma unroll
+            for (int r = 0; r < 3; r++) pb[r] = u.b_old[3 * (size_t)ip + r];
             if (nobs > 0) {
                 if constexpr (NA == 6) {
                     // the chunk's old W rows (one contiguous range, 144 B per
@@ -433,30 +445,39 @@ __device__ __forceinline__ void linearize_chunk_body(
             // point without observations gets db = V*^-1 eB (= 0) all the same
             if (tid < np) {
                 const int i = p0 + tid;
-                double rhs[3] = {u.eB_old[3 * (size_t)i], u.eB_old[3 * (size_t)i + 1],
-                                 u.eB_old[3 * (size_t)i + 2]};
+                double rhs[3] = {pe[0], pe[1], pe[2]};
                 const int lo1 = lptr_raw[tid + 1] - obase;
                 for (int lo = lptr_raw[tid] - obase; lo < lo1; lo++) {
 #pragma unroll
                     for (int r = 0; r < 3; r++) rhs[r] -= rows[3 * NA * lo + NA * r];
                 }
-                const double *vi = u.Vinv + 9 * (size_t)i;
                 double dpg = 0.0;
 #pragma unroll
                 for (int r = 0; r < 3; r++) {
-                    const double dbr = vi[r] * rhs[0] + vi[r + 3] * rhs[1] + vi[r + 6] * rhs[2];
-                    const double bnr = u.b_old[3 * (size_t)i + r] + dbr;
+                    const double dbr = pv[r] * rhs[0] + pv[r + 3] * rhs[1] + pv[r + 6] * rhs[2];
+                    const double bnr = pb[r] + dbr;
                     u.db[3 * (size_t)i + r] = dbr;
                     u.b_new[3 * (size_t)i + r] = bnr;
-                    dpg += dbr * (u.lambda * dbr + u.eB_old[3 * (size_t)i + r]);
+                    rows[LW + 3 * tid + r] = bnr;   // (after every t_o read: barrier B)
+                    dpg += dbr * (u.lambda * dbr + pe[r]);
                 }
                 dpl[tid] = dpg;
             }
         }
-        // (workgroup-scope release / acquire) the point lanes' b_new stores are
-        // visible to the projection lanes, which read b_new through u.b_new
-        // (not the __restrict__ b: the loads must stay after the barrier)
         __syncthreads();
+        // every lane takes its observation's b_new from LDS (a long track's
+        // segment: from k_long_db's b_new) before the projections overwrite the
+        // rows
+        if (!seg && nobs > 0) {
+            const int lp = obs_lpt[obase + min(min(tid >> 1, BA_CH_OBS - 1), nobs - 1)];
+#pragma unroll
+            for (int c = 0; c < 3; c++) bu[c] = rows[LW + 3 * lp + c];
+        } else if (nobs > 0) {
+#pragma unroll
+            for (int c = 0; c < 3; c++) bu[c] = b[3 * (size_t)p0 + c];
+        }
+        __syncthreads();
+        STAMP(23);
     }
     double sse = 0.0;
     if (nobs > 0) {   // (nu > 0 too)
@@ -471,9 +492,9 @@ __device__ __forceinline__ void linearize_chunk_body(
         {
             const int o = obase + min(lo, nobs - 1);
             const int j = obs_cam[o], i = p0 + obs_lpt[o];
-            const double *bsrc = UPD ? u.b_new : b;
-            const double bi[3] = {bsrc[3 * (size_t)i], bsrc[3 * (size_t)i + 1],
-                                  bsrc[3 * (size_t)i + 2]};
+            double bi[3];
+#pragma unroll
+            for (int c = 0; c < 3; c++) bi[c] = UPD ? bu[c] : b[3 * (size_t)i + c];
             cam_view<NA> cv(a, K4, rot, j);
             double xh[2];
             cv.project(bi, xh);

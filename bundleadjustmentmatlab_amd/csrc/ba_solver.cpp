@@ -1042,12 +1042,16 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
 void kt_begin(ba_ktimer *t, hipStream_t s)
 {
     if (t->nev + 2 > KT_MAX_EV) return;
+    while (t->ncreated < t->nev + 2) {
+        if (hipEventCreate(&t->ev[t->ncreated]) != hipSuccess) return;   // (kt_end skips too)
+        t->ncreated++;
+    }
     (void)hipEventRecord(t->ev[t->nev], s);
 }
 
 void kt_end(ba_ktimer *t, hipStream_t s, int kid)
 {
-    if (t->nev + 2 > KT_MAX_EV) return;
+    if (t->nev + 2 > KT_MAX_EV || t->nev + 2 > t->ncreated) return;
     (void)hipEventRecord(t->ev[t->nev + 1], s);
     t->kid[t->nev / 2] = kid;
     t->nev += 2;
@@ -1212,6 +1216,8 @@ static void comm_release(ncclComm_t comm)
     ncclCommDestroy(comm);   // its id was released while this context held it
 }
 
+static void kt_retire(const ba_ktimer *kt);
+
 static void ctx_free(vlgba_ctx *c)
 {
     if (!c) return;
@@ -1224,7 +1230,8 @@ static void ctx_free(vlgba_ctx *c)
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->d.kt) {
-        for (auto &e : c->d.kt->ev) (void)hipEventDestroy(e);
+        kt_retire(c->d.kt);
+        for (int q = 0; q < c->d.kt->ncreated; q++) (void)hipEventDestroy(c->d.kt->ev[q]);
         delete c->d.kt;
     }
     ba_chol_free(&c->d);
@@ -1784,6 +1791,10 @@ static int ctx_create(const vlgba_problem *p, const vlgba_options *o, vlgba_ctx 
             rc = upload(c->d.pivot, o->pivot, (size_t)p->m, c->d.stream);
             if (rc) break;
         }
+        if (std::getenv("VLGBA_KTIME_ALL")) {   // every context times its passes
+            rc = vlgba_set_timing(c, 1);
+            if (rc) break;
+        }
         if (pt_ptr_out) *pt_ptr_out = pt_ptr_all;
         if (h_out) *h_out = std::move(h);
     } while (0);
@@ -2161,7 +2172,16 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
             kt->ms[kt->kid[q / 2]] += ms;
             kt->calls[kt->kid[q / 2]]++;
         }
-        if (kt) kt->nev = 0;
+        if (kt) {
+            kt->nev = 0;
+            // the solve's algorithmic flops (ba_chol_setup's count) on the timers
+            // that ran them: one-launch / per-level CR, or the envelope's steps,
+            // separator SYRK and backward solve
+            const bool cr = d.cr_nlev > 0;
+            kt->flops[cr ? KT_CR_FACTOR : KT_FACTOR] += d.fl_factor;
+            kt->flops[KT_SYRK] += d.fl_syrk;
+            kt->flops[cr ? KT_CR_BACK : KT_BACKWARD] += d.fl_back;
+        }
     }
     info->old_sse = hs[0];
     info->new_sse = hs[1];
@@ -2507,24 +2527,66 @@ int vlgba_set_timing(vlgba_ctx *c, int on)
     if (on && !c->d.kt) {
         c->d.kt = new (std::nothrow) ba_ktimer();
         if (!c->d.kt) return VLGBA_E_NOMEM;
-        for (auto &e : c->d.kt->ev) VLGBA_CHECK(hipEventCreate(&e));
     }
     c->timing = on;
     if (c->d.kt) c->d.kt->on = on;
     return 0;
 }
 
+// kernel times of the contexts destroyed with timing on (VLGBA_KTIME_ALL=1:
+// every context times its passes -- the growing replay's device-busy split)
+static std::mutex g_kt_mu;
+static double g_kt_ms[KT_N], g_kt_flops[KT_N];
+static long long g_kt_calls[KT_N];
+
+static void kt_retire(const ba_ktimer *kt)
+{
+    std::lock_guard<std::mutex> lk(g_kt_mu);
+    for (int k = 0; k < KT_N; k++) {
+        g_kt_ms[k] += kt->ms[k];
+        g_kt_calls[k] += kt->calls[k];
+        g_kt_flops[k] += kt->flops[k];
+    }
+}
+
 int vlgba_kernel_ms(vlgba_ctx *c, double *ms, long long *calls, int reset)
 {
-    if (!c || !c->d.kt) return VLGBA_E_ARG;
+    if (!c) {   // process-wide: the destroyed contexts' timers
+        std::lock_guard<std::mutex> lk(g_kt_mu);
+        for (int k = 0; k < KT_N; k++) {
+            if (ms) ms[k] = g_kt_ms[k];
+            if (calls) calls[k] = g_kt_calls[k];
+            if (reset) {
+                g_kt_ms[k] = 0.0;
+                g_kt_calls[k] = 0;
+                g_kt_flops[k] = 0.0;
+            }
+        }
+        return 0;
+    }
+    if (!c->d.kt) return VLGBA_E_ARG;
     for (int k = 0; k < KT_N; k++) {
         if (ms) ms[k] = c->d.kt->ms[k];
         if (calls) calls[k] = c->d.kt->calls[k];
         if (reset) {
             c->d.kt->ms[k] = 0.0;
             c->d.kt->calls[k] = 0;
+            c->d.kt->flops[k] = 0.0;
         }
     }
+    return 0;
+}
+
+int vlgba_kernel_flops(vlgba_ctx *c, double *flops)
+{
+    if (!flops) return VLGBA_E_ARG;
+    if (!c) {
+        std::lock_guard<std::mutex> lk(g_kt_mu);
+        for (int k = 0; k < KT_N; k++) flops[k] = g_kt_flops[k];
+        return 0;
+    }
+    if (!c->d.kt) return VLGBA_E_ARG;
+    for (int k = 0; k < KT_N; k++) flops[k] = c->d.kt->flops[k];
     return 0;
 }
 

@@ -31,7 +31,7 @@ extern "C" {
  * point changes: 1 = the round-1/2 layouts; 2 = vlgba_stats.pinv_passes /
  * spin_retries, vlgba_step_info.spin_retry, VLGBA_NPLAN 28; 3 =
  * vlgba_stats.nd_retries, vlgba_step_info.nd_retry, vlgba_comm_release,
- * VLGBA_NKERNELS 18 (k_update_linearize).  Callers check it
+ * VLGBA_NKERNELS 18 (k_update_linearize), vlgba_kernel_flops.  Callers check it
  * once at load time with VLGBA_ABI_CHECK() (the MEX gateways and the Python
  * loader do): the library compares the version and the struct sizes the
  * caller was compiled with against its own and returns 0 or VLGBA_E_ABI. */
@@ -230,9 +230,17 @@ int vlgba_set_timing(vlgba_ctx *ctx, int on);
 int vlgba_phase_ms(vlgba_ctx *ctx, double *ms7);
 /* per-kernel device time accumulated over the passes run with timing on
  * (HIP events around every launch): ms[k], calls[k] for k < VLGBA_NKERNELS,
- * named by vlgba_kernel_name(k); reset = 1 clears the accumulators. */
+ * named by vlgba_kernel_name(k); reset = 1 clears the accumulators.  ctx NULL:
+ * the process-wide sums of the contexts destroyed with timing on (environment
+ * VLGBA_KTIME_ALL=1 switches timing on at every vlgba_create: the growing
+ * replay's device-busy time). */
 #define VLGBA_NKERNELS 18
 int vlgba_kernel_ms(vlgba_ctx *ctx, double *ms, long long *calls, int reset);
+/* the reduced solve's algorithmic flops (vlgba_plan_info [25..27]) of the timed
+ * passes, on the timer that ran them (k_cr_factor / k_factor_step, k_syrk,
+ * k_cr_back / k_backward); ctx NULL: process-wide as vlgba_kernel_ms.  Cleared
+ * by vlgba_kernel_ms(.., reset = 1). */
+int vlgba_kernel_flops(vlgba_ctx *ctx, double *flops);
 const char *vlgba_kernel_name(int k);
 /* execution-plan sizes of this rank (roofline accounting in bench.py):
  * [0] observations [1] points [2] cameras [3] num_a [4] Schur chunks

@@ -61,12 +61,15 @@ def main():
         life_us = v[11] / wgs / 100.0
         print(f"  s_memtime clock {ghz:.2f} GHz; mean workgroup lifetime {life_us:.1f} us; "
               f"sum of lifetimes {v[11] / 100.0:.0f} us")
-    lin = ["prologue", "projections", "W", "V/eB", "U/eA partials", "sse reduce"]
-    tot = sum(v[16:22])
-    print(f"k_linearize_chunk: {v[22]:.0f} workgroups per pass")
-    for i, name in enumerate(lin):
-        print(f"  {name:14s} {v[16 + i] / 1e6:9.2f} Mcycles  {100 * v[16 + i] / max(tot, 1):5.1f}%  "
-              f"{v[16 + i] / max(v[22], 1):9.0f} cycles/workgroup")
+    # the linearisation body (k_linearize_chunk, or the fused k_update_linearize:
+    # its update phase is stamp 23, between the prologue and the projections)
+    lin = [(16, "prologue"), (23, "update (fused)"), (17, "projections"), (18, "W"),
+           (19, "V/eB"), (20, "U/eA partials"), (21, "sse reduce")]
+    tot = sum(v[i] for i, _ in lin)
+    print(f"linearisation body: {v[22]:.0f} workgroups per pass")
+    for i, name in lin:
+        print(f"  {name:14s} {v[i] / 1e6:9.2f} Mcycles  {100 * v[i] / max(tot, 1):5.1f}%  "
+              f"{v[i] / max(v[22], 1):9.0f} cycles/workgroup")
     ba.close()
 
 
