@@ -654,30 +654,42 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
     std::vector<chunk_out> co(nthr);
     parallel_ranges(nchk, nthr, [&](int t, int c0, int c1) {
         chunk_out &o = co[t];
-        std::vector<int> slot_of(nb, -1), eslot_of(m, -1), tpos, epos;
+        // per chunk: its cameras' local ids (e-slots, by first touch) and a
+        // local nes x nes table of slot ids -- one global block lookup per
+        // camera pair of the chunk instead of two per (obs, obs) term (the
+        // m x m table does not stay in cache at ~1000 cameras); slots are
+        // still numbered by first touch in (point, a, b) order
+        std::vector<int> eslot_of(m, -1), tpos, epos, le, lslot;
         for (int c = c0; c < c1; c++) {
-            const int p = cbeg[c], q = cend[c], obase = lptr[p];
+            const int p = cbeg[c], q = cend[c], obase = lptr[p], nob = lptr[q] - obase;
             const bool mf = cmf[c] != 0;
             const size_t s0 = o.blk.size(), e0 = o.cam.size();
+            le.resize(nob);
+            for (int a = obase; a < obase + nob; a++) {
+                const int j = lcam[a];
+                if (eslot_of[j] < 0) {
+                    eslot_of[j] = (int)(o.cam.size() - e0);
+                    o.cam.push_back(j);
+                    o.ecnt.push_back(0);
+                }
+                o.ecnt[e0 + eslot_of[j]]++;
+                le[a - obase] = eslot_of[j];
+            }
+            const int nce = (int)(o.cam.size() - e0);
+            lslot.assign((size_t)nce * nce, -1);
             for (int i = p; i < q; i++)
                 for (int a = lptr[i]; a < lptr[i + 1]; a++) {
-                    const int j = lcam[a];
-                    if (eslot_of[j] < 0) {
-                        eslot_of[j] = (int)(o.cam.size() - e0);
-                        o.cam.push_back(j);
-                        o.ecnt.push_back(0);
-                    }
-                    o.ecnt[e0 + eslot_of[j]]++;
+                    const int j = lcam[a], ea = le[a - obase];
                     for (int b = lptr[i]; b < lptr[i + 1]; b++) {
                         const int k = lcam[b];
                         if (j < k) continue;
-                        const int blk = hb.find(j, k);
-                        if (slot_of[blk] < 0) {
-                            slot_of[blk] = (int)(o.blk.size() - s0);
-                            o.blk.push_back(blk);
+                        int &sl = lslot[(size_t)ea * nce + le[b - obase]];
+                        if (sl < 0) {
+                            sl = (int)(o.blk.size() - s0);
+                            o.blk.push_back(hb.find(j, k));
                             o.tcnt.push_back(0);
                         }
-                        o.tcnt[s0 + slot_of[blk]]++;
+                        o.tcnt[s0 + sl]++;
                     }
                 }
             const int ns = (int)(o.blk.size() - s0), nes = (int)(o.cam.size() - e0);
@@ -695,18 +707,16 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
             o.eobs.resize(ub + epos[nes]);
             for (int i = p; i < q; i++)
                 for (int a = lptr[i]; a < lptr[i + 1]; a++) {
-                    const int j = lcam[a];
-                    o.eobs[ub + epos[eslot_of[j]]++] = (unsigned short)(a - obase);
+                    const int j = lcam[a], ea = le[a - obase];
+                    o.eobs[ub + epos[ea]++] = (unsigned short)(a - obase);
                     if (mf) continue;
                     for (int b = lptr[i]; b < lptr[i + 1]; b++) {
-                        const int k = lcam[b];
-                        if (j < k) continue;
-                        const size_t at = tb + tpos[slot_of[hb.find(j, k)]]++;
+                        if (j < lcam[b]) continue;
+                        const size_t at = tb + tpos[lslot[(size_t)ea * nce + le[b - obase]]]++;
                         o.term[2 * at] = (unsigned short)(a - obase);
                         o.term[2 * at + 1] = (unsigned short)(b - obase);
                     }
                 }
-            for (size_t sl = s0; sl < o.blk.size(); sl++) slot_of[o.blk[sl]] = -1;
             for (size_t e = e0; e < o.cam.size(); e++) eslot_of[o.cam[e]] = -1;
         }
     }, &cwork);
