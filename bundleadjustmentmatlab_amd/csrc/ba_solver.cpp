@@ -228,6 +228,18 @@ struct host_blocks {
     bool dense_tab = true;
     std::vector<int> tab;                                // m*m block ids (dense)
     std::vector<std::vector<std::pair<int, int>>> rows;  // sparse fallback: (k, id)
+    // empty, keeping the vectors' capacity (a context per growing-replay solve:
+    // reused storage is not page-faulted in again, ctx_setup's per-thread pool)
+    void reset()
+    {
+        jk.clear();
+        ptr.clear();
+        term.clear();
+        m = 0;
+        dense_tab = true;
+        tab.clear();
+        rows.clear();
+    }
     int find(int j, int k) const
     {
         if (dense_tab) return tab[(size_t)j * m + k];
@@ -393,6 +405,23 @@ struct host_plan {
     std::vector<int> ch_blob, ch_obase;            // [nch+1]
     int max_blob = 0;      // term chunks: largest record
     int mf_max_blob = 0;   // MFMA groups: largest group record block (staged in LDS)
+    // empty, keeping every vector's capacity (host_blocks::reset)
+    void reset()
+    {
+        for (std::vector<int> *v :
+             {&ch_pt, &ch_slot, &ch_eslot, &slot_blk, &slot_tptr, &eslot_optr, &blk_sptr,
+              &blk_slots, &cam_eptr, &cam_eslots, &grp_ch, &grp_gs, &grp_ge, &gslot_blk, &gecam,
+              &blk_gptr, &blk_gslots, &cam_gptr, &cam_gslots, &seg_pt, &seg_long, &long_pt,
+              &long_o0, &long_seg0, &long_ebase, &cam_lptr, &cam_lobs, &cam_ltrk, &ch_blob,
+              &ch_obase})
+            v->clear();
+        for (std::vector<unsigned short> *v : {&slot_term, &eslot_obs, &cs_g, &ce_g}) v->clear();
+        blob.clear();
+        max_terms = max_slots = 0;
+        n_terms = 0;
+        grp_max_s = grp_max_e = mf_max_s = mf_max_e = nch_mf = ngrp_mf = 0;
+        nch_reg = nseg = max_lcam = max_blob = mf_max_blob = 0;
+    }
 };
 
 static int plan_threads(long long work, long long min_work);
@@ -640,9 +669,17 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
     // per-term lists (term chunks only: the MFMA records are dense) and the
     // per-camera observation lists, grouped by slot / e-slot in that order
     const int nchk = (int)cbeg.size();
-    struct chunk_out {
+    // (cache-line aligned: every push_back writes a vector header, and the
+    // headers of neighbouring threads' outputs must not share a line)
+    struct alignas(128) chunk_out {
         std::vector<int> blk, tcnt, cam, ecnt, ns, nes;
         std::vector<unsigned short> term, eobs;
+        void clear()
+        {
+            for (std::vector<int> *v : {&blk, &tcnt, &cam, &ecnt, &ns, &nes}) v->clear();
+            term.clear();
+            eobs.clear();
+        }
     };
     std::vector<long long> cwork(nchk + 1, 0);   // per chunk: its terms and observations
     for (int c = 0; c < nchk; c++) {
@@ -651,8 +688,33 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
         cwork[c + 1] = cwork[c] + w;
     }
     const int nthr = plan_threads(cwork[nchk], 20000);
-    std::vector<chunk_out> co(nthr);
+    // the per-thread outputs live in the calling thread's scratch (capacity kept
+    // from one context to the next: no page faults on the replay's plans)
+    // (a reference: the pool threads' lambda must reach THIS thread's scratch,
+    // not their own thread_local instance)
+    static thread_local std::vector<chunk_out> co_tl;
+    std::vector<chunk_out> &co = co_tl;
+    if ((int)co.size() < nthr) co.resize(nthr);
+    for (chunk_out &o : co) o.clear();
+#ifdef BA_PLAN_TIMING
+    std::vector<double> thr_ms(nthr, 0.0), thr_start(nthr, 0.0);
+    PLAN_T("chunks prep");
+    const auto tpr0 = std::chrono::steady_clock::now();
+#endif
     parallel_ranges(nchk, nthr, [&](int t, int c0, int c1) {
+#ifdef BA_PLAN_TIMING
+        const auto tt0 = std::chrono::steady_clock::now();
+        thr_start[t] = std::chrono::duration<double, std::milli>(tt0 - tpr0).count();
+        struct tdone {
+            std::chrono::steady_clock::time_point t0;
+            double *out;
+            ~tdone()
+            {
+                *out = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() -
+                                                                 t0).count();
+            }
+        } tdone_{tt0, &thr_ms[t]};
+#endif
         chunk_out &o = co[t];
         // per chunk: its cameras' local ids (e-slots, by first touch) and a
         // local nes x nes table of slot ids -- one global block lookup per
@@ -720,6 +782,11 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
             for (size_t e = e0; e < o.cam.size(); e++) eslot_of[o.cam[e]] = -1;
         }
     }, &cwork);
+#ifdef BA_PLAN_TIMING
+    std::fprintf(stderr, "   (chunk threads:");
+    for (int q = 0; q < nthr; q++) std::fprintf(stderr, " %.2f+%.2f", thr_start[q], thr_ms[q]);
+    std::fprintf(stderr, " ms)\n");
+#endif
     PLAN_T("chunks");
     // concatenate in chunk order
     P.max_slots = 0;
@@ -759,7 +826,6 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
             if (cmf[c]) P.nch_mf++;
         }
     }
-    co.clear();
     PLAN_T("concat");
     // long tracks: segment chunks (one point each, <= BA_CH_OBS observations;
     // every observation its own camera slot: a point sees a camera once)
@@ -1449,8 +1515,13 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
     }
     bool fast = !d.ordered && !stage_mode;
     int p_long = d.n;
-    host_blocks hb;
-    host_plan plan;
+    // the host plan in this thread's scratch: its storage is kept from one
+    // context to the next (the growing replay creates one per solve on its two
+    // prefetch workers)
+    static thread_local host_blocks hb;
+    static thread_local host_plan plan;
+    hb.reset();
+    plan.reset();
     ST_MARK("lists");
     plan_host(p->m, na, d.n, lptr, lcam, pt_ptr_all, h.cam, c->p0, c->p1, o0, lower_blocks,
               all_diag, d.no_mfma != 0, fast, p_long, hb, plan);

@@ -113,6 +113,11 @@ def test_converged_cost_within_1e6(gpu, oracle, kind, opts):
     line = [f"{kind}: GPU final {e_g:.10f}, oracle final {e_r:.10f} ({(e_g - e_r) / e_r:+.2e})"]
     if kind == "cfg1":
         assert abs(e_g - e_r) <= 1e-6 * e_r, (got[4], ref[4])
+    # the direct difference on every scene, with the bar the reference's own
+    # sensitivity sets: its final cost moves by up to 1.2e-4 when
+    # lambda0 moves by one part in 1e9 on these models
+    # (profiles/r05d_converged_bias.json; test_gpu_converged_bias.py)
+    assert abs(e_g - e_r) <= 1e-4 * e_r, (got[4], ref[4])
     for who, start, e_start in (("GPU's", got, e_g), ("oracle's", ref, e_r)):
         g = gpu.bundle_euclid(*start[:4], x, "visibility", vis, *opts, **kw)[4]
         r = oracle.bundle_euclid_ref(*start[:4], x, "visibility", vis, *opts, **ref_kw)[4]

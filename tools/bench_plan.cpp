@@ -32,11 +32,15 @@ double ms_since(std::chrono::steady_clock::time_point t)
 int main(int argc, char **argv)
 {
     if (argc < 2) {
-        std::fprintf(stderr, "usage: bench_plan problem.bin [reps]\n");
+        std::fprintf(stderr, "usage: bench_plan problem.bin [reps [problem2.bin ...]]\n");
         return 2;
     }
     const int reps = argc > 2 ? std::atoi(argv[2]) : 3;
-    FILE *f = std::fopen(argv[1], "rb");
+    // further problem files: planned one after another in this process (the
+    // per-thread plan storage reused across different problems, as in a replay)
+    for (int fi = 1; fi < argc; fi = (fi == 1 ? 3 : fi + 1)) {
+    if (fi >= argc) break;
+    FILE *f = std::fopen(argv[fi], "rb");
     if (!f) return 2;
     int hdr[3];
     if (std::fread(hdr, sizeof(int), 3, f) != 3) return 2;
@@ -73,8 +77,11 @@ int main(int argc, char **argv)
         auto t2 = std::chrono::steady_clock::now();
         bool fast = true;
         int p_long = n;
-        host_blocks hb;
-        host_plan P;
+        // the plan storage as ctx_setup keeps it: per thread, reset per context
+        static host_blocks hb;
+        static host_plan P;
+        hb.reset();
+        P.reset();
         plan_host(m, na, n, lptr, lcam, pt_ptr_all, h.cam, 0, n, 0, true, true, false, fast,
                   p_long, hb, P);
         const double t_plan = ms_since(t2);
@@ -121,6 +128,7 @@ int main(int argc, char **argv)
                     "(blocks %d, chunks %zu, groups %zu, blob %zu, fast %d)  hash %016llx\n",
                     m, n, N, t_sort, t_order, t_plan, (int)hb.jk.size() / 2, P.ch_pt.size() - 1,
                     P.grp_ch.size() - 1, P.blob.size(), fast ? 1 : 0, H.h);
+    }
     }
     return 0;
 }
