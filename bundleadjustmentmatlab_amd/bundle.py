@@ -442,11 +442,17 @@ def _adjuster_fingerprint(K, m, n, obs_pt, obs_cam, obs_x, o, num_vis, semantics
     """What a prebuilt adjuster was made for: sizes, the parsed
     options, K and a hash of the observation list -- a context built for
     another subset or other options with the same counts must not be used."""
-    import hashlib
-    h = hashlib.blake2b(digest_size=16)
+    # xxh3 (~25x blake2b's speed; the growing replay fingerprints every solve's
+    # observations twice, at build and at use), over the arrays' own buffers
+    try:
+        import xxhash
+        h = xxhash.xxh3_128()
+    except ImportError:
+        import hashlib
+        h = hashlib.blake2b(digest_size=16)
     for arr, dt in ((obs_pt, np.int32), (obs_cam, np.int32), (obs_x, np.float64),
                     (K, np.float64)):
-        h.update(np.ascontiguousarray(arr, dtype=dt).tobytes())
+        h.update(memoryview(np.ascontiguousarray(arr, dtype=dt)).cast("B"))
     piv = o["pivot"] if o["fix_pivot"] else None
     if piv is not None:
         h.update(np.asarray(piv, dtype=bool).tobytes())

@@ -88,6 +88,10 @@ struct ba_camred {
     double *sse_out, *sse_out2;
 };
 
+// the operand window of the linearisation's division-free quotients
+// (dehom_fast, ba_kernels.hip): biased exponents 723 + [0, BA_EWIN]
+#define BA_EWIN 600u
+
 struct ba_dev {
     int m, n, na, N, js;
     int device, ncu;   // HIP device ordinal and its CU count
@@ -213,6 +217,9 @@ struct ba_dev {
     double *epart;     // [nge][NA] per group e-slot
     double *upart;     // [nes][NA(NA+1)/2 + NA] per-chunk U_j (lower) | eA_j partials
     double *chsse;     // [3][nch] per-chunk partials: linearisation SSE, new SSE, point dpg
+    int *redo;         // [2 + nch] count, chunks to linearise again with '/' (k_linearize_redo)
+    int fast_dehom;    // NA = 6: division-free projection quotients (VLGBA_FAST_DEHOM=1: on)
+    unsigned ewin;     // their operand window (BA_EWIN; 0 under VLGBA_DEBUG_REDO=1)
     // fused update (fast path, ba_launch_update -> k_update_linearize): the
     // next linearisation's buffers, swapped in by an accepted step
     int fused;

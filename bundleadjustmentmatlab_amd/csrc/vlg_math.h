@@ -117,16 +117,23 @@ VLG_HD void vlg_rot_b(const double R[9], const double b[3], double S[3])
     S[2] = R[2] * b[0] + R[5] * b[1] + R[8] * b[2];
 }
 
-VLG_HD void vlg_project_s(const double Kc[9], const double S[3], const double t[3], double x[2])
+/* the homogeneous image point Kc * (S + t) before the division */
+VLG_HD void vlg_project_h(const double Kc[9], const double S[3], const double t[3], double xn[3])
 {
     double Rb0 = S[0] + t[0];
     double Rb1 = S[1] + t[1];
     double Rb2 = S[2] + t[2];
-    double x0 = Kc[0] * Rb0 + Kc[3] * Rb1 + Kc[6] * Rb2;
-    double x1 = Kc[1] * Rb0 + Kc[4] * Rb1 + Kc[7] * Rb2;
-    double x2 = Kc[2] * Rb0 + Kc[5] * Rb1 + Kc[8] * Rb2;
-    x[0] = x0 / x2;
-    x[1] = x1 / x2;
+    xn[0] = Kc[0] * Rb0 + Kc[3] * Rb1 + Kc[6] * Rb2;
+    xn[1] = Kc[1] * Rb0 + Kc[4] * Rb1 + Kc[7] * Rb2;
+    xn[2] = Kc[2] * Rb0 + Kc[5] * Rb1 + Kc[8] * Rb2;
+}
+
+VLG_HD void vlg_project_s(const double Kc[9], const double S[3], const double t[3], double x[2])
+{
+    double xn[3];
+    vlg_project_h(Kc, S, t, xn);
+    x[0] = xn[0] / xn[2];
+    x[1] = xn[1] / xn[2];
 }
 
 VLG_HD void vlg_project(const double Kc[9], const double R[9], const double t[3],

@@ -31,11 +31,12 @@ extern "C" {
  * point changes: 1 = the round-1/2 layouts; 2 = vlgba_stats.pinv_passes /
  * spin_retries, vlgba_step_info.spin_retry, VLGBA_NPLAN 28; 3 =
  * vlgba_stats.nd_retries, vlgba_step_info.nd_retry, vlgba_comm_release,
- * VLGBA_NKERNELS 18 (k_update_linearize), vlgba_kernel_flops.  Callers check it
+ * VLGBA_NKERNELS 18 (k_update_linearize), vlgba_kernel_flops; 4 =
+ * vlgba_debug_dehom.  Callers check it
  * once at load time with VLGBA_ABI_CHECK() (the MEX gateways and the Python
  * loader do): the library compares the version and the struct sizes the
  * caller was compiled with against its own and returns 0 or VLGBA_E_ABI. */
-#define VLGBA_ABI_VERSION 3
+#define VLGBA_ABI_VERSION 4
 
 /* camera models (vlgba_problem.model) */
 #define VLGBA_MODEL_EUCLIDEAN 0   /* bundle_euclid.m: a = [w; T; (K)], num_a 6/7/10     */
@@ -352,6 +353,13 @@ int vlgba_comm_release(const void *id128);
  * algorithm, vlg_libm.h) for n host arguments -- the parity tests compare them
  * with the host libm bit for bit.  |x| < 105414350. */
 int vlgba_debug_sincos(const double *x, double *s, double *c, long long n);
+/* Diagnostics: the linearisation's division-free quotients on n host triples
+ * xn [3 * n]: fast [4 * n] = (x0 / x2, x1 / x2) by the shared reciprocal and
+ * (x0 / 1e-10, x1 / 1e-10) as the FD quotient forms them; ref [4 * n] the same
+ * four by IEEE division; win [n]: bit 0 where x0, x1, x2 are inside the window
+ * the shared-reciprocal quotients claim bit-identity for, bit 1 where x0 and
+ * x1 are finite and inside the FD quotient's window. */
+int vlgba_debug_dehom(const double *xn, double *fast, double *ref, int *win, long long n);
 /* the pinv fallback of the reduced solve (rocSOLVER dsyevd + the pinv kernels)
  * on a host ld x ld symmetric S (lower triangle read) and e_: da = pinv(S) e_
  * with MATLAB's tolerance ld * eps(max |eigenvalue|). */
