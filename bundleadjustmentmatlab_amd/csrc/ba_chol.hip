@@ -2329,6 +2329,9 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
                 w[nw++] = fw(L - 1, k, 4);
             }
         }
+        // (Tried in round 5: own D_k waited for alone and its loads issued
+        // before the neighbours' wait -- 81 -> 86 us: the second poll-and-
+        // barrier costs more than the overlapped loads save.)
         cr32_wait_flags(flag, nw, w, epoch, status);
         CR_ST(1);
         // the survivor's r_k: the neighbours' y and its own r_k of level L-1

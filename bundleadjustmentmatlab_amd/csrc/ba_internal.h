@@ -234,6 +234,7 @@ struct ba_dev {
     int grp_max_s, grp_max_e;         // LDS accumulator sizes (largest non-direct group)
     unsigned *blob;                   // per-chunk metadata records (see build_plan)
     int *ch_blob, *ch_obase;          // [nch+1] record offsets (words), first local obs
+    int *ch_cam;                      // [2 nch] lowest / highest camera of a chunk's obs
     unsigned char *obs_lpt;           // [N] chunk-local point of each observation
     int max_blob;                     // term groups: largest chunk record
     int ngrp_mf;                      // leading MFMA groups
@@ -300,6 +301,7 @@ struct ba_dev {
 #define BA_GACC 4096       // max doubles of LDS block accumulators per Schur group
 #define BA_GE_CAP 128      // cameras per Schur group
 #define BA_GROUPS 2048     // target number of Schur groups (workgroups)
+#define BA_MF_GROUPS 768   // MFMA Schur groups: one round of 3 workgroups x 256 CUs
 #define BA_GROUP_CH 64     // max chunks per Schur group
 // MFMA Schur path (k_schur_mfma): a chunk is 4 K-blocks of 5 points (one per
 // wave), its cameras span NA * cameras <= 16 * BA_MF_RT slab columns

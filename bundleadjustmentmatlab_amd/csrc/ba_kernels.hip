@@ -443,8 +443,8 @@ __device__ __forceinline__ void linearize_chunk_body(
     const double *__restrict__ b, ba_flags f, const unsigned char *__restrict__ pivot,
     double *__restrict__ W, double *__restrict__ V, double *__restrict__ eB,
     double *__restrict__ upart, double *__restrict__ part_sse, int nch_reg,
-    const int *__restrict__ seg_pt, double *__restrict__ vseg, ba_upd u, int ch,
-    int *__restrict__ redo, unsigned ewin)
+    const int *__restrict__ seg_pt, double *__restrict__ vseg, const int *__restrict__ ch_cam,
+    ba_upd u, int ch, int *__restrict__ redo, unsigned ewin)
 {
     constexpr int NC0 = (NA + 4) / 2;       // lane 0: base + FD columns [0, NC0)
     constexpr int RS = 2 * NA + 8;          // LDS row: A (2 NA), B (6), e (2)
@@ -515,15 +515,24 @@ __device__ __forceinline__ void linearize_chunk_body(
             const int ne = nobs * 3 * NA;
             const double *wsrc = u.W_old + (size_t)3 * NA * obase;
             double dl[NA];
-            // the point lanes' operands (eB, V*^-1, b): in flight with the W rows
-            const int ip = np > 0 ? p0 + min(tid, np - 1) : 0;
-            double pe[3], pv[9], pb[3];
-#pragma unroll
-            for (int r = 0; r < 3; r++) pe[r] = u.eB_old[3 * (size_t)ip + r];
-#pragma unroll
-            for (int r = 0; r < 9; r++) pv[r] = u.Vinv[9 * (size_t)ip + r];
-#pragma unroll
-            for (int r = 0; r < 3; r++) pb[r] = u.b_old[3 * (size_t)ip + r];
+            const int ocam = nobs > 0 ? obs_cam[obase + min(tid, nobs - 1)] : 0;
+            // the da rows of the chunk's cameras (a narrow range: consecutive
+            // points see neighbouring cameras) by LDS-DMA into the row area's
+            // tail, beside the W rows: the lanes index them with their camera
+            // after the barrier, so no load waits on another.  A wider range
+            // loads each lane's da row from its camera index (dependent).
+            const int clo = ch_cam[2 * ch], span = ch_cam[2 * ch + 1] - clo + 1;
+            const bool dstage = NA == 6 && span * NA <= NROWS - LW;
+            if (dstage && nobs > 0) {
+#if defined(__HIP_DEVICE_COMPILE__)
+                const int nb = 8 * NA * span;
+                if ((tid >> 6) < ((nb + 1023) >> 10))
+                    __builtin_amdgcn_global_load_lds(
+                        reinterpret_cast<const char *>(u.da + (size_t)NA * clo) +
+                            min((tid >> 6) * 1024 + 16 * (tid & 63), nb - 16),
+                        &rows[LW + 128 * (tid >> 6)], 16, 0, 0);
+#endif
+            }
             if (nobs > 0) {
                 if constexpr (NA == 6) {
                     // the chunk's old W rows (one contiguous range, 144 B per
@@ -548,18 +557,33 @@ __device__ __forceinline__ void linearize_chunk_body(
                         if (e < ne) rows[e] = __builtin_nontemporal_load(wsrc + e);
                     }
                 }
-                const double *dd = u.da + (size_t)NA * obs_cam[obase + min(tid, nobs - 1)];
+                if (!dstage) {
+                    const double *dd = u.da + (size_t)NA * ocam;
 #pragma unroll
-                for (int k = 0; k < NA; k++) dl[k] = dd[k];
-#pragma unroll
-                for (int k = 0; k < NA; k++)
-                    if (k >= u.ndb) dl[k] = 0.0;
+                    for (int k = 0; k < NA; k++) dl[k] = dd[k];
+                }
             }
+            // the point lanes' operands (eB, V*^-1, b): in flight through t_o
+            const int ip = np > 0 ? p0 + min(tid, np - 1) : 0;
+            double pe[3], pv[9], pb[3];
+#pragma unroll
+            for (int r = 0; r < 3; r++) pe[r] = u.eB_old[3 * (size_t)ip + r];
+#pragma unroll
+            for (int r = 0; r < 9; r++) pv[r] = u.Vinv[9 * (size_t)ip + r];
+#pragma unroll
+            for (int r = 0; r < 3; r++) pb[r] = u.b_old[3 * (size_t)ip + r];
             __syncthreads();
             // t_o[r] = W_o(:, r)' da_j (mex_bundle_3_db_new.c:113-120), into the
             // row's first slot (only this lane reads the row)
             if (tid < nobs) {
                 double *wo = rows + 3 * NA * tid;
+                if (dstage) {
+#pragma unroll
+                    for (int k = 0; k < NA; k++) dl[k] = rows[LW + NA * (ocam - clo) + k];
+                }
+#pragma unroll
+                for (int k = 0; k < NA; k++)   // da(1:ndb) only (mex_bundle_3 :113-120)
+                    if (k >= u.ndb) dl[k] = 0.0;
 #pragma unroll
                 for (int r = 0; r < 3; r++) {
                     double *w = wo + NA * r;
@@ -791,10 +815,11 @@ __device__ __forceinline__ void linearize_chunk_body(
         const double *__restrict__ b, ba_flags f, const unsigned char *__restrict__ pivot, \
         double *__restrict__ W, double *__restrict__ V, double *__restrict__ eB,           \
         double *__restrict__ upart, double *__restrict__ part_sse, int nch_reg,            \
-        const int *__restrict__ seg_pt, double *__restrict__ vseg
+        const int *__restrict__ seg_pt, double *__restrict__ vseg,                         \
+        const int *__restrict__ ch_cam
 #define BA_LIN_PASS                                                                        \
     ch_pt, ch_obase, ch_eslot, eslot_optr, eslot_obs, pt_ptr, obs_cam, obs_lpt, obs_x, K4, a, \
-        rot, b, f, pivot, W, V, eB, upart, part_sse, nch_reg, seg_pt, vseg
+        rot, b, f, pivot, W, V, eB, upart, part_sse, nch_reg, seg_pt, vseg, ch_cam
 
 // the linearisation at the current parameters (after set_params, the ordered
 // and stage paths' fast twin)
@@ -2350,17 +2375,17 @@ static void lin_chunk_launch(ba_dev *d, ba_flags f, const double *a, const doubl
         k_update_linearize<NA, FAST><<<d->nch, 256, 0, d->stream>>>(
             d->ch_pt, d->ch_obase, d->ch_eslot, d->eslot_optr, d->eslot_obs, d->pt_ptr,
             d->obs_cam, d->obs_lpt, d->obs_x, d->K4, a, rot, b, f, d->pivot, W, V, eB, upart,
-            chsse, d->nch_reg, d->seg_pt, d->vseg, *u, d->redo, d->ewin);
+            chsse, d->nch_reg, d->seg_pt, d->vseg, d->ch_cam, *u, d->redo, d->ewin);
     else
         k_linearize_chunk<NA, FAST><<<d->nch, 256, 0, d->stream>>>(
             d->ch_pt, d->ch_obase, d->ch_eslot, d->eslot_optr, d->eslot_obs, d->pt_ptr,
             d->obs_cam, d->obs_lpt, d->obs_x, d->K4, a, rot, b, f, d->pivot, W, V, eB, upart,
-            chsse, d->nch_reg, d->seg_pt, d->vseg, d->redo, d->ewin);
+            chsse, d->nch_reg, d->seg_pt, d->vseg, d->ch_cam, d->redo, d->ewin);
     if (FAST)
         k_linearize_redo<NA><<<1, 256, 0, d->stream>>>(
             d->ch_pt, d->ch_obase, d->ch_eslot, d->eslot_optr, d->eslot_obs, d->pt_ptr,
             d->obs_cam, d->obs_lpt, d->obs_x, d->K4, a, rot, b, f, d->pivot, W, V, eB, upart,
-            chsse, d->nch_reg, d->seg_pt, d->vseg, d->redo, d->nch);
+            chsse, d->nch_reg, d->seg_pt, d->vseg, d->ch_cam, d->redo, d->nch);
 }
 
 int ba_launch_linearize(ba_dev *d, ba_flags f)

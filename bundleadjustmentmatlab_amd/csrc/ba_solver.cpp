@@ -17,6 +17,7 @@
 #include "../../include/vlgba.h"
 
 #include <rccl/rccl.h>
+#include <climits>
 #include <rocsolver/rocsolver.h>   // types only: the library is dlopen'ed on first use
 
 #include <dlfcn.h>
@@ -883,13 +884,31 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
     P.grp_ch.assign(1, 0);
     P.grp_gs.assign(1, 0);
     P.grp_ge.assign(1, 0);
+    // The MFMA segment's chunks are spread evenly over BA_MF_GROUPS groups
+    // (fractional: group k ends near chunk (k + 1) nseg / G): one workgroup
+    // per slot of k_schur_mfma's 3 x 256 CUs, no partly filled last round
+    // (config 3: 1953 groups of 13 chunks -- 2.54 rounds -- took 179-183 us,
+    // 1536 groups 167-169, 768 groups 155; 1024 / 2304 / 3072: 182-187,
+    // profiles/r05i_*, r05j_*).  The term segment keeps BA_GROUPS' cap.
+    // VLGBA_SCHUR_GROUPS overrides G (measurement).
+    static const int Genv = [] {
+        const char *e = std::getenv("VLGBA_SCHUR_GROUPS");
+        const int v = e ? std::atoi(e) : 0;
+        return v > 0 ? v : 0;
+    }();
+    int seg0 = 0, kseg = 0;
     for (int c = 0; c < nch;) {
         const bool mf = c < P.nch_mf;
         const int cend = mf ? P.nch_mf : nch, nseg = mf ? P.nch_mf : nch - P.nch_mf;
+        if (c == 0 || c == P.nch_mf) seg0 = c, kseg = 0;
         // the MFMA kernel has no direct mode: one chunk's blocks must always fit
         const int gs_cap = mf ? std::max(BA_MF_GACC / (na * na), cmax * (cmax + 1) / 2)
                               : BA_GACC / (na * na);
-        const int gmax = std::min(BA_GROUP_CH, std::max(1, (nseg + BA_GROUPS - 1) / BA_GROUPS));
+        const int G = Genv ? Genv : (mf ? BA_MF_GROUPS : 0);
+        const long long tend = G ? seg0 + ((long long)(kseg + 1) * nseg + G - 1) / G : 0;
+        const int gmax = G ? (int)std::min<long long>(BA_GROUP_CH, std::max<long long>(1, tend - c))
+                           : std::min(BA_GROUP_CH, std::max(1, (nseg + BA_GROUPS - 1) / BA_GROUPS));
+        kseg++;
         const int ge_cap = mf ? std::max(BA_MF_GE_CAP, cmax) : BA_GE_CAP;
         std::vector<int> gs, ge;
         int d = c;
@@ -1611,14 +1630,32 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         TRY(upload(d.blob, plan.blob.data(), plan.blob.size(), s));
         TRY(upload(d.ch_blob, plan.ch_blob.data(), plan.ch_blob.size(), s));
         TRY(upload(d.ch_obase, plan.ch_obase.data(), plan.ch_obase.size(), s));
-        {   // chunk-local point of every observation (k_linearize_chunk)
+        {   // chunk-local point of every observation (k_linearize_chunk) and
+            // each chunk's camera range (k_update_linearize's da staging)
             std::vector<unsigned char> lpt(d.N > 0 ? d.N : 1, 0);
             for (size_t ch = 0; ch + 1 < plan.ch_pt.size(); ch++)
                 for (int i = plan.ch_pt[ch]; i < plan.ch_pt[ch + 1]; i++)
                     for (int o = lptr[i]; o < lptr[i + 1]; o++)
                         lpt[o] = (unsigned char)(i - plan.ch_pt[ch]);
+            const size_t nchk = plan.ch_obase.size() - 1;
+            std::vector<int> ccam(2 * std::max<size_t>(nchk, 1), 0);
+            for (size_t ch = 0; ch < nchk; ch++) {
+                int lo = INT_MAX, hi = -1;
+                for (int o = plan.ch_obase[ch]; o < plan.ch_obase[ch + 1]; o++) {
+                    lo = std::min(lo, lcam[o]);
+                    hi = std::max(hi, lcam[o]);
+                }
+                ccam[2 * ch] = hi < 0 ? 0 : lo;
+                ccam[2 * ch + 1] = hi < 0 ? 0 : hi;
+            }
+            // VLGBA_DA_STAGE=0 (A/B): every range too wide, each lane loads its da row
+            const char *dse = std::getenv("VLGBA_DA_STAGE");
+            if (dse && dse[0] == '0')
+                for (size_t ch = 0; ch < nchk; ch++) ccam[2 * ch + 1] = ccam[2 * ch] + (1 << 20);
             TRY(ctx_alloc(c, &d.obs_lpt, lpt.size()));
             TRY(upload(d.obs_lpt, lpt.data(), lpt.size(), s));
+            TRY(ctx_alloc(c, &d.ch_cam, ccam.size()));
+            TRY(upload(d.ch_cam, ccam.data(), ccam.size(), s));
             VLGBA_CHECK(hipStreamSynchronize(s));
         }
         d.grp_max_s = plan.grp_max_s;

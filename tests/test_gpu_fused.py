@@ -144,3 +144,31 @@ def test_fused_update_whole_solve(gpu, oracle):
             end = out[who][0][-1]
             if len(e2):
                 assert e2[-1] >= end * (1 - 1e-6), (who, other, end, e2[-1])
+
+
+@pytest.mark.parametrize("kind", ["banded", "long"])
+def test_da_staging_bit_identical(gpu, monkeypatch, kind):
+    """The fused update stages each chunk's da rows in LDS when its cameras
+    span a narrow range (ch_cam) and loads every lane's row from its camera
+    index otherwise (VLGBA_DA_STAGE=0 forces that): the same step and
+    linearisation bit for bit."""
+    sc = _scene(kind)
+    a, b = _start(sc, 6)
+    res = []
+    for stage in ("1", "0"):
+        monkeypatch.setenv("VLGBA_DA_STAGE", stage)
+        ba = _make(gpu, sc, 6, {}, True)
+        ba.set_params(a, b)
+        i1 = ba.step(relinearize=False, update_lm=True)
+        i2 = ba.step(relinearize=False, update_lm=True)
+        da, db = ba.last_step()
+        res.append((i1.new_sse, i2.new_sse, da.copy(), db.copy(), ba.linearization(),
+                    ba.get_params()))
+        ba.close()
+    (s1, t1, da1, db1, l1, p1), (s0, t0, da0, db0, l0, p0) = res
+    assert s1 == s0 and t1 == t0
+    assert np.array_equal(da1, da0) and np.array_equal(db1, db0)
+    for k in l1:
+        assert np.array_equal(l1[k], l0[k]), k
+    for x, y in zip(p1, p0):
+        assert np.array_equal(x, y)
