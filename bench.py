@@ -55,6 +55,8 @@ def main():
                          "2 for cfg5, 0 for cfg5x)")
     ap.add_argument("--config", default="cfg3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="cfg3: skip the config-5 replay carried in the line")
     ap.add_argument("--host-scene", action="store_true",
                     help="generate the banded configs with numpy instead of on the GPU")
     ap.add_argument("--cpu-sample-points", type=int, default=0,
@@ -246,9 +248,18 @@ def main():
         "solve_fallbacks": fallbacks,
         "cpu_baseline": cpu,
     }
+    ba.close()
+    if rank == 0 and world == 1 and args.config == "cfg3" and not args.no_other_configs:
+        # config 5 (the growing replay) measured in the same driver run: three
+        # timed replays after one untimed, its CPU baseline beside it
+        try:
+            out["other_configs"] = {"cfg5": replay_summary(
+                replay_line("cfg5", 3, 1, not args.no_cpu_baseline))}
+        except Exception as e:   # noqa: BLE001 -- the cfg3 line stands on its own
+            log(f"[bench] cfg5 replay failed: {e!r}")
+            out["other_configs"] = {"cfg5": {"error": repr(e)}}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    ba.close()
     if world > 1:
         dist.destroy_process_group()
 
@@ -343,13 +354,35 @@ def bench_incremental(args):
     Each solve picks its shard count with dist.choose_shards over the GPUs
     present (1 -> 8 elastic point sharding: rank threads, RCCL between
     distinct GPUs).  A step is one whole replay; value = BA solves/s."""
+    print(json.dumps(replay_line(args.config, args.steps, args.warmup,
+                                 not args.no_cpu_baseline)), flush=True)
+
+
+def replay_summary(line):
+    """The config-5 replay's headline fields, carried in the default (cfg3)
+    bench line so that the driver's run measures config 5 too."""
+    keep = ("metric", "value", "unit", "lm_iterations_per_s", "ms_per_step", "steps", "warmup")
+    out = {k: line[k] for k in keep}
+    out["workload"] = line["config"]["workload"]
+    cb = line.get("cpu_baseline")
+    if cb:
+        out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
+    rf = line.get("roofline") or {}
+    out["roofline"] = {k: rf.get(k) for k in ("device_busy_frac", "kernel", "bound", "frac")}
+    out["host_device_split_s"] = line["host_device_split_s"]
+    return out
+
+
+def replay_line(config, steps, warmup, with_cpu):
+    """One growing-replay bench line (dict): `steps` timed replays after
+    `warmup` untimed ones."""
     import torch
     from bundleadjustmentmatlab_amd.dist import OBS_PER_SHARD
     from bundleadjustmentmatlab_amd.incremental import incremental_bundle
     from bundleadjustmentmatlab_amd.scene import make_config
     ndev = max(1, torch.cuda.device_count())
     torch.cuda.set_device(0)
-    sc = make_config(args.config)
+    sc = make_config(config)
     devices = list(range(ndev))
     t_start = time.perf_counter()
 
@@ -359,7 +392,7 @@ def bench_incremental(args):
             log(f"[bench] {len(solves)} solves, {time.perf_counter() - t_start:.1f} s: "
                 f"{q['cameras']} cams {q['observations']} obs, solve {1e3 * q['seconds']:.1f} ms "
                 f"(solve time so far {sum(s['seconds'] for s in solves):.1f} s)")
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         incremental_bundle(sc, devices=devices, progress=progress)
     # the CPU baseline's sample: every k-th BA call of the last timed replay
     # (its inputs by reference -- the replay builds them fresh per call -- and
@@ -384,8 +417,8 @@ def bench_incremental(args):
     t0 = time.perf_counter()
     res = None
     try:
-        for q in range(args.steps):
-            spy_on[0] = q == args.steps - 1
+        for q in range(steps):
+            spy_on[0] = q == steps - 1
             spy.count = 0
             res = incremental_bundle(sc, devices=devices, progress=progress)
     finally:
@@ -400,14 +433,14 @@ def bench_incremental(args):
     obs_passes = sum(q["passes"] * q["observations"] for q in sol)
     out = {
         "metric": "incremental BA solves/sec (test_incremental-style growing BA)",
-        "value": args.steps * len(sol) / dt, "unit": "BA solves/s",
-        "lm_iterations_per_s": args.steps * passes / dt,
-        "observations_per_s": args.steps * obs_passes / dt,
-        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True, "scaling": "weak",
+        "value": steps * len(sol) / dt, "unit": "BA solves/s",
+        "lm_iterations_per_s": steps * passes / dt,
+        "observations_per_s": steps * obs_passes / dt,
+        "n_gpus": 1, "steps": steps, "warmup": warmup,
+        "ms_per_step": 1e3 * dt / steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (seeded generate_scene_and_motion restatement, SURVEY.md 8.d)",
-        "config": {"workload": f"{args.config}: {sc.m} cams x {sc.n} pts x {sc.num_obs} obs, "
+        "config": {"workload": f"{config}: {sc.m} cams x {sc.n} pts x {sc.num_obs} obs, "
                                f"{len(sol)} growing solves per replay",
                    "cameras": sc.m, "points": sc.n, "observations": sc.num_obs,
                    "parallelism": f"elastic point shard over {ndev} GPU(s)",
@@ -420,7 +453,7 @@ def bench_incremental(args):
                                             if len(q["error"])))},
         "time_split_s": {"solves": sum(q["seconds"] for q in sol),
                          "resections": sum(q["seconds"] for q in res["resections"]),
-                         "replay": dt / args.steps},
+                         "replay": dt / steps},
         # where a replay's solve time goes: the LM loops (vlgba_run: device passes
         # + the host's per-pass decisions), the wait for the context the worker
         # thread built ahead (its host plan + uploads; create_worker is the
@@ -433,7 +466,7 @@ def bench_incremental(args):
             "create_worker": sum(q["create"] or 0.0 for q in sol),
             "solve_calls_rest": sum(q["seconds"] - q["lm_seconds"] - q["wait_create"]
                                     for q in sol),
-            "host_glue": dt / args.steps - sum(q["seconds"] for q in sol) -
+            "host_glue": dt / steps - sum(q["seconds"] for q in sol) -
                          sum(q["seconds"] for q in res["resections"])},
         "elastic": {"obs_per_shard": OBS_PER_SHARD, "max_solve_observations":
                     max(q["observations"] for q in sol),
@@ -443,11 +476,10 @@ def bench_incremental(args):
                             ("; every solve of this scene is below it, so the elastic "
                              "count is 1 throughout" if max(q["observations"] for q in sol)
                              < 2 * OBS_PER_SHARD else "")},
-        "cpu_baseline": None if args.no_cpu_baseline else replay_cpu_baseline(sample, k_every,
-                                                                              ncalls),
+        "cpu_baseline": replay_cpu_baseline(sample, k_every, ncalls) if with_cpu else None,
     }
-    out["roofline"] = replay_roofline(sc, devices, dt / args.steps)
-    print(json.dumps(out), flush=True)
+    out["roofline"] = replay_roofline(sc, devices, dt / steps)
+    return out
 
 
 def replay_roofline(sc, devices, replay_s):
