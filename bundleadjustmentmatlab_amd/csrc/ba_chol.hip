@@ -2470,6 +2470,121 @@ __global__ __launch_bounds__(256) void k_assemble_tiles(
     }
 }
 
+// k_schur_reduce and k_assemble_tiles in one launch (opt-in,
+// VLGBA_FUSE_REDUCE=1: measured no faster than the two launches, 25.8 us
+// against 11.7 + 14.8 at config 3, profiles/r05t_*; single rank, no long
+// tracks: nothing to all-reduce between them): BA_RA_STRIPS workgroups per
+// envelope tile, each a strip of rows, form every lower entry of the co-visible blocks
+// that falls in the strip exactly as k_schur_reduce forms it -- the damped
+// U_j term, then the group partials subtracted in slot order -- and the
+// diagonal strips the rhs of their rows (eA_j minus the group e-partials in
+// order) with the pinv rule of k_assemble_tiles.  Bit-identical S and rhs;
+// the block list (sblk) is not written (every reader of it -- the re-solve,
+// the pinv fallbacks, vlgba_get_reduced_system -- runs the Schur phase again
+// with the separate kernels).
+#ifndef BA_RA_STRIPS
+#define BA_RA_STRIPS 8    // 8-row strips (4: 26.4 us, 8: 25.8, 16: 41 -- the
+                          // block-list scan repeats per strip)
+#endif
+__global__ __launch_bounds__(256) void k_reduce_assemble(
+    double *__restrict__ S, long long lds, const int *__restrict__ env,
+    const int *__restrict__ tb_ptr, const int *__restrict__ tb_blk,
+    const int *__restrict__ blk_jk, int na, long long ld, double *__restrict__ rhs,
+    double *__restrict__ status, const int *__restrict__ crow, const int *__restrict__ rowsrc,
+    const double *__restrict__ spart, const double *__restrict__ epart,
+    const int *__restrict__ blk_gptr, const int *__restrict__ blk_gslots,
+    const int *__restrict__ cam_gptr, const int *__restrict__ cam_gslots,
+    const double *__restrict__ U, const double *__restrict__ eA, double lambda, int owner)
+{
+    constexpr int SR = NB / BA_RA_STRIPS;   // strip rows
+    __shared__ double T[SR * (NB + 1)];
+    const int tile = blockIdx.x / BA_RA_STRIPS, strip = blockIdx.x % BA_RA_STRIPS;
+    const int tid = threadIdx.x;
+    const int ti = env[2 * tile], tk = env[2 * tile + 1];
+    for (int q = tid; q < SR * (NB + 1); q += 256) T[q] = 0.0;
+    if (blockIdx.x == 0 && tid == 0) {
+        status[0] = 0.0;   // non-positive pivot
+        status[1] = 0.0;   // bounded hand-off spin gave up
+    }
+    __syncthreads();
+    const long long r0 = (long long)NB * ti + SR * strip, c0 = (long long)NB * tk;
+    const int na2 = na * na;
+    const int u0 = tb_ptr[tile], nq = (tb_ptr[tile + 1] - u0) * na2;
+    for (int q = tid; q < nq; q += 256) {
+        const int u = q / na2, l = q - na2 * u;
+        const int bk = tb_blk[u0 + u];
+        const int r = l % na, c = l / na;
+        const int bj = blk_jk[2 * bk], bc = blk_jk[2 * bk + 1];
+        long long row, col;
+        if (!crow) {
+            row = (long long)na * bj + r;
+            col = (long long)na * bc + c;
+        } else {
+            row = crow[bj] + r;
+            col = crow[bc] + c;
+            if (row < col && bj != bc) {
+                const long long t = row;
+                row = col;
+                col = t;
+            }
+        }
+        if (row < col || row < r0 || row >= r0 + SR || col < c0 || col >= c0 + NB) continue;
+        double acc = 0.0;
+        if (bj == bc && owner) {
+            const double uu = U[(size_t)na2 * bj + r + na * c];
+            acc = (r == c) ? (1 + lambda) * uu : uu;
+        }
+        int p = blk_gptr[bk];
+        const int pe = blk_gptr[bk + 1];
+        for (; p + 8 <= pe; p += 8) {
+            double v[8];
+#pragma unroll
+            for (int t = 0; t < 8; t++) v[t] = spart[(size_t)na2 * blk_gslots[p + t] + l];
+#pragma unroll
+            for (int t = 0; t < 8; t++) acc -= v[t];
+        }
+        for (; p < pe; p++) acc -= spart[(size_t)na2 * blk_gslots[p] + l];
+        T[(row - r0) * (NB + 1) + (col - c0)] = acc;
+    }
+    __syncthreads();
+    if (ti == tk && tid < SR) {   // the rows' rhs, then the pinv rule (k_assemble_tiles)
+        const int rr = SR * strip + tid;
+        double *dg = T + tid * (NB + 1) + rr;
+        const long long r = r0 + tid;
+        const long long src = rowsrc ? (long long)rowsrc[r] : (r < ld ? r : -1);
+        double e = 0.0;
+        if (src >= 0) {
+            const int j = (int)(src / na), rc = (int)(src - (long long)na * j);
+            e = owner ? eA[(size_t)na * j + rc] : 0.0;
+            int q = cam_gptr[j];
+            const int qe = cam_gptr[j + 1];
+            for (; q + 8 <= qe; q += 8) {
+                double v[8];
+#pragma unroll
+                for (int t = 0; t < 8; t++) v[t] = epart[(size_t)na * cam_gslots[q + t] + rc];
+#pragma unroll
+                for (int t = 0; t < 8; t++) e -= v[t];
+            }
+            for (; q < qe; q++) e -= epart[(size_t)na * cam_gslots[q] + rc];
+        }
+        rhs[r] = e;
+        if (*dg == 0.0) {
+            *dg = 1.0;
+            rhs[r] = 0.0;
+        } else if (r >= ld) {
+            rhs[r] = 0.0;
+        }
+    }
+    __syncthreads();
+    double *base = S + r0 + lds * c0;
+    const int r = tid & (SR - 1), cq = tid / SR;
+#pragma unroll
+    for (int u = 0; u < NB * SR / 256; u++) {
+        const int c = cq + (256 / SR) * u;
+        base[r + lds * c] = T[r * (NB + 1) + c];
+    }
+}
+
 // zero every envelope tile of S (fill from the previous factorisation)
 __global__ void k_zero_env(double *__restrict__ S, long long lds, const int *__restrict__ env)
 {
@@ -3171,6 +3286,15 @@ void ba_chol_free(ba_dev *d)
 int ba_assemble_tiles(ba_dev *d)
 {
     const bool nd = d->nd_np > 0;
+    if (d->fuse_red) {   // the Schur phase left the block sums to this launch
+        k_reduce_assemble<<<BA_RA_STRIPS * d->n_env, 256, 0, d->stream>>>(
+            d->S, nd ? d->slds : d->lds, d->env_tiles, d->tb_ptr, d->tb_blk, d->blk_jk, d->na,
+            nd ? d->slds : d->ld, nd ? d->nd_rhs : d->rhs, d->scal + 4,
+            nd ? d->nd_crow : nullptr, nd ? d->nd_rowsrc : nullptr, d->spart, d->epart,
+            d->blk_gptr, d->blk_gslots, d->cam_gptr, d->cam_gslots, d->U, d->eA, d->red_lambda,
+            d->schur_owner);
+        return -(int)hipGetLastError();
+    }
     k_assemble_tiles<<<d->n_env, 256, 0, d->stream>>>(
         d->S, nd ? d->slds : d->lds, d->env_tiles, d->tb_ptr, d->tb_blk, d->blk_jk, d->sblk, d->na,
         nd ? d->slds : d->ld, nd ? d->nd_rhs : d->rhs, d->scal + 4, nd ? d->nd_crow : nullptr,

@@ -265,6 +265,9 @@ struct ba_dev {
     double *xh_out;    // [N][2] projections (stage 1 and stage 3)
     double *B_out;     // [N][6] point Jacobians (stage 1)
     unsigned char *obs_vis;  // [N] stage 3: 0 = structural-only pair (no projection)
+    int fuse_red;      // this pass: k_schur_reduce folded into the assembly (k_reduce_assemble)
+    int fuse_red_ok;   // allowed (VLGBA_FUSE_REDUCE=1; off by default: no faster)
+    double red_lambda; // ... at this lambda
     int schur_owner;   // this rank adds U* / eA into the reduced system (every rank
                        // adds its own partials)
     int dpg_lambda;    // this rank adds the lambda dp'dp part of the camera dpg

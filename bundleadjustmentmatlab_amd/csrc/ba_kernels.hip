@@ -2532,6 +2532,10 @@ static int launch_schur_fast(ba_dev *d, double lambda)
         VLGBA_CHECK(hipStreamWaitEvent(d->stream, d->ev_join, 0));
         d->join_pending = 0;
     }
+    if (d->fuse_red) {   // the block sums are formed by the assembly (k_reduce_assemble)
+        d->red_lambda = lambda;
+        return 0;
+    }
     KT_B(d);
     ba_longs lg{};
     if (d->nl > 0) {

@@ -1722,6 +1722,8 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         // linearisation, but 6 % slower on MI355X
         d.fast_dehom = fq && fq[0] == '1';
         d.ewin = (rd && rd[0] == '1') ? 0u : BA_EWIN;
+        const char *fr = std::getenv("VLGBA_FUSE_REDUCE");
+        d.fuse_red_ok = fr && fr[0] == '1';   // opt-in: no faster
         TRY(upload(d.ch_pt, plan.ch_pt.data(), plan.ch_pt.size(), s));
         TRY(upload(d.ch_eslot, plan.ch_eslot.data(), plan.ch_eslot.size(), s));
         TRY(upload(d.eslot_optr, plan.eslot_optr.data(), plan.eslot_optr.size(), s));
@@ -2274,9 +2276,15 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
     } else {
         mark(c, 1);
     }
+    // single rank, no long tracks, envelope tiles, VLGBA_FUSE_REDUCE=1: the
+    // block sums ride in the assembly launch (k_reduce_assemble)
+    d.fuse_red = c->world == 1 && !c->comm && !d.ordered && !d.parity && d.nl == 0 &&
+                 d.n_env > 0 && d.fuse_red_ok;
     TRY(schur_phase(c, lam));
     mark(c, 4);
-    TRY(ba_launch_assemble(&d));
+    const int arc = ba_launch_assemble(&d);
+    d.fuse_red = 0;
+    TRY(arc);
     mark(c, 5);
     TRY(ba_chol_solve(&d));
     for (int w = 4; w <= 5; w++) {   // test hooks: as if a pivot failed / a spin gave up
