@@ -739,7 +739,8 @@ __device__ __forceinline__ void factor_step_two(double *__restrict__ S, long lon
                                                 double *__restrict__ rhs,
                                                 double *__restrict__ y,
                                                 double *__restrict__ status, int b, int sep0,
-                                                unsigned *__restrict__ kflag, unsigned epoch)
+                                                unsigned *__restrict__ kflag, unsigned epoch,
+                                                int ntr, int tstride)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double *As = sm, *Bs = sm + NB * LP;
@@ -749,23 +750,29 @@ __device__ __forceinline__ void factor_step_two(double *__restrict__ S, long lon
     const bool kin = Tp > 0 && prev[0] == k;   // column k-1 reaches row k
     d4 acc[2][2];
     FS_ST(0);
-    if (b > T) {   // a trailing pair of column k-1 below row k
+    if (b > T) {
+        // trailing pairs q = b - T - 1 + u tstride (< ntr) of column k-1
+        // below row k, one after another: fewer workgroups than pairs keeps
+        // them off most CUs, so the diagonal factor's chain seldom shares one
         const int *pl = prev + (kin ? 1 : 0);
         const int Tr = Tp - (kin ? 1 : 0);
-        int q = b - T - 1, jj = 0;
-        while (q >= Tr - jj) {
-            q -= Tr - jj;
-            jj++;
+        for (int q0 = b - T - 1; q0 < ntr; q0 += tstride) {
+            int q = q0, jj = 0;
+            while (q >= Tr - jj) {
+                q -= Tr - jj;
+                jj++;
+            }
+            const int j = pl[jj], i = pl[jj + q];
+            double vc[16];
+            fetch_tile(S, lds, i, j, vc);
+            mfma_64x64_glb(S, lds, i, j, k - 1, acc);
+            put_tile(As, vc, false);
+            __syncthreads();
+            acc_to_lds(acc, As, -1.0, true);
+            __syncthreads();
+            store_tile(S, lds, i, j, As);
+            __syncthreads();   // As read by every thread before the next pair's put
         }
-        const int j = pl[jj], i = pl[jj + q];
-        double vc[16];
-        fetch_tile(S, lds, i, j, vc);
-        mfma_64x64_glb(S, lds, i, j, k - 1, acc);
-        put_tile(As, vc, false);
-        __syncthreads();
-        acc_to_lds(acc, As, -1.0, true);
-        __syncthreads();
-        store_tile(S, lds, i, j, As);
         FS_END();
         return;
     }
@@ -857,11 +864,12 @@ __global__ __launch_bounds__(256) void k_factor_step(double *__restrict__ S, lon
                                                      double *__restrict__ rhs,
                                                      double *__restrict__ y,
                                                      double *__restrict__ status,
-                                                     unsigned *__restrict__ kflag, unsigned epoch)
+                                                     unsigned *__restrict__ kflag, unsigned epoch,
+                                                     int ntr, int tstride)
 {
     if (kflag)
         factor_step_two(S, lds, k, pan, T, prev, Tp, linv, rhs, y, status, blockIdx.x, INT_MAX,
-                        kflag, epoch);
+                        kflag, epoch, ntr, tstride);
     else
         factor_step_body(S, lds, k, pan, T, prev, Tp, linv, rhs, y, status, blockIdx.x, INT_MAX,
                          nullptr, 0);
@@ -870,10 +878,18 @@ __global__ __launch_bounds__(256) void k_factor_step(double *__restrict__ S, lon
 // one step of every arc of the nested dissection: column k[t] of arc t takes
 // workgroups [b0[t], b0[t+1]) (k_factor_step's roles), pan / prev as offsets
 // into the panel list
+// Workgroup order (grouped, the default): every arc's workgroup 0 first, then
+// every arc's panel tiles, then every arc's trailing pairs (pb / tb: prefix
+// counts of the panels / trailing pairs over the arcs).  Arc-major order
+// (b0, VLGBA_ND_GROUPED=0) puts arc 1's workgroup 0 behind all of arc 0's
+// trailing pairs: once those outnumber the free workgroup slots, arc 1's
+// diagonal factor -- the chain of its step -- starts only when the first of
+// them retire.  The roles are the same either way (bit-identical).
 struct nd_step {
-    int np;
+    int np, grouped;
     int k[BA_ND_MAX], T[BA_ND_MAX], Tp[BA_ND_MAX], pofs[BA_ND_MAX], qofs[BA_ND_MAX];
-    int b0[BA_ND_MAX + 1];
+    int ntr[BA_ND_MAX], ts[BA_ND_MAX];   // trailing pairs / their workgroups (stride)
+    int b0[BA_ND_MAX + 1], pb[BA_ND_MAX + 1], tb[BA_ND_MAX + 1];
 };
 
 __global__ __launch_bounds__(256) void k_factor_multi(double *__restrict__ S, long long lds,
@@ -886,15 +902,30 @@ __global__ __launch_bounds__(256) void k_factor_multi(double *__restrict__ S, lo
                                                       unsigned *__restrict__ kflag,
                                                       unsigned epoch)
 {
-    const int b = blockIdx.x;
-    int t = 0;
-    while (t + 1 < P.np && b >= P.b0[t + 1]) t++;
+    const int b = blockIdx.x, np = P.np;
+    int t = 0, role;
+    if (!P.grouped) {
+        while (t + 1 < np && b >= P.b0[t + 1]) t++;
+        role = b - P.b0[t];
+    } else if (b < np) {   // workgroup 0 of arc b
+        t = b;
+        role = 0;
+    } else if (b < np + P.pb[np]) {   // a panel tile
+        const int q = b - np;
+        while (t + 1 < np && q >= P.pb[t + 1]) t++;
+        role = 1 + q - P.pb[t];
+    } else {   // a trailing pair
+        const int q = b - np - P.pb[np];
+        while (t + 1 < np && q >= P.tb[t + 1]) t++;
+        role = 1 + P.T[t] + q - P.tb[t];
+    }
     if (kflag)
         factor_step_two(S, lds, P.k[t], pan_list + P.pofs[t], P.T[t], pan_list + P.qofs[t],
-                        P.Tp[t], linv, rhs, y, status, b - P.b0[t], sep0, kflag, epoch);
+                        P.Tp[t], linv, rhs, y, status, role, sep0, kflag, epoch, P.ntr[t],
+                        P.ts[t]);
     else
         factor_step_body(S, lds, P.k[t], pan_list + P.pofs[t], P.T[t], pan_list + P.qofs[t],
-                         P.Tp[t], linv, rhs, y, status, b - P.b0[t], sep0, nullptr, 0);
+                         P.Tp[t], linv, rhs, y, status, role, sep0, nullptr, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -2991,6 +3022,12 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
     }
     // nested dissection (not for tridiagonal S, which the cyclic reduction takes)
     d->nd_np = 0;
+    {
+        const char *eg = std::getenv("VLGBA_ND_GROUPED");
+        d->nd_grouped = !(eg && eg[0] == '0');
+        const char *et = std::getenv("VLGBA_TRAIL_WGS");
+        d->trail_cap = et ? std::atoi(et) : 0;
+    }
     const int na = d->na, m = d->m;
     std::vector<int> crow, tpart;   // row of camera j; part of tile (arc t, separator np)
     if (!tridiag && (d->dense_solve == 0 || d->dense_solve == 4) && m >= 2 && nt > 1) {
@@ -3322,6 +3359,14 @@ int ba_chol_fix_diag(ba_dev *d)
     return -(int)hipGetLastError();
 }
 
+// workgroups for ntr trailing pairs beside `other` workgroups of the same
+// launch: at most d->trail_cap - other (VLGBA_TRAIL_WGS; 0: one per pair)
+static int trail_wgs(const ba_dev *d, int ntr, int other)
+{
+    if (d->trail_cap <= 0 || ntr == 0) return ntr;
+    return std::max(1, std::min(ntr, d->trail_cap - other));
+}
+
 // the envelope's tile columns k0 .. k1-1 (k_factor_step), column k0 taking no
 // pending update of column k0-1
 static void envelope_columns(ba_dev *d, int k0, int k1, long long L, double *rhs,
@@ -3334,11 +3379,13 @@ static void envelope_columns(ba_dev *d, int k0, int k1, long long L, double *rhs
         const int q0 = k > k0 ? d->pan_ptr_h[k - 1] : 0, Tp = k > k0 ? p0 - q0 : 0;
         // column k-1's trailing pairs below row k (see k_factor_step)
         const int kin = Tp > 0 && d->h_pan_list[q0] == k;
-        const int Tr = Tp - kin;
+        const int Tr = Tp - kin, ntr = Tr * (Tr + 1) / 2;
+        // with the hand-off a trailing workgroup may take several pairs
+        const int nw = kflag ? trail_wgs(d, ntr, 1 + T) : ntr;
         KT_B(d);
-        k_factor_step<<<1 + T + Tr * (Tr + 1) / 2, 256, kflag ? smem2 : smem3, d->stream>>>(
+        k_factor_step<<<1 + T + nw, 256, kflag ? smem2 : smem3, d->stream>>>(
             d->S, L, k, d->pan_list + p0, T, d->pan_list + q0, Tp, d->linv, rhs, d->ywork,
-            d->scal + 4, kflag, d->fac_epoch);
+            d->scal + 4, kflag, d->fac_epoch, ntr, nw);
         KT_E(d, KT_FACTOR);
     }
 }
@@ -3488,6 +3535,7 @@ int ba_chol_solve(ba_dev *d, int nospin)
         for (int t = 0; t < np; t++) nsteps = std::max(nsteps, d->nd_a0[t + 1] - d->nd_a0[t]);
         for (int st = 0; st < nsteps; st++) {
             nd_step P{};
+            P.grouped = d->nd_grouped;
             int nbk = 0;
             for (int t = 0; t < np; t++) {
                 const int k = d->nd_a0[t] + st;
@@ -3504,9 +3552,32 @@ int ba_chol_solve(ba_dev *d, int nospin)
                 P.Tp[u] = Tp;
                 P.pofs[u] = p0;
                 P.qofs[u] = q0;
+                const int ntr = Tr * (Tr + 1) / 2 - nsr * (nsr + 1) / 2;
+                P.ntr[u] = ntr;
                 P.b0[u] = nbk;
-                nbk += 1 + T + Tr * (Tr + 1) / 2 - nsr * (nsr + 1) / 2;
+                P.pb[u + 1] = P.pb[u] + T;
+                nbk += 1 + T;
             }
+            // the trailing workgroups: each arc's share of the cap (with the hand-off)
+            int ttot = 0;
+            for (int u = 0; u < P.np; u++) ttot += P.ntr[u];
+            const int tw = kflag ? trail_wgs(d, ttot, nbk) : ttot;
+            for (int u = 0; u < P.np; u++) {
+                const int nw = tw == ttot ? P.ntr[u]
+                                          : (P.ntr[u] == 0 ? 0
+                                                           : std::max(1, (int)((long long)tw *
+                                                                               P.ntr[u] / ttot)));
+                P.ts[u] = nw;
+                P.tb[u + 1] = P.tb[u] + nw;
+            }
+            if (!P.grouped) {   // arc-major: arc u's trailing workgroups follow its panels
+                int acc = 0;
+                for (int u = 0; u < P.np; u++) {
+                    P.b0[u] = acc;
+                    acc += 1 + P.T[u] + P.ts[u];
+                }
+            }
+            nbk += P.tb[P.np];
             P.b0[P.np] = nbk;
             KT_B(d);
             k_factor_multi<<<nbk, 256, kflag ? sizeof(double) * 2 * NB * LP : smem3, d->stream>>>(

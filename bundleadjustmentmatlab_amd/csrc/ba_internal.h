@@ -166,6 +166,8 @@ struct ba_dev {
     // the arcs' contribution to the separator block is one SYRK
     // (k_sep_update / k_sep_reduce), then the separator's columns.
     int nd_np;                    // arcs (0: natural order)
+    int nd_grouped;               // k_factor_multi's workgroups grouped by role (nd_step)
+    int trail_cap;                // envelope launches' workgroup cap for trailing pairs (0: none)
     int nd_a0[BA_ND_MAX + 1];     // first tile of arc t; nd_a0[nd_np] = first separator tile
     long long slds;               // rows of the reordered system (nt * 64)
     int *nd_crow;                 // device [m] first row of camera j
@@ -254,6 +256,8 @@ struct ba_dev {
     // track order, found once at setup (k_long_pairs): [nb + 1], [pairs]
     int *lpair_ptr;
     int2 *lpair;
+    int *lblk;     // blocks with long-track pairs, most pairs first (k_schur_long_acc)
+    int nlb;       // their count (0: k_schur_reduce streams the pairs itself)
     double *vseg;                     // [nseg][12] V | eB partials per segment
     double *dpg_long;                 // [nl] point part of dp'(lambda dp + g)
     int mf_max_s, mf_max_e, mf_max_blob;   // MFMA groups' LDS sizes

@@ -1826,6 +1826,63 @@ __global__ void k_schur_reduce(const int *__restrict__ blk_jk, const int *__rest
     if (l < NN) sblk[(size_t)NN * bk + l] = acc;
 }
 
+// The long tracks' (obs, obs) terms of the co-visible blocks after
+// k_schur_reduce has written their slot sums (it then skips its pair loop):
+// four lanes per block, lane q a (NA+1)/2-row x (NA+1)/2-column quarter of
+// S_jk, each entry of it taking the block's pairs in track order with
+// k_schur_reduce's expression -- the same operations on the same values in the
+// same order, so bit-identical.  A lane's Y / W rows come straight from
+// global memory (no LDS staging, no barriers): 2 (NA+1)/2 x 3 values per pair
+// for (NA+1)^2/4 entries, against six LDS reads per entry.  lblk: the blocks
+// with pairs, most pairs first (the lanes of a wave loop about as long).
+template <int NA>
+__global__ __launch_bounds__(256) void k_schur_long_acc(const int *__restrict__ lblk, int nlb,
+                                                        const int *__restrict__ pair_ptr,
+                                                        const int2 *__restrict__ pair,
+                                                        const double *__restrict__ ylong,
+                                                        const double *__restrict__ W, int L0,
+                                                        double *__restrict__ sblk)
+{
+    constexpr int WS = 3 * NA, NN = NA * NA, RH = (NA + 1) / 2;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int li = t >> 2, q = t & 3;
+    if (li >= nlb) return;
+    const int bk = lblk[li];
+    const int r0 = (q & 1) ? RH : 0, nr = (q & 1) ? NA - RH : RH;
+    const int c0 = (q & 2) ? RH : 0, nc = (q & 2) ? NA - RH : RH;
+    double *sb = sblk + (size_t)NN * bk;
+    double acc[RH][RH];
+#pragma unroll
+    for (int i = 0; i < RH; i++)
+#pragma unroll
+        for (int j = 0; j < RH; j++)
+            acc[i][j] = (i < nr && j < nc) ? sb[(r0 + i) + NA * (c0 + j)] : 0.0;
+    const int p1 = pair_ptr[bk + 1];
+    for (int p = pair_ptr[bk]; p < p1; p++) {
+        const int2 pr = pair[p];
+        const double *y = ylong + (size_t)WS * pr.x + r0;
+        const double *w = W + (size_t)WS * ((size_t)L0 + pr.y) + c0;
+        double yv[3][RH], wv[3][RH];
+#pragma unroll
+        for (int m = 0; m < 3; m++)
+#pragma unroll
+            for (int i = 0; i < RH; i++) {
+                yv[m][i] = i < nr ? y[i + NA * m] : 0.0;
+                wv[m][i] = i < nc ? w[i + NA * m] : 0.0;
+            }
+#pragma unroll
+        for (int i = 0; i < RH; i++)
+#pragma unroll
+            for (int j = 0; j < RH; j++)
+                acc[i][j] -= yv[0][i] * wv[0][j] + yv[1][i] * wv[1][j] + yv[2][i] * wv[2][j];
+    }
+#pragma unroll
+    for (int i = 0; i < RH; i++)
+#pragma unroll
+        for (int j = 0; j < RH; j++)
+            if (i < nr && j < nc) sb[(r0 + i) + NA * (c0 + j)] = acc[i][j];
+}
+
 // t_o = Y_o eB_i for given Y (stage-2 entry; k_damp_point forms it otherwise)
 template <int NA>
 __global__ void k_point_yeb(const int *__restrict__ pt_ptr, const double *__restrict__ Y,
@@ -2538,7 +2595,7 @@ static int launch_schur_fast(ba_dev *d, double lambda)
     }
     KT_B(d);
     ba_longs lg{};
-    if (d->nl > 0) {
+    if (d->nl > 0 && !d->nlb) {
         lg.pair_ptr = d->lpair_ptr;
         lg.pair = d->lpair;
         lg.ylong = d->ylong;
@@ -2548,6 +2605,9 @@ static int launch_schur_fast(ba_dev *d, double lambda)
     k_schur_reduce<NA><<<d->nb, bs, 0, d->stream>>>(
         d->blk_jk, d->blk_gptr, d->blk_gslots, d->cam_gptr, d->cam_gslots, d->spart, d->epart,
         d->U, d->eA, d->nb, lambda, d->schur_owner, d->sblk, d->rhs, lg);
+    if (d->nl > 0 && d->nlb)   // the long tracks' terms after the slot sums
+        k_schur_long_acc<NA><<<(4 * d->nlb + 255) / 256, 256, 0, d->stream>>>(
+            d->lblk, d->nlb, d->lpair_ptr, d->lpair, d->ylong, d->W, d->long_o0_h, d->sblk);
     KT_E(d, KT_SCHUR_RED);
     return -(int)hipGetLastError();
 }

@@ -1803,6 +1803,22 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         TRY(ctx_alloc(c, &d.lpair, (size_t)tot + 1));
         TRY(upload(d.lpair_ptr, h.data(), (size_t)d.nb + 1, s));
         TRY(ba_launch_long_pairs(&d, 1, nullptr));
+        // the blocks with pairs for k_schur_long_acc, most pairs first
+        // (VLGBA_LONG_ACC=0: k_schur_reduce streams them itself)
+        const char *la = std::getenv("VLGBA_LONG_ACC");
+        if (!(la && la[0] == '0')) {
+            std::vector<int> lb;
+            for (int b = 0; b < d.nb; b++)
+                if (h[b + 1] > h[b]) lb.push_back(b);
+            std::stable_sort(lb.begin(), lb.end(), [&](int x, int y) {
+                return h[x + 1] - h[x] > h[y + 1] - h[y];
+            });
+            d.nlb = (int)lb.size();
+            if (d.nlb > 0) {
+                TRY(ctx_alloc(c, &d.lblk, lb.size()));
+                TRY(upload(d.lblk, lb.data(), lb.size(), s));
+            }
+        }
         ST_MARK("long_pairs");
     }
     VLGBA_CHECK(hipMemsetAsync(d.scal, 0, 8 * sizeof(double), s));

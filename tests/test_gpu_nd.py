@@ -138,6 +138,54 @@ def test_nd_spin_timeout_resolves_bit_identically(gpu, monkeypatch):
     assert np.array_equal(p0[0], p1[0]) and np.array_equal(p0[1], p1[1])
 
 
+@pytest.mark.parametrize("kind,m,num_a", [("ladybug", 300, 6), ("ladybug", 90, 7)])
+def test_nd_grouped_order_bit_identical(gpu, monkeypatch, kind, m, num_a):
+    """k_factor_multi's workgroups grouped by role (every arc's diagonal
+    workgroup, then the panels, then the trailing pairs: the default) against
+    the arc-major order (VLGBA_ND_GROUPED=0): the same roles, so whole LM runs
+    agree bit for bit."""
+    sc = _scene(kind, m, seed=6)
+    a, b = _params(sc, num_a)
+
+    def run():
+        with gpu.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, num_a, solver="nd",
+                                stop_rel=1e-9, max_iter=8) as ba:
+            ba.set_params(a, b)
+            ba.step(relinearize=True, update_lm=False)
+            da, db = ba.last_step()
+            err, st = ba.run()
+            return da.copy(), err.copy(), [x.copy() for x in ba.get_params()], ba.plan_info()
+    da0, e0, p0, plan = run()
+    monkeypatch.setenv("VLGBA_ND_GROUPED", "0")
+    da1, e1, p1, _ = run()
+    assert plan["nd_arcs"] >= 2, plan
+    assert np.array_equal(da0, da1)
+    assert np.array_equal(e0, e1)
+    assert np.array_equal(p0[0], p1[0]) and np.array_equal(p0[1], p1[1])
+
+
+@pytest.mark.parametrize("solver,cap", [("nd", 24), ("envelope", 24), ("nd", 300)])
+def test_trailing_workgroup_cap_bit_identical(gpu, monkeypatch, solver, cap):
+    """VLGBA_TRAIL_WGS caps an envelope launch's workgroups: the trailing
+    pairs of column k-1 then take several pairs per workgroup (strided), each
+    with the same operations -- whole LM runs bit for bit equal to one pair per
+    workgroup."""
+    sc = _scene("ladybug", 300, seed=8)
+    a, b = _params(sc, 6)
+
+    def run():
+        with gpu.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, 6, solver=solver,
+                                stop_rel=1e-9, max_iter=6) as ba:
+            ba.set_params(a, b)
+            err, st = ba.run()
+            return err.copy(), [x.copy() for x in ba.get_params()]
+    e0, p0 = run()
+    monkeypatch.setenv("VLGBA_TRAIL_WGS", str(cap))
+    e1, p1 = run()
+    assert np.array_equal(e0, e1)
+    assert np.array_equal(p0[0], p1[0]) and np.array_equal(p0[1], p1[1])
+
+
 def test_nd_projective(gpu):
     """The projective camera (num_a = 12: 64-row tiles hold 5 1/3 cameras, so
     cameras straddle tiles inside every part) on the nested-dissection order,
