@@ -1857,24 +1857,49 @@ __global__ __launch_bounds__(256) void k_schur_long_acc(const int *__restrict__ 
 #pragma unroll
         for (int j = 0; j < RH; j++)
             acc[i][j] = (i < nr && j < nc) ? sb[(r0 + i) + NA * (c0 + j)] : 0.0;
-    const int p1 = pair_ptr[bk + 1];
-    for (int p = pair_ptr[bk]; p < p1; p++) {
-        const int2 pr = pair[p];
-        const double *y = ylong + (size_t)WS * pr.x + r0;
-        const double *w = W + (size_t)WS * ((size_t)L0 + pr.y) + c0;
-        double yv[3][RH], wv[3][RH];
+    // LA_U pairs per round, all their loads in flight before the first
+    // subtraction (a round costs one memory latency, not LA_U); the next
+    // round's pair indices are fetched during this one.  Past the end a slot
+    // re-reads the block's first pair and takes +0 instead (its term is then
+    // +0 and acc - (+0) is acc bit for bit, -0 included): the subtractions are
+    // unconditional, so the compiler cannot sink a slot's loads behind the
+    // previous slot's arithmetic.
+    constexpr int LA_U = 4;
+    const int pb = pair_ptr[bk], np = pair_ptr[bk + 1] - pb;
+    int2 nx[LA_U];
 #pragma unroll
-        for (int m = 0; m < 3; m++)
+    for (int u = 0; u < LA_U; u++) nx[u] = pair[pb + (u < np ? u : 0)];
+    for (int u0 = 0; u0 < np; u0 += LA_U) {
+        double yv[LA_U][3][RH], wv[LA_U][3][RH];
 #pragma unroll
-            for (int i = 0; i < RH; i++) {
-                yv[m][i] = i < nr ? y[i + NA * m] : 0.0;
-                wv[m][i] = i < nc ? w[i + NA * m] : 0.0;
-            }
+        for (int u = 0; u < LA_U; u++) {
+            const double *y = ylong + (size_t)WS * nx[u].x + r0;
+            const double *w = W + (size_t)WS * ((size_t)L0 + nx[u].y) + c0;
+            const bool ok = u0 + u < np;
 #pragma unroll
-        for (int i = 0; i < RH; i++)
+            for (int m = 0; m < 3; m++)
 #pragma unroll
-            for (int j = 0; j < RH; j++)
-                acc[i][j] -= yv[0][i] * wv[0][j] + yv[1][i] * wv[1][j] + yv[2][i] * wv[2][j];
+                for (int i = 0; i < RH; i++) {
+                    const double a = i < nr ? y[i + NA * m] : 0.0;
+                    const double b = i < nc ? w[i + NA * m] : 0.0;
+                    yv[u][m][i] = ok ? a : 0.0;
+                    wv[u][m][i] = ok ? b : 0.0;
+                }
+        }
+#pragma unroll
+        for (int u = 0; u < LA_U; u++) {
+            const int q = u0 + LA_U + u;
+            nx[u] = pair[pb + (q < np ? q : 0)];
+        }
+#pragma unroll
+        for (int u = 0; u < LA_U; u++) {
+#pragma unroll
+            for (int i = 0; i < RH; i++)
+#pragma unroll
+                for (int j = 0; j < RH; j++)
+                    acc[i][j] -= yv[u][0][i] * wv[u][0][j] + yv[u][1][i] * wv[u][1][j] +
+                                 yv[u][2][i] * wv[u][2][j];
+        }
     }
 #pragma unroll
     for (int i = 0; i < RH; i++)
