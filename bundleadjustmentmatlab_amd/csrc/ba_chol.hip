@@ -34,6 +34,7 @@
 #include "ba_internal.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <utility>
 #include <climits>
@@ -117,6 +118,29 @@ template <bool SC> __device__ __forceinline__ void stg(double *p, double v)
         *p = v;
 }
 
+// fetch_tile / store_tile with device-coherent (sc1) accesses: tiles handed
+// between the envelope runner and the column launches running beside it
+__device__ __forceinline__ void fetch_tile_sc(const double *S, long long lds, int ti, int tj,
+                                              double v[16])
+{
+    const double *base = S + (long long)NB * ti + lds * (long long)NB * tj;
+    const int r = threadIdx.x & 63, c0 = threadIdx.x >> 6;
+#pragma unroll
+    for (int u = 0; u < 16; u++) v[u] = ldg<true>(base + r + lds * (c0 + 4 * u));
+}
+
+__device__ __forceinline__ void store_tile_sc(double *S, long long lds, int ti, int tj,
+                                              const double *T)
+{
+    double *base = S + (long long)NB * ti + lds * (long long)NB * tj;
+    const int r = threadIdx.x & 63, c0 = threadIdx.x >> 6;
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) v[u] = T[r * LP + c0 + 4 * u];
+#pragma unroll
+    for (int u = 0; u < 16; u++) stg<true>(base + r + lds * (c0 + 4 * u), v[u]);
+}
+
 // LDS T[r][c] -> row-major 64x64 dst[r*64 + c]
 __device__ __forceinline__ void store_rowmajor(double *__restrict__ dst, const double *T)
 {
@@ -187,6 +211,7 @@ __device__ __forceinline__ void mfma_64x64(const double *As, const double *Bs, d
 // operands read straight from S (column-major, L2) in the 16x16x4 operand
 // layout instead of from LDS: the same MFMA chain as mfma_64x64 on the
 // loaded tiles, bit for bit, without their 64 KB of LDS.
+template <bool SCB = false>
 __device__ __forceinline__ void mfma_64x64_glb(const double *__restrict__ S, long long lds,
                                                int ia, int jb, int kc, d4 acc[2][2])
 {
@@ -207,8 +232,8 @@ __device__ __forceinline__ void mfma_64x64_glb(const double *__restrict__ S, lon
             const long long kk = lds * (4 * (8 * h + s) + lk);
             a0[s] = A[r0 + li + kk];
             a1[s] = A[r0 + 16 + li + kk];
-            b0[s] = B[c0 + li + kk];
-            b1[s] = B[c0 + 16 + li + kk];
+            b0[s] = ldg<SCB>(B + c0 + li + kk);
+            b1[s] = ldg<SCB>(B + c0 + 16 + li + kk);
         }
 #pragma unroll
         for (int s = 0; s < 8; s++) {
@@ -727,6 +752,59 @@ __device__ __forceinline__ void factor_step_body(double *__restrict__ S, long lo
     FS_END();
 }
 
+// Runner mode (k_env_runner beside the column launches, VLGBA_ENV_RUNNER): a
+// persistent workgroup per run of columns [k0, kend) factors every diagonal
+// tile and forms the first panel tile L_k+1,k itself, so the column launches
+// lose workgroup 0 and that panel.  The tiles the two exchange inside a launch
+// go through sc1 stores / loads and a flag each (epoch = fac_epoch):
+//   lflag[k]   L_k,k-1 stored by the runner (the panels' pending update reads it)
+//   dflag[k]   A_kk's last trailing update (column k-2) stored
+//   uflag[k+1] A_k+1,k's pending update of column k-1 stored (the runner's panel)
+//   pflag[k+1] r_k+1's update by column k-1's panel stored (before the runner's)
+// (a profile: column c reaches row i for every c from row i's first column on,
+// so these are the only writes the runner waits for; every other write it
+// reads was made by a launch that ended before one of those flags was set).
+struct env_rm {
+    unsigned *lflag, *dflag, *uflag, *pflag;
+    int kend;   // the run's end column (exclusive); 0: not in runner mode
+};
+
+// wave 0 spins on flag[idx] == epoch (bounded; timeout: status[1]); all waves
+// then pass a barrier.  Returns false on a timeout.
+__device__ __forceinline__ bool env_wait(const unsigned *flag, int idx, unsigned epoch,
+                                         double *status)
+{
+    __shared__ int to;
+    const int tid = threadIdx.x;
+    if (tid < 64) {
+        bool ok = false;
+        for (unsigned spins = 0; spins < BA_BACK_SPIN_MAX; spins++) {
+            const unsigned f = __hip_atomic_load((const gu32_t *)(flag + idx), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            if (f == epoch) {
+                ok = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (tid == 0) {
+            to = ok ? 0 : 1;
+            if (!ok) status[1] = 1.0;
+        }
+    }
+    __syncthreads();
+    return to == 0;
+}
+
+__device__ __forceinline__ void env_publish(unsigned *flag, int idx, unsigned epoch)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store((gu32_t *)(flag + idx), epoch, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // factor_step_body with the in-launch hand-off on two LDS tiles instead of
 // three (two workgroups per CU): the pending updates' operands come straight
 // from S (mfma_64x64_glb), workgroup 0 factors in As -> Bs, a panel keeps
@@ -740,7 +818,7 @@ __device__ __forceinline__ void factor_step_two(double *__restrict__ S, long lon
                                                 double *__restrict__ y,
                                                 double *__restrict__ status, int b, int sep0,
                                                 unsigned *__restrict__ kflag, unsigned epoch,
-                                                int ntr, int tstride)
+                                                int ntr, int tstride, env_rm R = env_rm{})
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double *As = sm, *Bs = sm + NB * LP;
@@ -770,9 +848,19 @@ __device__ __forceinline__ void factor_step_two(double *__restrict__ S, long lon
             __syncthreads();
             acc_to_lds(acc, As, -1.0, true);
             __syncthreads();
-            store_tile(S, lds, i, j, As);
+            if (R.kend && i == k + 1 && j == k + 1 && k + 1 < R.kend) {
+                // A_k+1,k+1's last trailing update: the runner reads it at column k+1
+                store_tile_sc(S, lds, i, j, As);
+                env_publish(R.dflag, k + 1, epoch);
+            } else {
+                store_tile(S, lds, i, j, As);
+            }
             __syncthreads();   // As read by every thread before the next pair's put
         }
+        FS_END();
+        return;
+    }
+    if (b == 0 && R.kend) {   // the runner factors A_kk
         FS_END();
         return;
     }
@@ -815,10 +903,27 @@ __device__ __forceinline__ void factor_step_two(double *__restrict__ S, long lon
         for (int t0 = 1; t0 < Tp && !iin; t0 += 64)
             iin = __any(t0 + lane < Tp && prev[t0 + lane] == i);
     }
-    if (iin) mfma_64x64_glb(S, lds, i, k, k - 1, acc);
+    const bool lrun = R.kend && i == k + 1 && k + 1 < R.kend;   // the runner's panel
+    if (lrun && !iin) {   // no pending update: the runner reads A_k+1,k as it is
+        FS_END();
+        return;
+    }
+    if (iin && R.kend) {   // L_k,k-1 is the runner's
+        if (!env_wait(R.lflag, k, epoch, status)) return;
+        mfma_64x64_glb<true>(S, lds, i, k, k - 1, acc);
+    } else if (iin) {
+        mfma_64x64_glb(S, lds, i, k, k - 1, acc);
+    }
     put_tile(As, vc, false);
     __syncthreads();
     if (iin) acc_to_lds(acc, As, -1.0, true);
+    if (lrun) {   // A_k+1,k after its pending update, for the runner
+        __syncthreads();
+        store_tile_sc(S, lds, i, k, As);
+        env_publish(R.uflag, k + 1, epoch);
+        FS_END();
+        return;
+    }
     if (tid < 64) {   // wave 0 waits for workgroup 0's flag
         for (unsigned spins = 0;; spins++) {
             const unsigned f = __hip_atomic_load((const gu32_t *)(kflag + k), __ATOMIC_RELAXED,
@@ -852,7 +957,15 @@ __device__ __forceinline__ void factor_step_two(double *__restrict__ S, long lon
     store_tile(S, lds, i, k, As);
     double ri[1];
     gemv64(As, yk, part, nullptr, 1.0, ri);   // (L_ik y_k)[tid] for tid < 64
-    if (tid < NB && i < sep0) rhs[(long long)NB * i + tid] -= ri[0];
+    if (R.kend && i == k + 2 && k + 2 < R.kend) {   // the runner updates r_k+2 next
+        if (tid < NB) {
+            double *rp = rhs + (long long)NB * i + tid;
+            stg<true>(rp, ldg<true>(rp) - ri[0]);
+        }
+        env_publish(R.pflag, k + 2, epoch);
+    } else if (tid < NB && i < sep0) {
+        rhs[(long long)NB * i + tid] -= ri[0];
+    }
     FS_ST(3);
     FS_END();
 }
@@ -865,11 +978,11 @@ __global__ __launch_bounds__(256) void k_factor_step(double *__restrict__ S, lon
                                                      double *__restrict__ y,
                                                      double *__restrict__ status,
                                                      unsigned *__restrict__ kflag, unsigned epoch,
-                                                     int ntr, int tstride)
+                                                     int ntr, int tstride, env_rm R)
 {
     if (kflag)
         factor_step_two(S, lds, k, pan, T, prev, Tp, linv, rhs, y, status, blockIdx.x, INT_MAX,
-                        kflag, epoch, ntr, tstride);
+                        kflag, epoch, ntr, tstride, R);
     else
         factor_step_body(S, lds, k, pan, T, prev, Tp, linv, rhs, y, status, blockIdx.x, INT_MAX,
                          nullptr, 0);
@@ -889,6 +1002,7 @@ struct nd_step {
     int np, grouped;
     int k[BA_ND_MAX], T[BA_ND_MAX], Tp[BA_ND_MAX], pofs[BA_ND_MAX], qofs[BA_ND_MAX];
     int ntr[BA_ND_MAX], ts[BA_ND_MAX];   // trailing pairs / their workgroups (stride)
+    int kend[BA_ND_MAX];                 // runner mode: arc t's end column (else 0)
     int b0[BA_ND_MAX + 1], pb[BA_ND_MAX + 1], tb[BA_ND_MAX + 1];
 };
 
@@ -900,7 +1014,7 @@ __global__ __launch_bounds__(256) void k_factor_multi(double *__restrict__ S, lo
                                                       double *__restrict__ y,
                                                       double *__restrict__ status,
                                                       unsigned *__restrict__ kflag,
-                                                      unsigned epoch)
+                                                      unsigned epoch, env_rm R)
 {
     const int b = blockIdx.x, np = P.np;
     int t = 0, role;
@@ -919,13 +1033,117 @@ __global__ __launch_bounds__(256) void k_factor_multi(double *__restrict__ S, lo
         while (t + 1 < np && q >= P.tb[t + 1]) t++;
         role = 1 + P.T[t] + q - P.tb[t];
     }
+    R.kend = P.kend[t];
     if (kflag)
         factor_step_two(S, lds, P.k[t], pan_list + P.pofs[t], P.T[t], pan_list + P.qofs[t],
                         P.Tp[t], linv, rhs, y, status, role, sep0, kflag, epoch, P.ntr[t],
-                        P.ts[t]);
+                        P.ts[t], R);
     else
         factor_step_body(S, lds, P.k[t], pan_list + P.pofs[t], P.T[t], pan_list + P.qofs[t],
                          P.Tp[t], linv, rhs, y, status, role, sep0, nullptr, 0);
+}
+
+// ---------------------------------------------------------------------------
+// k_env_runner: one persistent workgroup per run of columns [k0[t], k1[t])
+// (the nested dissection's arcs side by side, or the natural order's one run),
+// launched on the side stream beside the per-column launches.  Per column k:
+//   A_kk (after its last trailing update: dflag[k] when column k-2 reaches row
+//   k) and column k-1's pending update from the workgroup's own LDS copy of
+//   L_k,k-1; the factor, L_kk^-1, y_k, published (kflag[k]) exactly as
+//   factor_step_two's workgroup 0; then, when row k+1 is in column k's panel,
+//   L_k+1,k = A_k+1,k L_kk^-T (after column k-1's panel's r_k+1 update, pflag,
+//   and its pending update, uflag) stored with sc1, r_k+1 -= L_k+1,k y_k, lflag[k+1] --
+//   the tile stays in LDS for column k+1.  Every tile sees the same operations
+//   in the same order as in the column launches alone: bit-identical.  A wait
+//   that gives up sets status[1] and ends the workgroup (the host re-solves
+//   without hand-offs).
+// ---------------------------------------------------------------------------
+struct env_runs {
+    int np;
+    int k0[BA_ND_MAX], k1[BA_ND_MAX];
+};
+
+__global__ __launch_bounds__(256) void k_env_runner(double *S, long long lds,
+                                                    const int *__restrict__ pan_ptr,
+                                                    const int *__restrict__ pan_list, env_runs Rn,
+                                                    double *linv, double *rhs, double *y,
+                                                    double *status, unsigned *kflag,
+                                                    env_rm R, unsigned epoch)
+{
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double *As = sm, *Bs = sm + NB * LP;
+    double *Ls = sm + 2 * NB * LP, *Ps = sm + 3 * NB * LP;
+    __shared__ double yk[NB], rk[NB];
+    __shared__ double part[4][NB];
+    const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    if (t >= Rn.np) return;
+    const int k0 = Rn.k0[t], k1 = Rn.k1[t];
+    bool have_l = false;   // Ls holds L_k,k-1
+    d4 acc[2][2];
+    // row i among column c's panel rows (a wave-wide search, every wave)
+    auto reaches = [&](int c, int i) {
+        const int q0 = pan_ptr[c], n = pan_ptr[c + 1] - q0;
+        bool f = false;
+        for (int u = 0; u < n && !f; u += 64) f = __any(u + lane < n && pan_list[q0 + u + lane] == i);
+        return f;
+    };
+    for (int k = k0; k < k1; k++) {
+        const int p0 = pan_ptr[k], T = pan_ptr[k + 1] - p0;
+        if (k - 2 >= k0 && reaches(k - 2, k) && !env_wait(R.dflag, k, epoch, status)) return;
+        double vk[16];
+        fetch_tile_sc(S, lds, k, k, vk);
+        if (tid < NB) rk[tid] = ldg<true>(rhs + (long long)NB * k + tid);
+        if (have_l) mfma_64x64(Ls, Ls, acc);
+        __syncthreads();
+        put_tile(As, vk, false);
+        __syncthreads();
+        if (have_l) {
+            acc_to_lds(acc, As, -1.0, true);
+            __syncthreads();
+        }
+        const bool ok = potrf64_via32(As, Bs, As + 32);
+        gemv64(Bs, rk, part, yk, 1.0);   // y_k = L^-1 r_k
+        {
+            double *lo = linv + (long long)NB * NB * k;
+            for (int q = tid; q < NB * NB; q += blockDim.x)
+                stg<true>(lo + q, Bs[(q >> 6) * LP + (q & 63)]);
+            if (tid < NB) stg<true>(y + (long long)NB * k + tid, yk[tid]);
+            if (tid == 0 && !ok) status[0] = 1.0;
+        }
+        env_publish(kflag, k, epoch);
+        have_l = false;
+        if (k + 1 < k1 && T > 0 && pan_list[p0] == k + 1) {
+            // launch k-1 ended (its trailing update of A_k+1,k and its panel's
+            // r_k+1 update), and column k-1's pending update of A_k+1,k stored
+            if (k > k0 && reaches(k - 1, k + 1)) {
+                // column k-1's panel updated r_k+1; its pending update of A_k+1,k
+                if (!env_wait(R.pflag, k + 1, epoch, status)) return;
+                const bool kin = pan_ptr[k] > pan_ptr[k - 1] && pan_list[pan_ptr[k - 1]] == k;
+                if (kin && !env_wait(R.uflag, k + 1, epoch, status)) return;
+            }
+            double va[16];
+            fetch_tile_sc(S, lds, k + 1, k, va);
+            put_tile(Ps, va, false);
+            __syncthreads();
+            mfma_64x64(Ps, Bs, acc);   // L[r][c] = sum_t A[r][t] Li[c][t]
+            __syncthreads();
+            acc_to_lds(acc, Ps, 1.0, false);
+            __syncthreads();
+            store_tile_sc(S, lds, k + 1, k, Ps);
+            double ri[1];
+            gemv64(Ps, yk, part, nullptr, 1.0, ri);   // (L y_k)[tid] for tid < 64
+            if (tid < NB) {
+                double *rp = rhs + (long long)NB * (k + 1) + tid;
+                stg<true>(rp, ldg<true>(rp) - ri[0]);
+            }
+            env_publish(R.lflag, k + 1, epoch);
+            double *sw = Ls;
+            Ls = Ps;
+            Ps = sw;
+            have_l = true;
+        }
+        __syncthreads();
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -3258,6 +3476,13 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
         TRY_RC(dev_alloc(&d->kflag, sizeof(unsigned) * (size_t)nt));
         VLGBA_CHECK(hipMemsetAsync(d->kflag, 0, sizeof(unsigned) * (size_t)nt, d->stream));
         d->fac_epoch = 0;
+        // runner mode's flags: lflag | dflag | uflag | pflag, nt each
+        const char *er = std::getenv("VLGBA_ENV_RUNNER");
+        d->env_runner = er && er[0] == '1';
+        if (d->env_runner && d->pan_ptr) {
+            TRY_RC(dev_alloc(&d->rflag, sizeof(unsigned) * 4 * (size_t)nt));
+            VLGBA_CHECK(hipMemsetAsync(d->rflag, 0, sizeof(unsigned) * 4 * (size_t)nt, d->stream));
+        }
     }
     TRY_RC(dev_alloc(&d->env_tiles, sizeof(int) * (env.size() + 1)));
     if (!list.empty())
@@ -3290,6 +3515,8 @@ void ba_chol_free(ba_dev *d)
     d->cr_eptr_h = d->cr_kptr_h = nullptr;
     if (d->xgran) ba_dfree(d->xgran);
     d->xgran = nullptr;
+    if (d->rflag) ba_dfree(d->rflag);
+    d->rflag = nullptr;
     if (d->crflag) ba_dfree(d->crflag);
     d->crflag = nullptr;
     d->cr_fused = 0;
@@ -3367,6 +3594,42 @@ static int trail_wgs(const ba_dev *d, int ntr, int other)
     return std::max(1, std::min(ntr, d->trail_cap - other));
 }
 
+// runner mode (k_env_runner) for this factorization?  Needs the hand-off, the
+// device panel pointers and the flags; off under per-kernel timing (one stream)
+// and, for the rest of the process, after any runner hand-off gave up: the
+// runner needs its side stream on a hardware queue of its own (with the
+// library stream's column launches queued behind it on a shared queue every
+// wait times out)
+static std::atomic<int> g_env_runner_off{0};
+
+void ba_env_runner_disable() { g_env_runner_off.store(1); }
+
+static bool env_run_on(const ba_dev *d, const unsigned *kflag)
+{
+    return d->env_runner && kflag && d->pan_ptr && d->rflag && d->side &&
+           !(d->kt && d->kt->on) && !g_env_runner_off.load();
+}
+
+static env_rm env_rm_of(const ba_dev *d, int kend)
+{
+    return env_rm{d->rflag, d->rflag + d->nt, d->rflag + 2 * (size_t)d->nt,
+                  d->rflag + 3 * (size_t)d->nt, kend};
+}
+
+// fork the side stream off the library stream and start the runner there
+static int env_runner_start(ba_dev *d, const env_runs &Rn, long long L, double *rhs)
+{
+    const size_t smem4 = sizeof(double) * 4 * NB * LP;
+    TRY_RC(ba_ensure_dyn_lds((const void *)k_env_runner, smem4));
+    VLGBA_CHECK(hipEventRecord(d->ev_fork, d->stream));
+    VLGBA_CHECK(hipStreamWaitEvent(d->side, d->ev_fork, 0));
+    k_env_runner<<<Rn.np, 256, smem4, d->side>>>(d->S, L, d->pan_ptr, d->pan_list, Rn, d->linv,
+                                                 rhs, d->ywork, d->scal + 4, d->kflag,
+                                                 env_rm_of(d, 0), d->fac_epoch);
+    VLGBA_CHECK(hipEventRecord(d->ev_join, d->side));
+    return -(int)hipGetLastError();
+}
+
 // the envelope's tile columns k0 .. k1-1 (k_factor_step), column k0 taking no
 // pending update of column k0-1
 static void envelope_columns(ba_dev *d, int k0, int k1, long long L, double *rhs,
@@ -3374,6 +3637,14 @@ static void envelope_columns(ba_dev *d, int k0, int k1, long long L, double *rhs
 {
     // two LDS tiles with the hand-off (two workgroups per CU), three without
     const size_t smem3 = sizeof(double) * 3 * NB * LP, smem2 = sizeof(double) * 2 * NB * LP;
+    const bool run = env_run_on(d, kflag) && k1 > k0;
+    if (run) {
+        env_runs Rn{};
+        Rn.np = 1;
+        Rn.k0[0] = k0;
+        Rn.k1[0] = k1;
+        if (env_runner_start(d, Rn, L, rhs)) return;
+    }
     for (int k = k0; k < k1; k++) {
         const int p0 = d->pan_ptr_h[k], T = d->pan_ptr_h[k + 1] - p0;
         const int q0 = k > k0 ? d->pan_ptr_h[k - 1] : 0, Tp = k > k0 ? p0 - q0 : 0;
@@ -3385,9 +3656,10 @@ static void envelope_columns(ba_dev *d, int k0, int k1, long long L, double *rhs
         KT_B(d);
         k_factor_step<<<1 + T + nw, 256, kflag ? smem2 : smem3, d->stream>>>(
             d->S, L, k, d->pan_list + p0, T, d->pan_list + q0, Tp, d->linv, rhs, d->ywork,
-            d->scal + 4, kflag, d->fac_epoch, ntr, nw);
+            d->scal + 4, kflag, d->fac_epoch, ntr, nw, env_rm_of(d, run ? k1 : 0));
         KT_E(d, KT_FACTOR);
     }
+    if (run) (void)hipStreamWaitEvent(d->stream, d->ev_join, 0);
 }
 
 // x = L^-T y of the envelope factor (ywork holds y; consumed)
@@ -3533,6 +3805,16 @@ int ba_chol_solve(ba_dev *d, int nospin)
         TRY_RC(ba_ensure_dyn_lds((const void *)k_factor_multi, smem3));
         int nsteps = 0;
         for (int t = 0; t < np; t++) nsteps = std::max(nsteps, d->nd_a0[t + 1] - d->nd_a0[t]);
+        const bool run = env_run_on(d, kflag);
+        if (run) {
+            env_runs Rn{};
+            Rn.np = np;
+            for (int t = 0; t < np; t++) {
+                Rn.k0[t] = d->nd_a0[t];
+                Rn.k1[t] = d->nd_a0[t + 1];
+            }
+            TRY_RC(env_runner_start(d, Rn, L, d->nd_rhs));
+        }
         for (int st = 0; st < nsteps; st++) {
             nd_step P{};
             P.grouped = d->nd_grouped;
@@ -3554,6 +3836,7 @@ int ba_chol_solve(ba_dev *d, int nospin)
                 P.qofs[u] = q0;
                 const int ntr = Tr * (Tr + 1) / 2 - nsr * (nsr + 1) / 2;
                 P.ntr[u] = ntr;
+                P.kend[u] = run ? d->nd_a0[t + 1] : 0;
                 P.b0[u] = nbk;
                 P.pb[u + 1] = P.pb[u] + T;
                 nbk += 1 + T;
@@ -3583,9 +3866,10 @@ int ba_chol_solve(ba_dev *d, int nospin)
             k_factor_multi<<<nbk, 256, kflag ? sizeof(double) * 2 * NB * LP : smem3, d->stream>>>(
                 d->S, L, d->pan_list, P, s0, d->linv,
                                                           d->nd_rhs, d->ywork, d->scal + 4, kflag,
-                                                          d->fac_epoch);
+                                                          d->fac_epoch, env_rm_of(d, 0));
             KT_E(d, KT_FACTOR);
         }
+        if (run) VLGBA_CHECK(hipStreamWaitEvent(d->stream, d->ev_join, 0));
         if (d->nd_nrec > 0) {
             const size_t smem2 = sizeof(double) * 2 * NB * LP;
             TRY_RC(ba_ensure_dyn_lds((const void *)k_sep_update, smem2));

@@ -127,6 +127,8 @@ struct ba_dev {
     unsigned long long *xgran64;  // [nt][128] x_k granules of the one-launch backward
     unsigned *kflag;   // [nt] envelope factor: L_kk^-1 / y_k published (epoch fac_epoch)
     unsigned fac_epoch;
+    unsigned *rflag;    // [4 nt] runner mode's flags (k_env_runner; VLGBA_ENV_RUNNER=1)
+    int env_runner;
     int *env_tiles;    // device [n_env][2] (i, k) tiles inside the envelope
     int *tb_ptr, *tb_blk;  // device: per envelope tile, the co-visible blocks overlapping it
     int n_env;
@@ -345,6 +347,7 @@ void *ba_dmalloc(size_t bytes);   // per-device caching allocator (ba_solver.cpp
 // per (kernel, device), thread-safe; ba_solver.cpp)
 int ba_ensure_dyn_lds(const void *fn, size_t bytes);
 void ba_dfree(void *p);
+void ba_env_runner_disable();   // after a runner hand-off timeout (ba_chol.hip)
 int ba_launch_schur_fast(ba_dev *d, double lambda);   // fused damp + Vinv + Y + S + e_
 // long tracks: count (fill = 0, into cnt[nb]) / write (fill = 1, at lpair_ptr) the
 // per-block (obs, obs) pairs of k_schur_reduce (context setup)

@@ -2076,6 +2076,11 @@ static int resolve_nospin(vlgba_ctx *c, double lam, double hs[6])
     if (d.parity) TRY(ba_launch_parity_new_sums(&d, lam));
     TRY(collect_scalars(c, false, hs));
     c->spin_retries++;
+    // a hand-off that gave up under the envelope runner (most likely its side
+    // stream sharing a hardware queue with the library stream, so the column
+    // launches queue behind it): the column launches alone from now on
+    if (d.env_runner) ba_env_runner_disable();
+    d.env_runner = 0;
     return 0;
 }
 

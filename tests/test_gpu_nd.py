@@ -186,6 +186,36 @@ def test_trailing_workgroup_cap_bit_identical(gpu, monkeypatch, solver, cap):
     assert np.array_equal(p0[0], p1[0]) and np.array_equal(p0[1], p1[1])
 
 
+@pytest.mark.parametrize("solver,m,num_a", [("nd", 300, 6), ("envelope", 300, 6),
+                                             ("nd", 90, 7), ("envelope", 120, 10)])
+def test_env_runner_bit_identical(gpu, monkeypatch, solver, m, num_a):
+    """Runner mode (VLGBA_ENV_RUNNER=1: k_env_runner, one persistent workgroup
+    per arc on the side stream, factors the diagonal tiles and forms each
+    column's first panel tile while the column launches run the other panels
+    and the trailing updates; the tiles they exchange go through sc1 stores
+    and flags) against the column launches alone: the same operations in the
+    same order on every tile, so whole LM runs agree bit for bit, and no
+    hand-off gives up (no re-solve)."""
+    sc = _scene("ladybug", m, seed=12)
+    a, b = _params(sc, num_a)
+
+    def run():
+        with gpu.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, num_a,
+                                solver=solver, stop_rel=1e-9, max_iter=8) as ba:
+            ba.set_params(a, b)
+            ba.step(relinearize=True, update_lm=False)
+            da, db = ba.last_step()
+            err, st = ba.run()
+            return da.copy(), err.copy(), st, [x.copy() for x in ba.get_params()]
+    da0, e0, s0, p0 = run()
+    monkeypatch.setenv("VLGBA_ENV_RUNNER", "1")
+    da1, e1, s1, p1 = run()
+    assert s1.spin_retries == 0 and s0.spin_retries == 0
+    assert np.array_equal(da0, da1)
+    assert np.array_equal(e0, e1)
+    assert np.array_equal(p0[0], p1[0]) and np.array_equal(p0[1], p1[1])
+
+
 def test_nd_projective(gpu):
     """The projective camera (num_a = 12: 64-row tiles hold 5 1/3 cameras, so
     cameras straddle tiles inside every part) on the nested-dissection order,
