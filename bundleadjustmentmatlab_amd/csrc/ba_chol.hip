@@ -3482,6 +3482,15 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
         if (d->env_runner && d->pan_ptr) {
             TRY_RC(dev_alloc(&d->rflag, sizeof(unsigned) * 4 * (size_t)nt));
             VLGBA_CHECK(hipMemsetAsync(d->rflag, 0, sizeof(unsigned) * 4 * (size_t)nt, d->stream));
+            // the runner's own stream, at the highest priority: a hardware
+            // queue apart from the library stream's
+            if (!d->rstream) {
+                int lo = 0, hi = 0;
+                (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+                if (hipStreamCreateWithPriority(&d->rstream, hipStreamNonBlocking, hi) !=
+                    hipSuccess)
+                    d->rstream = nullptr;
+            }
         }
     }
     TRY_RC(dev_alloc(&d->env_tiles, sizeof(int) * (env.size() + 1)));
@@ -3517,6 +3526,11 @@ void ba_chol_free(ba_dev *d)
     d->xgran = nullptr;
     if (d->rflag) ba_dfree(d->rflag);
     d->rflag = nullptr;
+    if (d->rstream) {
+        (void)hipStreamSynchronize(d->rstream);
+        (void)hipStreamDestroy(d->rstream);
+    }
+    d->rstream = nullptr;
     if (d->crflag) ba_dfree(d->crflag);
     d->crflag = nullptr;
     d->cr_fused = 0;
@@ -3602,11 +3616,16 @@ static int trail_wgs(const ba_dev *d, int ntr, int other)
 // wait times out)
 static std::atomic<int> g_env_runner_off{0};
 
-void ba_env_runner_disable() { g_env_runner_off.store(1); }
+void ba_env_runner_disable()
+{
+    if (!g_env_runner_off.exchange(1))
+        std::fprintf(stderr, "[vlgba] envelope runner off for this process: a hand-off timed "
+                             "out (its stream shares a hardware queue?)\n");
+}
 
 static bool env_run_on(const ba_dev *d, const unsigned *kflag)
 {
-    return d->env_runner && kflag && d->pan_ptr && d->rflag && d->side &&
+    return d->env_runner && kflag && d->pan_ptr && d->rflag && d->rstream &&
            !(d->kt && d->kt->on) && !g_env_runner_off.load();
 }
 
@@ -3622,11 +3641,11 @@ static int env_runner_start(ba_dev *d, const env_runs &Rn, long long L, double *
     const size_t smem4 = sizeof(double) * 4 * NB * LP;
     TRY_RC(ba_ensure_dyn_lds((const void *)k_env_runner, smem4));
     VLGBA_CHECK(hipEventRecord(d->ev_fork, d->stream));
-    VLGBA_CHECK(hipStreamWaitEvent(d->side, d->ev_fork, 0));
-    k_env_runner<<<Rn.np, 256, smem4, d->side>>>(d->S, L, d->pan_ptr, d->pan_list, Rn, d->linv,
-                                                 rhs, d->ywork, d->scal + 4, d->kflag,
-                                                 env_rm_of(d, 0), d->fac_epoch);
-    VLGBA_CHECK(hipEventRecord(d->ev_join, d->side));
+    VLGBA_CHECK(hipStreamWaitEvent(d->rstream, d->ev_fork, 0));
+    k_env_runner<<<Rn.np, 256, smem4, d->rstream>>>(d->S, L, d->pan_ptr, d->pan_list, Rn,
+                                                    d->linv, rhs, d->ywork, d->scal + 4,
+                                                    d->kflag, env_rm_of(d, 0), d->fac_epoch);
+    VLGBA_CHECK(hipEventRecord(d->ev_join, d->rstream));
     return -(int)hipGetLastError();
 }
 

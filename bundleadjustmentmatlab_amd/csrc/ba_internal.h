@@ -129,6 +129,7 @@ struct ba_dev {
     unsigned fac_epoch;
     unsigned *rflag;    // [4 nt] runner mode's flags (k_env_runner; VLGBA_ENV_RUNNER=1)
     int env_runner;
+    hipStream_t rstream;   // the runner's stream (highest priority)
     int *env_tiles;    // device [n_env][2] (i, k) tiles inside the envelope
     int *tb_ptr, *tb_blk;  // device: per envelope tile, the co-visible blocks overlapping it
     int n_env;
