@@ -35,6 +35,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <mutex>
 #include <cstdio>
 #include <utility>
 #include <climits>
@@ -3482,15 +3483,6 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
         if (d->env_runner && d->pan_ptr) {
             TRY_RC(dev_alloc(&d->rflag, sizeof(unsigned) * 4 * (size_t)nt));
             VLGBA_CHECK(hipMemsetAsync(d->rflag, 0, sizeof(unsigned) * 4 * (size_t)nt, d->stream));
-            // the runner's own stream, at the highest priority: a hardware
-            // queue apart from the library stream's
-            if (!d->rstream) {
-                int lo = 0, hi = 0;
-                (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-                if (hipStreamCreateWithPriority(&d->rstream, hipStreamNonBlocking, hi) !=
-                    hipSuccess)
-                    d->rstream = nullptr;
-            }
         }
     }
     TRY_RC(dev_alloc(&d->env_tiles, sizeof(int) * (env.size() + 1)));
@@ -3526,11 +3518,7 @@ void ba_chol_free(ba_dev *d)
     d->xgran = nullptr;
     if (d->rflag) ba_dfree(d->rflag);
     d->rflag = nullptr;
-    if (d->rstream) {
-        (void)hipStreamSynchronize(d->rstream);
-        (void)hipStreamDestroy(d->rstream);
-    }
-    d->rstream = nullptr;
+    d->rstream = nullptr;   // the process's (env_runner_stream)
     if (d->crflag) ba_dfree(d->crflag);
     d->crflag = nullptr;
     d->cr_fused = 0;
@@ -3623,10 +3611,47 @@ void ba_env_runner_disable()
                              "out (its stream shares a hardware queue?)\n");
 }
 
-static bool env_run_on(const ba_dev *d, const unsigned *kflag)
+// runs shorter than VLGBA_ENV_RUNNER_MIN columns (default 8) keep the column
+// launches alone: the fork / join of the runner's stream (two cross-stream
+// event waits a factorization) outweighs a few columns' savings (~3-5 us each)
+static int env_run_min()
 {
-    return d->env_runner && kflag && d->pan_ptr && d->rflag && d->rstream &&
-           !(d->kt && d->kt->on) && !g_env_runner_off.load();
+    const char *e = std::getenv("VLGBA_ENV_RUNNER_MIN");
+    return e ? std::max(1, std::atoi(e)) : 8;
+}
+
+// the runner's stream: one per device for the process, at the highest
+// priority, made on first use (a stream per context cost ~1 ms a context in
+// the growing replay).  Two contexts factoring on one device at once
+// serialise their runners; the later one's hand-offs may then give up (the
+// re-solve path) -- correct, only slower.
+static hipStream_t env_runner_stream()
+{
+    static std::mutex mu;
+    static hipStream_t st[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!st[dev]) {
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        if (hipStreamCreateWithPriority(&st[dev], hipStreamNonBlocking, hi) != hipSuccess)
+            st[dev] = nullptr;
+    }
+    return st[dev];
+}
+
+static bool env_run_on(ba_dev *d, const unsigned *kflag, int ncols)
+{
+    if (!(d->env_runner && kflag && d->pan_ptr && d->rflag && !(d->kt && d->kt->on) &&
+          !g_env_runner_off.load() && ncols >= env_run_min()))
+        return false;
+    if (!d->rstream) d->rstream = env_runner_stream();
+    if (!d->rstream) {
+        d->env_runner = 0;
+        return false;
+    }
+    return true;
 }
 
 static env_rm env_rm_of(const ba_dev *d, int kend)
@@ -3656,7 +3681,7 @@ static void envelope_columns(ba_dev *d, int k0, int k1, long long L, double *rhs
 {
     // two LDS tiles with the hand-off (two workgroups per CU), three without
     const size_t smem3 = sizeof(double) * 3 * NB * LP, smem2 = sizeof(double) * 2 * NB * LP;
-    const bool run = env_run_on(d, kflag) && k1 > k0;
+    const bool run = k1 > k0 && env_run_on(d, kflag, k1 - k0);
     if (run) {
         env_runs Rn{};
         Rn.np = 1;
@@ -3824,7 +3849,7 @@ int ba_chol_solve(ba_dev *d, int nospin)
         TRY_RC(ba_ensure_dyn_lds((const void *)k_factor_multi, smem3));
         int nsteps = 0;
         for (int t = 0; t < np; t++) nsteps = std::max(nsteps, d->nd_a0[t + 1] - d->nd_a0[t]);
-        const bool run = env_run_on(d, kflag);
+        const bool run = env_run_on(d, kflag, nsteps);
         if (run) {
             env_runs Rn{};
             Rn.np = np;

@@ -209,6 +209,7 @@ def test_env_runner_bit_identical(gpu, monkeypatch, solver, m, num_a):
             return da.copy(), err.copy(), st, [x.copy() for x in ba.get_params()]
     da0, e0, s0, p0 = run()
     monkeypatch.setenv("VLGBA_ENV_RUNNER", "1")
+    monkeypatch.setenv("VLGBA_ENV_RUNNER_MIN", "1")   # these runs are short
     da1, e1, s1, p1 = run()
     assert s1.spin_retries == 0 and s0.spin_retries == 0
     assert np.array_equal(da0, da1)
