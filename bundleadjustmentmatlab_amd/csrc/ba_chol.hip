@@ -753,7 +753,8 @@ __device__ __forceinline__ void factor_step_body(double *__restrict__ S, long lo
     FS_END();
 }
 
-// Runner mode (k_env_runner beside the column launches, VLGBA_ENV_RUNNER): a
+// Runner mode (k_env_runner beside the column launches; the default,
+// VLGBA_ENV_RUNNER=0 turns it off): a
 // persistent workgroup per run of columns [k0, kend) factors every diagonal
 // tile and forms the first panel tile L_k+1,k itself, so the column launches
 // lose workgroup 0 and that panel.  The tiles the two exchange inside a launch
@@ -3478,8 +3479,8 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
         VLGBA_CHECK(hipMemsetAsync(d->kflag, 0, sizeof(unsigned) * (size_t)nt, d->stream));
         d->fac_epoch = 0;
         // runner mode's flags: lflag | dflag | uflag | pflag, nt each
-        const char *er = std::getenv("VLGBA_ENV_RUNNER");
-        d->env_runner = er && er[0] == '1';
+        const char *er = std::getenv("VLGBA_ENV_RUNNER");   // "0": the column launches alone
+        d->env_runner = !(er && er[0] == '0');
         if (d->env_runner && d->pan_ptr) {
             TRY_RC(dev_alloc(&d->rflag, sizeof(unsigned) * 4 * (size_t)nt));
             VLGBA_CHECK(hipMemsetAsync(d->rflag, 0, sizeof(unsigned) * 4 * (size_t)nt, d->stream));

@@ -127,7 +127,7 @@ struct ba_dev {
     unsigned long long *xgran64;  // [nt][128] x_k granules of the one-launch backward
     unsigned *kflag;   // [nt] envelope factor: L_kk^-1 / y_k published (epoch fac_epoch)
     unsigned fac_epoch;
-    unsigned *rflag;    // [4 nt] runner mode's flags (k_env_runner; VLGBA_ENV_RUNNER=1)
+    unsigned *rflag;    // [4 nt] runner mode's flags (k_env_runner; off: VLGBA_ENV_RUNNER=0)
     int env_runner;
     hipStream_t rstream;   // the runner's stream (highest priority)
     int *env_tiles;    // device [n_env][2] (i, k) tiles inside the envelope

@@ -189,7 +189,7 @@ def test_trailing_workgroup_cap_bit_identical(gpu, monkeypatch, solver, cap):
 @pytest.mark.parametrize("solver,m,num_a", [("nd", 300, 6), ("envelope", 300, 6),
                                              ("nd", 90, 7), ("envelope", 120, 10)])
 def test_env_runner_bit_identical(gpu, monkeypatch, solver, m, num_a):
-    """Runner mode (VLGBA_ENV_RUNNER=1: k_env_runner, one persistent workgroup
+    """Runner mode (the default; VLGBA_ENV_RUNNER=0 turns it off: k_env_runner, one persistent workgroup
     per arc on the side stream, factors the diagonal tiles and forms each
     column's first panel tile while the column launches run the other panels
     and the trailing updates; the tiles they exchange go through sc1 stores
@@ -207,6 +207,7 @@ def test_env_runner_bit_identical(gpu, monkeypatch, solver, m, num_a):
             da, db = ba.last_step()
             err, st = ba.run()
             return da.copy(), err.copy(), st, [x.copy() for x in ba.get_params()]
+    monkeypatch.setenv("VLGBA_ENV_RUNNER", "0")
     da0, e0, s0, p0 = run()
     monkeypatch.setenv("VLGBA_ENV_RUNNER", "1")
     monkeypatch.setenv("VLGBA_ENV_RUNNER_MIN", "1")   # these runs are short
