@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # variant, tools/ab_build.sh); the package's own build otherwise
 LIB_PATH = os.environ.get("VLGBA_LIB") or os.path.join(_HERE, "libvlgba.so")
 
-ABI_VERSION = 4   # VLGBA_ABI_VERSION: the struct layouts below
+ABI_VERSION = 5   # VLGBA_ABI_VERSION: the struct layouts below
 
 c_int, c_double, c_ll = ctypes.c_int, ctypes.c_double, ctypes.c_longlong
 c_dp = ctypes.POINTER(ctypes.c_double)
@@ -120,7 +120,6 @@ SIGNATURES = {
     "vlgba_comm_release": (c_int, [ctypes.c_void_p]),
     "vlgba_device_count": (c_int, []),
     "vlgba_debug_sincos": (c_int, [c_dp, c_dp, c_dp, c_ll]),
-    "vlgba_debug_dehom": (c_int, [c_dp, c_dp, c_dp, c_ip, c_ll]),
     "vlgba_debug_pinv_solve": (c_int, [c_int, c_dp, c_dp, c_dp]),
     "vlgba_debug_force_status": (c_int, [ctypes.c_void_p, c_int, c_int]),
     "vlgba_debug_nd_plan": (c_int, [c_int, c_int, c_ip, c_int, c_ip, c_ip]),

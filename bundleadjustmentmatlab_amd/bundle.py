@@ -307,7 +307,9 @@ class BundleAdjuster:
 
     def force_status(self, word, passes=1):
         """Fault injection: the next ``passes`` passes report a non-positive
-        pivot (word 4: pinv step) or a hand-off timeout (word 5: re-solve)."""
+        pivot (word 4: pinv step) or a hand-off timeout (word 5: re-solve);
+        word 6: the next ``passes`` starts of the envelope runner fail (the
+        factorization then runs with the column launches alone)."""
         check(self._L.vlgba_debug_force_status(self._h, int(word), int(passes)),
               "vlgba_debug_force_status")
 
@@ -399,7 +401,7 @@ class BundleAdjuster:
                  "tiles", "cr_levels", "cr_elim", "cr_keep", "ordered", "schur_terms",
                  "blob_words", "mfma", "cr_rows", "mfma_groups", "reordered", "long_points",
                  "nd_arcs", "nd_sep_tiles", "solve_flops_factor", "solve_flops_syrk",
-                 "solve_flops_back")
+                 "solve_flops_back", "env_runner_runs")
 
     def plan_info(self):
         """Execution-plan sizes of this rank (vlgba_plan_info)."""
@@ -433,15 +435,16 @@ def euclid_obs_adjuster(K, m, n, obs_pt, obs_cam, obs_x, *varargin, num_vis=0.0,
                         num_vis=num_vis, device=device, rank=rank, world_size=world_size,
                         comm_id=comm_id, semantics=semantics, **solver)
     ba.fingerprint = _adjuster_fingerprint(K, m, n, obs_pt, obs_cam, obs_x, o, num_vis,
-                                           semantics, rank, world_size)
+                                           semantics, rank, world_size, device, comm_id)
     return ba
 
 
 def _adjuster_fingerprint(K, m, n, obs_pt, obs_cam, obs_x, o, num_vis, semantics, rank,
-                          world_size):
-    """What a prebuilt adjuster was made for (ADVICE r4): sizes, the parsed
-    options, K and a hash of the observation list -- a context built for
-    another subset or other options with the same counts must not be used."""
+                          world_size, device, comm_id):
+    """What a prebuilt adjuster was made for (ADVICE r4, r5): sizes, the parsed
+    options, K, a hash of the observation list, the device and the RCCL id
+    -- a context built for another subset, other options, another GPU or
+    another communicator with the same counts must not be used."""
     # xxh3 (~25x blake2b's speed; the growing replay fingerprints every solve's
     # observations twice, at build and at use), over the arrays' own buffers
     try:
@@ -456,9 +459,12 @@ def _adjuster_fingerprint(K, m, n, obs_pt, obs_cam, obs_x, o, num_vis, semantics
     piv = o["pivot"] if o["fix_pivot"] else None
     if piv is not None:
         h.update(np.asarray(piv, dtype=bool).tobytes())
+    if comm_id is not None:
+        h.update(bytes(comm_id))
     return (int(m), int(n), int(o["num_variableK"]), bool(o["fix_structure"]),
             bool(o["fix_motion"]), bool(o["fix_pivot"]), bool(o["verbose"]), float(num_vis),
-            semantics, int(rank), int(world_size), h.hexdigest())
+            semantics, int(rank), int(world_size), int(device), comm_id is not None,
+            h.hexdigest())
 
 
 def bundle_euclid_obs(K, Te, w, Xe, obs_pt, obs_cam, obs_x, *varargin, num_vis=0.0, device=0,
@@ -482,7 +488,7 @@ def bundle_euclid_obs(K, Te, w, Xe, obs_pt, obs_cam, obs_x, *varargin, num_vis=0
             raise ValueError("bundle_euclid_obs: solver options belong to the prebuilt adjuster")
         ba = adjuster.result() if hasattr(adjuster, "result") else adjuster
         want = _adjuster_fingerprint(K, m, n, obs_pt, obs_cam, obs_x, o, num_vis, semantics,
-                                     rank, world_size)
+                                     rank, world_size, device, comm_id)
         if getattr(ba, "fingerprint", None) != want:
             ba.close()
             raise ValueError("bundle_euclid_obs: the prebuilt adjuster is for another problem "

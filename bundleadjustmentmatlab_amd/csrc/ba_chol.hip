@@ -768,13 +768,15 @@ __device__ __forceinline__ void factor_step_body(double *__restrict__ S, long lo
 // reads was made by a launch that ended before one of those flags was set).
 struct env_rm {
     unsigned *lflag, *dflag, *uflag, *pflag;
+    unsigned *rto;   // a runner hand-off gave up (the host turns this context's runner off)
     int kend;   // the run's end column (exclusive); 0: not in runner mode
 };
 
-// wave 0 spins on flag[idx] == epoch (bounded; timeout: status[1]); all waves
-// then pass a barrier.  Returns false on a timeout.
+// wave 0 spins on flag[idx] == epoch (bounded; timeout: status[1] and the
+// runner's own word *rto); all waves then pass a barrier.  Returns false on a
+// timeout.
 __device__ __forceinline__ bool env_wait(const unsigned *flag, int idx, unsigned epoch,
-                                         double *status)
+                                         double *status, unsigned *rto)
 {
     __shared__ int to;
     const int tid = threadIdx.x;
@@ -791,7 +793,10 @@ __device__ __forceinline__ bool env_wait(const unsigned *flag, int idx, unsigned
         }
         if (tid == 0) {
             to = ok ? 0 : 1;
-            if (!ok) status[1] = 1.0;
+            if (!ok) {
+                status[1] = 1.0;
+                __hip_atomic_store((gu32_t *)rto, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
     __syncthreads();
@@ -911,7 +916,7 @@ __device__ __forceinline__ void factor_step_two(double *__restrict__ S, long lon
         return;
     }
     if (iin && R.kend) {   // L_k,k-1 is the runner's
-        if (!env_wait(R.lflag, k, epoch, status)) return;
+        if (!env_wait(R.lflag, k, epoch, status, R.rto)) return;
         mfma_64x64_glb<true>(S, lds, i, k, k - 1, acc);
     } else if (iin) {
         mfma_64x64_glb(S, lds, i, k, k - 1, acc);
@@ -1091,7 +1096,7 @@ __global__ __launch_bounds__(256) void k_env_runner(double *S, long long lds,
     };
     for (int k = k0; k < k1; k++) {
         const int p0 = pan_ptr[k], T = pan_ptr[k + 1] - p0;
-        if (k - 2 >= k0 && reaches(k - 2, k) && !env_wait(R.dflag, k, epoch, status)) return;
+        if (k - 2 >= k0 && reaches(k - 2, k) && !env_wait(R.dflag, k, epoch, status, R.rto)) return;
         double vk[16];
         fetch_tile_sc(S, lds, k, k, vk);
         if (tid < NB) rk[tid] = ldg<true>(rhs + (long long)NB * k + tid);
@@ -1119,9 +1124,9 @@ __global__ __launch_bounds__(256) void k_env_runner(double *S, long long lds,
             // r_k+1 update), and column k-1's pending update of A_k+1,k stored
             if (k > k0 && reaches(k - 1, k + 1)) {
                 // column k-1's panel updated r_k+1; its pending update of A_k+1,k
-                if (!env_wait(R.pflag, k + 1, epoch, status)) return;
+                if (!env_wait(R.pflag, k + 1, epoch, status, R.rto)) return;
                 const bool kin = pan_ptr[k] > pan_ptr[k - 1] && pan_list[pan_ptr[k - 1]] == k;
-                if (kin && !env_wait(R.uflag, k + 1, epoch, status)) return;
+                if (kin && !env_wait(R.uflag, k + 1, epoch, status, R.rto)) return;
             }
             double va[16];
             fetch_tile_sc(S, lds, k + 1, k, va);
@@ -2721,121 +2726,6 @@ __global__ __launch_bounds__(256) void k_assemble_tiles(
     }
 }
 
-// k_schur_reduce and k_assemble_tiles in one launch (opt-in,
-// VLGBA_FUSE_REDUCE=1: measured no faster than the two launches, 25.8 us
-// against 11.7 + 14.8 at config 3, profiles/r05t_*; single rank, no long
-// tracks: nothing to all-reduce between them): BA_RA_STRIPS workgroups per
-// envelope tile, each a strip of rows, form every lower entry of the co-visible blocks
-// that falls in the strip exactly as k_schur_reduce forms it -- the damped
-// U_j term, then the group partials subtracted in slot order -- and the
-// diagonal strips the rhs of their rows (eA_j minus the group e-partials in
-// order) with the pinv rule of k_assemble_tiles.  Bit-identical S and rhs;
-// the block list (sblk) is not written (every reader of it -- the re-solve,
-// the pinv fallbacks, vlgba_get_reduced_system -- runs the Schur phase again
-// with the separate kernels).
-#ifndef BA_RA_STRIPS
-#define BA_RA_STRIPS 8    // 8-row strips (4: 26.4 us, 8: 25.8, 16: 41 -- the
-                          // block-list scan repeats per strip)
-#endif
-__global__ __launch_bounds__(256) void k_reduce_assemble(
-    double *__restrict__ S, long long lds, const int *__restrict__ env,
-    const int *__restrict__ tb_ptr, const int *__restrict__ tb_blk,
-    const int *__restrict__ blk_jk, int na, long long ld, double *__restrict__ rhs,
-    double *__restrict__ status, const int *__restrict__ crow, const int *__restrict__ rowsrc,
-    const double *__restrict__ spart, const double *__restrict__ epart,
-    const int *__restrict__ blk_gptr, const int *__restrict__ blk_gslots,
-    const int *__restrict__ cam_gptr, const int *__restrict__ cam_gslots,
-    const double *__restrict__ U, const double *__restrict__ eA, double lambda, int owner)
-{
-    constexpr int SR = NB / BA_RA_STRIPS;   // strip rows
-    __shared__ double T[SR * (NB + 1)];
-    const int tile = blockIdx.x / BA_RA_STRIPS, strip = blockIdx.x % BA_RA_STRIPS;
-    const int tid = threadIdx.x;
-    const int ti = env[2 * tile], tk = env[2 * tile + 1];
-    for (int q = tid; q < SR * (NB + 1); q += 256) T[q] = 0.0;
-    if (blockIdx.x == 0 && tid == 0) {
-        status[0] = 0.0;   // non-positive pivot
-        status[1] = 0.0;   // bounded hand-off spin gave up
-    }
-    __syncthreads();
-    const long long r0 = (long long)NB * ti + SR * strip, c0 = (long long)NB * tk;
-    const int na2 = na * na;
-    const int u0 = tb_ptr[tile], nq = (tb_ptr[tile + 1] - u0) * na2;
-    for (int q = tid; q < nq; q += 256) {
-        const int u = q / na2, l = q - na2 * u;
-        const int bk = tb_blk[u0 + u];
-        const int r = l % na, c = l / na;
-        const int bj = blk_jk[2 * bk], bc = blk_jk[2 * bk + 1];
-        long long row, col;
-        if (!crow) {
-            row = (long long)na * bj + r;
-            col = (long long)na * bc + c;
-        } else {
-            row = crow[bj] + r;
-            col = crow[bc] + c;
-            if (row < col && bj != bc) {
-                const long long t = row;
-                row = col;
-                col = t;
-            }
-        }
-        if (row < col || row < r0 || row >= r0 + SR || col < c0 || col >= c0 + NB) continue;
-        double acc = 0.0;
-        if (bj == bc && owner) {
-            const double uu = U[(size_t)na2 * bj + r + na * c];
-            acc = (r == c) ? (1 + lambda) * uu : uu;
-        }
-        int p = blk_gptr[bk];
-        const int pe = blk_gptr[bk + 1];
-        for (; p + 8 <= pe; p += 8) {
-            double v[8];
-#pragma unroll
-            for (int t = 0; t < 8; t++) v[t] = spart[(size_t)na2 * blk_gslots[p + t] + l];
-#pragma unroll
-            for (int t = 0; t < 8; t++) acc -= v[t];
-        }
-        for (; p < pe; p++) acc -= spart[(size_t)na2 * blk_gslots[p] + l];
-        T[(row - r0) * (NB + 1) + (col - c0)] = acc;
-    }
-    __syncthreads();
-    if (ti == tk && tid < SR) {   // the rows' rhs, then the pinv rule (k_assemble_tiles)
-        const int rr = SR * strip + tid;
-        double *dg = T + tid * (NB + 1) + rr;
-        const long long r = r0 + tid;
-        const long long src = rowsrc ? (long long)rowsrc[r] : (r < ld ? r : -1);
-        double e = 0.0;
-        if (src >= 0) {
-            const int j = (int)(src / na), rc = (int)(src - (long long)na * j);
-            e = owner ? eA[(size_t)na * j + rc] : 0.0;
-            int q = cam_gptr[j];
-            const int qe = cam_gptr[j + 1];
-            for (; q + 8 <= qe; q += 8) {
-                double v[8];
-#pragma unroll
-                for (int t = 0; t < 8; t++) v[t] = epart[(size_t)na * cam_gslots[q + t] + rc];
-#pragma unroll
-                for (int t = 0; t < 8; t++) e -= v[t];
-            }
-            for (; q < qe; q++) e -= epart[(size_t)na * cam_gslots[q] + rc];
-        }
-        rhs[r] = e;
-        if (*dg == 0.0) {
-            *dg = 1.0;
-            rhs[r] = 0.0;
-        } else if (r >= ld) {
-            rhs[r] = 0.0;
-        }
-    }
-    __syncthreads();
-    double *base = S + r0 + lds * c0;
-    const int r = tid & (SR - 1), cq = tid / SR;
-#pragma unroll
-    for (int u = 0; u < NB * SR / 256; u++) {
-        const int c = cq + (256 / SR) * u;
-        base[r + lds * c] = T[r * (NB + 1) + c];
-    }
-}
-
 // zero every envelope tile of S (fill from the previous factorisation)
 __global__ void k_zero_env(double *__restrict__ S, long long lds, const int *__restrict__ env)
 {
@@ -3245,8 +3135,6 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
     {
         const char *eg = std::getenv("VLGBA_ND_GROUPED");
         d->nd_grouped = !(eg && eg[0] == '0');
-        const char *et = std::getenv("VLGBA_TRAIL_WGS");
-        d->trail_cap = et ? std::atoi(et) : 0;
     }
     const int na = d->na, m = d->m;
     std::vector<int> crow, tpart;   // row of camera j; part of tile (arc t, separator np)
@@ -3478,12 +3366,15 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
         TRY_RC(dev_alloc(&d->kflag, sizeof(unsigned) * (size_t)nt));
         VLGBA_CHECK(hipMemsetAsync(d->kflag, 0, sizeof(unsigned) * (size_t)nt, d->stream));
         d->fac_epoch = 0;
-        // runner mode's flags: lflag | dflag | uflag | pflag, nt each
-        const char *er = std::getenv("VLGBA_ENV_RUNNER");   // "0": the column launches alone
-        d->env_runner = !(er && er[0] == '0');
+        // runner mode's flags: lflag | dflag | uflag | pflag, nt each, then
+        // the runner's timeout word.  Opt-in (VLGBA_ENV_RUNNER=1): the runner
+        // makes progress only while its stream has a hardware queue of its own
+        const char *er = std::getenv("VLGBA_ENV_RUNNER");
+        d->env_runner = er && er[0] == '1';
         if (d->env_runner && d->pan_ptr) {
-            TRY_RC(dev_alloc(&d->rflag, sizeof(unsigned) * 4 * (size_t)nt));
-            VLGBA_CHECK(hipMemsetAsync(d->rflag, 0, sizeof(unsigned) * 4 * (size_t)nt, d->stream));
+            const size_t nw = 4 * (size_t)nt + 1;
+            TRY_RC(dev_alloc(&d->rflag, sizeof(unsigned) * nw));
+            VLGBA_CHECK(hipMemsetAsync(d->rflag, 0, sizeof(unsigned) * nw, d->stream));
         }
     }
     TRY_RC(dev_alloc(&d->env_tiles, sizeof(int) * (env.size() + 1)));
@@ -3553,15 +3444,6 @@ void ba_chol_free(ba_dev *d)
 int ba_assemble_tiles(ba_dev *d)
 {
     const bool nd = d->nd_np > 0;
-    if (d->fuse_red) {   // the Schur phase left the block sums to this launch
-        k_reduce_assemble<<<BA_RA_STRIPS * d->n_env, 256, 0, d->stream>>>(
-            d->S, nd ? d->slds : d->lds, d->env_tiles, d->tb_ptr, d->tb_blk, d->blk_jk, d->na,
-            nd ? d->slds : d->ld, nd ? d->nd_rhs : d->rhs, d->scal + 4,
-            nd ? d->nd_crow : nullptr, nd ? d->nd_rowsrc : nullptr, d->spart, d->epart,
-            d->blk_gptr, d->blk_gslots, d->cam_gptr, d->cam_gslots, d->U, d->eA, d->red_lambda,
-            d->schur_owner);
-        return -(int)hipGetLastError();
-    }
     k_assemble_tiles<<<d->n_env, 256, 0, d->stream>>>(
         d->S, nd ? d->slds : d->lds, d->env_tiles, d->tb_ptr, d->tb_blk, d->blk_jk, d->sblk, d->na,
         nd ? d->slds : d->ld, nd ? d->nd_rhs : d->rhs, d->scal + 4, nd ? d->nd_crow : nullptr,
@@ -3589,27 +3471,25 @@ int ba_chol_fix_diag(ba_dev *d)
     return -(int)hipGetLastError();
 }
 
-// workgroups for ntr trailing pairs beside `other` workgroups of the same
-// launch: at most d->trail_cap - other (VLGBA_TRAIL_WGS; 0: one per pair)
-static int trail_wgs(const ba_dev *d, int ntr, int other)
-{
-    if (d->trail_cap <= 0 || ntr == 0) return ntr;
-    return std::max(1, std::min(ntr, d->trail_cap - other));
-}
-
 // runner mode (k_env_runner) for this factorization?  Needs the hand-off, the
 // device panel pointers and the flags; off under per-kernel timing (one stream)
-// and, for the rest of the process, after any runner hand-off gave up: the
-// runner needs its side stream on a hardware queue of its own (with the
-// library stream's column launches queued behind it on a shared queue every
-// wait times out)
-static std::atomic<int> g_env_runner_off{0};
-
-void ba_env_runner_disable()
+// and, for the rest of this context, after one of the runner's own hand-offs
+// gave up (ba_env_runner_timed_out): the runner needs its side stream on a
+// hardware queue of its own (with the library stream's column launches queued
+// behind it on a shared queue every wait times out)
+int ba_env_runner_timed_out(ba_dev *d)
 {
-    if (!g_env_runner_off.exchange(1))
-        std::fprintf(stderr, "[vlgba] envelope runner off for this process: a hand-off timed "
-                             "out (its stream shares a hardware queue?)\n");
+    if (!d->env_runner || !d->rflag) return 0;
+    unsigned *rto = d->rflag + 4 * (size_t)d->nt;
+    unsigned h = 0;
+    if (hipMemcpyAsync(&h, rto, sizeof h, hipMemcpyDeviceToHost, d->stream) != hipSuccess ||
+        hipStreamSynchronize(d->stream) != hipSuccess)
+        return -1;
+    if (!h) return 0;
+    d->env_runner = 0;
+    std::fprintf(stderr, "[vlgba] envelope runner off for this context: one of its hand-offs "
+                         "timed out (its stream shares a hardware queue?)\n");
+    return 1;
 }
 
 // runs shorter than VLGBA_ENV_RUNNER_MIN columns (default 8) keep the column
@@ -3645,7 +3525,7 @@ static hipStream_t env_runner_stream()
 static bool env_run_on(ba_dev *d, const unsigned *kflag, int ncols)
 {
     if (!(d->env_runner && kflag && d->pan_ptr && d->rflag && !(d->kt && d->kt->on) &&
-          !g_env_runner_off.load() && ncols >= env_run_min()))
+          ncols >= env_run_min()))
         return false;
     if (!d->rstream) d->rstream = env_runner_stream();
     if (!d->rstream) {
@@ -3657,13 +3537,20 @@ static bool env_run_on(ba_dev *d, const unsigned *kflag, int ncols)
 
 static env_rm env_rm_of(const ba_dev *d, int kend)
 {
+    if (!d->rflag) return env_rm{};
     return env_rm{d->rflag, d->rflag + d->nt, d->rflag + 2 * (size_t)d->nt,
-                  d->rflag + 3 * (size_t)d->nt, kend};
+                  d->rflag + 3 * (size_t)d->nt, d->rflag + 4 * (size_t)d->nt, kend};
 }
 
-// fork the side stream off the library stream and start the runner there
+// fork the side stream off the library stream and start the runner there.
+// Nonzero: nothing was launched (the caller runs the column launches alone)
+// or the launch failed (the error is returned).
 static int env_runner_start(ba_dev *d, const env_runs &Rn, long long L, double *rhs)
 {
+    if (d->debug_runner_fail > 0) {   // vlgba_debug_force_status word 6
+        d->debug_runner_fail--;
+        return -(int)hipErrorLaunchFailure;
+    }
     const size_t smem4 = sizeof(double) * 4 * NB * LP;
     TRY_RC(ba_ensure_dyn_lds((const void *)k_env_runner, smem4));
     VLGBA_CHECK(hipEventRecord(d->ev_fork, d->stream));
@@ -3671,24 +3558,27 @@ static int env_runner_start(ba_dev *d, const env_runs &Rn, long long L, double *
     k_env_runner<<<Rn.np, 256, smem4, d->rstream>>>(d->S, L, d->pan_ptr, d->pan_list, Rn,
                                                     d->linv, rhs, d->ywork, d->scal + 4,
                                                     d->kflag, env_rm_of(d, 0), d->fac_epoch);
+    TRY_RC(-(int)hipGetLastError());
     VLGBA_CHECK(hipEventRecord(d->ev_join, d->rstream));
-    return -(int)hipGetLastError();
+    d->runner_runs++;
+    return 0;
 }
 
 // the envelope's tile columns k0 .. k1-1 (k_factor_step), column k0 taking no
-// pending update of column k0-1
-static void envelope_columns(ba_dev *d, int k0, int k1, long long L, double *rhs,
-                             unsigned *kflag)
+// pending update of column k0-1.  A runner that does not start leaves the
+// columns to the launches alone (the same factorization, bit for bit).
+static int envelope_columns(ba_dev *d, int k0, int k1, long long L, double *rhs,
+                            unsigned *kflag)
 {
     // two LDS tiles with the hand-off (two workgroups per CU), three without
     const size_t smem3 = sizeof(double) * 3 * NB * LP, smem2 = sizeof(double) * 2 * NB * LP;
-    const bool run = k1 > k0 && env_run_on(d, kflag, k1 - k0);
+    bool run = k1 > k0 && env_run_on(d, kflag, k1 - k0);
     if (run) {
         env_runs Rn{};
         Rn.np = 1;
         Rn.k0[0] = k0;
         Rn.k1[0] = k1;
-        if (env_runner_start(d, Rn, L, rhs)) return;
+        if (env_runner_start(d, Rn, L, rhs)) run = false;
     }
     for (int k = k0; k < k1; k++) {
         const int p0 = d->pan_ptr_h[k], T = d->pan_ptr_h[k + 1] - p0;
@@ -3696,15 +3586,15 @@ static void envelope_columns(ba_dev *d, int k0, int k1, long long L, double *rhs
         // column k-1's trailing pairs below row k (see k_factor_step)
         const int kin = Tp > 0 && d->h_pan_list[q0] == k;
         const int Tr = Tp - kin, ntr = Tr * (Tr + 1) / 2;
-        // with the hand-off a trailing workgroup may take several pairs
-        const int nw = kflag ? trail_wgs(d, ntr, 1 + T) : ntr;
+        const int nw = ntr;   // one workgroup per trailing pair
         KT_B(d);
         k_factor_step<<<1 + T + nw, 256, kflag ? smem2 : smem3, d->stream>>>(
             d->S, L, k, d->pan_list + p0, T, d->pan_list + q0, Tp, d->linv, rhs, d->ywork,
             d->scal + 4, kflag, d->fac_epoch, ntr, nw, env_rm_of(d, run ? k1 : 0));
         KT_E(d, KT_FACTOR);
     }
-    if (run) (void)hipStreamWaitEvent(d->stream, d->ev_join, 0);
+    if (run) VLGBA_CHECK(hipStreamWaitEvent(d->stream, d->ev_join, 0));
+    return -(int)hipGetLastError();
 }
 
 // x = L^-T y of the envelope factor (ywork holds y; consumed)
@@ -3850,7 +3740,7 @@ int ba_chol_solve(ba_dev *d, int nospin)
         TRY_RC(ba_ensure_dyn_lds((const void *)k_factor_multi, smem3));
         int nsteps = 0;
         for (int t = 0; t < np; t++) nsteps = std::max(nsteps, d->nd_a0[t + 1] - d->nd_a0[t]);
-        const bool run = env_run_on(d, kflag, nsteps);
+        bool run = env_run_on(d, kflag, nsteps);
         if (run) {
             env_runs Rn{};
             Rn.np = np;
@@ -3858,7 +3748,7 @@ int ba_chol_solve(ba_dev *d, int nospin)
                 Rn.k0[t] = d->nd_a0[t];
                 Rn.k1[t] = d->nd_a0[t + 1];
             }
-            TRY_RC(env_runner_start(d, Rn, L, d->nd_rhs));
+            if (env_runner_start(d, Rn, L, d->nd_rhs)) run = false;   // the launches alone
         }
         for (int st = 0; st < nsteps; st++) {
             nd_step P{};
@@ -3889,7 +3779,7 @@ int ba_chol_solve(ba_dev *d, int nospin)
             // the trailing workgroups: each arc's share of the cap (with the hand-off)
             int ttot = 0;
             for (int u = 0; u < P.np; u++) ttot += P.ntr[u];
-            const int tw = kflag ? trail_wgs(d, ttot, nbk) : ttot;
+            const int tw = ttot;   // one workgroup per trailing pair
             for (int u = 0; u < P.np; u++) {
                 const int nw = tw == ttot ? P.ntr[u]
                                           : (P.ntr[u] == 0 ? 0
@@ -3925,13 +3815,13 @@ int ba_chol_solve(ba_dev *d, int nospin)
                                                              d->nd_part, d->nd_rhs);
             KT_E(d, KT_SYRK);
         }
-        envelope_columns(d, s0, nt, L, d->nd_rhs, kflag);
+        TRY_RC(envelope_columns(d, s0, nt, L, d->nd_rhs, kflag));
         TRY_RC(envelope_backward(d, L, d->nd_x, nospin));
         k_nd_scatter<<<(int)((d->lds + 255) / 256), 256, 0, d->stream>>>(d->nd_prow, d->nd_x,
                                                                          d->da, d->lds);
         return -(int)hipGetLastError();
     }
-    envelope_columns(d, 0, nt, d->lds, d->rhs, kflag);
+    TRY_RC(envelope_columns(d, 0, nt, d->lds, d->rhs, kflag));
     TRY_RC(envelope_backward(d, d->lds, d->da, nospin));
     return -(int)hipGetLastError();
 }

@@ -88,10 +88,6 @@ struct ba_camred {
     double *sse_out, *sse_out2;
 };
 
-// the operand window of the linearisation's division-free quotients
-// (dehom_fast, ba_kernels.hip): biased exponents 723 + [0, BA_EWIN]
-#define BA_EWIN 600u
-
 struct ba_dev {
     int m, n, na, N, js;
     int device, ncu;   // HIP device ordinal and its CU count
@@ -127,8 +123,11 @@ struct ba_dev {
     unsigned long long *xgran64;  // [nt][128] x_k granules of the one-launch backward
     unsigned *kflag;   // [nt] envelope factor: L_kk^-1 / y_k published (epoch fac_epoch)
     unsigned fac_epoch;
-    unsigned *rflag;    // [4 nt] runner mode's flags (k_env_runner; off: VLGBA_ENV_RUNNER=0)
+    unsigned *rflag;    // [4 nt + 1] runner mode's flags + its timeout word (k_env_runner;
+                        // opt-in: VLGBA_ENV_RUNNER=1)
     int env_runner;
+    int runner_runs;          // runner launches made (vlgba_plan_info [28])
+    int debug_runner_fail;    // the next starts fail (vlgba_debug_force_status word 6)
     hipStream_t rstream;   // the runner's stream (highest priority)
     int *env_tiles;    // device [n_env][2] (i, k) tiles inside the envelope
     int *tb_ptr, *tb_blk;  // device: per envelope tile, the co-visible blocks overlapping it
@@ -170,7 +169,6 @@ struct ba_dev {
     // (k_sep_update / k_sep_reduce), then the separator's columns.
     int nd_np;                    // arcs (0: natural order)
     int nd_grouped;               // k_factor_multi's workgroups grouped by role (nd_step)
-    int trail_cap;                // envelope launches' workgroup cap for trailing pairs (0: none)
     int nd_a0[BA_ND_MAX + 1];     // first tile of arc t; nd_a0[nd_np] = first separator tile
     long long slds;               // rows of the reordered system (nt * 64)
     int *nd_crow;                 // device [m] first row of camera j
@@ -222,9 +220,6 @@ struct ba_dev {
     double *epart;     // [nge][NA] per group e-slot
     double *upart;     // [nes][NA(NA+1)/2 + NA] per-chunk U_j (lower) | eA_j partials
     double *chsse;     // [3][nch] per-chunk partials: linearisation SSE, new SSE, point dpg
-    int *redo;         // [2 + nch] count, chunks to linearise again with '/' (k_linearize_redo)
-    int fast_dehom;    // NA = 6: division-free projection quotients (VLGBA_FAST_DEHOM=1: on)
-    unsigned ewin;     // their operand window (BA_EWIN; 0 under VLGBA_DEBUG_REDO=1)
     // fused update (fast path, ba_launch_update -> k_update_linearize): the
     // next linearisation's buffers, swapped in by an accepted step
     int fused;
@@ -272,8 +267,6 @@ struct ba_dev {
     double *xh_out;    // [N][2] projections (stage 1 and stage 3)
     double *B_out;     // [N][6] point Jacobians (stage 1)
     unsigned char *obs_vis;  // [N] stage 3: 0 = structural-only pair (no projection)
-    int fuse_red;      // this pass: k_schur_reduce folded into the assembly (k_reduce_assemble)
-    int fuse_red_ok;   // allowed (VLGBA_FUSE_REDUCE=1; off by default: no faster)
     double red_lambda; // ... at this lambda
     int schur_owner;   // this rank adds U* / eA into the reduced system (every rank
                        // adds its own partials)
@@ -348,7 +341,9 @@ void *ba_dmalloc(size_t bytes);   // per-device caching allocator (ba_solver.cpp
 // per (kernel, device), thread-safe; ba_solver.cpp)
 int ba_ensure_dyn_lds(const void *fn, size_t bytes);
 void ba_dfree(void *p);
-void ba_env_runner_disable();   // after a runner hand-off timeout (ba_chol.hip)
+// after a re-solve: did one of the runner's own hand-offs time out?  Then the
+// runner is off for this context (1); 0: no; < 0: error (ba_chol.hip)
+int ba_env_runner_timed_out(ba_dev *d);
 int ba_launch_schur_fast(ba_dev *d, double lambda);   // fused damp + Vinv + Y + S + e_
 // long tracks: count (fill = 0, into cnt[nb]) / write (fill = 1, at lpair_ptr) the
 // per-block (obs, obs) pairs of k_schur_reduce (context setup)

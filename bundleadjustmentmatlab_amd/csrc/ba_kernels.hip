@@ -92,131 +92,8 @@ __device__ __forceinline__ void block_sum_to(double v, double *out)
 // the unperturbed camera components of a camera column, a0 itself for a
 // point column), so the columns are bit-identical to project_col's.
 // -------------------------------------------------------------------------
-// ---- the two divisions of a projection without v_div_scale / v_div_fixup --
-// x0 / x2 and x1 / x2 exactly as the compiler's IEEE division forms each of
-// them (v_div_scale of both operands, v_rcp_f64, two Newton steps of the
-// reciprocal, the quotient, one remainder step in v_div_fmas, v_div_fixup),
-// with the reciprocal formed once for the two quotients.  When every operand
-// has a biased exponent in [723, 1323] (|x| in [2^-300, 2^301)) the division
-// scales nothing (operand exponent gap < 768, no denormal operand, reciprocal
-// or quotient, numerator exponent > 53), v_div_fmas is a plain fma and
-// v_div_fixup returns its operand, so each quotient is the division's bit
-// for bit (tests/test_gpu_fast_dehom.py compares them on random and edge
-// operands).  An operand outside the window (zeros included) raises g above
-// BA_EWIN; the chunk is then linearised again with '/' (k_linearize_redo).
-// The FD quotient (vlg_fd_quot's Markstein step) without its range branch:
-// |d| in [2^-300, 2^301) (inside vlg_fd_quot's [2^-900, 2^900]) or d = 0.
-#ifndef BA_SCHED_MASK
-#define BA_SCHED_MASK 0x20   // VMEM reads may cross
-#endif
-__device__ __forceinline__ unsigned ba_ewin(double x)
-{
-    return ((unsigned)(__builtin_bit_cast(unsigned long long, x) >> 52) & 0x7ffu) - 723u;
-}
-__device__ __forceinline__ unsigned umax2(unsigned a, unsigned b) { return a > b ? a : b; }
-
-__device__ __forceinline__ void dehom_fast(const double xn[3], double x[2], unsigned &g)
-{
-    g = umax2(g, umax2(ba_ewin(xn[0]), umax2(ba_ewin(xn[1]), ba_ewin(xn[2]))));
-    const double d = xn[2];
-    double y = __builtin_amdgcn_rcp(d);
-    double e = fma(-d, y, 1.0);
-    y = fma(y, e, y);
-    e = fma(-d, y, 1.0);
-    y = fma(y, e, y);
-    const double q0 = xn[0] * y, q1 = xn[1] * y;
-    x[0] = fma(fma(-d, q0, xn[0]), y, q0);
-    x[1] = fma(fma(-d, q1, xn[1]), y, q1);
-}
-
-// d = 0 is common (a translation column leaves the other image coordinate
-// unchanged) and in the window: frexp's exponent of a zero is 0, and the
-// Markstein step returns +0 for either zero, so the sign is d's (that of d / h,
-// h > 0; for d != 0 the result already has it).  d is finite: both of its
-// terms passed dehom_fast's window.
-__device__ __forceinline__ double fd_quot_fast(double d, unsigned &g)
-{
-    g = umax2(g, (unsigned)(__builtin_amdgcn_frexp_exp(d) + 299));
-    const double q = d * VLG_FD_RH;
-    const double r = fma(-q, VLG_FD_H, d);
-    return __builtin_copysign(fma(r, VLG_FD_RH, q), d);
-}
-
-__global__ void k_debug_dehom(const double *__restrict__ xn, double *__restrict__ fast,
-                              double *__restrict__ ref, int *__restrict__ win, long long n)
-{
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const double v[3] = {xn[3 * i], xn[3 * i + 1], xn[3 * i + 2]};
-    unsigned g = 0, gd = 0;
-    double x[2];
-    dehom_fast(v, x, g);
-    fast[4 * i] = x[0];
-    fast[4 * i + 1] = x[1];
-    fast[4 * i + 2] = fd_quot_fast(v[0], gd);
-    fast[4 * i + 3] = fd_quot_fast(v[1], gd);
-    ref[4 * i] = v[0] / v[2];
-    ref[4 * i + 1] = v[1] / v[2];
-    ref[4 * i + 2] = v[0] / VLG_FD_H;
-    ref[4 * i + 3] = v[1] / VLG_FD_H;
-    // (in the kernels d = x1 - xh is finite: both terms passed the quotient window)
-    const bool dfin = isfinite(v[0]) && isfinite(v[1]);
-    win[i] = (g <= BA_EWIN ? 1 : 0) | (gd <= BA_EWIN && dfin ? 2 : 0);
-}
-
-extern "C" int vlgba_debug_dehom(const double *xn, double *fast, double *ref, int *win,
-                                 long long n)
-{
-    if (n < 0 || (n > 0 && (!xn || !fast || !ref || !win))) return VLGBA_E_ARG;
-    if (n == 0) return 0;
-    double *d = nullptr;
-    VLGBA_CHECK(hipMalloc(&d, sizeof(double) * 11 * (size_t)n + sizeof(int) * (size_t)n));
-    int rc = 0;
-    int *dw = reinterpret_cast<int *>(d + 11 * n);
-    do {
-        if (hipMemcpy(d, xn, sizeof(double) * 3 * n, hipMemcpyHostToDevice) != hipSuccess) {
-            rc = -1;
-            break;
-        }
-        const long long nb = (n + 255) / 256;
-        hipLaunchKernelGGL(k_debug_dehom, dim3((unsigned)nb), dim3(256), 0, 0, d, d + 3 * n,
-                           d + 7 * n, dw, n);
-        if (hipGetLastError() != hipSuccess) { rc = -1; break; }
-        if (hipMemcpy(fast, d + 3 * n, sizeof(double) * 4 * n, hipMemcpyDeviceToHost) !=
-                hipSuccess ||
-            hipMemcpy(ref, d + 7 * n, sizeof(double) * 4 * n, hipMemcpyDeviceToHost) !=
-                hipSuccess ||
-            hipMemcpy(win, dw, sizeof(int) * n, hipMemcpyDeviceToHost) != hipSuccess)
-            rc = -1;
-    } while (0);
-    (void)hipFree(d);
-    return rc;
-}
-
-template <bool FAST>
-__device__ __forceinline__ void project_sx(const double Kc[9], const double S[3],
-                                           const double t[3], double x[2], unsigned &g)
-{
-    if constexpr (FAST) {
-        double xn[3];
-        vlg_project_h(Kc, S, t, xn);
-        dehom_fast(xn, x, g);
-    } else {
-        vlg_project_s(Kc, S, t, x);
-    }
-}
-
-template <bool FAST>
-__device__ __forceinline__ double fd_q(double d, unsigned &g)
-{
-    if constexpr (FAST) return fd_quot_fast(d, g);
-    else return vlg_fd_quot(d);
-}
-
-template <bool FAST>
 __device__ __forceinline__ void fd_columns_6(const cam_view<6> &cv, const double b[3],
-                                             const double xh[2], int half, double *row,
-                                             unsigned &g)
+                                             const double xh[2], int half, double *row)
 {
     const double *t0 = cv.a0 + 3;
 #pragma unroll
@@ -231,13 +108,10 @@ __device__ __forceinline__ void fd_columns_6(const cam_view<6> &cv, const double
             bb[c] = half ? b[c] + H_FD * ((c == t) ? 1.0 : 0.0) : b[c];
         }
         vlg_rot_b(Rk, bb, S);
-        project_sx<FAST>(cv.Kc, S, tt, x1, g);
+        vlg_project_s(cv.Kc, S, tt, x1);
         const int col = half ? 6 + t : t;
-        row[2 * col] = fd_q<FAST>(x1[0] - xh[0], g);
-        row[2 * col + 1] = fd_q<FAST>(x1[1] - xh[1], g);
-        // FAST has no branch between the rounds: keep the scheduler from
-        // interleaving their arithmetic (registers), loads may move up
-        if constexpr (FAST) __builtin_amdgcn_sched_barrier(BA_SCHED_MASK);
+        row[2 * col] = vlg_fd_quot(x1[0] - xh[0]);
+        row[2 * col + 1] = vlg_fd_quot(x1[1] - xh[1]);
     }
     double S[3], R4[9];
     const double *Rs4 = cv.R + 36;
@@ -251,9 +125,9 @@ __device__ __forceinline__ void fd_columns_6(const cam_view<6> &cv, const double
             double tt[3], x1[2];
 #pragma unroll
             for (int c = 0; c < 3; c++) tt[c] = t0[c] + H_FD * ((3 + c == k) ? 1.0 : 0.0);
-            project_sx<FAST>(cv.Kc, S, tt, x1, g);
-            row[2 * k] = fd_q<FAST>(x1[0] - xh[0], g);
-            row[2 * k + 1] = fd_q<FAST>(x1[1] - xh[1], g);
+            vlg_project_s(cv.Kc, S, tt, x1);
+            row[2 * k] = vlg_fd_quot(x1[0] - xh[0]);
+            row[2 * k + 1] = vlg_fd_quot(x1[1] - xh[1]);
         }
     }
 }
@@ -432,7 +306,7 @@ struct ba_upd {
     const double *dpg_long;
 };
 
-template <int NA, bool UPD, bool FAST>
+template <int NA, bool UPD>
 __device__ __forceinline__ void linearize_chunk_body(
     const int *__restrict__ ch_pt, const int *__restrict__ ch_obase,
     const int *__restrict__ ch_eslot, const int *__restrict__ eslot_optr,
@@ -444,7 +318,7 @@ __device__ __forceinline__ void linearize_chunk_body(
     double *__restrict__ W, double *__restrict__ V, double *__restrict__ eB,
     double *__restrict__ upart, double *__restrict__ part_sse, int nch_reg,
     const int *__restrict__ seg_pt, double *__restrict__ vseg, const int *__restrict__ ch_cam,
-    ba_upd u, int ch, int *__restrict__ redo, unsigned ewin)
+    ba_upd u, int ch)
 {
     constexpr int NC0 = (NA + 4) / 2;       // lane 0: base + FD columns [0, NC0)
     constexpr int RS = 2 * NA + 8;          // LDS row: A (2 NA), B (6), e (2)
@@ -470,10 +344,6 @@ __device__ __forceinline__ void linearize_chunk_body(
     // lane addresses live through the projections: spills)
     __shared__ double dpl[UPD ? BA_CH_PTS : 1];
     static_assert(BA_CH_PTS <= 64, "the point lanes are wave 0");
-    // FAST: the lanes' projection quotients by dehom_fast / fd_quot_fast; a
-    // chunk with an operand outside their window goes on the redo list
-    // (k_linearize_redo redoes it with '/' after the launch)
-    __shared__ int badw[4];
     const int tid = threadIdx.x;
     // a segment chunk (ch >= nch_reg) holds part of one long track: its V / eB
     // sums are partials (vseg), added up per track by k_long_vsum
@@ -636,7 +506,6 @@ __device__ __forceinline__ void linearize_chunk_body(
         STAMP(23);
     }
     double sse = 0.0;
-    unsigned g = 0;   // FAST: the largest operand-window key of this lane
     if (nobs > 0) {   // (nu > 0 too)
         m_eobl = __hip_atomic_load(eslot_obs + u0 + min(tid, nu - 1), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -655,16 +524,9 @@ __device__ __forceinline__ void linearize_chunk_body(
             cam_view<NA> cv(a, K4, rot, j);
             double xh[2];
             double *row = rows + RS * lo;
-            if constexpr (NA == 6 && FAST) {
-                {
-                    double S[3];
-                    vlg_rot_b(cv.Rl, bi, S);
-                    project_sx<true>(cv.Kc, S, cv.a0 + 3, xh, g);
-                }
-                fd_columns_6<true>(cv, bi, xh, half, row, g);
-            } else if constexpr (NA == 6) {
+            if constexpr (NA == 6) {
                 cv.project(bi, xh);
-                fd_columns_6<false>(cv, bi, xh, half, row, g);
+                fd_columns_6(cv, bi, xh, half, row);
             } else {
                 cv.project(bi, xh);
                 // the NA + 3 FD columns of [A | B] (mex_bundle_1 :201-219) split
@@ -692,16 +554,8 @@ __device__ __forceinline__ void linearize_chunk_body(
         }
     }
     if (tid < nu) eobl[tid] = (unsigned short)m_eobl;
-    if constexpr (FAST) {
-        const bool bad = __any(g > ewin);
-        if ((tid & 63) == 0) badw[tid >> 6] = bad;
-    }
     __syncthreads();
     STAMP(17);
-    if constexpr (FAST) {
-        if (tid == 0 && (badw[0] | badw[1] | badw[2] | badw[3]))
-            redo[1 + atomicAdd(redo, 1)] = ch;
-    }
     if constexpr (UPD) {   // the chunk's point part of dp'(lambda dp + g), points in order
         if (tid == 0) {
             double acc = 0.0;
@@ -823,47 +677,20 @@ __device__ __forceinline__ void linearize_chunk_body(
 
 // the linearisation at the current parameters (after set_params, the ordered
 // and stage paths' fast twin)
-// FAST (NA = 6, VLGBA_FAST_DEHOM=1): the division-free quotients, the
-// chunks outside their window listed in redo; ewin = BA_EWIN (0 under
-// VLGBA_DEBUG_REDO=1: every chunk is redone, the tests' check of the redo)
-template <int NA, bool FAST>
-__global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(BA_LIN_ARGS,
-                                                                            int *redo,
-                                                                            unsigned ewin)
+template <int NA>
+__global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(BA_LIN_ARGS)
 {
-    linearize_chunk_body<NA, false, FAST>(BA_LIN_PASS, ba_upd{}, blockIdx.x, redo, ewin);
+    linearize_chunk_body<NA, false>(BA_LIN_PASS, ba_upd{}, blockIdx.x);
 }
 
 // the fused update: the point update of the pass, then the linearisation at
 // (a_new, b_new) (a, rot, b = a_new, rot_new, b_new; W .. part_sse = the
 // second buffers)
-template <int NA, bool FAST>
-__global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_update_linearize(BA_LIN_ARGS,
-                                                                             ba_upd u,
-                                                                             int *redo,
-                                                                             unsigned ewin)
-{
-    linearize_chunk_body<NA, true, FAST>(BA_LIN_PASS, u, blockIdx.x, redo, ewin);
-}
-
-// The chunks the fast quotients could not vouch for (an operand outside
-// dehom_fast's window: a zero or huge homogeneous coordinate, a denormal FD
-// difference), linearised again with '/' into the same outputs, one after the
-// other in one workgroup; redo[0] (their count) is reset for the next launch.
-// Normally the list is empty and the launch returns at once.  Runs before
-// anything reads the chunks' outputs (k_long_vsum, the sums, the next pass).
 template <int NA>
-__global__ __launch_bounds__(256) void k_linearize_redo(BA_LIN_ARGS, int *redo, int nch_total)
+__global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_update_linearize(BA_LIN_ARGS,
+                                                                             ba_upd u)
 {
-    const int cnt = redo[0];
-    for (int k = 0; k < cnt; k++) {
-        linearize_chunk_body<NA, false, false>(BA_LIN_PASS, ba_upd{}, redo[1 + k], redo, 0u);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0 && cnt > 0) {
-        redo[0] = 0;
-        redo[1 + nch_total] += cnt;   // running total (VLGBA_REDO_REPORT=1 prints it)
-    }
+    linearize_chunk_body<NA, true>(BA_LIN_PASS, u, blockIdx.x);
 }
 
 // U_j, eA_j from the per-chunk partials (fast path).  One 256-lane workgroup
@@ -2446,28 +2273,23 @@ int ba_launch_rotations(ba_dev *d, const double *a, double *rot, int all5)
     return -(int)hipGetLastError();
 }
 
-// the fast-path linearisation at (a, rot, b) into (W, V, eB, upart, chsse),
-// then the redo of the chunks its quotients could not vouch for
-template <int NA, bool FAST>
+// the fast-path linearisation at (a, rot, b) into (W, V, eB, upart, chsse);
+// u: the fused point update first (k_update_linearize)
+template <int NA>
 static void lin_chunk_launch(ba_dev *d, ba_flags f, const double *a, const double *rot,
                              const double *b, double *W, double *V, double *eB, double *upart,
                              double *chsse, const ba_upd *u)
 {
     if (u)
-        k_update_linearize<NA, FAST><<<d->nch, 256, 0, d->stream>>>(
+        k_update_linearize<NA><<<d->nch, 256, 0, d->stream>>>(
             d->ch_pt, d->ch_obase, d->ch_eslot, d->eslot_optr, d->eslot_obs, d->pt_ptr,
             d->obs_cam, d->obs_lpt, d->obs_x, d->K4, a, rot, b, f, d->pivot, W, V, eB, upart,
-            chsse, d->nch_reg, d->seg_pt, d->vseg, d->ch_cam, *u, d->redo, d->ewin);
+            chsse, d->nch_reg, d->seg_pt, d->vseg, d->ch_cam, *u);
     else
-        k_linearize_chunk<NA, FAST><<<d->nch, 256, 0, d->stream>>>(
+        k_linearize_chunk<NA><<<d->nch, 256, 0, d->stream>>>(
             d->ch_pt, d->ch_obase, d->ch_eslot, d->eslot_optr, d->eslot_obs, d->pt_ptr,
             d->obs_cam, d->obs_lpt, d->obs_x, d->K4, a, rot, b, f, d->pivot, W, V, eB, upart,
-            chsse, d->nch_reg, d->seg_pt, d->vseg, d->ch_cam, d->redo, d->ewin);
-    if (FAST)
-        k_linearize_redo<NA><<<1, 256, 0, d->stream>>>(
-            d->ch_pt, d->ch_obase, d->ch_eslot, d->eslot_optr, d->eslot_obs, d->pt_ptr,
-            d->obs_cam, d->obs_lpt, d->obs_x, d->K4, a, rot, b, f, d->pivot, W, V, eB, upart,
-            chsse, d->nch_reg, d->seg_pt, d->vseg, d->ch_cam, d->redo, d->nch);
+            chsse, d->nch_reg, d->seg_pt, d->vseg, d->ch_cam);
 }
 
 int ba_launch_linearize(ba_dev *d, ba_flags f)
@@ -2475,13 +2297,8 @@ int ba_launch_linearize(ba_dev *d, ba_flags f)
     if (!d->ordered) {
         KT_B(d);
         if (d->nch > 0)
-            BA_DISPATCH(d->na, (d->fast_dehom && NA == 6
-                                    ? lin_chunk_launch<NA, NA == 6>(d, f, d->a, d->rot, d->b,
-                                                                    d->W, d->V, d->eB,
-                                                                    d->upart, d->chsse, nullptr)
-                                    : lin_chunk_launch<NA, false>(d, f, d->a, d->rot, d->b,
-                                                                  d->W, d->V, d->eB, d->upart,
-                                                                  d->chsse, nullptr)));
+            BA_DISPATCH(d->na, (lin_chunk_launch<NA>(d, f, d->a, d->rot, d->b, d->W, d->V,
+                                                     d->eB, d->upart, d->chsse, nullptr)));
         if (d->nl > 0)   // long tracks: V / eB = sum of their segments' partials
             k_long_vsum<<<d->nl, 64, 0, d->stream>>>(d->long_pt, d->long_seg0, d->vseg, d->V,
                                                      d->eB);
@@ -2614,10 +2431,6 @@ static int launch_schur_fast(ba_dev *d, double lambda)
         VLGBA_CHECK(hipStreamWaitEvent(d->stream, d->ev_join, 0));
         d->join_pending = 0;
     }
-    if (d->fuse_red) {   // the block sums are formed by the assembly (k_reduce_assemble)
-        d->red_lambda = lambda;
-        return 0;
-    }
     KT_B(d);
     ba_longs lg{};
     if (d->nl > 0 && !d->nlb) {
@@ -2715,13 +2528,8 @@ static int launch_update_fused(ba_dev *d, double lambda, ba_flags f)
                                d->dpg_long)));
     const ba_upd u{d->W, d->da, d->eB, d->Vinv, d->b, d->ndb, lambda, d->db, d->b_new,
                    d->chsse2 + 2 * (size_t)d->nch, d->seg_long, d->long_o0, d->dpg_long};
-    BA_DISPATCH(d->na, (d->fast_dehom && NA == 6
-                            ? lin_chunk_launch<NA, NA == 6>(d, f, d->a_new, d->rot_new,
-                                                            d->b_new, d->W2, d->V2, d->eB2,
-                                                            d->upart2, d->chsse2, &u)
-                            : lin_chunk_launch<NA, false>(d, f, d->a_new, d->rot_new,
-                                                          d->b_new, d->W2, d->V2, d->eB2,
-                                                          d->upart2, d->chsse2, &u)));
+    BA_DISPATCH(d->na, (lin_chunk_launch<NA>(d, f, d->a_new, d->rot_new, d->b_new, d->W2,
+                                             d->V2, d->eB2, d->upart2, d->chsse2, &u)));
     if (d->nl > 0)   // long tracks: V2 / eB2 = sum of their segments' partials
         k_long_vsum<<<d->nl, 64, 0, d->stream>>>(d->long_pt, d->long_seg0, d->vseg, d->V2,
                                                  d->eB2);

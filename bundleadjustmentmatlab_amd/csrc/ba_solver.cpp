@@ -1328,17 +1328,45 @@ static ncclResult_t comm_acquire(ncclComm_t *comm, int world, const void *id128,
     return r;
 }
 
+// idle communicators kept at most (a caller that makes a fresh unique id per
+// solve and never calls vlgba_comm_release would otherwise keep one per rank
+// per solve for the life of the process): past the cap one idle communicator
+// of another id is destroyed, with a warning the first time
+#ifndef BA_COMM_IDLE_CAP
+#define BA_COMM_IDLE_CAP 64
+#endif
+
 static void comm_release(ncclComm_t comm)
 {
+    ncclComm_t evict = nullptr;
     {
         std::lock_guard<std::mutex> lk(g_comm_mu);
         auto it = g_comm_key.find(comm);
-        if (it != g_comm_key.end()) {
-            g_comm_idle.emplace(it->second, comm);
-            return;
+        if (it == g_comm_key.end()) {
+            evict = comm;   // its id was released while this context held it
+        } else {
+            const comm_key key = it->second;
+            g_comm_idle.emplace(key, comm);
+            if (g_comm_idle.size() > BA_COMM_IDLE_CAP) {
+                for (auto q = g_comm_idle.begin(); q != g_comm_idle.end(); ++q)
+                    if (q->first < key || key < q->first) {
+                        evict = q->second;
+                        g_comm_key.erase(evict);
+                        g_comm_idle.erase(q);
+                        break;
+                    }
+                static bool warned = false;
+                if (evict && !warned) {
+                    warned = true;
+                    std::fprintf(stderr, "[vlgba] more than %d idle RCCL communicators: "
+                                         "destroying the oldest ids' (call vlgba_comm_release "
+                                         "for ids that will not be used again)\n",
+                                 BA_COMM_IDLE_CAP);
+                }
+            }
         }
     }
-    ncclCommDestroy(comm);   // its id was released while this context held it
+    if (evict) ncclCommDestroy(evict);
 }
 
 static void kt_retire(const ba_ktimer *kt);
@@ -1348,12 +1376,6 @@ static void ctx_free(vlgba_ctx *c)
     if (!c) return;
     if (c->d.stream) (void)hipStreamSynchronize(c->d.stream);
     if (c->d.side) (void)hipStreamSynchronize(c->d.side);
-    if (c->d.redo && std::getenv("VLGBA_REDO_REPORT")) {   // chunks redone with '/'
-        int total = 0;
-        if (hipMemcpy(&total, c->d.redo + 1 + c->d.nch, sizeof(int), hipMemcpyDeviceToHost) ==
-            hipSuccess)
-            std::fprintf(stderr, "[vlgba] chunks linearised again with '/': %d\n", total);
-    }
     for (void *p : c->allocs) ba_dfree(p);
     for (void *p : {(void *)c->pinv_S, (void *)c->pinv_ev, (void *)c->pinv_e, (void *)c->pinv_w,
                     (void *)c->pinv_info})
@@ -1714,16 +1736,6 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         TRY(upload(d.cam_gslots, plan.cam_gslots.data(), plan.cam_gslots.size(), s));
         TRY(ctx_alloc(c, &d.upart, (size_t)(na * (na + 1) / 2 + na) * d.nes));
         TRY(ctx_alloc(c, &d.chsse, 3 * (size_t)d.nch));   // lin SSE | new SSE | dpg
-        TRY(ctx_alloc(c, &d.redo, 2 + (size_t)d.nch));    // count | chunk list | total
-        VLGBA_CHECK(hipMemsetAsync(d.redo, 0, sizeof(int), s));
-        VLGBA_CHECK(hipMemsetAsync(d.redo + 1 + d.nch, 0, sizeof(int), s));
-        const char *fq = std::getenv("VLGBA_FAST_DEHOM"), *rd = std::getenv("VLGBA_DEBUG_REDO");
-        // opt-in (VLGBA_FAST_DEHOM=1): 15 % fewer instructions in the
-        // linearisation, but 6 % slower on MI355X
-        d.fast_dehom = fq && fq[0] == '1';
-        d.ewin = (rd && rd[0] == '1') ? 0u : BA_EWIN;
-        const char *fr = std::getenv("VLGBA_FUSE_REDUCE");
-        d.fuse_red_ok = fr && fr[0] == '1';   // opt-in: no faster
         TRY(upload(d.ch_pt, plan.ch_pt.data(), plan.ch_pt.size(), s));
         TRY(upload(d.ch_eslot, plan.ch_eslot.data(), plan.ch_eslot.size(), s));
         TRY(upload(d.eslot_optr, plan.eslot_optr.data(), plan.eslot_optr.size(), s));
@@ -2076,11 +2088,10 @@ static int resolve_nospin(vlgba_ctx *c, double lam, double hs[6])
     if (d.parity) TRY(ba_launch_parity_new_sums(&d, lam));
     TRY(collect_scalars(c, false, hs));
     c->spin_retries++;
-    // a hand-off that gave up under the envelope runner (most likely its side
+    // one of the envelope runner's own hand-offs gave up (most likely its side
     // stream sharing a hardware queue with the library stream, so the column
-    // launches queue behind it): the column launches alone from now on
-    if (d.env_runner) ba_env_runner_disable();
-    d.env_runner = 0;
+    // launches queue behind it): this context's column launches alone from now on
+    TRY(std::min(0, ba_env_runner_timed_out(&d)));
     return 0;
 }
 
@@ -2297,15 +2308,9 @@ static int lm_pass(vlgba_ctx *c, int relinearize, vlgba_step_info *info)
     } else {
         mark(c, 1);
     }
-    // single rank, no long tracks, envelope tiles, VLGBA_FUSE_REDUCE=1: the
-    // block sums ride in the assembly launch (k_reduce_assemble)
-    d.fuse_red = c->world == 1 && !c->comm && !d.ordered && !d.parity && d.nl == 0 &&
-                 d.n_env > 0 && d.fuse_red_ok;
     TRY(schur_phase(c, lam));
     mark(c, 4);
-    const int arc = ba_launch_assemble(&d);
-    d.fuse_red = 0;
-    TRY(arc);
+    TRY(ba_launch_assemble(&d));
     mark(c, 5);
     TRY(ba_chol_solve(&d));
     for (int w = 4; w <= 5; w++) {   // test hooks: as if a pivot failed / a spin gave up
@@ -2704,8 +2709,11 @@ int vlgba_get_step(vlgba_ctx *c, double *da, double *db)
 
 int vlgba_debug_force_status(vlgba_ctx *c, int word, int passes)
 {
-    if (!c || (word != 4 && word != 5) || passes < 0) return VLGBA_E_ARG;
-    (word == 4 ? c->debug_pivots : c->debug_timeouts) = passes;
+    if (!c || word < 4 || word > 6 || passes < 0) return VLGBA_E_ARG;
+    if (word == 6)
+        c->d.debug_runner_fail = passes;
+    else
+        (word == 4 ? c->debug_pivots : c->debug_timeouts) = passes;
     return 0;
 }
 
@@ -2805,7 +2813,7 @@ int vlgba_plan_info(vlgba_ctx *c, long long *info, int len)
                                       d.ngrp_mf, c->pperm.empty() ? 0 : 1, d.nl, d.nd_np,
                                       d.nd_np ? d.nt - d.nd_a0[d.nd_np] : 0,
                                       (long long)d.fl_factor, (long long)d.fl_syrk,
-                                      (long long)d.fl_back};
+                                      (long long)d.fl_back, d.runner_runs};
     for (int k = 0; k < len && k < VLGBA_NPLAN; k++) info[k] = v[k];
     return VLGBA_NPLAN;
 }

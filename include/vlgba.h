@@ -32,11 +32,12 @@ extern "C" {
  * spin_retries, vlgba_step_info.spin_retry, VLGBA_NPLAN 28; 3 =
  * vlgba_stats.nd_retries, vlgba_step_info.nd_retry, vlgba_comm_release,
  * VLGBA_NKERNELS 18 (k_update_linearize), vlgba_kernel_flops; 4 =
- * vlgba_debug_dehom.  Callers check it
- * once at load time with VLGBA_ABI_CHECK() (the MEX gateways and the Python
+ * vlgba_debug_dehom; 5 = vlgba_debug_dehom removed, VLGBA_NPLAN 29 (the
+ * envelope runner's launch count), vlgba_debug_force_status word 6.  Callers
+ * check it once at load time with VLGBA_ABI_CHECK() (the MEX gateways and the Python
  * loader do): the library compares the version and the struct sizes the
  * caller was compiled with against its own and returns 0 or VLGBA_E_ABI. */
-#define VLGBA_ABI_VERSION 4
+#define VLGBA_ABI_VERSION 5
 
 /* camera models (vlgba_problem.model) */
 #define VLGBA_MODEL_EUCLIDEAN 0   /* bundle_euclid.m: a = [w; T; (K)], num_a 6/7/10     */
@@ -260,9 +261,10 @@ const char *vlgba_kernel_name(int k);
  * reduced solve's algorithmic flops in the launches timed as k_factor_step /
  * k_cr_factor (the one-launch cyclic reduction: all of it) [26] in the
  * separator SYRK (k_syrk) [27] in the backward solve (k_backward / k_cr_back):
- * tile-dense potrf + trtri, GEMMs and GEMVs, each counted once.  Writes
- * min(len, VLGBA_NPLAN) entries, returns VLGBA_NPLAN. */
-#define VLGBA_NPLAN 28
+ * tile-dense potrf + trtri, GEMMs and GEMVs, each counted once [28] envelope
+ * runner launches (k_env_runner, opt-in VLGBA_ENV_RUNNER=1) made by this
+ * context so far.  Writes min(len, VLGBA_NPLAN) entries, returns VLGBA_NPLAN. */
+#define VLGBA_NPLAN 29
 int vlgba_plan_info(vlgba_ctx *ctx, long long *info, int len);
 
 /* ---- stage entries with the reference MEX argument layouts ---------------
@@ -341,7 +343,11 @@ int vlgba_resect(const vlgba_resect_problem *prob, const vlgba_options *opt, dou
                  double *error_out, int error_cap, int *num_error, vlgba_stats *stats);
 
 /* Multi-GPU: rank 0 creates the 128-byte RCCL unique id, the caller
- * broadcasts it (e.g. torch.distributed) and passes it as opt->comm_id. */
+ * broadcasts it (e.g. torch.distributed) and passes it as opt->comm_id.
+ * NOTE: reuse one id for every solve of a device set, or release each id
+ * with vlgba_comm_release once no context will pass it again -- the library
+ * keeps the communicators an id made (below); past 64 idle ones it destroys
+ * those of the oldest ids, with a warning. */
 int vlgba_get_unique_id(void *id128);
 /* The library keeps RCCL communicators for the next context created with the
  * same (id, world size, rank).  A caller that will not pass an id again
@@ -353,13 +359,6 @@ int vlgba_comm_release(const void *id128);
  * algorithm, vlg_libm.h) for n host arguments -- the parity tests compare them
  * with the host libm bit for bit.  |x| < 105414350. */
 int vlgba_debug_sincos(const double *x, double *s, double *c, long long n);
-/* Diagnostics: the linearisation's division-free quotients on n host triples
- * xn [3 * n]: fast [4 * n] = (x0 / x2, x1 / x2) by the shared reciprocal and
- * (x0 / 1e-10, x1 / 1e-10) as the FD quotient forms them; ref [4 * n] the same
- * four by IEEE division; win [n]: bit 0 where x0, x1, x2 are inside the window
- * the shared-reciprocal quotients claim bit-identity for, bit 1 where x0 and
- * x1 are finite and inside the FD quotient's window. */
-int vlgba_debug_dehom(const double *xn, double *fast, double *ref, int *win, long long n);
 /* the pinv fallback of the reduced solve (rocSOLVER dsyevd + the pinv kernels)
  * on a host ld x ld symmetric S (lower triangle read) and e_: da = pinv(S) e_
  * with MATLAB's tolerance ld * eps(max |eigenvalue|). */
@@ -367,8 +366,10 @@ int vlgba_debug_pinv_solve(int ld, const double *S, const double *e_, double *da
 /* Fault injection (tests / the bench's fallback timing): the next `passes`
  * passes of ctx report word 4 = a non-positive pivot (the pass then takes the
  * pinv step) or word 5 = a hand-off spin timeout of the one-launch solve (the
- * pass is solved again without spins).  VLGBA_DEBUG_SPIN_TIMEOUT="rank:passes"
- * sets word 5 at context creation. */
+ * pass is solved again without spins), or word 6 = the envelope runner
+ * (k_env_runner, opt-in VLGBA_ENV_RUNNER=1) fails to start (the factorization
+ * then runs with the column launches alone).  VLGBA_DEBUG_SPIN_TIMEOUT=
+ * "rank:passes" sets word 5 at context creation. */
 int vlgba_debug_force_status(vlgba_ctx *ctx, int word, int passes);
 /* The envelope solve's nested-dissection planner on the host (no GPU): for
  * m cameras of num_a parameters and the co-visible blocks blk_jk [2 * nb]

@@ -164,58 +164,47 @@ def test_nd_grouped_order_bit_identical(gpu, monkeypatch, kind, m, num_a):
     assert np.array_equal(p0[0], p1[0]) and np.array_equal(p0[1], p1[1])
 
 
-@pytest.mark.parametrize("solver,cap", [("nd", 24), ("envelope", 24), ("nd", 300)])
-def test_trailing_workgroup_cap_bit_identical(gpu, monkeypatch, solver, cap):
-    """VLGBA_TRAIL_WGS caps an envelope launch's workgroups: the trailing
-    pairs of column k-1 then take several pairs per workgroup (strided), each
-    with the same operations -- whole LM runs bit for bit equal to one pair per
-    workgroup."""
-    sc = _scene("ladybug", 300, seed=8)
-    a, b = _params(sc, 6)
-
-    def run():
-        with gpu.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, 6, solver=solver,
-                                stop_rel=1e-9, max_iter=6) as ba:
-            ba.set_params(a, b)
-            err, st = ba.run()
-            return err.copy(), [x.copy() for x in ba.get_params()]
-    e0, p0 = run()
-    monkeypatch.setenv("VLGBA_TRAIL_WGS", str(cap))
-    e1, p1 = run()
-    assert np.array_equal(e0, e1)
-    assert np.array_equal(p0[0], p1[0]) and np.array_equal(p0[1], p1[1])
-
-
 @pytest.mark.parametrize("solver,m,num_a", [("nd", 300, 6), ("envelope", 300, 6),
                                              ("nd", 90, 7), ("envelope", 120, 10)])
 def test_env_runner_bit_identical(gpu, monkeypatch, solver, m, num_a):
-    """Runner mode (the default; VLGBA_ENV_RUNNER=0 turns it off: k_env_runner, one persistent workgroup
-    per arc on the side stream, factors the diagonal tiles and forms each
-    column's first panel tile while the column launches run the other panels
-    and the trailing updates; the tiles they exchange go through sc1 stores
-    and flags) against the column launches alone: the same operations in the
-    same order on every tile, so whole LM runs agree bit for bit, and no
-    hand-off gives up (no re-solve)."""
+    """Runner mode (opt-in, VLGBA_ENV_RUNNER=1: k_env_runner, one persistent
+    workgroup per arc on the side stream, factors the diagonal tiles and forms
+    each column's first panel tile while the column launches run the other
+    panels and the trailing updates; the tiles they exchange go through sc1
+    stores and flags) against the column launches alone: the same operations
+    in the same order on every tile, so whole LM runs agree bit for bit, and
+    no hand-off gives up (no re-solve).  The context's runner-launch count
+    proves the runner really ran (a runner switched off earlier in the
+    process would otherwise make this test compare the launches with
+    themselves).  fail_starts: the first starts of the runner fail
+    (vlgba_debug_force_status word 6) -- those factorizations run with the
+    column launches alone, bit for bit the same."""
     sc = _scene("ladybug", m, seed=12)
     a, b = _params(sc, num_a)
 
-    def run():
+    def run(fail_starts=0):
         with gpu.BundleAdjuster(sc.K, sc.obs_pt, sc.obs_cam, sc.obs_x, sc.n, num_a,
                                 solver=solver, stop_rel=1e-9, max_iter=8) as ba:
+            if fail_starts:
+                ba.force_status(6, fail_starts)
             ba.set_params(a, b)
             ba.step(relinearize=True, update_lm=False)
             da, db = ba.last_step()
             err, st = ba.run()
-            return da.copy(), err.copy(), st, [x.copy() for x in ba.get_params()]
-    monkeypatch.setenv("VLGBA_ENV_RUNNER", "0")
-    da0, e0, s0, p0 = run()
+            return (da.copy(), err.copy(), st, [x.copy() for x in ba.get_params()],
+                    ba.plan_info()["env_runner_runs"])
+    monkeypatch.delenv("VLGBA_ENV_RUNNER", raising=False)   # the default: off
+    da0, e0, s0, p0, r0 = run()
     monkeypatch.setenv("VLGBA_ENV_RUNNER", "1")
     monkeypatch.setenv("VLGBA_ENV_RUNNER_MIN", "1")   # these runs are short
-    da1, e1, s1, p1 = run()
-    assert s1.spin_retries == 0 and s0.spin_retries == 0
-    assert np.array_equal(da0, da1)
-    assert np.array_equal(e0, e1)
-    assert np.array_equal(p0[0], p1[0]) and np.array_equal(p0[1], p1[1])
+    da1, e1, s1, p1, r1 = run()
+    da2, e2, s2, p2, r2 = run(fail_starts=2)
+    assert r0 == 0 and r1 > 0 and 0 <= r2 < r1, (r0, r1, r2)
+    assert s0.spin_retries == 0 and s1.spin_retries == 0 and s2.spin_retries == 0
+    for da, e, p in ((da1, e1, p1), (da2, e2, p2)):
+        assert np.array_equal(da0, da)
+        assert np.array_equal(e0, e)
+        assert np.array_equal(p0[0], p[0]) and np.array_equal(p0[1], p[1])
 
 
 def test_nd_projective(gpu):
