@@ -221,9 +221,11 @@ def main():
     for nm, s in big:
         rows[(nm, s)] = gpu_big(pkg, nm, s)
         print(f"[bias] GPU {nm} seed {s} done {time.time() - t0:.0f}s", flush=True)
-    for f in futs + big_futs:
+    from concurrent.futures import as_completed
+    for f in as_completed(futs + big_futs):   # a line per result: the box's silence watchdog
         key, out = f.result()
         rows[key].update(out)
+        print(f"[bias] oracle {key[0]} {key[1]} done {time.time() - t0:.0f}s", flush=True)
     print(f"[bias] oracle done {time.time() - t0:.0f}s", flush=True)
     pool.shutdown()
     if big_pool:
