@@ -229,6 +229,8 @@ struct ba_dev {
     // and its workgroups per CU (VLGBA_PIPE_WGS caps it; 0: the occupancy),
     // or the whole grid (VLGBA_PIPE_GRID: tests give every workgroup many chunks)
     int lin_pipe, pipe_wgs, pipe_grid;
+    int pipe_diag;   // VLGBA_PIPE_DIAG (timing only, wrong results): 1 the memory wave
+                     // skips the W pieces (t_o), 2 waves 0-3 skip the chunk's work
     int ns, nes;
     int ch_max_terms, ch_max_slots;   // per-chunk maxima: LDS staging of the term lists
     long long nterm_fast;             // (obs, obs) Schur terms of the chunk plan

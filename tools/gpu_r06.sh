@@ -42,13 +42,18 @@ for step in "$@"; do
     abpipe)
       # A/B of the fused kernel's forms, one box: VLGBA_LIN_PIPE=0 / 1, and the
       # pipelined form's workgroups per CU (AB_WGS, default "5 4 3")
-      for v in "0 0" ${AB_WGS:-"1 5" "1 4" "1 3"} "0 0"; do
+      if [ -n "$AB_DIAG" ]; then
+        list=("0 0 0" "1 5 0" "1 5 1" "1 5 2" "1 4 1" "1 4 2" "1 3 2")
+      else
+        list=("0 0 0" "1 5 0" "1 4 0" "1 3 0" "0 0 0")
+      fi
+      for v in "${list[@]}"; do
         set -- $v
-        VLGBA_LIN_PIPE=$1 VLGBA_PIPE_WGS=$2 timeout -k 10 300 python -u bench.py --steps 100 \
-          --warmup 50 --no-cpu-baseline --no-other-configs > gpurun_out/ab_pipe_$1_$2.json \
-          2> gpurun_out/ab_pipe_$1_$2.log || exit 1
-        echo "pipe=$1 wgs=$2 $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_pipe_$1_$2.json)"
-        grep -o 'k_update_linearize[a-z_]*=[0-9.]*us' gpurun_out/ab_pipe_$1_$2.log | head -2
+        VLGBA_LIN_PIPE=$1 VLGBA_PIPE_WGS=$2 VLGBA_PIPE_DIAG=$3 timeout -k 10 300 python -u bench.py --steps 100 \
+          --warmup 50 --no-cpu-baseline --no-other-configs > gpurun_out/ab_pipe_$1_$2_$3.json \
+          2> gpurun_out/ab_pipe_$1_$2_$3.log || exit 1
+        echo "pipe=$1 wgs=$2 diag=$3 $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_pipe_$1_$2_$3.json)"
+        grep -o 'k_update_linearize[a-z_]*=[0-9.]*us' gpurun_out/ab_pipe_$1_$2_$3.log | head -2
       done ;;
     bias)
       timeout -k 10 900 python -u tools/converged_bias.py --sets cfg2,cfg3 --big-seeds 12 \
