@@ -224,13 +224,6 @@ struct ba_dev {
     // next linearisation's buffers, swapped in by an accepted step
     int fused;
     double *W2, *V2, *eB2, *upart2, *chsse2;
-    // the fused kernel's software-pipelined form (k_update_linearize_pipe:
-    // NA = 6, no segment chunks; VLGBA_LIN_PIPE=0 keeps k_update_linearize)
-    // and its workgroups per CU (VLGBA_PIPE_WGS caps it; 0: the occupancy),
-    // or the whole grid (VLGBA_PIPE_GRID: tests give every workgroup many chunks)
-    int lin_pipe, pipe_wgs, pipe_grid;
-    int pipe_diag;   // VLGBA_PIPE_DIAG (timing only, wrong results): 1 the memory wave
-                     // skips the W pieces (t_o), 2 waves 0-3 skip the chunk's work
     int ns, nes;
     int ch_max_terms, ch_max_slots;   // per-chunk maxima: LDS staging of the term lists
     long long nterm_fast;             // (obs, obs) Schur terms of the chunk plan

@@ -693,362 +693,6 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_update_linearize(BA_
     linearize_chunk_body<NA, true>(BA_LIN_PASS, u, blockIdx.x);
 }
 
-// -------------------------------------------------------------------------
-// The fused update + linearisation, software-pipelined (NA = 6, regular
-// chunks).  k_update_linearize's workgroup waits for its
-// chunk's old W rows (144 B per observation: the 432 MB W stream at config 3)
-// before it can project, so every workgroup runs a memory phase and then a
-// VALU phase (37 % / 46 % of its time, profiles/r05e_stamps_fused.txt) and
-// the kernel takes close to the SUM of the two.  Here a workgroup is
-// persistent (chunks blockIdx.x, + gridDim.x, ...) and has a fifth wave, the
-// memory wave, that prepares chunk i + 1 while waves 0-3 linearise chunk i:
-//   memory wave   the chunk's metadata (point and camera-slot offsets), then
-//                 the update (mex_bundle_3_db_new.c:99-146): its old W rows
-//                 in pieces of BA_PIPE_PO observations (coalesced 16-byte
-//                 loads, the next piece in flight while this one is used),
-//                 t_o = W_o' da (:113-120), rhs = eB_i - t_o1 - t_o2 - ...,
-//                 db_i = V*_i^-1 rhs, b_new, the point part of dp'(lambda dp +
-//                 g) -- the same expressions in the same order as
-//                 k_update_linearize -- with b_new handed over in LDS
-//                 (double-buffered by chunk parity)
-//   waves 0-3     the projections at (a_new, b_new) and the W / V, eB / U,
-//                 eA phases, exactly as k_update_linearize
-// Two workgroup barriers per chunk (chunk start, rows complete), both
-// LDS-only fences: no wave waits there for its own global loads or stores,
-// so the memory wave's loads stay in flight across them and the compute
-// waves' W / V / U stores drain behind the next chunk.  The chunk's SSE
-// partial (block_sum_to's wave sums, then their sum in wave order) is
-// finished by thread 0 after the next chunk start.  Bit-identical to
-// k_update_linearize (tests/test_gpu_fused.py).
-// -------------------------------------------------------------------------
-#ifndef BA_PIPE_WGS
-#define BA_PIPE_WGS 5   // workgroups per CU the LDS budget is sized for
-#endif
-#if BA_PIPE_WGS >= 5
-#define BA_PIPE_PO 32   // observations per W piece of the memory wave
-#define BA_PIPE_DS 52   // da rows staged per chunk (its camera span)
-#else
-#define BA_PIPE_PO 64
-#define BA_PIPE_DS 128
-#endif
-
-// workgroup barrier ordering LDS only (no wait for outstanding global loads
-// or stores: __syncthreads would wait for both)
-__device__ __forceinline__ void lds_barrier()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-// x as a value the compiler cannot see through: the lane-dependent values a
-// persistent loop derives from the thread id are then formed inside each
-// iteration instead of being hoisted out of the loop and kept live (spilled)
-// through the projections
-__device__ __forceinline__ int opaque_int(int x)
-{
-    asm volatile("" : "+v"(x));
-    return x;
-}
-
-// __shfl_down(v, off, 64) by ds_bpermute from the lane index `lane` (no
-// mbcnt: the loop-invariant lane id would be hoisted)
-__device__ __forceinline__ double shfl_down64(double v, int off, int lane)
-{
-    const int src = (lane + off < 64 ? lane + off : lane) << 2;
-    const int lo = __builtin_amdgcn_ds_bpermute(src, __double2loint(v));
-    const int hi = __builtin_amdgcn_ds_bpermute(src, __double2hiint(v));
-    return __hiloint2double(hi, lo);
-}
-
-// one wave's LDS writes visible to its other lanes
-__device__ __forceinline__ void wave_lds_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-}
-
-template <int NA>
-__global__ __launch_bounds__(320, 7) void k_update_linearize_pipe(BA_LIN_ARGS, ba_upd u, int diag)
-{
-    static_assert(NA == 6, "the pipelined kernel is the fix_calibration model's");
-    constexpr int RS = 2 * NA + 8;          // LDS row: A (2 NA), B (6), e (2)
-    constexpr int NU = NA * (NA + 1) / 2;
-    constexpr int PO = BA_PIPE_PO, NDS = BA_PIPE_DS;
-    constexpr int PU = (PO * 3 * NA / 2 + 63) / 64;   // 16-byte units per lane per piece
-    __shared__ __attribute__((aligned(16))) double rows[BA_CH_OBS * RS];
-    __shared__ __attribute__((aligned(16))) double wbuf[PO * 3 * NA];
-    __shared__ double dst[NDS * NA];
-    __shared__ double bnew[2][BA_CH_PTS * 3];
-    __shared__ int lptr[2][BA_CH_PTS + 1];
-    __shared__ int eoff[2][BA_CH_OBS + 1];
-    __shared__ int cinf[2][8];   // p0 np obase nobs e0 nes u0 nu
-    __shared__ unsigned short eobl[BA_CH_OBS];
-    __shared__ unsigned char wz[BA_CH_OBS];
-    __shared__ double red[2][4];
-    static_assert(BA_CH_PTS <= 64, "the point lanes are the memory wave's");
-    const int tid = threadIdx.x;
-    const int G = gridDim.x;
-
-    if (tid >= 256) {
-        // ================= the memory wave =================
-        const int l = tid - 256;
-        auto prep = [&](int c, int q) {
-            const int p0 = ch_pt[c], np = ch_pt[c + 1] - p0;
-            const int obase = ch_obase[c], nobs = ch_obase[c + 1] - obase;
-            const int e0 = ch_eslot[c], nes = ch_eslot[c + 1] - e0;
-            const int clo = ch_cam[2 * c], span = ch_cam[2 * c + 1] - clo + 1;
-            const bool dstage = span <= NDS;
-            const v2d *wsrc = reinterpret_cast<const v2d *>(u.W_old + (size_t)3 * NA * obase);
-            v2d pr[PU];
-            auto piece_load = [&](int o0) {
-                const int nv = min(PO, nobs - o0) * (3 * NA / 2);
-#pragma unroll
-                for (int k = 0; k < PU; k++) {
-                    const int t = l + 64 * k;
-                    pr[k] = __builtin_nontemporal_load(wsrc + (3 * NA / 2) * o0 + min(t, nv - 1));
-                }
-            };
-            if (nobs > 0) piece_load(0);
-            for (int t = l; t <= np; t += 64) lptr[q][t] = pt_ptr[p0 + t];
-            for (int t = l; t <= nes; t += 64) eoff[q][t] = eslot_optr[e0 + t];
-            if (dstage && nobs > 0)
-                for (int t = l; t < span * NA; t += 64) dst[t] = u.da[(size_t)NA * clo + t];
-            // the point lanes' eB (V*^-1 and b after the pieces: registers)
-            const int ip = np > 0 ? p0 + min(l, np - 1) : 0;
-            double pe[3], rhs[3];
-#pragma unroll
-            for (int r = 0; r < 3; r++) pe[r] = u.eB_old[3 * (size_t)ip + r];
-#pragma unroll
-            for (int r = 0; r < 3; r++) rhs[r] = pe[r];
-            wave_lds_sync();
-            const int lo0 = l < np ? lptr[q][l] - obase : 0;
-            const int lo1 = l < np ? lptr[q][l + 1] - obase : 0;
-            for (int o0 = 0; o0 < ((diag & 1) ? 0 : nobs); o0 += PO) {
-                const int no = min(PO, nobs - o0), nv = no * (3 * NA / 2);
-                v2d *w2 = reinterpret_cast<v2d *>(wbuf);
-#pragma unroll
-                for (int k = 0; k < PU; k++)
-                    if (l + 64 * k < nv) w2[l + 64 * k] = pr[k];
-                if (o0 + PO < nobs) piece_load(o0 + PO);   // in flight through this piece
-                wave_lds_sync();
-                // t_o[r] = W_o(:, r)' da_j (mex_bundle_3_db_new.c:113-120), into
-                // the row's first slot (only this lane reads the row)
-                if (l < no) {
-                    const int oc = obs_cam[obase + o0 + l];
-                    double dl[NA];
-                    if (dstage) {
-#pragma unroll
-                        for (int k = 0; k < NA; k++) dl[k] = dst[NA * (oc - clo) + k];
-                    } else {
-#pragma unroll
-                        for (int k = 0; k < NA; k++) dl[k] = u.da[(size_t)NA * oc + k];
-                    }
-#pragma unroll
-                    for (int k = 0; k < NA; k++)   // da(1:ndb) only (mex_bundle_3 :113-120)
-                        if (k >= u.ndb) dl[k] = 0.0;
-                    double *wo = wbuf + 3 * NA * l;
-#pragma unroll
-                    for (int r = 0; r < 3; r++) {
-                        double *w = wo + NA * r;
-                        const double t = w[0] * dl[0] + w[1] * dl[1] + w[2] * dl[2] +
-                                         w[3] * dl[3] + w[4] * dl[4] + w[5] * dl[5];
-                        w[0] = t;
-                    }
-                }
-                wave_lds_sync();
-                // rhs = eB_i - t_o1 - t_o2 - ... (cameras ascending): this
-                // piece's observations of the lane's point, in order
-                if (l < np) {
-                    const int a1 = min(lo1, o0 + no);
-                    for (int lo = max(lo0, o0); lo < a1; lo++) {
-#pragma unroll
-                        for (int r = 0; r < 3; r++) rhs[r] -= wbuf[3 * NA * (lo - o0) + NA * r];
-                    }
-                }
-                wave_lds_sync();
-            }
-            // db_i = V*_i^-1 rhs, b_new, dp'(lambda dp + g) (:99-146,
-            // bundle_euclid.m:213-217); a point without observations gets
-            // db = V*^-1 eB (= 0) all the same
-            double dpg = 0.0;
-            if (l < np) {
-                const int i = p0 + l;
-                double pv[9], pb[3];
-#pragma unroll
-                for (int r = 0; r < 9; r++) pv[r] = u.Vinv[9 * (size_t)i + r];
-#pragma unroll
-                for (int r = 0; r < 3; r++) pb[r] = u.b_old[3 * (size_t)i + r];
-#pragma unroll
-                for (int r = 0; r < 3; r++) {
-                    const double dbr = pv[r] * rhs[0] + pv[r + 3] * rhs[1] + pv[r + 6] * rhs[2];
-                    const double bnr = pb[r] + dbr;
-                    u.db[3 * (size_t)i + r] = dbr;
-                    u.b_new[3 * (size_t)i + r] = bnr;
-                    bnew[q][3 * l + r] = bnr;
-                    dpg += dbr * (u.lambda * dbr + pe[r]);
-                }
-            }
-            // the chunk's point part of dp'(lambda dp + g), points in order
-            double acc = 0.0;
-            for (int k = 0; k < np; k++) acc += __shfl(dpg, k, 64);
-            if (l == 0) {
-                u.part_dpg[c] = acc;
-                const int u0 = eoff[q][0];
-                cinf[q][0] = p0;
-                cinf[q][1] = np;
-                cinf[q][2] = obase;
-                cinf[q][3] = nobs;
-                cinf[q][4] = e0;
-                cinf[q][5] = nes;
-                cinf[q][6] = u0;
-                cinf[q][7] = eoff[q][nes] - u0;
-            }
-        };
-        if ((int)blockIdx.x < nch_reg) prep(blockIdx.x, 0);
-        int i = 0;
-        for (int ch = blockIdx.x; ch < nch_reg; ch += G, i++) {
-            lds_barrier();   // chunk i's start
-            if (ch + G < nch_reg) prep(ch + G, (i + 1) & 1);
-            lds_barrier();   // chunk i's rows complete
-        }
-        lds_barrier();
-        return;
-    }
-
-    // ================= waves 0-3: the linearisation =================
-    int i = 0;
-    for (int ch = blockIdx.x; ch < nch_reg; ch += G, i++) {
-        const int q = i & 1;
-        const int tid = opaque_int(threadIdx.x);
-        lds_barrier();   // chunk i's start: its metadata and b_new in LDS (parity q)
-        // (uniform: scalar registers, not 8 VGPRs live through the projections)
-        const int p0 = __builtin_amdgcn_readfirstlane(cinf[q][0]);
-        const int np = __builtin_amdgcn_readfirstlane(cinf[q][1]);
-        const int obase = __builtin_amdgcn_readfirstlane(cinf[q][2]);
-        const int nobs = __builtin_amdgcn_readfirstlane(cinf[q][3]);
-        const int e0 = __builtin_amdgcn_readfirstlane(cinf[q][4]);
-        const int nes = __builtin_amdgcn_readfirstlane(cinf[q][5]);
-        const int u0 = __builtin_amdgcn_readfirstlane(cinf[q][6]);
-        const int nu = __builtin_amdgcn_readfirstlane(cinf[q][7]);
-        if (tid == 0 && i > 0)   // the previous chunk's SSE (block_sum_to's order)
-            part_sse[ch - G] = ((red[q ^ 1][0] + red[q ^ 1][1]) + red[q ^ 1][2]) + red[q ^ 1][3];
-        double sse = 0.0;
-        int m_eobl = 0;
-        if (diag & 2) {   // timing only: waves 0-3 idle (nothing of rows is read)
-            lds_barrier();
-            if ((tid & 63) == 0) red[q][tid >> 6] = 0.0;
-            continue;
-        }
-        if (nobs > 0) {   // (nu > 0 too)
-            m_eobl = __hip_atomic_load(eslot_obs + u0 + min(tid, nu - 1), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-            // lanes past the chunk's observations project its last one again
-            // into rows nobs .. BA_CH_OBS - 1, which nothing reads (lanes past
-            // BA_CH_OBS rows, when it is < 128, into the last row: the same
-            // values as any lane that writes it)
-            const int lo = min(tid >> 1, BA_CH_OBS - 1), half = tid & 1;
-            const bool live = (tid >> 1) < nobs;
-            const int o = obase + min(lo, nobs - 1);
-            const int j = obs_cam[o], lp = obs_lpt[o];
-            double bi[3];
-#pragma unroll
-            for (int c = 0; c < 3; c++) bi[c] = bnew[q][3 * lp + c];
-            cam_view<NA> cv(a, K4, rot, j);
-            double xh[2];
-            double *row = rows + RS * lo;
-            cv.project(bi, xh);
-            fd_columns_6(cv, bi, xh, half, row);
-            if (!half) {
-                const double e0v = obs_x[2 * (size_t)o] - xh[0];
-                const double e1v = obs_x[2 * (size_t)o + 1] - xh[1];
-                row[2 * NA + 6] = e0v;
-                row[2 * NA + 7] = e1v;
-                if (live) sse = e0v * e0v + e1v * e1v;
-                wz[lo] = f.fix_structure || f.fix_motion || (f.has_pivot && pivot[j]);
-            }
-        }
-        if (tid < nu) eobl[tid] = (unsigned short)m_eobl;
-        lds_barrier();   // chunk i's rows complete
-        // W_ij = A^T B onto a zeroed output (:305-314), as k_update_linearize
-        {
-            v2d *wdst = reinterpret_cast<v2d *>(W + (size_t)3 * NA * obase);
-            constexpr int NP = 3 * NA / 2;
-            for (int t = tid; t < nobs * NP; t += 256) {
-                const int lo = t / NP, e = t - NP * lo, c = e / (NA / 2), r = 2 * (e - (NA / 2) * c);
-                const double *row = rows + RS * lo;
-                const double2 a0 = *reinterpret_cast<const double2 *>(row + 2 * r);
-                const double2 a1 = *reinterpret_cast<const double2 *>(row + 2 * r + 2);
-                const double2 bc = *reinterpret_cast<const double2 *>(row + 2 * NA + 2 * c);
-                const long long keep = wz[lo] ? 0 : -1;
-                const double v0 = 0.0 + (a0.x * bc.x + a0.y * bc.y);
-                const double v1 = 0.0 + (a1.x * bc.x + a1.y * bc.y);
-                const v2d w2 = {__builtin_bit_cast(double, __builtin_bit_cast(long long, v0) & keep),
-                                __builtin_bit_cast(double, __builtin_bit_cast(long long, v1) & keep)};
-                __builtin_nontemporal_store(w2, wdst + t);
-            }
-        }
-        // V_i += B^T B, eB_i += B^T e over the point's cameras (:293-302, :326-332)
-        for (int t = tid; t < np * 12; t += 256) {
-            const int pl = t / 12, e = t % 12, ip = p0 + pl;
-            const int lo0 = lptr[q][pl] - obase, lo1 = lptr[q][pl + 1] - obase;
-            const int r = (e < 9) ? e % 3 : e - 9, c = (e < 9) ? e / 3 : 3;
-            double acc = 0.0;
-            for (int lo = lo0; lo < lo1; lo++) {
-                const double *B = rows + RS * lo + 2 * NA;
-                acc += B[2 * r] * B[2 * c] + B[2 * r + 1] * B[2 * c + 1];
-            }
-            if (f.fix_structure) acc = 0.0;
-            if (e < 9) V[9 * (size_t)ip + e] = acc;
-            else eB[3 * (size_t)ip + e - 9] = acc;
-        }
-        // U_j (lower triangle) / eA_j partials per camera of the chunk
-        for (int t = tid; t < nes * (NU + NA); t += 256) {
-            const int s = t / (NU + NA), lq = t % (NU + NA);
-            int r, c;
-            if (lq < NU) {
-                int tt = lq;
-                c = 0;
-                while (tt >= NA - c) { tt -= NA - c; c++; }
-                r = c + tt;
-            } else {
-                r = lq - NU;
-                c = NA;
-            }
-            const int cc = (c < NA) ? 2 * c : 2 * NA + 6;
-            double acc = 0.0;
-            int uu = eoff[q][s] - u0;
-            const int u1 = eoff[q][s + 1] - u0;
-            for (; uu + 3 < u1; uu += 4) {
-                double pp[4];
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const double *rw = rows + RS * eobl[uu + k];
-                    pp[k] = rw[2 * r] * rw[cc] + rw[2 * r + 1] * rw[cc + 1];
-                }
-#pragma unroll
-                for (int k = 0; k < 4; k++) acc += pp[k];
-            }
-            for (; uu < u1; uu++) {
-                const double *row = rows + RS * eobl[uu];
-                acc += row[2 * r] * row[cc] + row[2 * r + 1] * row[cc + 1];
-            }
-            upart[(size_t)(NU + NA) * (e0 + s) + lq] = acc;
-        }
-        // this wave's part of the chunk's SSE (block_sum_to's shuffle order)
-        double v = sse;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v += shfl_down64(v, off, tid & 63);
-        if ((tid & 63) == 0) red[q][tid >> 6] = v;
-    }
-    lds_barrier();
-    if (tid == 0 && i > 0) {
-        const int q = (i - 1) & 1;
-        part_sse[blockIdx.x + (i - 1) * G] = ((red[q][0] + red[q][1]) + red[q][2]) + red[q][3];
-    }
-}
-
 // U_j, eA_j from the per-chunk partials (fast path).  One 256-lane workgroup
 // per camera: lane (entry l, stream p) sums the camera's partials p, p + P,
 // p + 2P, ... (P = 256 / (NU + NA) streams, so ~P loads are in flight per
@@ -2884,25 +2528,8 @@ static int launch_update_fused(ba_dev *d, double lambda, ba_flags f)
                                d->dpg_long)));
     const ba_upd u{d->W, d->da, d->eB, d->Vinv, d->b, d->ndb, lambda, d->db, d->b_new,
                    d->chsse2 + 2 * (size_t)d->nch, d->seg_long, d->long_o0, d->dpg_long};
-    if (d->lin_pipe && d->na == 6 && d->nl == 0 && d->nch == d->nch_reg) {
-        // persistent workgroups: as many as fit on the chip (the occupancy of
-        // the LDS budget, BA_PIPE_WGS per CU), at most one per chunk
-        static int occ = 0;
-        if (occ == 0 &&
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_update_linearize_pipe<6>, 320,
-                                                         0) != hipSuccess)
-            occ = 1;
-        const int per_cu = std::max(1, d->pipe_wgs > 0 ? std::min(d->pipe_wgs, occ) : occ);
-        const int G = std::min(d->nch, d->pipe_grid > 0 ? d->pipe_grid : per_cu * d->ncu);
-        k_update_linearize_pipe<6><<<G, 320, 0, d->stream>>>(
-            d->ch_pt, d->ch_obase, d->ch_eslot, d->eslot_optr, d->eslot_obs, d->pt_ptr,
-            d->obs_cam, d->obs_lpt, d->obs_x, d->K4, d->a_new, d->rot_new, d->b_new, f, d->pivot,
-            d->W2, d->V2, d->eB2, d->upart2, d->chsse2, d->nch_reg, d->seg_pt, d->vseg,
-            d->ch_cam, u, d->pipe_diag);
-    } else {
-        BA_DISPATCH(d->na, (lin_chunk_launch<NA>(d, f, d->a_new, d->rot_new, d->b_new, d->W2,
-                                                 d->V2, d->eB2, d->upart2, d->chsse2, &u)));
-    }
+    BA_DISPATCH(d->na, (lin_chunk_launch<NA>(d, f, d->a_new, d->rot_new, d->b_new, d->W2,
+                                             d->V2, d->eB2, d->upart2, d->chsse2, &u)));
     if (d->nl > 0)   // long tracks: V2 / eB2 = sum of their segments' partials
         k_long_vsum<<<d->nl, 64, 0, d->stream>>>(d->long_pt, d->long_seg0, d->vseg, d->V2,
                                                  d->eB2);

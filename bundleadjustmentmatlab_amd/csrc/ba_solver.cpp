@@ -1766,13 +1766,6 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         TRY(ctx_alloc(c, &d.upart2, (size_t)(na * (na + 1) / 2 + na) * d.nes));
         TRY(ctx_alloc(c, &d.chsse2, 3 * (size_t)d.nch));
         d.fused = 1;
-        const char *pe = std::getenv("VLGBA_LIN_PIPE"), *pw = std::getenv("VLGBA_PIPE_WGS");
-        d.lin_pipe = !(pe && pe[0] == '0');
-        d.pipe_wgs = pw ? std::max(0, std::atoi(pw)) : 0;
-        const char *pg = std::getenv("VLGBA_PIPE_GRID");
-        d.pipe_grid = pg ? std::max(0, std::atoi(pg)) : 0;
-        const char *pd = std::getenv("VLGBA_PIPE_DIAG");
-        d.pipe_diag = pd ? std::atoi(pd) : 0;
     }
     TRY(ctx_alloc(c, &d.blk_jk, 2 * (size_t)d.nb));
     TRY(ctx_alloc(c, &d.blk_ptr, (size_t)d.nb + 1));

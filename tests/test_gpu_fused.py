@@ -173,42 +173,3 @@ def test_da_staging_bit_identical(gpu, monkeypatch, kind):
     for x, y in zip(p1, p0):
         assert np.array_equal(x, y)
 
-
-@pytest.mark.parametrize("kind,kw,grid", [("banded", {}, 0), ("banded", {}, 7),
-                                          ("banded", {}, 1), ("fixstruct", dict(fix_structure=True), 3),
-                                          ("fixmotion", dict(fix_motion=True), 5),
-                                          ("pivot", dict(pivot="first2"), 2)])
-def test_pipelined_update_bit_identical(gpu, monkeypatch, kind, kw, grid):
-    """k_update_linearize_pipe (NA = 6, no segment chunks; the default) against
-    k_update_linearize (VLGBA_LIN_PIPE=0): persistent workgroups, the memory
-    wave preparing the next chunk's update while waves 0-3 linearise this
-    one, the same expressions in the same order -- so every pass of a whole
-    LM run (the step, the pass scalars including the new SSE and dp'g, the
-    linearisation an accepted step takes) is bit for bit the same.  grid > 0
-    (VLGBA_PIPE_GRID) gives each workgroup many chunks, so the chunk-parity
-    hand-off is exercised on a small scene; grid = 1: one workgroup walks
-    every chunk."""
-    sc = _scene(kind)
-    a, b = _start(sc, 6)
-    out = {}
-    for pipe in ("1", "0"):
-        monkeypatch.setenv("VLGBA_LIN_PIPE", pipe)
-        if grid:
-            monkeypatch.setenv("VLGBA_PIPE_GRID", str(grid))
-        ba = _make(gpu, sc, 6, kw, True)
-        ba.set_params(a, b)
-        infos, steps = [], []
-        for _ in range(4):
-            i = ba.step(relinearize=True, update_lm=True)
-            infos.append((i.old_sse, i.new_sse, i.dpg, i.accepted, i.lambda_))
-            da, db = ba.last_step()
-            steps.append((da.copy(), db.copy()))
-        out[pipe] = (infos, steps, ba.get_params(), ba.linearization())
-        ba.close()
-    p, n = out["1"], out["0"]
-    assert p[0] == n[0]
-    for (da1, db1), (da0, db0) in zip(p[1], n[1]):
-        assert np.array_equal(da1, da0) and np.array_equal(db1, db0)
-    assert np.array_equal(p[2][0], n[2][0]) and np.array_equal(p[2][1], n[2][1])
-    for nm in ("W", "V", "eB", "U", "eA"):
-        assert np.array_equal(p[3][nm], n[3][nm]), nm

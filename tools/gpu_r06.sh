@@ -39,22 +39,6 @@ for step in "$@"; do
       timeout -k 10 600 python -u -m pytest tests/test_gpu_fused.py -x -v --timeout 300 \
         --timeout-method thread > gpurun_out/test_fused.log 2>&1; rc=$?
       tail -15 gpurun_out/test_fused.log; [ $rc -eq 0 ] || exit $rc ;;
-    abpipe)
-      # A/B of the fused kernel's forms, one box: VLGBA_LIN_PIPE=0 / 1, and the
-      # pipelined form's workgroups per CU (AB_WGS, default "5 4 3")
-      if [ -n "$AB_DIAG" ]; then
-        list=("0 0 0" "1 5 0" "1 5 1" "1 5 2" "1 4 1" "1 4 2" "1 3 2")
-      else
-        list=("0 0 0" "1 5 0" "1 4 0" "1 3 0" "0 0 0")
-      fi
-      for v in "${list[@]}"; do
-        set -- $v
-        VLGBA_LIN_PIPE=$1 VLGBA_PIPE_WGS=$2 VLGBA_PIPE_DIAG=$3 timeout -k 10 300 python -u bench.py --steps 100 \
-          --warmup 50 --no-cpu-baseline --no-other-configs > gpurun_out/ab_pipe_$1_$2_$3.json \
-          2> gpurun_out/ab_pipe_$1_$2_$3.log || exit 1
-        echo "pipe=$1 wgs=$2 diag=$3 $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_pipe_$1_$2_$3.json)"
-        grep -o 'k_update_linearize[a-z_]*=[0-9.]*us' gpurun_out/ab_pipe_$1_$2_$3.log | head -2
-      done ;;
     bias)
       timeout -k 10 900 python -u tools/converged_bias.py --sets cfg2,cfg3 --big-seeds 12 \
         --out gpurun_out/bias_big.json > gpurun_out/bias_big.log 2>&1 || exit 1
