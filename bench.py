@@ -53,6 +53,11 @@ def main():
                          "clocks have ramped -- a 20-step region right after 3 warmups "
                          "measured 0.66 ms/pass against 0.62 steady, tools/step_times.py; "
                          "2 for cfg5, 0 for cfg5x)")
+    ap.add_argument("--clock-ramp", type=float, default=0.25,
+                    help="pass/solve modes: seconds of untimed passes before the W warmup "
+                         "steps (default 0.25; 0: none), so the timed steps see the clock "
+                         "the GPU holds under load (DVFS: the first ~30 ms of passes run "
+                         "slower whatever W is; recorded in the line as clock_ramp)")
     ap.add_argument("--config", default="cfg3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-other-configs", action="store_true",
@@ -134,9 +139,30 @@ def main():
     kms = ba.kernel_ms(reset=True)
     ba.set_timing(False)
     ph = {k: float(np.median([p[k] for p in phases])) for k in phases[0]}
-    # the W warmup steps after the timing-mode passes: the first passes after
-    # switching it off carry one-time costs (measured: ~0.8 ms over a 20-step
+    # clock ramp: untimed passes for --clock-ramp seconds (every one a full
+    # pass, like the timed ones), so the measurement is the steady state and
+    # not the GPU's DVFS ramp from idle (a 20-step region right after a few
+    # warmups ran ~6 % slow: 0.609 vs 0.573 ms, BENCH_r05 against the 100 / 50
+    # runs); then the W warmup steps: the first passes after switching the
+    # timing mode off carry one-time costs (measured: ~0.8 ms over a 20-step
     # region when the timed steps followed it directly)
+    # (a pass count, the same on every rank: each pass holds collectives)
+    ramp = {"seconds": 0.0, "passes": 0}
+    if args.clock_ramp > 0:
+        t_r = time.perf_counter()
+        for _ in range(3):
+            ba.step(relinearize=True, update_lm=False)
+        ba.sync()
+        t_pass = max((time.perf_counter() - t_r) / 3, 1e-5)
+        n_ramp = int(min(args.clock_ramp / t_pass, 20000))
+        if world > 1:
+            tt = torch.tensor([n_ramp], dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            n_ramp = int(tt.item())
+        for _ in range(n_ramp):
+            ba.step(relinearize=True, update_lm=False)
+        ba.sync()
+        ramp = {"seconds": time.perf_counter() - t_r, "passes": 3 + n_ramp}
     for _ in range(args.warmup):
         ba.step(relinearize=True, update_lm=False)
     ba.sync()
@@ -242,6 +268,7 @@ def main():
                                  ("gloo host all-reduce (ranks share a GPU)" if world > 1 else
                                   None)},
         "phases_ms": ph,
+        "clock_ramp": ramp,
         "roofline": roof,
         "whole_pass": whole_pass(plan, ms_step),
         "solve_roofline": {k: roofs[k] for k in SOLVE_FLOPS if k in roofs},

@@ -5,6 +5,7 @@
 #   pmc       PMC passes of the cfg3 bench (one counter set per run, no trace
 #             domains) -> gpurun_out/pmc/<set>/ ; PMC_SETS overrides the sets
 #   kstats    rocprofv3 --kernel-trace --stats of the cfg3 bench -> gpurun_out/kstats/
+#   stream    tools/build/ubench_stream (HBM read / write / copy rates)
 #   bias      tools/converged_bias.py --sets cfg2,cfg3 --big-seeds 12
 # usage: tools/gpu_r06.sh step [step ...]
 set -o pipefail
@@ -22,7 +23,7 @@ for step in "$@"; do
       else
         sets=("SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES"
               "SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_INSTS_VALU SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE GRBM_COUNT"
-              "TA_TA_BUSY_sum TA_BUFFER_READ_WAVEFRONTS_sum TD_TD_BUSY_sum")
+              "TA_TA_BUSY_sum TA_FLAT_READ_WAVEFRONTS_sum TD_TD_BUSY_sum TD_TC_STALL_sum")
       fi
       for i in "${!sets[@]}"; do
         out=gpurun_out/pmc/set$i
@@ -39,6 +40,9 @@ for step in "$@"; do
       timeout -k 10 600 python -u -m pytest tests/test_gpu_fused.py -x -v --timeout 300 \
         --timeout-method thread > gpurun_out/test_fused.log 2>&1; rc=$?
       tail -15 gpurun_out/test_fused.log; [ $rc -eq 0 ] || exit $rc ;;
+    stream)
+      timeout -k 10 120 tools/build/ubench_stream > gpurun_out/ubench_stream.txt 2>&1 || exit 1
+      cat gpurun_out/ubench_stream.txt ;;
     bias)
       timeout -k 10 900 python -u tools/converged_bias.py --sets cfg2,cfg3 --big-seeds 12 \
         --out gpurun_out/bias_big.json > gpurun_out/bias_big.log 2>&1 || exit 1
