@@ -304,6 +304,7 @@ struct ba_upd {
     double *db, *b_new, *part_dpg;
     const int *seg_long, *long_o0;
     const double *dpg_long;
+    int pf_dist;   // > 0: touch the W rows of chunk ch + pf_dist into the caches
 };
 
 template <int NA, bool UPD>
@@ -433,6 +434,22 @@ __device__ __forceinline__ void linearize_chunk_body(
                     for (int k = 0; k < NA; k++) dl[k] = dd[k];
                 }
             }
+            // pf_dist > 0: one load per 128-byte line of the old W rows of
+            // chunk ch + pf_dist (a workgroup of a later generation on this
+            // XCD), so that its update phase finds them in L2 / MALL; in
+            // flight beside this chunk's loads, waited for at the barrier
+            unsigned pfv = 0;
+            {
+                const int nx = ch + u.pf_dist;
+                if (u.pf_dist > 0 && nx < nch_reg) {
+                    const int ob = ch_obase[nx];
+                    const int nb = (ch_obase[nx + 1] - ob) * 8 * 3 * NA;
+                    if (128 * tid < nb)
+                        pfv = *reinterpret_cast<const unsigned *>(
+                            reinterpret_cast<const char *>(u.W_old + (size_t)3 * NA * ob) +
+                            128 * tid);
+                }
+            }
             // the point lanes' operands (eB, V*^-1, b): in flight through t_o
             const int ip = np > 0 ? p0 + min(tid, np - 1) : 0;
             double pe[3], pv[9], pb[3];
@@ -443,6 +460,7 @@ __device__ __forceinline__ void linearize_chunk_body(
 #pragma unroll
             for (int r = 0; r < 3; r++) pb[r] = u.b_old[3 * (size_t)ip + r];
             __syncthreads();
+            asm volatile("" ::"v"(pfv));   // (the prefetch's value: nothing reads it)
             // t_o[r] = W_o(:, r)' da_j (mex_bundle_3_db_new.c:113-120), into the
             // row's first slot (only this lane reads the row)
             if (tid < nobs) {
@@ -2527,7 +2545,8 @@ static int launch_update_fused(ba_dev *d, double lambda, ba_flags f)
                                d->Vinv, d->b, d->ndb, lambda, d->db, d->b_new,
                                d->dpg_long)));
     const ba_upd u{d->W, d->da, d->eB, d->Vinv, d->b, d->ndb, lambda, d->db, d->b_new,
-                   d->chsse2 + 2 * (size_t)d->nch, d->seg_long, d->long_o0, d->dpg_long};
+                   d->chsse2 + 2 * (size_t)d->nch, d->seg_long, d->long_o0, d->dpg_long,
+                   d->w_prefetch};
     BA_DISPATCH(d->na, (lin_chunk_launch<NA>(d, f, d->a_new, d->rot_new, d->b_new, d->W2,
                                              d->V2, d->eB2, d->upart2, d->chsse2, &u)));
     if (d->nl > 0)   // long tracks: V2 / eB2 = sum of their segments' partials
