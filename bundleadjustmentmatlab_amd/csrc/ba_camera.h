@@ -29,12 +29,20 @@ struct cam_view<NA, false> {
     __device__ __forceinline__ cam_view(const double *__restrict__ a,
                                         const double *__restrict__ K4,
                                         const double *__restrict__ rot, int j)
+        : cam_view(a, K4, rot, j, j)
+    {
+    }
+    // jr: the camera's row of rot (a staged copy of part of the table, e.g.
+    // in LDS), j: its index into a and K4
+    __device__ __forceinline__ cam_view(const double *__restrict__ a,
+                                        const double *__restrict__ K4,
+                                        const double *__restrict__ rot, int jr, int j)
     {
 #pragma unroll
         for (int c = 0; c < NA; c++) a0[c] = a[(size_t)NA * j + c];
 #pragma unroll
         for (int c = 0; c < 4; c++) k4[c] = K4[4 * (size_t)j + c];
-        R = rot + 45 * (size_t)j;
+        R = rot + 45 * (size_t)jr;
 #pragma unroll
         for (int q = 0; q < 9; q++) Rl[q] = R[q];
         vlg_calib(Kc, k4, a0, NA - 6);

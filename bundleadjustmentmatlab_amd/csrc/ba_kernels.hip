@@ -297,6 +297,26 @@ __global__ __launch_bounds__(256) void k_linearize(
 // the pass's new SSE and, if the step is accepted, the next pass's old SSE
 // (bundle_euclid.m:139 of the next iteration recomputes exactly that, App. A
 // Q12).  One pass over the observations instead of two.
+// BA_LIN_CAMS (NA = 6): the rotation-table rows (45 doubles) of the chunk's
+// cameras -- a chunk of consecutive points sees a narrow camera range, ~7
+// cameras at config 3 -- staged in LDS by LDS-DMA with the chunk's other
+// operands, so the projections read R(w), R(w + h e_k), R(w + 0) from LDS
+// instead of every lane fetching its camera's 360 bytes of them through the
+// vector-memory path (the kernel's busiest unit: TD 90 %, TA 80 % busy,
+// profiles/r06/pmc_cfg3_summary.csv): 298 -> 277-279 us at config 3
+// (profiles/r06/ab_lin_cams.txt).  Chunks whose cameras span more than
+// BA_LIN_CAMS read the table from memory as before.  The same values: bit for
+// bit the same columns.  (Staging a and K4 as well measured 326-328 us.)  0: off.
+#ifndef BA_LIN_CAMS
+#define BA_LIN_CAMS 10
+#endif
+// waves per SIMD the NA = 6 linearisation kernels are compiled for: 6 with the
+// staged cameras (80 VGPRs; their LDS allows 6 workgroups per CU), else 7 (72
+// VGPRs, 7 workgroups per CU)
+#ifndef BA_LIN_WAVES
+#define BA_LIN_WAVES (BA_LIN_CAMS > 0 ? 6 : 7)
+#endif
+
 struct ba_upd {
     const double *W_old, *da, *eB_old, *Vinv, *b_old;
     int ndb;
@@ -345,6 +365,9 @@ __device__ __forceinline__ void linearize_chunk_body(
     // lane addresses live through the projections: spills)
     __shared__ double dpl[UPD ? BA_CH_PTS : 1];
     static_assert(BA_CH_PTS <= 64, "the point lanes are wave 0");
+    // the chunk's rotation-table rows (BA_LIN_CAMS cameras)
+    constexpr int NCAMS = (NA == 6 && BA_LIN_CAMS > 0) ? BA_LIN_CAMS : 0;
+    __shared__ __attribute__((aligned(16))) double camr[NCAMS > 0 ? 45 * NCAMS : 1];
     const int tid = threadIdx.x;
     // a segment chunk (ch >= nch_reg) holds part of one long track: its V / eB
     // sums are partials (vseg), added up per track by k_long_vsum
@@ -371,6 +394,25 @@ __device__ __forceinline__ void linearize_chunk_body(
             __builtin_amdgcn_global_load_lds(pt_ptr + p0 + min(tid, np), lptr_raw + 64 * wv, 4, 0,
                                              0);
     }
+    // the chunk's camera range (ch_cam: lowest / highest camera of the chunk)
+    const int cam_lo = ch_cam[2 * ch], cam_n = ch_cam[2 * ch + 1] - cam_lo + 1;
+    const bool camst = NCAMS > 0 && nobs > 0 && cam_n <= NCAMS;   // (uniform)
+    if (NCAMS > 0 && camst) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        // one contiguous range, one dword per lane (exec-masked past its end)
+        const int lane = tid & 63;
+        auto stage = [&](const double *src, int ndw, double *dst) {
+            const char *s8 = reinterpret_cast<const char *>(src);
+            for (int q = tid >> 6; 64 * q < ndw; q += 4)   // (wave-uniform)
+                if (64 * q + lane < ndw)
+                    __builtin_amdgcn_global_load_lds(s8 + 4 * (64 * q + lane),
+                                                     reinterpret_cast<int *>(dst) + 64 * q, 4, 0,
+                                                     0);
+        };
+        stage(rot + 45 * (size_t)cam_lo, 90 * cam_n, &camr[0]);
+#endif
+        if constexpr (!UPD) __syncthreads();   // (UPD: the update's barriers)
+    }
     int m_eobl = 0;
     STAMP(16);
     double bu[3] = {0.0, 0.0, 0.0};   // UPD: this lane's point at b_new
@@ -392,7 +434,7 @@ __device__ __forceinline__ void linearize_chunk_body(
             // tail, beside the W rows: the lanes index them with their camera
             // after the barrier, so no load waits on another.  A wider range
             // loads each lane's da row from its camera index (dependent).
-            const int clo = ch_cam[2 * ch], span = ch_cam[2 * ch + 1] - clo + 1;
+            const int clo = cam_lo, span = cam_n;
             const bool dstage = NA == 6 && span * NA <= NROWS - LW;
             if (dstage && nobs > 0) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -450,15 +492,21 @@ __device__ __forceinline__ void linearize_chunk_body(
                             128 * tid);
                 }
             }
-            // the point lanes' operands (eB, V*^-1, b): in flight through t_o
+            // the point lanes' operands (eB, V*^-1, b): in flight through t_o;
+            // wave 0 only (the point lanes, np <= 64; wave-uniform): the
+            // other waves' clamped copies were TD-path traffic for nothing
+            // (the kernel's vector-memory data path is its busiest unit, TD
+            // busy 90 %: 316 -> 298-301 us, profiles/r06/ab_lin.txt)
             const int ip = np > 0 ? p0 + min(tid, np - 1) : 0;
-            double pe[3], pv[9], pb[3];
+            double pe[3] = {0.0, 0.0, 0.0}, pv[9] = {}, pb[3] = {0.0, 0.0, 0.0};
+            if (__builtin_amdgcn_readfirstlane(tid >> 6) == 0) {
 #pragma unroll
-            for (int r = 0; r < 3; r++) pe[r] = u.eB_old[3 * (size_t)ip + r];
+                for (int r = 0; r < 3; r++) pe[r] = u.eB_old[3 * (size_t)ip + r];
 #pragma unroll
-            for (int r = 0; r < 9; r++) pv[r] = u.Vinv[9 * (size_t)ip + r];
+                for (int r = 0; r < 9; r++) pv[r] = u.Vinv[9 * (size_t)ip + r];
 #pragma unroll
-            for (int r = 0; r < 3; r++) pb[r] = u.b_old[3 * (size_t)ip + r];
+                for (int r = 0; r < 3; r++) pb[r] = u.b_old[3 * (size_t)ip + r];
+            }
             __syncthreads();
             asm volatile("" ::"v"(pfv));   // (the prefetch's value: nothing reads it)
             // t_o[r] = W_o(:, r)' da_j (mex_bundle_3_db_new.c:113-120), into the
@@ -539,13 +587,22 @@ __device__ __forceinline__ void linearize_chunk_body(
             double bi[3];
 #pragma unroll
             for (int c = 0; c < 3; c++) bi[c] = UPD ? bu[c] : b[3 * (size_t)i + c];
-            cam_view<NA> cv(a, K4, rot, j);
             double xh[2];
             double *row = rows + RS * lo;
             if constexpr (NA == 6) {
-                cv.project(bi, xh);
-                fd_columns_6(cv, bi, xh, half, row);
+                // the rotations from LDS (staged) or the table: one code path
+                // each, so every load has its address space at compile time
+                auto proj6 = [&](const double *rt, int jr) {
+                    cam_view<NA> cv6(a, K4, rt, jr, j);
+                    cv6.project(bi, xh);
+                    fd_columns_6(cv6, bi, xh, half, row);
+                };
+                if (NCAMS > 0 && camst)
+                    proj6(&camr[0], j - cam_lo);
+                else
+                    proj6(rot, j);
             } else {
+                cam_view<NA> cv(a, K4, rot, j);
                 cv.project(bi, xh);
                 // the NA + 3 FD columns of [A | B] (mex_bundle_1 :201-219) split
                 // evenly: lane 0 columns [0, NC0), lane 1 [NC0, NA + 3), one
@@ -696,7 +753,7 @@ __device__ __forceinline__ void linearize_chunk_body(
 // the linearisation at the current parameters (after set_params, the ordered
 // and stage paths' fast twin)
 template <int NA>
-__global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(BA_LIN_ARGS)
+__global__ __launch_bounds__(256, (NA == 6) ? BA_LIN_WAVES : 1) void k_linearize_chunk(BA_LIN_ARGS)
 {
     linearize_chunk_body<NA, false>(BA_LIN_PASS, ba_upd{}, blockIdx.x);
 }
@@ -705,7 +762,7 @@ __global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_linearize_chunk(BA_L
 // (a_new, b_new) (a, rot, b = a_new, rot_new, b_new; W .. part_sse = the
 // second buffers)
 template <int NA>
-__global__ __launch_bounds__(256, (NA == 6) ? 7 : 1) void k_update_linearize(BA_LIN_ARGS,
+__global__ __launch_bounds__(256, (NA == 6) ? BA_LIN_WAVES : 1) void k_update_linearize(BA_LIN_ARGS,
                                                                              ba_upd u)
 {
     linearize_chunk_body<NA, true>(BA_LIN_PASS, u, blockIdx.x);

@@ -48,6 +48,25 @@ for step in "$@"; do
           2> gpurun_out/ab_pf_$v.log || exit 1
         echo "pf=$v $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_pf_$v.json) $(grep -o 'k_update_linearize=[0-9.]*us' gpurun_out/ab_pf_$v.log | head -1)"
       done ;;
+    ablin)
+      # bit identity of the A/B builds (tools/ab_build.sh) against AB_REF (default v0) on
+      # tools/lin_dump.py's scenes, then the cfg3 bench of each, alternated twice
+      ref=${AB_REF:-v0}
+      for v in $(ls tools/build/ab); do
+        VLGBA_LIB=tools/build/ab/$v/libvlgba.so timeout -k 10 300 python -u tools/lin_dump.py \
+          gpurun_out/lin_$v.npz > gpurun_out/lin_$v.log 2>&1 || { tail -5 gpurun_out/lin_$v.log; exit 1; }
+      done
+      for v in $(ls tools/build/ab); do
+        echo "$v vs $ref: $(python tools/lin_dump.py --compare gpurun_out/lin_$v.npz gpurun_out/lin_$ref.npz | tail -1)"
+      done
+      for r in 1 2; do
+        for v in $(ls tools/build/ab); do
+          VLGBA_LIB=tools/build/ab/$v/libvlgba.so timeout -k 10 300 python -u bench.py --steps 100 \
+            --warmup 50 --no-cpu-baseline --no-other-configs > gpurun_out/ab_${v}_$r.json \
+            2> gpurun_out/ab_${v}_$r.log || { tail -5 gpurun_out/ab_${v}_$r.log; exit 1; }
+          echo "$v run $r $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_${v}_$r.json) $(grep -o 'k_update_linearize=[0-9.]*us' gpurun_out/ab_${v}_$r.log | head -1)"
+        done
+      done ;;
     stream)
       timeout -k 10 120 tools/build/ubench_stream > gpurun_out/ubench_stream.txt 2>&1 || exit 1
       cat gpurun_out/ubench_stream.txt ;;
