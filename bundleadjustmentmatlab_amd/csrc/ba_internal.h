@@ -224,7 +224,6 @@ struct ba_dev {
     // next linearisation's buffers, swapped in by an accepted step
     int fused;
     double *W2, *V2, *eB2, *upart2, *chsse2;
-    int w_prefetch;   // k_update_linearize: W-row prefetch distance in chunks (0: off)
     int ns, nes;
     int ch_max_terms, ch_max_slots;   // per-chunk maxima: LDS staging of the term lists
     long long nterm_fast;             // (obs, obs) Schur terms of the chunk plan

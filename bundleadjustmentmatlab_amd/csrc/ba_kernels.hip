@@ -324,7 +324,6 @@ struct ba_upd {
     double *db, *b_new, *part_dpg;
     const int *seg_long, *long_o0;
     const double *dpg_long;
-    int pf_dist;   // > 0: touch the W rows of chunk ch + pf_dist into the caches
 };
 
 template <int NA, bool UPD>
@@ -476,22 +475,6 @@ __device__ __forceinline__ void linearize_chunk_body(
                     for (int k = 0; k < NA; k++) dl[k] = dd[k];
                 }
             }
-            // pf_dist > 0: one load per 128-byte line of the old W rows of
-            // chunk ch + pf_dist (a workgroup of a later generation on this
-            // XCD), so that its update phase finds them in L2 / MALL; in
-            // flight beside this chunk's loads, waited for at the barrier
-            unsigned pfv = 0;
-            {
-                const int nx = ch + u.pf_dist;
-                if (u.pf_dist > 0 && nx < nch_reg) {
-                    const int ob = ch_obase[nx];
-                    const int nb = (ch_obase[nx + 1] - ob) * 8 * 3 * NA;
-                    if (128 * tid < nb)
-                        pfv = *reinterpret_cast<const unsigned *>(
-                            reinterpret_cast<const char *>(u.W_old + (size_t)3 * NA * ob) +
-                            128 * tid);
-                }
-            }
             // the point lanes' operands (eB, V*^-1, b): in flight through t_o;
             // wave 0 only (the point lanes, np <= 64; wave-uniform): the
             // other waves' clamped copies were TD-path traffic for nothing
@@ -508,7 +491,6 @@ __device__ __forceinline__ void linearize_chunk_body(
                 for (int r = 0; r < 3; r++) pb[r] = u.b_old[3 * (size_t)ip + r];
             }
             __syncthreads();
-            asm volatile("" ::"v"(pfv));   // (the prefetch's value: nothing reads it)
             // t_o[r] = W_o(:, r)' da_j (mex_bundle_3_db_new.c:113-120), into the
             // row's first slot (only this lane reads the row)
             if (tid < nobs) {
@@ -1314,6 +1296,22 @@ __device__ __forceinline__ double row4_bcast(double v, int rg)
 #ifndef BA_MF_PIPE
 #define BA_MF_PIPE 0
 #endif
+// BA_MF_GATHER: the 16 lanes of a row need the same V*^-1 and eB entries (the
+// row's point), so each row loads them once -- lane li one entry -- and the
+// chunk's processing broadcasts them (DPP row_newbcast): one load per lane
+// instead of ten, a fifth of the kernel's vector-memory data traffic (TD
+// busy 78 %, profiles/r06/pmc_cfg3_summary.csv), and 18 fewer VGPRs held
+// per chunk in flight.  The same values: bit-identical.
+#ifndef BA_MF_GATHER
+#define BA_MF_GATHER 1
+#endif
+// lane Q's value to every lane of its 16-lane row (v_mov_b64 DPP row_newbcast)
+template <int Q> __device__ __forceinline__ double row16_bcast_c(double v)
+{
+    const long long u = __builtin_bit_cast(long long, v);
+    const long long r = __builtin_amdgcn_mov_dpp(u, 0x150 + Q, 0xf, 0xf, true);   // v_mov_b64_dpp
+    return __builtin_bit_cast(double, r);
+}
 #ifndef BA_MF_WAVES
 #define BA_MF_WAVES 3
 #endif
@@ -1376,6 +1374,9 @@ __global__ __launch_bounds__(256, (NA == 6) ? BA_MF_WAVES : 1) void k_schur_mfma
     // (symmetric); vf[6]: the s = 3 Y MFMA's A fragment V*^-1[lk][li] of point
     // 5w + 4 (zero outside rows li < 3, K lk < 3)
     auto load = [&](int k, double (&wf)[4][RT], double (&vf)[7], double (&ef)[4]) {
+        // BA_MF_GATHER: vf[0] holds the row's gathered entry (lane li: V*^-1
+        // entry li < 6, eB entry li - 6 < 3, eB of point 5 w + 4 for li >= 9),
+        // vf[6] as before; the rest is formed by process()
         const unsigned *r = rec + gbo[k];
         const int np = gp0[k + 1] - gp0[k], i0 = gp0[k], ob = gob[k];
         const int C = (int)(r[1] & 0xffu);
@@ -1399,7 +1400,16 @@ __global__ __launch_bounds__(256, (NA == 6) ? BA_MF_WAVES : 1) void k_schur_mfma
             for (int s = 0; s < 3; s++) wf[s][t] = wbase[oA + NA * s];
             wf[3][t] = wbase[o4];
         }
-        {
+        if (BA_MF_GATHER) {
+            // V*^-1 entries (0,0) (1,0) (2,0) (1,1) (2,1) (2,2) -> lanes 0..5
+            const int vo = li + (li >= 3 ? 1 : 0) + (li >= 5 ? 2 : 0);
+            const double *src = li < 6   ? vbase + (pvA ? 9 * pA + vo : vz)
+                                : li < 9 ? ebase + (pvA ? 3 * pA + li - 6 : ez)
+                                         : ebase + (pv4 ? 3 * p4 + lk : ez);
+            vf[0] = *src;
+            const bool dv = p4 < np && li < 3 && lk < 3;
+            vf[6] = vbase[dv ? 9 * p4 + lk + 3 * li : vz];
+        } else {
             const int oe = pvA ? 3 * pA : ez;
 #pragma unroll
             for (int s = 0; s < 3; s++) ef[s] = ebase[oe + s];
@@ -1421,8 +1431,27 @@ __global__ __launch_bounds__(256, (NA == 6) ? BA_MF_WAVES : 1) void k_schur_mfma
 #pragma unroll
     for (int t = 0; t < RT; t++) eacc[t] = 0.0;
     // one chunk: Y tiles, e_ sums, lower S tiles; flush at a change of cameras
-    auto process = [&](int k, const double (&wc)[4][RT], const double (&vc)[7],
-                       const double (&ec)[4]) {
+    auto process = [&](int k, const double (&wc)[4][RT], const double (&vg)[7],
+                       const double (&eg)[4]) {
+        double vc[7], ec[4];
+        if (BA_MF_GATHER) {   // the row's entries from its lanes 0..9
+            vc[0] = row16_bcast_c<0>(vg[0]);
+            vc[1] = row16_bcast_c<1>(vg[0]);
+            vc[2] = row16_bcast_c<2>(vg[0]);
+            vc[3] = row16_bcast_c<3>(vg[0]);
+            vc[4] = row16_bcast_c<4>(vg[0]);
+            vc[5] = row16_bcast_c<5>(vg[0]);
+            vc[6] = vg[6];
+            ec[0] = row16_bcast_c<6>(vg[0]);
+            ec[1] = row16_bcast_c<7>(vg[0]);
+            ec[2] = row16_bcast_c<8>(vg[0]);
+            ec[3] = row16_bcast_c<9>(vg[0]);
+        } else {
+#pragma unroll
+            for (int u = 0; u < 7; u++) vc[u] = vg[u];
+#pragma unroll
+            for (int s = 0; s < 4; s++) ec[s] = eg[s];
+        }
         const unsigned *r = rec + gbo[k];
         const unsigned h1 = r[1];
         const int C = (int)(h1 & 0xffu), fl = (int)((h1 >> 8) & 0xffu), Rc = NA * C;
@@ -2602,8 +2631,7 @@ static int launch_update_fused(ba_dev *d, double lambda, ba_flags f)
                                d->Vinv, d->b, d->ndb, lambda, d->db, d->b_new,
                                d->dpg_long)));
     const ba_upd u{d->W, d->da, d->eB, d->Vinv, d->b, d->ndb, lambda, d->db, d->b_new,
-                   d->chsse2 + 2 * (size_t)d->nch, d->seg_long, d->long_o0, d->dpg_long,
-                   d->w_prefetch};
+                   d->chsse2 + 2 * (size_t)d->nch, d->seg_long, d->long_o0, d->dpg_long};
     BA_DISPATCH(d->na, (lin_chunk_launch<NA>(d, f, d->a_new, d->rot_new, d->b_new, d->W2,
                                              d->V2, d->eB2, d->upart2, d->chsse2, &u)));
     if (d->nl > 0)   // long tracks: V2 / eB2 = sum of their segments' partials

@@ -1766,8 +1766,6 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         TRY(ctx_alloc(c, &d.upart2, (size_t)(na * (na + 1) / 2 + na) * d.nes));
         TRY(ctx_alloc(c, &d.chsse2, 3 * (size_t)d.nch));
         d.fused = 1;
-        const char *wp = std::getenv("VLGBA_W_PREFETCH");   // chunks ahead (A/B)
-        d.w_prefetch = wp ? std::max(0, std::atoi(wp)) : 0;
     }
     TRY(ctx_alloc(c, &d.blk_jk, 2 * (size_t)d.nb));
     TRY(ctx_alloc(c, &d.blk_ptr, (size_t)d.nb + 1));

@@ -40,14 +40,6 @@ for step in "$@"; do
       timeout -k 10 600 python -u -m pytest tests/test_gpu_fused.py -x -v --timeout 300 \
         --timeout-method thread > gpurun_out/test_fused.log 2>&1; rc=$?
       tail -15 gpurun_out/test_fused.log; [ $rc -eq 0 ] || exit $rc ;;
-    abpf)
-      # A/B of the fused kernel's W-row prefetch distance (VLGBA_W_PREFETCH, chunks ahead)
-      for v in 0 ${AB_PF:-1792 3584 896} 0; do
-        VLGBA_W_PREFETCH=$v timeout -k 10 300 python -u bench.py --steps 100 --warmup 50 \
-          --no-cpu-baseline --no-other-configs > gpurun_out/ab_pf_$v.json \
-          2> gpurun_out/ab_pf_$v.log || exit 1
-        echo "pf=$v $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_pf_$v.json) $(grep -o 'k_update_linearize=[0-9.]*us' gpurun_out/ab_pf_$v.log | head -1)"
-      done ;;
     ablin)
       # bit identity of the A/B builds (tools/ab_build.sh) against AB_REF (default v0) on
       # tools/lin_dump.py's scenes, then the cfg3 bench of each, alternated twice
