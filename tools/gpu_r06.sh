@@ -51,6 +51,7 @@ for step in "$@"; do
       for v in $(ls tools/build/ab); do
         echo "$v vs $ref: $(python tools/lin_dump.py --compare gpurun_out/lin_$v.npz gpurun_out/lin_$ref.npz | tail -1)"
       done
+      rm -f gpurun_out/lin_*.npz   # (the merge back is capped at 64 MiB)
       for r in 1 2; do
         for v in $(ls tools/build/ab); do
           VLGBA_LIB=tools/build/ab/$v/libvlgba.so timeout -k 10 300 python -u bench.py --steps 100 \
