@@ -127,18 +127,6 @@ def main():
 
     ba.step(relinearize=True, update_lm=False)   # first touch, outside everything
     ba.sync()
-    # per-phase and per-kernel device timing (HIP events around every launch on
-    # the library stream), in untimed passes
-    ba.set_timing(True)
-    ba.kernel_ms(reset=True)
-    phases = []
-    n_timed = max(1, min(3, args.steps))
-    for _ in range(n_timed):
-        ba.step(relinearize=True, update_lm=False)
-        phases.append(ba.phase_ms())
-    kms = ba.kernel_ms(reset=True)
-    ba.set_timing(False)
-    ph = {k: float(np.median([p[k] for p in phases])) for k in phases[0]}
     # clock ramp: untimed passes for --clock-ramp seconds (every one a full
     # pass, like the timed ones), so the measurement is the steady state and
     # not the GPU's DVFS ramp from idle (a 20-step region right after a few
@@ -163,6 +151,21 @@ def main():
             ba.step(relinearize=True, update_lm=False)
         ba.sync()
         ramp = {"seconds": time.perf_counter() - t_r, "passes": 3 + n_ramp}
+    # per-phase and per-kernel device timing (HIP events around every launch on
+    # the library stream), in untimed passes after the clock ramp (at the
+    # steady-state clock, as the timed steps and rocprofv3's kernel trace see
+    # it: taken before the ramp they read the fused kernel ~8 % slow, 278 vs
+    # 258 us, profiles/r06/r06b_cfg3_kernel_stats.csv)
+    ba.set_timing(True)
+    ba.kernel_ms(reset=True)
+    phases = []
+    n_timed = max(1, min(10, args.steps))
+    for _ in range(n_timed):
+        ba.step(relinearize=True, update_lm=False)
+        phases.append(ba.phase_ms())
+    kms = ba.kernel_ms(reset=True)
+    ba.set_timing(False)
+    ph = {k: float(np.median([p[k] for p in phases])) for k in phases[0]}
     for _ in range(args.warmup):
         ba.step(relinearize=True, update_lm=False)
     ba.sync()
