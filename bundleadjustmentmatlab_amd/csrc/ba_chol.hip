@@ -3015,6 +3015,17 @@ int ba_chol_setup(ba_dev *d, const int *blk_jk, int nb)
             d->tb32 = TB;
             d->nt32 = nt32;
             ntc = nt32;
+            // direct assembly: every camera pair (j >= k) inside a group of G
+            // cameras is a block (the diagonal tiles the CR writes back are then
+            // fully rewritten by k_schur_reduce every pass)
+            long long inside = 0, want = 0;
+            for (int b = 0; b < nb; b++)
+                inside += blk_jk[2 * b] / G == blk_jk[2 * b + 1] / G;
+            for (int g0 = 0; g0 < d->m; g0 += G) {
+                const long long c = std::min(G, d->m - g0);
+                want += c * (c + 1) / 2;
+            }
+            d->asm_direct_ok = inside == want;
         }
     }
     bool tridiag = d->dense_solve == 0 && nt > 1;
@@ -3443,6 +3454,7 @@ void ba_chol_free(ba_dev *d)
 
 int ba_assemble_tiles(ba_dev *d)
 {
+    if (d->asm_direct) return 0;   // k_schur_reduce wrote S (and reset the status)
     const bool nd = d->nd_np > 0;
     k_assemble_tiles<<<d->n_env, 256, 0, d->stream>>>(
         d->S, nd ? d->slds : d->lds, d->env_tiles, d->tb_ptr, d->tb_blk, d->blk_jk, d->sblk, d->na,

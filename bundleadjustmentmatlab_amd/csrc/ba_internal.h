@@ -159,6 +159,13 @@ struct ba_dev {
     // per-level launches
     unsigned *crflag;             // [nlev][nt32][5]
     int cr_fused;
+    // direct assembly (camera-aligned CR, one rank, fast path): k_schur_reduce
+    // writes each block's lower entries straight into S (and the pinv rule
+    // of exactly-zero diagonals), so no k_assemble_tiles launch.  Needs every
+    // lower entry of every diagonal CR tile covered by a block (asm_direct_ok,
+    // ba_chol_setup): the CR writes only those tiles, so S's other entries
+    // keep the zeros of the setup.
+    int asm_direct_ok, asm_direct;
     // one-level nested dissection of the envelope (ba_chol_setup, auto mode
     // when S is not tridiagonal; dense_solve 4 forces it): the cameras split
     // into nd_np arcs of consecutive cameras minus the separator (cameras

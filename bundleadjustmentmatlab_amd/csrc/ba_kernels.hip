@@ -1600,6 +1600,13 @@ __global__ __launch_bounds__(256, (NA == 6) ? BA_MF_WAVES : 1) void k_schur_mfma
 // in LDS), compacts the matches in order, and every entry's lane subtracts
 // them -- the order and the expression of the former per-pair slots, so the
 // blocks are the same bit for bit.
+// k_schur_reduce's direct assembly (ba_dev::asm_direct): S == nullptr: none
+struct ba_direct {
+    double *S;
+    long long lds;
+    double *status;
+};
+
 struct ba_longs {
     const int *pair_ptr;                         // NULL: no long tracks
     const int2 *pair;                            // per block (j obs, k obs) in track order
@@ -1690,12 +1697,19 @@ __global__ void k_schur_reduce(const int *__restrict__ blk_jk, const int *__rest
                                const double *__restrict__ spart,
                                const double *__restrict__ epart, const double *__restrict__ U,
                                const double *__restrict__ eA, int nb, double lambda, int owner,
-                               double *__restrict__ sblk, double *__restrict__ rhs, ba_longs lg)
+                               double *__restrict__ sblk, double *__restrict__ rhs, ba_longs lg,
+                               ba_direct dir)
 {
     constexpr int NN = NA * NA, WS = 3 * NA;
     __shared__ double ys[BA_LMATCH_BATCH * WS], ws[BA_LMATCH_BATCH * WS];
+    __shared__ int dzero[NA];
+    __shared__ double erhs[NA];
     const int bk = blockIdx.x, l = threadIdx.x;
     if (bk >= nb) return;
+    if (dir.S && bk == 0 && l == 0) {   // (k_assemble_tiles' reset, which does not run)
+        dir.status[0] = 0.0;   // non-positive pivot
+        dir.status[1] = 0.0;   // bounded hand-off spin gave up
+    }
     const int j = blk_jk[2 * bk], k = blk_jk[2 * bk + 1];
     double acc = 0.0;
     if (l < NN) {
@@ -1728,7 +1742,8 @@ __global__ void k_schur_reduce(const int *__restrict__ blk_jk, const int *__rest
             for (int t = 0; t < 8; t++) e -= v[t];
         }
         for (; q < qe; q++) e -= epart[(size_t)NA * cam_eslots[q] + r];
-        rhs[(size_t)NA * j + r] = e;
+        if (!dir.S) rhs[(size_t)NA * j + r] = e;
+        else erhs[r] = e;   // (written below, after the diagonal's pinv rule)
     }
     if (lg.pair_ptr) {
         // the block's long-track terms in track order: the pairs' Y / W rows
@@ -1755,6 +1770,21 @@ __global__ void k_schur_reduce(const int *__restrict__ blk_jk, const int *__rest
         }
     }
     if (l < NN) sblk[(size_t)NN * bk + l] = acc;
+    if (dir.S) {
+        // k_assemble_tiles' work for this block: its lower entries into S, and
+        // for a diagonal block the rule for an exactly-zero diagonal (unit
+        // pivot, zero rhs: pinv semantics)
+        const int r = l % NA, c = l / NA;
+        if (l < NN && (j > k || r >= c)) {
+            const long long row = (long long)NA * j + r, col = (long long)NA * k + c;
+            const bool z = j == k && r == c && acc == 0.0;
+            dir.S[row + dir.lds * col] = z ? 1.0 : acc;
+            if (j == k && r == c) dzero[r] = z;
+        }
+        __syncthreads();
+        if (j == k && l >= NN && l < NN + NA)
+            rhs[(size_t)NA * j + (l - NN)] = dzero[l - NN] ? 0.0 : erhs[l - NN];
+    }
 }
 
 // The long tracks' (obs, obs) terms of the co-visible blocks after
@@ -2544,9 +2574,11 @@ static int launch_schur_fast(ba_dev *d, double lambda)
         lg.W = d->W;
         lg.L0 = d->long_o0_h;
     }
+    ba_direct dir{nullptr, 0, nullptr};
+    if (d->asm_direct) dir = ba_direct{d->S, d->lds, d->scal + 4};
     k_schur_reduce<NA><<<d->nb, bs, 0, d->stream>>>(
         d->blk_jk, d->blk_gptr, d->blk_gslots, d->cam_gptr, d->cam_gslots, d->spart, d->epart,
-        d->U, d->eA, d->nb, lambda, d->schur_owner, d->sblk, d->rhs, lg);
+        d->U, d->eA, d->nb, lambda, d->schur_owner, d->sblk, d->rhs, lg, dir);
     if (d->nl > 0 && d->nlb)   // the long tracks' terms after the slot sums
         k_schur_long_acc<NA><<<(4 * d->nlb + 255) / 256, 256, 0, d->stream>>>(
             d->lblk, d->nlb, d->lpair_ptr, d->lpair, d->ylong, d->W, d->long_o0_h, d->sblk);
@@ -2602,6 +2634,7 @@ int ba_launch_yeb(ba_dev *d)
 
 int ba_launch_assemble(ba_dev *d)
 {
+    if (d->asm_direct) return 0;   // k_schur_reduce assembled S (ba_dev::asm_direct)
     KT_B(d);
     TRY_RC(ba_assemble_tiles(d));
     KT_E(d, KT_ASSEMBLE);

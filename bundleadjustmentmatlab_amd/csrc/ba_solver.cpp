@@ -1778,6 +1778,14 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         ST_MARK("allocs");
         TRY(ba_chol_setup(&d, hb.jk.data(), d.nb));
         ST_MARK("chol_setup");
+        // direct assembly (ba_dev::asm_direct): one rank without a collective
+        // between the block sums and the solve, the fast path's block sums, no
+        // long tracks (k_schur_long_acc adds to the sums after them);
+        // VLGBA_ASM_DIRECT=0 keeps k_assemble_tiles (A/B)
+        const char *ad = std::getenv("VLGBA_ASM_DIRECT");
+        d.asm_direct = d.asm_direct_ok && !(ad && ad[0] == '0') && fast && !d.ordered &&
+                       c->world == 1 && !c->comm && d.nl == 0 && d.cr_nlev > 0 && d.cr32 &&
+                       d.nd_np == 0;
     } else {
         TRY(ctx_alloc(c, &d.da, (size_t)d.lds));
     }
