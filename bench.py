@@ -400,6 +400,7 @@ def replay_summary(line):
     rf = line.get("roofline") or {}
     out["roofline"] = {k: rf.get(k) for k in ("device_busy_frac", "kernel", "bound", "frac")}
     out["host_device_split_s"] = line["host_device_split_s"]
+    out["prefetch"] = line.get("prefetch")
     return out
 
 
@@ -506,6 +507,10 @@ def replay_line(config, steps, warmup, with_cpu):
                             ("; every solve of this scene is below it, so the elastic "
                              "count is 1 throughout" if max(q["observations"] for q in sol)
                              < 2 * OBS_PER_SHARD else "")},
+        # the prefetch workers (incremental.py): contexts used as built ahead,
+        # rebuilt after a wrong prediction, built on the replay thread, and the
+        # replay thread's wait for them by solve kind
+        "prefetch": res.get("prefetch"),
         "cpu_baseline": replay_cpu_baseline(sample, k_every, ncalls) if with_cpu else None,
     }
     out["roofline"] = replay_roofline(sc, devices, dt / steps)

@@ -190,6 +190,24 @@ struct host_obs {
 int sort_obs(const vlgba_problem *p, host_obs &h)
 {
     const long long N = p->num_obs;
+    // already point-major with cameras ascending within a point (the growing
+    // replay's subsets, bundle_euclid's visibility order): a copy
+    bool sorted = true;
+    for (long long o = 0; o < N && sorted; o++) {
+        const int i = p->obs_pt[o], j = p->obs_cam[o];
+        if (i < 0 || i >= p->n || j < 0 || j >= p->m) return VLGBA_E_ARG;
+        if (o > 0) {
+            const int i0 = p->obs_pt[o - 1], j0 = p->obs_cam[o - 1];
+            if (i < i0 || (i == i0 && j < j0)) sorted = false;
+            else if (i == i0 && j == j0) return VLGBA_E_ORDER;
+        }
+    }
+    if (sorted) {
+        h.pt.assign(p->obs_pt, p->obs_pt + N);
+        h.cam.assign(p->obs_cam, p->obs_cam + N);
+        h.x.assign(p->obs_x, p->obs_x + 2 * N);
+        return 0;
+    }
     std::vector<long long> cnt(p->n + 1, 0);
     for (long long o = 0; o < N; o++) {
         const int i = p->obs_pt[o], j = p->obs_cam[o];
@@ -377,7 +395,7 @@ void build_blocks(int m, const std::vector<int> &pt_ptr_all, const std::vector<i
 struct host_plan {
     std::vector<int> ch_pt, ch_slot, ch_eslot, slot_blk, slot_tptr, eslot_optr;
     std::vector<unsigned short> slot_term, eslot_obs;
-    std::vector<int> blk_sptr, blk_slots, cam_eptr, cam_eslots;
+    std::vector<int> cam_eptr, cam_eslots;
     int max_terms = 0, max_slots = 0;   // per chunk (LDS staging size)
     long long n_terms = 0;              // (obs, obs) Schur terms of all chunks
     // Schur groups: consecutive chunks whose co-visible blocks ("group slots")
@@ -410,8 +428,8 @@ struct host_plan {
     void reset()
     {
         for (std::vector<int> *v :
-             {&ch_pt, &ch_slot, &ch_eslot, &slot_blk, &slot_tptr, &eslot_optr, &blk_sptr,
-              &blk_slots, &cam_eptr, &cam_eslots, &grp_ch, &grp_gs, &grp_ge, &gslot_blk, &gecam,
+             {&ch_pt, &ch_slot, &ch_eslot, &slot_blk, &slot_tptr, &eslot_optr,
+              &cam_eptr, &cam_eslots, &grp_ch, &grp_gs, &grp_ge, &gslot_blk, &gecam,
               &blk_gptr, &blk_gslots, &cam_gptr, &cam_gslots, &seg_pt, &seg_long, &long_pt,
               &long_o0, &long_seg0, &long_ebase, &cam_lptr, &cam_lobs, &cam_ltrk, &ch_blob,
               &ch_obase})
@@ -868,10 +886,10 @@ bool build_plan(int m, int na, const std::vector<int> &lptr, const std::vector<i
         P.long_o0.push_back(lptr[i + 1]);
         P.long_seg0.push_back(P.nseg);
     }
-    // per block: its slots in chunk order; per camera: its e-slots in chunk
-    // order (cam_eslots currently = camera of e-slot) -- counting sorts that
-    // keep the id order (bucket: threads over id ranges for large inputs)
-    bucket(P.slot_blk, nb, P.blk_sptr, P.blk_slots);
+    // per camera: its e-slots in chunk order (cam_eslots currently = camera of
+    // e-slot) -- a counting sort that keeps the id order (bucket: threads over
+    // id ranges for large inputs).  (The per-block lists of the chunk slots are
+    // not built: the block sums read the group slots, blk_gptr / blk_gslots.)
     std::vector<int> ecam;
     ecam.swap(P.cam_eslots);
     bucket(ecam, m, P.cam_eptr, P.cam_eslots);
@@ -1554,6 +1572,60 @@ static void plan_host(int m, int na, int n, const std::vector<int> &lptr,
     }
 }
 
+// A context's plan arrays (~30 host vectors) go to the device as ONE copy:
+// each array at a 256-byte aligned offset of one device block and of the
+// context's pinned staging buffer (ba_aux::pin, which set_params reuses) --
+// one hipMemcpyAsync from pinned memory instead of one pageable copy per
+// array (the setup trace's plan_upload: 1.1 ms per context over the growing
+// replay, profiles/r06/r06f_cfg5x_setup_phases.txt).  The pointers stay valid
+// for the context's life (the block is one of its allocations).
+struct plan_batch {
+    struct item {
+        void **dst;
+        const void *src;
+        size_t bytes, off;
+    };
+    std::vector<item> items;
+    size_t total = 0;
+    template <typename T> void add(T **dst, const std::vector<T> &v)
+    {
+        items.push_back({(void **)dst, v.data(), sizeof(T) * v.size(), total});
+        total += (sizeof(T) * std::max<size_t>(v.size(), 1) + 255) & ~(size_t)255;
+    }
+    int commit(vlgba_ctx *c, hipStream_t s)
+    {
+        if (items.empty()) return 0;
+        char *dev = nullptr;
+        TRY(ctx_alloc(c, &dev, total));
+        ba_aux &x = c->aux;
+        const size_t need = (total + sizeof(double) - 1) / sizeof(double);
+        if (x.pin_cap < need) {
+            if (x.pin) (void)hipHostFree(x.pin);
+            size_t cap = 1 << 16;
+            while (cap < need) cap <<= 1;
+            x.pin = nullptr;
+            x.pin_cap = 0;
+            if (hipHostMalloc((void **)&x.pin, sizeof(double) * cap, hipHostMallocDefault) ==
+                hipSuccess)
+                x.pin_cap = cap;
+        }
+        char *stage = x.pin_cap >= need ? (char *)x.pin : nullptr;
+        for (const item &it : items) {
+            *it.dst = dev + it.off;
+            if (it.bytes == 0) continue;
+            if (stage)
+                std::memcpy(stage + it.off, it.src, it.bytes);
+            else   // (no pinned memory: array by array)
+                VLGBA_CHECK(hipMemcpyAsync(dev + it.off, it.src, it.bytes,
+                                           hipMemcpyHostToDevice, s));
+        }
+        if (stage)
+            VLGBA_CHECK(hipMemcpyAsync(dev, stage, total, hipMemcpyHostToDevice, s));
+        VLGBA_CHECK(hipStreamSynchronize(s));
+        return 0;
+    }
+};
+
 // Device buffers + host-side structure for the observations of points [p0, p1).
 static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
                      const std::vector<int> &pt_ptr_all, bool lower_blocks, bool all_diag,
@@ -1635,28 +1707,21 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         d.max_lcam = plan.max_lcam;
         d.long_o0_h = plan.long_o0.empty() ? 0 : plan.long_o0[0];
         d.p_long = p_long;
+        // the plan's arrays: one device block, one copy (plan_batch)
+        plan_batch pb;
         if (d.nl > 0) {
-            TRY(ctx_alloc(c, &d.seg_pt, plan.seg_pt.size()));
-            TRY(ctx_alloc(c, &d.seg_long, plan.seg_long.size()));
-            TRY(ctx_alloc(c, &d.long_pt, plan.long_pt.size()));
-            TRY(ctx_alloc(c, &d.long_o0, plan.long_o0.size()));
-            TRY(ctx_alloc(c, &d.long_seg0, plan.long_seg0.size()));
-            TRY(ctx_alloc(c, &d.long_ebase, plan.long_ebase.size()));
-            TRY(ctx_alloc(c, &d.cam_lptr, plan.cam_lptr.size()));
-            TRY(ctx_alloc(c, &d.cam_lobs, plan.cam_lobs.size()));
-            TRY(ctx_alloc(c, &d.cam_ltrk, plan.cam_ltrk.size()));
+            pb.add(&d.seg_pt, plan.seg_pt);
+            pb.add(&d.seg_long, plan.seg_long);
+            pb.add(&d.long_pt, plan.long_pt);
+            pb.add(&d.long_o0, plan.long_o0);
+            pb.add(&d.long_seg0, plan.long_seg0);
+            pb.add(&d.long_ebase, plan.long_ebase);
+            pb.add(&d.cam_lptr, plan.cam_lptr);
+            pb.add(&d.cam_lobs, plan.cam_lobs);
+            pb.add(&d.cam_ltrk, plan.cam_ltrk);
             TRY(ctx_alloc(c, &d.ylong, (size_t)3 * na * plan.cam_lobs.size()));
             TRY(ctx_alloc(c, &d.vseg, 12 * (size_t)plan.nseg));
             TRY(ctx_alloc(c, &d.dpg_long, (size_t)d.nl));
-            TRY(upload(d.seg_pt, plan.seg_pt.data(), plan.seg_pt.size(), s));
-            TRY(upload(d.seg_long, plan.seg_long.data(), plan.seg_long.size(), s));
-            TRY(upload(d.long_pt, plan.long_pt.data(), plan.long_pt.size(), s));
-            TRY(upload(d.long_o0, plan.long_o0.data(), plan.long_o0.size(), s));
-            TRY(upload(d.long_seg0, plan.long_seg0.data(), plan.long_seg0.size(), s));
-            TRY(upload(d.long_ebase, plan.long_ebase.data(), plan.long_ebase.size(), s));
-            TRY(upload(d.cam_lptr, plan.cam_lptr.data(), plan.cam_lptr.size(), s));
-            TRY(upload(d.cam_lobs, plan.cam_lobs.data(), plan.cam_lobs.size(), s));
-            TRY(upload(d.cam_ltrk, plan.cam_ltrk.data(), plan.cam_ltrk.size(), s));
         }
         d.ns = (int)plan.slot_blk.size();
         d.nes = (int)plan.eslot_optr.size() - 1;
@@ -1664,85 +1729,63 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         d.ch_max_slots = plan.max_slots;
         d.nterm_fast = plan.n_terms;
         d.blob_words = (long long)plan.blob.size();
-        TRY(ctx_alloc(c, &d.ch_pt, plan.ch_pt.size()));
-        TRY(ctx_alloc(c, &d.ch_eslot, plan.ch_eslot.size()));
-        TRY(ctx_alloc(c, &d.eslot_optr, plan.eslot_optr.size()));
-        TRY(ctx_alloc(c, &d.eslot_obs, plan.eslot_obs.size()));
-        TRY(ctx_alloc(c, &d.cam_eptr, plan.cam_eptr.size()));
-        TRY(ctx_alloc(c, &d.cam_eslots, plan.cam_eslots.size()));
         d.ngrp = (int)plan.grp_ch.size() - 1;
         d.ngrp_mf = plan.ngrp_mf;
         d.max_blob = plan.max_blob;
         d.mf_max_blob = plan.mf_max_blob;
         d.mf_max_s = plan.mf_max_s;
         d.mf_max_e = plan.mf_max_e;
-        TRY(ctx_alloc(c, &d.blob, plan.blob.size()));
-        TRY(ctx_alloc(c, &d.ch_blob, plan.ch_blob.size()));
-        TRY(ctx_alloc(c, &d.ch_obase, plan.ch_obase.size()));
-        TRY(upload(d.blob, plan.blob.data(), plan.blob.size(), s));
-        TRY(upload(d.ch_blob, plan.ch_blob.data(), plan.ch_blob.size(), s));
-        TRY(upload(d.ch_obase, plan.ch_obase.data(), plan.ch_obase.size(), s));
-        {   // chunk-local point of every observation (k_linearize_chunk) and
-            // each chunk's camera range (k_update_linearize's da staging)
-            std::vector<unsigned char> lpt(d.N > 0 ? d.N : 1, 0);
-            for (size_t ch = 0; ch + 1 < plan.ch_pt.size(); ch++)
-                for (int i = plan.ch_pt[ch]; i < plan.ch_pt[ch + 1]; i++)
-                    for (int o = lptr[i]; o < lptr[i + 1]; o++)
-                        lpt[o] = (unsigned char)(i - plan.ch_pt[ch]);
-            const size_t nchk = plan.ch_obase.size() - 1;
-            std::vector<int> ccam(2 * std::max<size_t>(nchk, 1), 0);
-            for (size_t ch = 0; ch < nchk; ch++) {
-                int lo = INT_MAX, hi = -1;
-                for (int o = plan.ch_obase[ch]; o < plan.ch_obase[ch + 1]; o++) {
-                    lo = std::min(lo, lcam[o]);
-                    hi = std::max(hi, lcam[o]);
-                }
-                ccam[2 * ch] = hi < 0 ? 0 : lo;
-                ccam[2 * ch + 1] = hi < 0 ? 0 : hi;
+        pb.add(&d.blob, plan.blob);
+        pb.add(&d.ch_blob, plan.ch_blob);
+        pb.add(&d.ch_obase, plan.ch_obase);
+        // chunk-local point of every observation (k_linearize_chunk) and each
+        // chunk's camera range (k_update_linearize's da staging)
+        std::vector<unsigned char> lpt(d.N > 0 ? d.N : 1, 0);
+        for (size_t ch = 0; ch + 1 < plan.ch_pt.size(); ch++)
+            for (int i = plan.ch_pt[ch]; i < plan.ch_pt[ch + 1]; i++)
+                for (int o = lptr[i]; o < lptr[i + 1]; o++)
+                    lpt[o] = (unsigned char)(i - plan.ch_pt[ch]);
+        const size_t nchk = plan.ch_obase.size() - 1;
+        std::vector<int> ccam(2 * std::max<size_t>(nchk, 1), 0);
+        for (size_t ch = 0; ch < nchk; ch++) {
+            int lo = INT_MAX, hi = -1;
+            for (int o = plan.ch_obase[ch]; o < plan.ch_obase[ch + 1]; o++) {
+                lo = std::min(lo, lcam[o]);
+                hi = std::max(hi, lcam[o]);
             }
-            // VLGBA_DA_STAGE=0 (A/B): every range too wide, each lane loads its da row
-            const char *dse = std::getenv("VLGBA_DA_STAGE");
-            if (dse && dse[0] == '0')
-                for (size_t ch = 0; ch < nchk; ch++) ccam[2 * ch + 1] = ccam[2 * ch] + (1 << 20);
-            TRY(ctx_alloc(c, &d.obs_lpt, lpt.size()));
-            TRY(upload(d.obs_lpt, lpt.data(), lpt.size(), s));
-            TRY(ctx_alloc(c, &d.ch_cam, ccam.size()));
-            TRY(upload(d.ch_cam, ccam.data(), ccam.size(), s));
-            VLGBA_CHECK(hipStreamSynchronize(s));
+            ccam[2 * ch] = hi < 0 ? 0 : lo;
+            ccam[2 * ch + 1] = hi < 0 ? 0 : hi;
         }
+        // VLGBA_DA_STAGE=0 (A/B): every range too wide, each lane loads its da row
+        const char *dse = std::getenv("VLGBA_DA_STAGE");
+        if (dse && dse[0] == '0')
+            for (size_t ch = 0; ch < nchk; ch++) ccam[2 * ch + 1] = ccam[2 * ch] + (1 << 20);
+        pb.add(&d.obs_lpt, lpt);
+        pb.add(&d.ch_cam, ccam);
         d.grp_max_s = plan.grp_max_s;
         d.grp_max_e = plan.grp_max_e;
         d.ngs = (int)plan.gslot_blk.size();
         d.nge = (int)plan.gecam.size();
         TRY(ctx_alloc(c, &d.spart, (size_t)na * na * d.ngs));
         TRY(ctx_alloc(c, &d.epart, (size_t)na * d.nge));
-        TRY(ctx_alloc(c, &d.grp_ch, plan.grp_ch.size()));
-        TRY(ctx_alloc(c, &d.grp_gs, plan.grp_gs.size()));
-        TRY(ctx_alloc(c, &d.grp_ge, plan.grp_ge.size()));
-        TRY(ctx_alloc(c, &d.cs_g, plan.cs_g.size()));
-        TRY(ctx_alloc(c, &d.ce_g, plan.ce_g.size()));
-        TRY(ctx_alloc(c, &d.blk_gptr, plan.blk_gptr.size()));
-        TRY(ctx_alloc(c, &d.blk_gslots, plan.blk_gslots.size()));
-        TRY(ctx_alloc(c, &d.cam_gptr, plan.cam_gptr.size()));
-        TRY(ctx_alloc(c, &d.cam_gslots, plan.cam_gslots.size()));
-        TRY(upload(d.grp_ch, plan.grp_ch.data(), plan.grp_ch.size(), s));
-        TRY(upload(d.grp_gs, plan.grp_gs.data(), plan.grp_gs.size(), s));
-        TRY(upload(d.grp_ge, plan.grp_ge.data(), plan.grp_ge.size(), s));
-        TRY(upload(d.cs_g, plan.cs_g.data(), plan.cs_g.size(), s));
-        TRY(upload(d.ce_g, plan.ce_g.data(), plan.ce_g.size(), s));
-        TRY(upload(d.blk_gptr, plan.blk_gptr.data(), plan.blk_gptr.size(), s));
-        TRY(upload(d.blk_gslots, plan.blk_gslots.data(), plan.blk_gslots.size(), s));
-        TRY(upload(d.cam_gptr, plan.cam_gptr.data(), plan.cam_gptr.size(), s));
-        TRY(upload(d.cam_gslots, plan.cam_gslots.data(), plan.cam_gslots.size(), s));
+        pb.add(&d.grp_ch, plan.grp_ch);
+        pb.add(&d.grp_gs, plan.grp_gs);
+        pb.add(&d.grp_ge, plan.grp_ge);
+        pb.add(&d.cs_g, plan.cs_g);
+        pb.add(&d.ce_g, plan.ce_g);
+        pb.add(&d.blk_gptr, plan.blk_gptr);
+        pb.add(&d.blk_gslots, plan.blk_gslots);
+        pb.add(&d.cam_gptr, plan.cam_gptr);
+        pb.add(&d.cam_gslots, plan.cam_gslots);
         TRY(ctx_alloc(c, &d.upart, (size_t)(na * (na + 1) / 2 + na) * d.nes));
         TRY(ctx_alloc(c, &d.chsse, 3 * (size_t)d.nch));   // lin SSE | new SSE | dpg
-        TRY(upload(d.ch_pt, plan.ch_pt.data(), plan.ch_pt.size(), s));
-        TRY(upload(d.ch_eslot, plan.ch_eslot.data(), plan.ch_eslot.size(), s));
-        TRY(upload(d.eslot_optr, plan.eslot_optr.data(), plan.eslot_optr.size(), s));
-        TRY(upload(d.eslot_obs, plan.eslot_obs.data(), plan.eslot_obs.size(), s));
-        TRY(upload(d.cam_eptr, plan.cam_eptr.data(), plan.cam_eptr.size(), s));
-        TRY(upload(d.cam_eslots, plan.cam_eslots.data(), plan.cam_eslots.size(), s));
-        VLGBA_CHECK(hipStreamSynchronize(s));   // plan vectors are local
+        pb.add(&d.ch_pt, plan.ch_pt);
+        pb.add(&d.ch_eslot, plan.ch_eslot);
+        pb.add(&d.eslot_optr, plan.eslot_optr);
+        pb.add(&d.eslot_obs, plan.eslot_obs);
+        pb.add(&d.cam_eptr, plan.cam_eptr);
+        pb.add(&d.cam_eslots, plan.cam_eslots);
+        TRY(pb.commit(c, s));   // (synchronous: the plan vectors are thread scratch)
         ST_MARK("plan_upload");
     }
     TRY(ctx_alloc(c, &d.U, (size_t)na * na * p->m + na * (size_t)p->m + 1));
@@ -1770,6 +1813,15 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
     TRY(ctx_alloc(c, &d.blk_jk, 2 * (size_t)d.nb));
     TRY(ctx_alloc(c, &d.blk_ptr, (size_t)d.nb + 1));
     TRY(ctx_alloc(c, &d.term, 2 * (size_t)d.T));
+    TRY(upload(d.blk_jk, hb.jk.data(), hb.jk.size(), s));
+    // the long tracks' pair counts per block (k_long_pairs) on the device while
+    // the host builds the solve's structure (ba_chol_setup); read back below
+    int *lp_cnt = nullptr;
+    if (fast && d.nl > 0) {
+        TRY(ctx_alloc(c, &lp_cnt, (size_t)d.nb + 1));
+        TRY(ctx_alloc(c, &d.lpair_ptr, (size_t)d.nb + 1));
+        TRY(ba_launch_long_pairs(&d, 0, lp_cnt));
+    }
     // blocks | rhs | old SSE contiguous: one all-reduce per pass (world > 1)
     TRY(ctx_alloc(c, &d.sblk, (size_t)na * na * d.nb + d.lds + 1));
     d.rhs = d.sblk + (size_t)na * na * d.nb;
@@ -1799,18 +1851,13 @@ static int ctx_setup(vlgba_ctx *c, const vlgba_problem *p, const host_obs &h,
         TRY(upload(d.obs_x, h.x.data() + 2 * o0, 2 * (size_t)d.N, s));
         if (p->K) TRY(upload(d.K4, p->K, 4 * (size_t)p->m, s));
         else VLGBA_CHECK(hipMemsetAsync(d.K4, 0, sizeof(double) * 4 * p->m, s));
-        TRY(upload(d.blk_jk, hb.jk.data(), hb.jk.size(), s));
         TRY(upload(d.blk_ptr, hb.ptr.data(), hb.ptr.size(), s));
         TRY(upload(d.term, hb.term.data(), hb.term.size(), s));
     }
     ST_MARK("uploads");
     if (fast && d.nl > 0) {   // the long tracks' per-block pair lists (k_long_pairs)
-        int *cnt = nullptr;
-        TRY(ctx_alloc(c, &cnt, (size_t)d.nb + 1));
-        TRY(ctx_alloc(c, &d.lpair_ptr, (size_t)d.nb + 1));
-        TRY(ba_launch_long_pairs(&d, 0, cnt));
         std::vector<int> h((size_t)d.nb + 1, 0);
-        TRY(download(h.data(), cnt, (size_t)d.nb, s));
+        TRY(download(h.data(), lp_cnt, (size_t)d.nb, s));
         VLGBA_CHECK(hipStreamSynchronize(s));
         long long tot = 0;
         for (int b = 0; b < d.nb; b++) {

@@ -27,11 +27,12 @@ before-triangulation solve (nothing but the new camera changes it), and up to
 the points whose triangulation fails the depth test for an after-triangulation
 one (predicted by triangulating on the cameras as they are; a wrong prediction
 is detected and that solve's context rebuilt) -- so two worker threads cut
-the next two solves' observation subsets and build their libvlgba contexts
-(the host plan of vlgba_create, which runs with the GIL released) while the
-current solve runs on the GPU ("reuse across
-growing calls").  Only the parameter upload and the LM loop stay on the
-replay's critical path.
+the next camera's two solves' observation subsets and build their libvlgba
+contexts (the host plan of vlgba_create, which runs with the GIL released)
+from the start of the current camera's after-triangulation solve on, two
+solves ahead of their use ("reuse across growing
+calls").  Only the parameter upload and the LM loop stay on the replay's
+critical path.
 """
 from __future__ import annotations
 
@@ -157,15 +158,23 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
         """worker: the solve's subset and (one rank) its context.  An item
         predicted across a triangulation comes with the candidates and a
         snapshot of the cameras, triangulated here (on the cameras before the
-        added one) to predict which points pass the depth test"""
-        if len(item) == 6:
-            tag, j, cam_on, x3, (Ts, ws, cand), add = item
+        added one) to predict which points pass the depth test.  A re-check
+        (a seventh entry: the future of the prediction made a camera earlier)
+        triangulates on the cameras as they are now and builds a context only
+        if that prediction came out different."""
+        early = item[6] if len(item) == 7 else None
+        if len(item) >= 6:
+            tag, j, cam_on, x3, (Ts, ws, cand), add = item[:6]
             pt_on = x3.copy()
             pt_on[cand] = _triangulate(sc, K, Ts, ws, cand, cam_on)[3] == 1.0
             if add is not None:
                 cam_on = cam_on.copy()
                 cam_on[add] = True
             item = (tag, j, cam_on, pt_on)
+            if early is not None:
+                e = early.result()[0]
+                if np.array_equal(e[2], cam_on) and np.array_equal(e[3], pt_on):
+                    return item, None, None, 0.0      # the same: nothing to build
         tag, j, cam_on, pt_on = item
         cams, pts = np.nonzero(cam_on)[0], np.nonzero(pt_on)[0]
         if len(pts) == 0 or len(cams) < 2:
@@ -187,7 +196,8 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
     # behind instead of one
     pool = ThreadPoolExecutor(max_workers=PREFETCH_WORKERS) if use_pf else None
     pending = {}
-    stats = {"prefetched": 0, "mispredicted": 0}
+    stats = {"prefetched": 0, "repredicted": 0, "mispredicted": 0, "built_inline": 0,
+             "wait_s": {"before-triangulation": 0.0, "after-triangulation": 0.0}}
 
     # visible counts over the status cameras, kept up to date as cameras join
     # (a bincount over every observation per solve otherwise)
@@ -198,29 +208,49 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
     cam_obs_pts = [sc.obs_pt[ids] for ids in cam_obs_ids]
     nvis_cur = nvis.copy()
 
+    def standin_pose(j):
+        """camera j's starting pose as the loop below sets it (the DLT
+        stand-in: the perturbed pose mapped into the current frame)"""
+        s_, R_, t_ = _similarity(sc, X)
+        Rc = vl_rodr(sc.w0[:, j]) @ R_.T
+        return vl_irodr(Rc), s_ * sc.T0[:, j] - Rc @ t_
+
     def next_sets(tag, j):
-        """the solves predicted at (tag, j), from the current state: at a
-        before-triangulation solve, the after-triangulation solve (the same
-        cameras and the points that pass the triangulation's depth test on the
-        cameras as they are now -- the worker triangulates; the solve in
-        between moves them a little, so a marginal point may still come out
-        the other way) and the next camera's before-triangulation solve (those
-        points, the camera added); nothing at an after-triangulation solve
-        (its successor was predicted with it).  The first solve of a replay
-        that starts after a triangulation predicts the next camera's."""
-        cand = np.nonzero((X[3] == 0) & (nvis_cur >= 2))[0]
+        """the solves predicted at (tag, j), from the current state.  At an
+        after-triangulation solve (its points are the next camera's), the next
+        camera jn's two solves: its before-triangulation solve exactly (these
+        cameras and jn, these points) and its after-triangulation solve -- the
+        points that will have >= 2 views once jn is in and pass the
+        triangulation's depth test on the cameras as they are now, jn at its
+        stand-in pose (the worker triangulates; the solves in between move the
+        cameras a little, so a marginal point may still come out the other way:
+        that solve's context is then rebuilt).  Both are built two solves ahead
+        of their use, so the workers keep ahead of the replay.  At a
+        before-triangulation solve only its own after-triangulation solve, if
+        nothing predicted it (the first solve of a replay)."""
         jn = next((q for q in range(j + 1, m) if not status[q]), None)
-        snap = (T.copy(), w.copy(), cand)
         out = []
-        if tag == "before-triangulation":
-            out.append(("after-triangulation", j, status.copy(), X[3] == 1, snap, None))
+        if tag == "after-triangulation":
             if jn is not None:
-                out.append(("before-triangulation", jn, status.copy(), X[3] == 1, snap, jn))
-        elif jn is not None and ("before-triangulation", jn) not in pending:
-            st = status.copy()
-            st[jn] = True
-            out.append(("before-triangulation", jn, st, X[3] == 1))
-        return out
+                st = status.copy()
+                st[jn] = True
+                pts = X[3] == 1
+                nv = nvis_cur.copy()
+                nv[cam_obs_pts[jn]] += 1
+                cand = np.nonzero((X[3] == 0) & (nv >= 2))[0]
+                Ts, ws = T.copy(), w.copy()
+                ws[:, jn], Ts[:, jn] = standin_pose(jn)
+                out.append(("before-triangulation", jn, st, pts))
+                out.append(("after-triangulation", jn, st, pts, (Ts, ws, cand), None))
+        else:
+            snap = (T.copy(), w.copy(), np.nonzero((X[3] == 0) & (nvis_cur >= 2))[0])
+            early = pending.get(("after-triangulation", j))
+            if early is None:
+                out.append(("after-triangulation", j, status.copy(), X[3] == 1, snap, None))
+            else:   # re-check the prediction made a camera ahead on today's cameras
+                out.append(("after-triangulation*", j, status.copy(), X[3] == 1, snap, None,
+                            early))
+        return [o for o in out if (o[0], o[1]) not in pending]
 
     def ba(tag, j):
         cams = np.nonzero(status)[0]
@@ -228,16 +258,31 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
         t0 = time.perf_counter()
         pre = create_s = sub = None
         if use_pf:
+            def fits(it):
+                return np.array_equal(it[2], status) and np.array_equal(it[3], X[3] == 1)
             fut = pending.pop((tag, j), None)
+            late = pending.pop((tag + "*", j), None)     # its re-check (after-triangulation)
             if fut is not None:
                 item, sub, pre, create_s = fut.result()
-                if not (np.array_equal(item[2], status) and np.array_equal(item[3], X[3] == 1)):
-                    if pre is not None:                  # a triangulation failed the depth
-                        pre.close()                      # test: this context is not the solve's
+                if not fits(item):                       # a triangulation failed the depth
+                    if pre is not None:                  # test: this context is not the solve's
+                        pre.close()
                     pre = create_s = sub = None
-                    stats["mispredicted"] += 1
+                    item2, sub2, pre2, cs2 = late.result() if late is not None else (None,) * 4
+                    if item2 is not None and (sub2 is not None or pre2 is not None) and \
+                            fits(item2):                 # the re-check's context is
+                        sub, pre, create_s = sub2, pre2, cs2
+                        stats["repredicted"] += 1
+                    else:
+                        if pre2 is not None:
+                            pre2.close()
+                        stats["mispredicted"] += 1
                 else:
                     stats["prefetched"] += 1
+                    if late is not None:
+                        pre2 = late.result()[2]
+                        if pre2 is not None:             # (a re-check that came out different
+                            pre2.close()                 # while the first guess was right)
             for nxt in next_sets(tag, j):                # the next solves' contexts, built
                 pending[(nxt[0], nxt[1])] = pool.submit(build, nxt)   # while this one runs
         if len(pts) == 0 or len(cams) < 2:
@@ -246,7 +291,10 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
             return
         if sub is None and use_pf:                       # nothing prefetched (the first
             _, sub, pre, create_s = build((tag, j, status.copy(), X[3] == 1))   # solve)
+            stats["built_inline"] += 1
         wait = time.perf_counter() - t0
+        if use_pf:
+            stats["wait_s"][tag] += wait
         pt, cam, ox = sub if sub is not None else _subset_obs(sc, cams, pts, status, X[3] == 1)
         world = world_of(len(pt))
         if world > 1:

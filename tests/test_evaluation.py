@@ -151,10 +151,14 @@ def test_incremental_prefetch_bookkeeping(monkeypatch, prefetch):
     assert all(a.closed for a in made)
     pf = res["prefetch"]
     if prefetch:   # every solve got a context: prefetched, or rebuilt after a wrong guess
-        assert pf["prefetched"] + pf["mispredicted"] + 1 >= len(calls)
+        # only the first solve builds its own (every later one was predicted a
+        # camera ahead: incremental.next_sets)
+        assert pf["built_inline"] == 1, pf
+        assert pf["prefetched"] + pf["repredicted"] + pf["mispredicted"] + 1 == len(calls), pf
         assert len(made) >= len(calls) and pf["prefetched"] >= len(calls) // 2
     else:
-        assert not made and pf == {"prefetched": 0, "mispredicted": 0}
+        assert not made and (pf["prefetched"], pf["repredicted"], pf["mispredicted"],
+                             pf["built_inline"]) == (0, 0, 0, 0)
 
 
 def test_triangulation_restatement():

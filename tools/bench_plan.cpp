@@ -97,7 +97,7 @@ int main(int argc, char **argv)
         H.add(hb.term);
         H.add(P.ch_pt); H.add(P.ch_slot); H.add(P.ch_eslot); H.add(P.slot_blk);
         H.add(P.slot_tptr); H.add(P.eslot_optr); H.add(P.slot_term); H.add(P.eslot_obs);
-        H.add(P.blk_sptr); H.add(P.blk_slots); H.add(P.cam_eptr); H.add(P.cam_eslots);
+        H.add(P.cam_eptr); H.add(P.cam_eslots);
         H.add(P.grp_ch); H.add(P.grp_gs); H.add(P.grp_ge); H.add(P.cs_g); H.add(P.ce_g);
         H.add(P.gslot_blk); H.add(P.gecam); H.add(P.blk_gptr); H.add(P.blk_gslots);
         H.add(P.cam_gptr); H.add(P.cam_gslots); H.add(P.seg_pt); H.add(P.seg_long);
