@@ -99,6 +99,9 @@ def _subset_obs(sc, cams, pts, cam_on=None, pt_on=None):
 
 
 PREFETCH_WORKERS = 2   # incremental_bundle's context builders (see below)
+# from this many points on, a solve's successors are predicted a camera
+# earlier (incremental_bundle.next_sets): cfg5x's large solves, not cfg5's
+PREDICT_EARLY_PTS = 3000
 
 
 def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, device=0,
@@ -215,19 +218,26 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
         Rc = vl_rodr(sc.w0[:, j]) @ R_.T
         return vl_irodr(Rc), s_ * sc.T0[:, j] - Rc @ t_
 
-    def next_sets(tag, j):
-        """the solves predicted at (tag, j), from the current state.  At an
+    def next_sets(tag, j, early):
+        """the solves predicted at (tag, j), from the current state.
+
+        ``early`` (solves of >= PREDICT_EARLY_PTS points, where building a
+        context takes about as long as the solve before it): at an
         after-triangulation solve (its points are the next camera's), the next
-        camera jn's two solves: its before-triangulation solve exactly (these
-        cameras and jn, these points) and its after-triangulation solve -- the
+        camera jn's two solves -- its before-triangulation solve exactly (these
+        cameras and jn, these points) and its after-triangulation solve: the
         points that will have >= 2 views once jn is in and pass the
         triangulation's depth test on the cameras as they are now, jn at its
         stand-in pose (the worker triangulates; the solves in between move the
-        cameras a little, so a marginal point may still come out the other way:
-        that solve's context is then rebuilt).  Both are built two solves ahead
-        of their use, so the workers keep ahead of the replay.  At a
-        before-triangulation solve only its own after-triangulation solve, if
-        nothing predicted it (the first solve of a replay)."""
+        cameras a little, so a marginal point may still come out the other
+        way).  Both are built two solves ahead of their use; at jn's
+        before-triangulation solve the after-triangulation prediction is
+        re-checked on the cameras of that moment (a context is built only if
+        it comes out different).  Smaller solves (the prediction work would
+        cost the replay thread more than the wait it saves): at a
+        before-triangulation solve its after-triangulation solve and the next
+        camera's before-triangulation solve (those points, the camera added),
+        at an after-triangulation solve the next camera's if not pending."""
         jn = next((q for q in range(j + 1, m) if not status[q]), None)
         out = []
         if tag == "after-triangulation":
@@ -235,21 +245,24 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
                 st = status.copy()
                 st[jn] = True
                 pts = X[3] == 1
-                nv = nvis_cur.copy()
-                nv[cam_obs_pts[jn]] += 1
-                cand = np.nonzero((X[3] == 0) & (nv >= 2))[0]
-                Ts, ws = T.copy(), w.copy()
-                ws[:, jn], Ts[:, jn] = standin_pose(jn)
                 out.append(("before-triangulation", jn, st, pts))
-                out.append(("after-triangulation", jn, st, pts, (Ts, ws, cand), None))
+                if early:
+                    nv = nvis_cur.copy()
+                    nv[cam_obs_pts[jn]] += 1
+                    cand = np.nonzero((X[3] == 0) & (nv >= 2))[0]
+                    Ts, ws = T.copy(), w.copy()
+                    ws[:, jn], Ts[:, jn] = standin_pose(jn)
+                    out.append(("after-triangulation", jn, st, pts, (Ts, ws, cand), None))
         else:
             snap = (T.copy(), w.copy(), np.nonzero((X[3] == 0) & (nvis_cur >= 2))[0])
-            early = pending.get(("after-triangulation", j))
-            if early is None:
+            first = pending.get(("after-triangulation", j))
+            if first is None:
                 out.append(("after-triangulation", j, status.copy(), X[3] == 1, snap, None))
+                if not early and jn is not None:
+                    out.append(("before-triangulation", jn, status.copy(), X[3] == 1, snap, jn))
             else:   # re-check the prediction made a camera ahead on today's cameras
                 out.append(("after-triangulation*", j, status.copy(), X[3] == 1, snap, None,
-                            early))
+                            first))
         return [o for o in out if (o[0], o[1]) not in pending]
 
     def ba(tag, j):
@@ -283,8 +296,9 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
                         pre2 = late.result()[2]
                         if pre2 is not None:             # (a re-check that came out different
                             pre2.close()                 # while the first guess was right)
-            for nxt in next_sets(tag, j):                # the next solves' contexts, built
-                pending[(nxt[0], nxt[1])] = pool.submit(build, nxt)   # while this one runs
+            for nxt in next_sets(tag, j, len(pts) >= PREDICT_EARLY_PTS):   # the next solves'
+                pending[(nxt[0], nxt[1])] = pool.submit(build, nxt)   # contexts, built
+                                                                      # while this one runs
         if len(pts) == 0 or len(cams) < 2:
             if pre is not None:
                 pre.close()
@@ -405,7 +419,10 @@ def _triangulate(sc, K, T, w, pts, status):
     A = np.zeros((len(pts), 2 * kmax, 4))                # zero rows leave V unchanged
     A[slot, 2 * rank] = ox[:, 0:1] * P[:, 2] - P[:, 0]
     A[slot, 2 * rank + 1] = ox[:, 1:2] * P[:, 2] - P[:, 1]
-    v = np.linalg.svd(A)[2][:, 3, :]                     # V(:, 4)
+    # V(:, 4) only: the reduced SVD (no 2 kmax x 2 kmax U per point -- with a
+    # long track in the batch that U was most of the replay's host time) gives
+    # the same V bit for bit (LAPACK's gesdd takes the same path for V)
+    v = np.linalg.svd(A, full_matrices=False)[2][:, 3, :]
     Xh = v / v[:, 3:4]
     depth = np.einsum("kj,kj->k", P[:, 2], Xh[slot])
     bad = np.zeros(len(pts), dtype=bool)

@@ -107,8 +107,8 @@ def test_incremental_obs_ranges_match_the_full_pass():
     assert inc._obs_of(shuffled, np.arange(4)) is None
 
 
-@pytest.mark.parametrize("prefetch", [True, False])
-def test_incremental_prefetch_bookkeeping(monkeypatch, prefetch):
+@pytest.mark.parametrize("prefetch,early", [(True, False), (True, True), (False, False)])
+def test_incremental_prefetch_bookkeeping(monkeypatch, prefetch, early):
     """The replay's solve sets (incremental._solve_sets, which the prefetching
     worker builds contexts from) follow the main loop's own status / X3d
     bookkeeping call by call, and every call gets the context built for its
@@ -142,6 +142,8 @@ def test_incremental_prefetch_bookkeeping(monkeypatch, prefetch):
     def fake_resect(K, T, w, Xs, xs, *opts, **kw):
         return K, T, w, [np.array([1.0])]
 
+    # early: every solve's successors predicted a camera ahead (next_sets)
+    monkeypatch.setattr(inc, "PREDICT_EARLY_PTS", 0 if early else 10 ** 9)
     monkeypatch.setattr(inc, "euclid_obs_adjuster", FakeAdjuster)
     monkeypatch.setattr(inc, "bundle_euclid_obs", fake_solve)
     monkeypatch.setattr(inc, "bundle_euclid_resect", fake_resect)
