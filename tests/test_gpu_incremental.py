@@ -52,6 +52,33 @@ def test_incremental_replay(gpu, oracle):
     assert min(e1) * (1 - 1e-7) <= e[1] <= max(e1) * (1 + 1e-7), (e, e1)
 
 
+@pytest.mark.parametrize("early", [False, True])
+def test_prefetched_replay_equals_unprefetched(gpu, monkeypatch, early):
+    """The prefetch workers (incremental.py: contexts built ahead, the
+    after-triangulation prediction re-checked a solve later; early = every
+    solve's successors predicted a camera ahead, as cfg5x's large solves are)
+    change no result: the whole replay -- every solve's error_ and the final
+    reconstruction -- equals the replay that builds each context when its
+    solve starts, bit for bit; and with prefetching on, every solve after the
+    first had a context ready or rebuilt."""
+    from bundleadjustmentmatlab_amd import incremental as inc
+    from bundleadjustmentmatlab_amd.scene import make_config
+    sc = make_config("cfg5", m=16, seed=7)
+    monkeypatch.setattr(inc, "PREDICT_EARLY_PTS", 0 if early else 10 ** 9)
+    a = inc.incremental_bundle(sc, prefetch=True)
+    b = inc.incremental_bundle(sc, prefetch=False)
+    assert len(a["solves"]) == len(b["solves"]) == 2 * (sc.m - 2)
+    for p, q in zip(a["solves"], b["solves"]):
+        assert (p["cameras"], p["points"], p["observations"]) == \
+            (q["cameras"], q["points"], q["observations"])
+        assert np.array_equal(p["error"], q["error"]), (p["error"], q["error"])
+    for k in ("K", "T", "w", "X", "status"):
+        assert np.array_equal(a[k], b[k]), k
+    pf = a["prefetch"]
+    assert pf["built_inline"] >= 1
+    assert pf["prefetched"] + pf["repredicted"] + pf["mispredicted"] + 1 == len(a["solves"]), pf
+
+
 def test_full_solve_config2_converges(gpu):
     """Config 2 (50 x 10k x 60k) LM to convergence: error_ non-increasing,
     ends at the noise level, and a second solve from the same start repeats
