@@ -1711,6 +1711,44 @@ __device__ __forceinline__ void load_rm32(const double *__restrict__ src, double
     for (int u = 0; u < 4; u++) T[(r0 + 8 * u) * LP + c] = v[u];
 }
 
+// One wave's copy of a whole 32 x 32 tile (load32 / load_rm32 with the 256
+// threads' elements on the 64 lanes of one wave: the same values at the same
+// LDS places), for the level records that wait for each operand's flag in the
+// wave that loads it (cr32_level_body's PW form)
+__device__ __forceinline__ void load32_wave(const double *__restrict__ S, long long lds, int TB,
+                                            long long ld, int ti, int tj, double *T, bool transposed,
+                                            bool diag)
+{
+    const int lane = threadIdx.x & 63, r = lane & 31, c0 = lane >> 5;
+    const long long gr = (long long)TB * ti + r;
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+        const int c = c0 + 2 * u;
+        const long long gc = (long long)TB * tj + c;
+        const bool ok = r < TB && c < TB && gr < ld && gc < ld;
+        v[u] = ok ? ldg<true>(S + gr + lds * gc) : ((diag && r == c) ? 1.0 : 0.0);
+    }
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+        const int c = c0 + 2 * u;
+        if (transposed)
+            T[c * LP + r] = v[u];
+        else
+            T[r * LP + c] = v[u];
+    }
+}
+
+__device__ __forceinline__ void load_rm32_wave(const double *__restrict__ src, double *T)
+{
+    const int lane = threadIdx.x & 63, c = lane & 31, r0 = lane >> 5;
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) v[u] = ldg<true>(src + (r0 + 2 * u) * T32 + c);
+#pragma unroll
+    for (int u = 0; u < 16; u++) T[(r0 + 2 * u) * LP + c] = v[u];
+}
+
 // acc (one 16 x 16 block per wave: rows 16 (w >> 1), cols 16 (w & 1)) of
 // A B^T over K = 32 (nt form, as mfma_64x64)
 __device__ __forceinline__ d4 mfma32_nt(const double *A, const double *Bt, d4 acc)
@@ -2137,12 +2175,45 @@ __device__ __forceinline__ void cr32_rupd(const double *Bs, const double *Cs, bo
     if (lane < 32) rk[r] = (rk[r] - t) - up[r];
 }
 
+// The one-launch CR's per-wave operand hand-off (k_cr32_fused, level L >= 1):
+// each wave polls only the flags of the operand it loads and loads it at once
+// (all 64 lanes, sc1), so an operand whose producer finished early is in LDS
+// while the wave of a later one still waits; one barrier after all of them.
+// The union of the waves' flags is the record's former flag set.
+struct cr32_pw {
+    const unsigned *flag;
+    unsigned epoch;
+    double *status;
+    int L, nt;
+};
+
+__device__ __forceinline__ void cr32_wave_wait(const cr32_pw &pw, const int *w, int nw)
+{
+    const int lane = threadIdx.x & 63;
+    int idx = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        if (lane == q && q < nw) idx = w[q];
+    for (unsigned spins = 0;; spins++) {
+        const bool ok = lane >= nw || __hip_atomic_load((const gu32_t *)(pw.flag + idx),
+                                                        __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT) == pw.epoch;
+        if (__all(ok)) break;
+        if (spins >= BA_BACK_SPIN_MAX) {
+            if (lane == 0) pw.status[1] = 1.0;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
 template <bool SC, class Mid>
 __device__ __forceinline__ void cr32_level_body(const cr32_lds &sh, double *S, long long lds,
                                                 int TB, long long ld, int k, int p, int q, int em,
                                                 int ep, int role, int nt, double *linv,
                                                 double *crL, double *rhs, double *y,
-                                                double *status, Mid mid)
+                                                double *status, Mid mid,
+                                                const cr32_pw *pw = nullptr)
 {
     double *As = sh.As, *Bs = sh.Bs, *Cs = sh.Cs, *Ds = sh.Ds, *Es = sh.Es, *Xs = sh.Xs;
     double *rk = sh.rk, *ym = sh.ym, *yp = sh.yp, *um = sh.um, *up = sh.up;
@@ -2157,13 +2228,58 @@ __device__ __forceinline__ void cr32_level_body(const cr32_lds &sh, double *S, l
             yp[tid] = (ep >= 0 && tid < TB) ? ldg<SC>(y + (long long)TB * ep + tid) : 0.0;
         }
     };
-    load32<SC>(S, lds, TB, ld, k, k, As, false, true);
-    load_rm32<SC>(crL + T2 * (nt + em), Bs);            // L(k, em)
-    if (ep >= 0) load_rm32<SC>(crL + T2 * ep, Cs);      // L(k, ep)
-    if (role == 1) load_rm32<SC>(crL + T2 * em, Ds);    // L(p, em)
-    if (role == 2) load_rm32<SC>(crL + T2 * (nt + ep), Ds);   // L(q, ep)
-    if (role == 0) load_r();
-    __syncthreads();
+    if (SC && pw) {   // per wave: its operand's flags, then its operand
+        auto fw = [&](int t, int r) { return 5 * ((pw->L - 1) * nt + t) + r; };
+        const bool own = pw->L >= 2;
+        int wl[4], n = 0;
+        if (w == 0) {          // D_k (its survivor record at L - 1)
+            if (own) {
+                wl[n++] = fw(k, 3);
+                if (role == 0) wl[n++] = fw(k, 4);
+            }
+            cr32_wave_wait(*pw, wl, n);
+            load32_wave(S, lds, TB, ld, k, k, As, false, true);
+        } else if (w == 1) {   // L(k, em) = role 2 of em (role 0 waits for all of em)
+            wl[n++] = fw(em, 2);
+            if (role == 0 || role == 1) wl[n++] = fw(em, 1);
+            if (role == 0) wl[n++] = fw(em, 0);
+            cr32_wave_wait(*pw, wl, n);
+            load_rm32_wave(crL + T2 * (nt + em), Bs);
+        } else if (w == 2) {   // L(k, ep) = role 1 of ep
+            if (ep >= 0) {
+                wl[n++] = fw(ep, 1);
+                if (role == 0 || role == 2) wl[n++] = fw(ep, 2);
+                if (role == 0) wl[n++] = fw(ep, 0);
+                cr32_wave_wait(*pw, wl, n);
+                load_rm32_wave(crL + T2 * ep, Cs);
+            }
+        } else if (role == 1 || role == 2) {   // the fill's L(p, em) | L(q, ep)
+            wl[n++] = role == 1 ? fw(em, 1) : fw(ep, 2);
+            cr32_wave_wait(*pw, wl, n);
+            load_rm32_wave(crL + T2 * (role == 1 ? em : nt + ep), Ds);
+        } else if (role == 0) {   // r_k, y_em, y_ep on this wave's first 32 lanes
+            wl[n++] = fw(em, 0);
+            if (ep >= 0) wl[n++] = fw(ep, 0);
+            if (own) wl[n++] = fw(k, 4);
+            cr32_wave_wait(*pw, wl, n);
+            const int i = tid & 63;
+            if (i < T32) {
+                const long long g = (long long)TB * k + i;
+                rk[i] = (i < TB && g < ld) ? ldg<SC>(rhs + g) : 0.0;
+                ym[i] = i < TB ? ldg<SC>(y + (long long)TB * em + i) : 0.0;
+                yp[i] = (ep >= 0 && i < TB) ? ldg<SC>(y + (long long)TB * ep + i) : 0.0;
+            }
+        }
+        __syncthreads();
+    } else {
+        load32<SC>(S, lds, TB, ld, k, k, As, false, true);
+        load_rm32<SC>(crL + T2 * (nt + em), Bs);            // L(k, em)
+        if (ep >= 0) load_rm32<SC>(crL + T2 * ep, Cs);      // L(k, ep)
+        if (role == 1) load_rm32<SC>(crL + T2 * em, Ds);    // L(p, em)
+        if (role == 2) load_rm32<SC>(crL + T2 * (nt + ep), Ds);   // L(q, ep)
+        if (role == 0) load_r();
+        __syncthreads();
+    }
     CR_SUB(4);
     if (surv) {
         d4 acc = {0.0, 0.0, 0.0, 0.0};
@@ -2468,6 +2584,9 @@ __global__ __launch_bounds__(256) void k_cr32_back_all(const int *__restrict__ e
 // launches).
 // ---------------------------------------------------------------------------
 #define BA_CR_MAXLEV 30
+#ifndef BA_CR_PW
+#define BA_CR_PW 1
+#endif
 struct cr32_fplan {
     int nl, nrec;
     int l0two;                     // level 0 in 2 records per tile (roles 4 | 2), else 3
@@ -2587,8 +2706,11 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
         }
         // (Tried in round 5: own D_k waited for alone and its loads issued
         // before the neighbours' wait -- 81 -> 86 us: the second poll-and-
-        // barrier costs more than the overlapped loads save.)
-        cr32_wait_flags(flag, nw, w, epoch, status);
+        // barrier costs more than the overlapped loads save.)  BA_CR_PW: the
+        // flags are polled per operand by the wave that loads it
+        // (cr32_level_body), no poll-and-barrier here
+        const bool skip = (role == 1 && p < 0) || (role == 2 && q < 0);
+        if (!BA_CR_PW || skip) cr32_wait_flags(flag, nw, w, epoch, status);
         CR_ST(1);
         // the survivor's r_k: the neighbours' y and its own r_k of level L-1
         auto mid = [&]() {
@@ -2598,9 +2720,10 @@ __global__ __launch_bounds__(256) void k_cr32_fused(double *S, long long lds, in
             if (L >= 2) w2[n2++] = fw(L - 1, k, 4);
             cr32_wait_flags(flag, n2, w2, epoch, status);
         };
-        if (!((role == 1 && p < 0) || (role == 2 && q < 0)))
+        const cr32_pw pw{flag, epoch, status, L, nt};
+        if (!skip)
             cr32_level_body<true>(sh, S, lds, TB, ld, k, p, q, em, ep, role, nt, linv, crL, rhs,
-                                  y, status, mid);
+                                  y, status, mid, BA_CR_PW ? &pw : nullptr);
         CR_ST(2);
         cr32_publish(flag + fw(L, k, role == 3 ? 4 : role), epoch);
         CR_ST(3);
