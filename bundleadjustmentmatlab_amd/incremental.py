@@ -166,6 +166,12 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
         triangulates on the cameras as they are now and builds a context only
         if that prediction came out different."""
         early = item[6] if len(item) == 7 else None
+        if len(item) == 5:   # derived: the prediction ``dep`` made, one camera added
+            tag, j, dep, add, _ = item
+            e = dep.result()[0]
+            cam_on = e[2].copy()
+            cam_on[add] = True
+            item = (tag, j, cam_on, e[3])
         if len(item) >= 6:
             tag, j, cam_on, x3, (Ts, ws, cand), add = item[:6]
             pt_on = x3.copy()
@@ -199,7 +205,10 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
     # behind instead of one
     pool = ThreadPoolExecutor(max_workers=PREFETCH_WORKERS) if use_pf else None
     pending = {}
+    derived_from = {}    # a derived solve's key -> the future of the prediction it adds to
+    discard = []         # futures of derived contexts found wrong (closed when built)
     stats = {"prefetched": 0, "repredicted": 0, "mispredicted": 0, "built_inline": 0,
+             "derived_rebuilt": 0,
              "wait_s": {"before-triangulation": 0.0, "after-triangulation": 0.0}}
 
     # visible counts over the status cameras, kept up to date as cameras join
@@ -233,7 +242,12 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
         way).  Both are built two solves ahead of their use; at jn's
         before-triangulation solve the after-triangulation prediction is
         re-checked on the cameras of that moment (a context is built only if
-        it comes out different).  Smaller solves (the prediction work would
+        it comes out different), and camera jn's successor's
+        before-triangulation solve is derived from it (its points, the next
+        camera added: two LM loops of lead instead of one; compared with the
+        exact sets at the after-triangulation solve and rebuilt there if they
+        differ -- cfg5x wait 2.3-3.3 -> 1.4-1.6 s, profiles/r06/ab_prefetch_derived.txt).
+        Smaller solves (the prediction work would
         cost the replay thread more than the wait it saves): at a
         before-triangulation solve its after-triangulation solve and the next
         camera's before-triangulation solve (those points, the camera added),
@@ -241,6 +255,12 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
         jn = next((q for q in range(j + 1, m) if not status[q]), None)
         out = []
         if tag == "after-triangulation":
+            d = derived_from.pop(("before-triangulation", jn), None)
+            if d is not None:
+                e = d.result()[0]   # (done: this solve's own context came from it or its twin)
+                if not (np.array_equal(e[2], status) and np.array_equal(e[3], X[3] == 1)):
+                    discard.append(pending.pop(("before-triangulation", jn)))
+                    stats["derived_rebuilt"] += 1   # rebuilt below from the exact sets
             if jn is not None:
                 st = status.copy()
                 st[jn] = True
@@ -263,6 +283,12 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
             else:   # re-check the prediction made a camera ahead on today's cameras
                 out.append(("after-triangulation*", j, status.copy(), X[3] == 1, snap, None,
                             first))
+            if early and jn is not None:
+                # the next camera's before-triangulation solve: this solve's predicted
+                # points (the re-check's, or the first prediction's), camera jn added --
+                # two LM loops of lead instead of one; checked against the exact sets at
+                # the after-triangulation solve and rebuilt if they differ
+                out.append(("before-triangulation", jn, out[-1][:2], jn, None))
         return [o for o in out if (o[0], o[1]) not in pending]
 
     def ba(tag, j):
@@ -296,9 +322,19 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
                         pre2 = late.result()[2]
                         if pre2 is not None:             # (a re-check that came out different
                             pre2.close()                 # while the first guess was right)
+            for f in [f for f in discard if f.done()]:   # wrong derived contexts, built
+                discard.remove(f)
+                pre2 = f.result()[2]
+                if pre2 is not None:
+                    pre2.close()
             for nxt in next_sets(tag, j, len(pts) >= PREDICT_EARLY_PTS):   # the next solves'
-                pending[(nxt[0], nxt[1])] = pool.submit(build, nxt)   # contexts, built
-                                                                      # while this one runs
+                if len(nxt) == 5:                                     # contexts, built
+                    dep = pending.get(nxt[2])                         # while this one runs
+                    if dep is None:
+                        continue
+                    nxt = nxt[:2] + (dep,) + nxt[3:]
+                    derived_from[(nxt[0], nxt[1])] = dep
+                pending[(nxt[0], nxt[1])] = pool.submit(build, nxt)
         if len(pts) == 0 or len(cams) < 2:
             if pre is not None:
                 pre.close()
@@ -372,7 +408,7 @@ def incremental_bundle(sc, fix_calibration=True, init_cams=(0, 1), align=True, d
             X[:, cand] = _triangulate(sc, K, T, w, cand, status)
             ba("after-triangulation", j)                 # :300-318
     finally:
-        for f in pending.values():                       # a prefetched context not used
+        for f in list(pending.values()) + discard:       # a prefetched context not used
             try:
                 pre = f.result()[2]
             except Exception:                            # noqa: BLE001 -- already failing
@@ -431,18 +467,33 @@ def _triangulate(sc, K, T, w, pts, status):
     return out
 
 
+_SIM_TRUTH = [None]   # (scene, point set, its ground-truth side of _similarity)
+
+
 def _similarity(sc, X):
     """(s, R, t) with X_current ~ s R X_truth + t, fitted (Umeyama) on the
-    points reconstructed so far; identity when the frame is not aligned yet."""
+    points reconstructed so far; identity when the frame is not aligned yet.
+    The ground-truth side (centroid, centred points, their square sum) depends
+    only on the point set, which the replay changes once per camera while this
+    runs about twice per camera: kept for the last set (the same arrays, so
+    the same values bit for bit)."""
     old = X[3] == 1
     if not np.any(old):
         return 1.0, np.eye(3), np.zeros(3)
-    A = sc.X[:3, old]
+    key = _SIM_TRUTH[0]
+    if key is not None and key[0] is sc and np.array_equal(key[1], old):
+        ca, Ac, den = key[2]
+    else:
+        A = sc.X[:3, old]
+        ca = A.mean(1, keepdims=True)
+        Ac = A - ca
+        den = (Ac ** 2).sum()
+        _SIM_TRUTH[0] = (sc, old, (ca, Ac, den))
     B = X[:3, old]
-    ca, cb = A.mean(1, keepdims=True), B.mean(1, keepdims=True)
-    U, sv, Vt = np.linalg.svd((B - cb) @ (A - ca).T)
+    cb = B.mean(1, keepdims=True)
+    U, sv, Vt = np.linalg.svd((B - cb) @ Ac.T)
     D = np.diag([1.0, 1.0, np.sign(np.linalg.det(U @ Vt))])
     R = U @ D @ Vt
-    s = (sv * np.diag(D)).sum() / ((A - ca) ** 2).sum()
+    s = (sv * np.diag(D)).sum() / den
     t = (cb - s * R @ ca).reshape(3)
     return s, R, t

@@ -163,6 +163,62 @@ def test_incremental_prefetch_bookkeeping(monkeypatch, prefetch, early):
                              pf["built_inline"]) == (0, 0, 0, 0)
 
 
+def test_incremental_prefetch_wrong_predictions(monkeypatch):
+    """Every prediction across a triangulation wrong (the workers' triangulation
+    rejects one more point than the replay's): each solve still gets the
+    context of its own exact sets -- the after-triangulation solves rebuilt
+    (mispredicted), the derived before-triangulation contexts (built from the
+    wrong prediction, incremental.next_sets) replaced at the solve before them
+    -- and every context built is closed."""
+    import threading
+    from types import SimpleNamespace
+
+    import bundleadjustmentmatlab_amd.incremental as inc
+    sc = make_config("cfg5x", m=16, seed=3)   # (new points appear at most cameras)
+    made, calls = [], []
+
+    class FakeAdjuster:
+        def __init__(self, K, m, n, pt, cam, ox, *opts, **kw):
+            self.key = (m, n, len(pt), ox.tobytes())
+            self.closed = False
+            made.append(self)
+
+        def close(self):
+            self.closed = True
+
+    def fake_solve(K, T, w, X, pt, cam, ox, *opts, adjuster=None, return_stats=False, **kw):
+        assert adjuster is not None and adjuster.key == (K.shape[1], X.shape[1], len(pt),
+                                                         ox.tobytes())
+        adjuster.close()
+        calls.append(len(pt))
+        return K, T, w, X, np.array([1.0, 0.5]), SimpleNamespace(iterations=1, accepted=1,
+                                                                 seconds=0.0)
+
+    tri = inc._triangulate
+
+    def worker_tri(sc_, K, T, w, pts, status):
+        out = tri(sc_, K, T, w, pts, status)
+        if threading.current_thread() is not threading.main_thread():
+            ok = np.nonzero(out[3] == 1.0)[0]
+            if len(ok):
+                out[:, ok[-1]] = 0.0
+        return out
+
+    monkeypatch.setattr(inc, "PREDICT_EARLY_PTS", 0)
+    monkeypatch.setattr(inc, "_triangulate", worker_tri)
+    monkeypatch.setattr(inc, "euclid_obs_adjuster", FakeAdjuster)
+    monkeypatch.setattr(inc, "bundle_euclid_obs", fake_solve)
+    monkeypatch.setattr(inc, "bundle_euclid_resect",
+                        lambda K, T, w, Xs, xs, *o, **kw: (K, T, w, [np.array([1.0])]))
+    res = inc.incremental_bundle(sc)
+    assert len(calls) == 2 * (sc.m - 2)
+    pf = res["prefetch"]
+    assert pf["derived_rebuilt"] >= 1 and pf["mispredicted"] >= 1, pf
+    assert pf["prefetched"] + pf["repredicted"] + pf["mispredicted"] + 1 == len(calls), pf
+    assert pf["built_inline"] == 1 + pf["mispredicted"], pf
+    assert all(a.closed for a in made)
+
+
 def test_triangulation_restatement():
     """incremental._triangulate (triangulation.m): noise-free observations in
     the true cameras give the true points back; a point behind one of its
