@@ -1701,7 +1701,12 @@ __global__ void k_schur_reduce(const int *__restrict__ blk_jk, const int *__rest
                                ba_direct dir)
 {
     constexpr int NN = NA * NA, WS = 3 * NA;
-    __shared__ double ys[BA_LMATCH_BATCH * WS], ws[BA_LMATCH_BATCH * WS];
+    // the long-track batches' Y / W rows: dynamic LDS, sized by the launch only
+    // when this launch takes the long tracks' pairs (lg.pair_ptr) -- static
+    // arrays (14 KB) held 11 of these one-wave workgroups on a CU where the
+    // wave slots allow more, so the ~6000 blocks of config 3 ran in 2+ rounds
+    extern __shared__ double lds_dyn[];
+    double *ys = lds_dyn, *ws = lds_dyn + BA_LMATCH_BATCH * WS;
     __shared__ int dzero[NA];
     __shared__ double erhs[NA];
     const int bk = blockIdx.x, l = threadIdx.x;
@@ -2576,7 +2581,8 @@ static int launch_schur_fast(ba_dev *d, double lambda)
     }
     ba_direct dir{nullptr, 0, nullptr};
     if (d->asm_direct) dir = ba_direct{d->S, d->lds, d->scal + 4};
-    k_schur_reduce<NA><<<d->nb, bs, 0, d->stream>>>(
+    const size_t lsh = lg.pair_ptr ? sizeof(double) * 2 * BA_LMATCH_BATCH * 3 * NA : 0;
+    k_schur_reduce<NA><<<d->nb, bs, lsh, d->stream>>>(
         d->blk_jk, d->blk_gptr, d->blk_gslots, d->cam_gptr, d->cam_gslots, d->spart, d->epart,
         d->U, d->eA, d->nb, lambda, d->schur_owner, d->sblk, d->rhs, lg, dir);
     if (d->nl > 0 && d->nlb)   // the long tracks' terms after the slot sums

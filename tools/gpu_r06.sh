@@ -57,7 +57,7 @@ for step in "$@"; do
           VLGBA_LIB=tools/build/ab/$v/libvlgba.so timeout -k 10 300 python -u bench.py --steps 100 \
             --warmup 50 --no-cpu-baseline --no-other-configs > gpurun_out/ab_${v}_$r.json \
             2> gpurun_out/ab_${v}_$r.log || { tail -5 gpurun_out/ab_${v}_$r.log; exit 1; }
-          echo "$v run $r $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_${v}_$r.json) $(grep -o 'k_update_linearize=[0-9.]*us' gpurun_out/ab_${v}_$r.log | head -1) $(grep -o 'k_schur_mfma=[0-9.]*us' gpurun_out/ab_${v}_$r.log | head -1) $(grep -o 'k_cr32_fused=[0-9.]*us' gpurun_out/ab_${v}_$r.log | head -1)"
+          echo "$v run $r $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_${v}_$r.json) $(grep -o 'k_update_linearize=[0-9.]*us' gpurun_out/ab_${v}_$r.log | head -1) $(grep -o 'k_schur_mfma=[0-9.]*us' gpurun_out/ab_${v}_$r.log | head -1) $(grep -o 'k_cr32_fused=[0-9.]*us' gpurun_out/ab_${v}_$r.log | head -1) $(grep -o 'k_schur_reduce=[0-9.]*us' gpurun_out/ab_${v}_$r.log | head -1)"
         done
       done ;;
     stream)
