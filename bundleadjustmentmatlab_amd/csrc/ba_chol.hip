@@ -2803,11 +2803,29 @@ __global__ __launch_bounds__(256) void k_assemble_tiles(
     const long long r0 = (long long)NB * ti, c0 = (long long)NB * tk;
     const int na2 = na * na;
     const int u0 = tb_ptr[blockIdx.x], nq = (tb_ptr[blockIdx.x + 1] - u0) * na2;
-    for (int q = tid; q < nq; q += 256) {   // (block, entry) pairs, all lanes busy
-        const int u = q / na2, l = q - na2 * u;
-        const int bk = tb_blk[u0 + u];
+    // (block, entry) pairs, all lanes busy; four a lane per step with their
+    // three dependent loads (block id, its cameras, the entry) in flight
+    // together -- each item writes its own tile entry, so the same tile
+    for (int q0 = tid; q0 < nq; q0 += 4 * 256) {
+        int lq[4], bq[4], jq[4], kq[4];
+        double vq[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const int q = min(q0 + 256 * t, nq - 1), u = q / na2;
+            lq[t] = q - na2 * u;
+            bq[t] = tb_blk[u0 + u];
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            jq[t] = blk_jk[2 * bq[t]];
+            kq[t] = blk_jk[2 * bq[t] + 1];
+            vq[t] = sblk[(size_t)na2 * bq[t] + lq[t]];
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+        if (q0 + 256 * t >= nq) break;
+        const int l = lq[t], bj = jq[t], bc = kq[t];
         const int r = l % na, c = l / na;
-        const int bj = blk_jk[2 * bk], bc = blk_jk[2 * bk + 1];
         long long row, col;
         if (!crow) {
             row = (long long)na * bj + r;
@@ -2822,7 +2840,8 @@ __global__ __launch_bounds__(256) void k_assemble_tiles(
             }
         }
         if (row < col || row < r0 || row >= r0 + NB || col < c0 || col >= c0 + NB) continue;
-        T[(row - r0) * (NB + 1) + (col - c0)] = sblk[(size_t)na2 * bk + l];
+        T[(row - r0) * (NB + 1) + (col - c0)] = vq[t];
+        }
     }
     __syncthreads();
     if (ti == tk && tid < NB) {   // pinv semantics for exactly-zero rows, padding rows
